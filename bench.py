@@ -1,0 +1,287 @@
+"""bench.py — device-resident GB/s of the N-way weighted model-tensor reduce.
+
+Metric (BASELINE.json): "device-resident GB/s, N-way weighted model-tensor
+reduce; 1/2/4/8 MI355X". A step is one aggregate of one batch: one launch of
+the fused HIP reduce over N flat parameter arenas already resident in HBM
+(the arithmetic of FedAvg.aggregate, dasklearn/gradient_aggregation/fedavg.py:12-26).
+
+Workload (default, --config north_star): 8 models x 11,181,642 fp32 params
+(ResNet-18/CIFAR-10 size), Dirichlet(1) weights, DLSIM_EXACT (bit-identical
+to the reference). Multi-GPU: one process per GPU (torchrun); the parameter
+axis is sharded — each rank owns an 11,181,642-element slice of every model
+(weak scaling: the global parameter count grows with N) and reduces it with
+no data-path collective; `value` = bytes all ranks processed / max-over-ranks
+time. The RCCL all-gather that would materialise the full output is timed
+separately (`allgather`), never inside `value`.
+
+Bytes per step per rank = (N_models + 1) * P * sizeof(dtype) (read N, write 1).
+Inputs rotate over 3 disjoint sets so the 256 MiB Infinity Cache cannot serve
+re-reads.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config NAME]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.join(ROOT, "decentralized-learning-simulator_amd")
+for _p in (ROOT, PKG_ROOT):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "device-resident GB/s, N-way weighted model-tensor reduce; 1/2/4/8 MI355X"
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+RESNET18_P = 11_181_642
+
+# name: (n_models, params per rank, dtype, weights, description)
+CONFIGS = {
+    "north_star": (8, RESNET18_P, "f32", "dirichlet",
+                   "8-way Dirichlet-weighted fp32 reduce, 11,181,642 params/rank (ResNet-18/CIFAR-10)"),
+    "cfg2": (8, 1_048_576, "f32", "uniform",
+             "8-way unweighted fp32 average, 1,048,576 params (CIFAR-10 model, ~1 M label)"),
+    "cfg2_gnlenet": (8, 85_354, "f32", "uniform",
+                     "8-way unweighted fp32 average of GNLeNet (85,354 params)"),
+    "cfg3": (17, RESNET18_P, "f32", "dirichlet",
+             "D-PSGD k=16 weighted neighbour mix, 17 x 11,181,642 fp32"),
+    "cfg4": (2, 125_000_000, "bf16", "age",
+             "gossip 2-way bf16 merge, 125,000,000 params/rank, age weights [3/8, 5/8]"),
+    "cfg5": (100, RESNET18_P, "f32", "dirichlet",
+             "FedAvg 100-client weighted fp32 reduce, 11,181,642 params/rank"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="north_star", choices=sorted(CONFIGS))
+    ap.add_argument("--mode", default="exact", choices=["exact", "fast"])
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling: split the config's params over ranks instead of per rank")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="budget for the CPU baseline sample (rank 0, N=1 only)")
+    return ap.parse_args()
+
+
+def weights_for(kind: str, n: int) -> list:
+    if kind == "dirichlet":
+        return [float(w) for w in np.random.default_rng(7).dirichlet(np.ones(n))]
+    if kind == "age":
+        return [3.0 / 8.0, 5.0 / 8.0][:n] if n == 2 else [1.0 / n] * n
+    return [float(1.0 / n)] * n  # fedavg.py:14-15
+
+
+def pmc_traffic(config: str, mode: str):
+    """Per-launch HBM bytes for this config from the committed PMC summary
+    (profiles/*pmc*.json, made by scripts/pmc_summary.py from rocprofv3 --pmc
+    runs of this same command; FETCH_SIZE doubled per the gfx950 rule)."""
+    import glob
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except Exception:
+            continue
+        ent = d.get(config, {}).get(mode)
+        if ent and "hbm_bytes_per_launch" in ent:
+            best = ent["hbm_bytes_per_launch"]
+    return best
+
+
+def cpu_baseline(n, p, dtype, weights, budget_s):
+    """The op-for-op PyTorch-CPU restatement of FedAvg.aggregate (oracle/,
+    validated bit-identical to the reference), timed on this host's cores at
+    the reference worker's 4 threads (broker.py:31, session_settings.py:52)."""
+    from oracle import fedavg_torch
+    threads = 4
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
+        g = torch.Generator().manual_seed(1234)
+        xs = [(torch.randn(p, generator=g) * 0.05).to(tdt) for _ in range(n)]
+        fedavg_torch.aggregate_flat(xs, weights)  # warm
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            fedavg_torch.aggregate_flat(xs, weights)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= budget_s or reps >= 500:
+                break
+        per = el / reps
+        bytes_ = (n + 1) * p * xs[0].element_size()
+        return {"value": round(bytes_ / per / 1e9, 3), "unit": "GB/s", "cores": threads,
+                "kind": "port",
+                "ms_per_step": round(per * 1e3, 3),
+                "sample": f"{reps} x the same {n}-way {p}-param {dtype} reduce on host tensors "
+                          f"({el:.1f} s), torch CPU ops in the reference's order at {threads} threads"}
+    finally:
+        torch.set_num_threads(prev)
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus != 1:
+            print(f"bench.py: --gpus {args.gpus} needs torchrun with that many ranks", file=sys.stderr)
+            sys.exit(2)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from dasklearn_amd import _native
+
+    n, p_cfg, dtype, wkind, desc = CONFIGS[args.config]
+    if args.strong and world > 1:
+        b, e = _native.shard_range(p_cfg, world, rank, 64)
+        p = e - b
+    else:
+        p = p_cfg
+    tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
+    esz = 2 if dtype == "bf16" else 4
+    mode = _native.DLSIM_EXACT if args.mode == "exact" else _native.DLSIM_FAST
+    weights = weights_for(wkind, n)
+    w32 = _native.fp32_weights(weights)
+
+    # 3 rotating input sets (each > 256 MiB Infinity Cache for the large configs)
+    sets = 3
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    arenas = []
+    for s in range(sets):
+        x = torch.empty((n, p), dtype=tdt, device=dev)
+        for i in range(n):
+            x[i].copy_(torch.randn(p, generator=g, device=dev) * 0.05)
+        arenas.append(x)
+    outs = [torch.empty(p, dtype=tdt, device=dev) for _ in range(sets)]
+    plans = [_native.ReducePlan([arenas[s][i] for i in range(n)], w32, outs[s], mode) for s in range(sets)]
+    stream = torch.cuda.current_stream(dev)
+
+    for k in range(args.warmup):
+        plans[k % sets].launch(stream)
+    torch.cuda.synchronize(dev)
+
+    K = args.steps
+    ev0 = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
+    ev1 = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(K):
+        ev0[k].record(stream)
+        plans[k % sets].launch(stream)
+        ev1[k].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+
+    kern_ms = sorted(ev0[k].elapsed_time(ev1[k]) for k in range(K))
+    kern_avg_ms = sum(kern_ms) / K
+    kern_med_ms = kern_ms[K // 2]
+
+    bytes_per_launch = (n + 1) * p * esz
+    el_t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    tot_b = torch.tensor([bytes_per_launch * K], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tot_b, op=dist.ReduceOp.SUM)
+    max_el = float(el_t.item())
+    total_bytes = float(tot_b.item())
+    value = total_bytes / max_el / 1e9
+
+    # copy ceiling on this device (same footprint as one step), reported beside
+    cb = (bytes_per_launch // 2) & ~15
+    src = torch.empty(cb, dtype=torch.uint8, device=dev).fill_(1)
+    dst = torch.empty_like(src)
+    for _ in range(5):
+        _native.probe_copy(src, dst)
+    c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    c0.record(stream)
+    for _ in range(20):
+        _native.probe_copy(src, dst)
+    c1.record(stream)
+    torch.cuda.synchronize(dev)
+    copy_gbps = 2 * cb * 20 / (c0.elapsed_time(c1) * 1e-3) / 1e9
+    del src, dst
+
+    allgather = None
+    if world > 1:
+        full = torch.empty(p * world, dtype=tdt, device=dev)
+        for _ in range(3):
+            dist.all_gather_into_tensor(full, outs[0])
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        a0 = time.perf_counter()
+        reps = 10
+        for _ in range(reps):
+            dist.all_gather_into_tensor(full, outs[0])
+        torch.cuda.synchronize(dev)
+        ag_ms = (time.perf_counter() - a0) / reps * 1e3
+        agt = torch.tensor([ag_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(agt, op=dist.ReduceOp.MAX)
+        allgather = {"ms": round(float(agt.item()), 4),
+                     "bytes_out_per_rank": p * esz * world,
+                     "note": "RCCL all_gather_into_tensor of the reduced shards (not in value)"}
+
+    result = None
+    if rank == 0:
+        achieved = bytes_per_launch / (kern_avg_ms * 1e-3) / 1e9
+        traffic = pmc_traffic(args.config, args.mode)
+        result = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": args.warmup,
+            "ms_per_step": round(max_el / K * 1e3, 5),
+            "higher_is_better": True,
+            "scaling": "strong" if (args.strong and world > 1) else "weak",
+            "vs_baseline": None,
+            "dtype": dtype,
+            "data": "synthetic: torch.randn*0.05 on device, 3 rotating input sets; "
+                    f"{wkind} weights",
+            "config": {"workload": args.config + ": " + desc, "n_models": n, "params_per_rank": p,
+                       "mode": args.mode, "parallelism": f"param-shard x{world}",
+                       "bytes_per_step_per_rank": bytes_per_launch},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                         "traffic": traffic,
+                         "kernel": "dlsim::k_wreduce_vec",
+                         "kernel_avg_us": round(kern_avg_ms * 1e3, 2),
+                         "kernel_median_us": round(kern_med_ms * 1e3, 2)},
+            "copy_ceiling_GBps": round(copy_gbps, 1),
+        }
+        if allgather:
+            result["allgather"] = allgather
+    if world > 1:
+        dist.barrier()
+    if rank == 0:
+        if world == 1 and not args.no_cpu_baseline:
+            result["cpu_baseline"] = cpu_baseline(n, p, dtype, weights, args.cpu_seconds)
+        else:
+            result["cpu_baseline"] = None
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,196 @@
+"""ctypes binding of the HIP C ABI (include/dlsim.h -> lib/libdlsim_hip.so).
+
+This is the only way the package computes: there is no CPU fallback. If the
+library is missing or no GPU is visible, calls raise loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Optional, Sequence
+
+import numpy as np
+
+LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libdlsim_hip.so")
+
+DLSIM_F32 = 0
+DLSIM_BF16 = 1
+DLSIM_EXACT = 0
+DLSIM_FAST = 1
+MAX_FUSED_INPUTS = 128
+
+# Every symbol include/dlsim.h declares (tests/test_abi.py checks the header
+# against this list and the library's exports).
+EXPORTS = (
+    "dlsim_wreduce",
+    "dlsim_wreduce_tensors",
+    "dlsim_shard_range",
+    "dlsim_probe_copy",
+    "dlsim_last_error",
+    "dlsim_version",
+)
+
+_lib = None
+_lock = threading.Lock()
+
+
+class DlsimError(RuntimeError):
+    """A dlsim_* call returned a negative code."""
+
+    def __init__(self, fn: str, rc: int, msg: str):
+        super().__init__(f"{fn} failed (rc={rc}): {msg}")
+        self.rc = rc
+
+
+def load() -> ctypes.CDLL:
+    """Load libdlsim_hip.so (built by __graft_entry__.build()); raise if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"HIP extension not built: {LIB_PATH} is missing. Run "
+                "`python -c 'import __graft_entry__ as g; g.build()'` at the repo root.")
+        lib = ctypes.CDLL(LIB_PATH)
+        vp, sz, i = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+        lib.dlsim_wreduce.argtypes = [ctypes.POINTER(vp), i, ctypes.POINTER(ctypes.c_float), vp,
+                                      sz, i, i, vp]
+        lib.dlsim_wreduce.restype = i
+        lib.dlsim_wreduce_tensors.argtypes = [ctypes.POINTER(vp), i, i, ctypes.POINTER(sz),
+                                              ctypes.POINTER(ctypes.c_float), ctypes.POINTER(vp),
+                                              i, i, vp]
+        lib.dlsim_wreduce_tensors.restype = i
+        lib.dlsim_shard_range.argtypes = [sz, i, i, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)]
+        lib.dlsim_shard_range.restype = i
+        lib.dlsim_probe_copy.argtypes = [vp, vp, sz, vp]
+        lib.dlsim_probe_copy.restype = i
+        lib.dlsim_last_error.argtypes = []
+        lib.dlsim_last_error.restype = ctypes.c_char_p
+        lib.dlsim_version.argtypes = []
+        lib.dlsim_version.restype = i
+        _lib = lib
+        return lib
+
+
+def _check(fn: str, rc: int) -> None:
+    if rc != 0:
+        msg = load().dlsim_last_error().decode(errors="replace")
+        raise DlsimError(fn, rc, msg)
+
+
+def version() -> int:
+    return load().dlsim_version()
+
+
+def shard_range(n_elems: int, world: int, rank: int, align_elems: int = 64):
+    lib = load()
+    b, e = ctypes.c_size_t(0), ctypes.c_size_t(0)
+    _check("dlsim_shard_range",
+           lib.dlsim_shard_range(n_elems, world, rank, align_elems, ctypes.byref(b), ctypes.byref(e)))
+    return b.value, e.value
+
+
+def fp32_weights(weights: Sequence[float]) -> np.ndarray:
+    """Python floats -> fp32 with round-to-nearest-even, as the reference's
+    `w * p1` converts a Python-float scalar (fedavg.py:25)."""
+    return np.asarray([float(w) for w in weights], dtype=np.float64).astype(np.float32)
+
+
+def dtype_code(torch_dtype) -> int:
+    import torch
+    if torch_dtype == torch.float32:
+        return DLSIM_F32
+    if torch_dtype == torch.bfloat16:
+        return DLSIM_BF16
+    raise TypeError(f"aggregation supports float32 and bfloat16 parameters, got {torch_dtype}")
+
+
+def _stream_handle(device, stream) -> Optional[int]:
+    import torch
+    if stream is None:
+        stream = torch.cuda.current_stream(device)
+    return stream.cuda_stream
+
+
+class ReducePlan:
+    """One prepared `dlsim_wreduce` call: pointer and weight arrays built once,
+    `launch()` is a single ctypes call (used by hot loops and bench.py)."""
+
+    def __init__(self, inputs, weights_f32: np.ndarray, out, mode: int = DLSIM_EXACT):
+        import torch
+        n = len(inputs)
+        if n < 1:
+            raise IndexError("list index out of range")
+        if len(weights_f32) != n:
+            raise AssertionError("weights/models length mismatch")
+        dt = dtype_code(out.dtype)
+        numel = out.numel()
+        for t in list(inputs) + [out]:
+            if not t.is_cuda:
+                raise ValueError("ReducePlan needs device tensors (no CPU path)")
+            if t.dtype != out.dtype or t.numel() != numel or not t.is_contiguous():
+                raise ValueError("inputs and output must be contiguous, same dtype and size")
+            if t.device != out.device:
+                raise ValueError("inputs and output must live on one device")
+        self.device = out.device
+        self.n, self.numel, self.dtype, self.mode = n, numel, dt, mode
+        self._keep = (list(inputs), out)  # keep storages alive while planned
+        self._ptrs = (ctypes.c_void_p * n)(*[t.data_ptr() for t in inputs])
+        self._w = np.ascontiguousarray(weights_f32, dtype=np.float32)
+        self._wp = self._w.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+        self._out = ctypes.c_void_p(out.data_ptr())
+        self._lib = load()
+        torch.cuda.current_device()  # a GPU must be present
+
+    def launch(self, stream=None) -> None:
+        rc = self._lib.dlsim_wreduce(self._ptrs, self.n, self._wp, self._out, self.numel,
+                                     self.dtype, self.mode, _stream_handle(self.device, stream))
+        _check("dlsim_wreduce", rc)
+
+
+def wreduce(inputs, weights_f32, out, mode: int = DLSIM_EXACT, stream=None):
+    """out = sum_i w_i * inputs[i] on the device (flat tensors), stream-ordered."""
+    ReducePlan(inputs, weights_f32, out, mode).launch(stream)
+    return out
+
+
+def wreduce_tensors(inputs_by_model, weights_f32, outs, mode: int = DLSIM_EXACT, stream=None):
+    """Tensor-list form: inputs_by_model[i][k] is tensor k of model i."""
+    lib = load()
+    n = len(inputs_by_model)
+    if n < 1:
+        raise IndexError("list index out of range")
+    t = len(outs)
+    dt = dtype_code(outs[0].dtype) if t else DLSIM_F32
+    flat = []
+    for row in inputs_by_model:
+        if len(row) != t:
+            raise ValueError("every model must have the same number of tensors")
+        for k, x in enumerate(row):
+            if not x.is_cuda or not x.is_contiguous() or x.dtype != outs[k].dtype \
+                    or x.numel() != outs[k].numel():
+                raise ValueError(f"tensor {k}: device/contiguity/dtype/size mismatch")
+            flat.append(x.data_ptr())
+    ptrs = (ctypes.c_void_p * len(flat))(*flat)
+    numels = (ctypes.c_size_t * t)(*[o.numel() for o in outs])
+    optrs = (ctypes.c_void_p * t)(*[o.data_ptr() for o in outs])
+    w = np.ascontiguousarray(weights_f32, dtype=np.float32)
+    if w.size != n:
+        raise AssertionError("weights/models length mismatch")
+    dev = outs[0].device if t else None
+    rc = lib.dlsim_wreduce_tensors(ptrs, n, t, numels, w.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                                   optrs, dt, mode, _stream_handle(dev, stream) if t else None)
+    _check("dlsim_wreduce_tensors", rc)
+    return outs
+
+
+def probe_copy(src, dst, stream=None) -> None:
+    lib = load()
+    nbytes = src.numel() * src.element_size()
+    _check("dlsim_probe_copy", lib.dlsim_probe_copy(src.data_ptr(), dst.data_ptr(), nbytes,
+                                                    _stream_handle(src.device, stream)))

@@ -1,0 +1,222 @@
+"""Parameter arenas: nn.Module parameters <-> flat device buffers.
+
+The reference folds parameters tensor by tensor, model by model
+(dasklearn/gradient_aggregation/fedavg.py:23-25: N x T Python iterations).
+Here a model's parameters() are one flat arena (concatenated in parameters()
+order, one arena per dtype), so one kernel launch reduces every tensor of
+every model. Three ways in:
+
+* device arena   — every parameter of a CUDA model is a view into one flat
+                   buffer in parameters() order (what `aggregate_modules`
+                   returns for device inputs): zero copies, one launch;
+* device tensors — CUDA parameters in separate storages: the tensor-list ABI
+                   entry (`dlsim_wreduce_tensors`) reads them in place;
+* host models    — CPU parameters (the reference's case: models reach the
+                   worker through torch-mp shared memory, model_trainer.py:129):
+                   packed into pinned staging, copied H2D per model on the
+                   current stream, reduced, copied back.
+
+The result is a fresh module with `copy.deepcopy(models[0])` semantics
+(fedavg.py:20): buffers and attributes copied from models[0]; parameters
+replaced — through the deepcopy memo, so they are never copied — by views of
+the reduced arena, keeping each original's requires_grad.
+"""
+from __future__ import annotations
+
+import copy
+from collections import OrderedDict
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+from torch import nn
+
+from . import _native
+
+
+class ParamLayout:
+    """parameters() of a module grouped by dtype, with flat offsets."""
+
+    def __init__(self, module: nn.Module):
+        self.params: List[nn.Parameter] = list(module.parameters())
+        self.shapes = [tuple(p.shape) for p in self.params]
+        self.groups: "OrderedDict[torch.dtype, List[int]]" = OrderedDict()
+        for k, p in enumerate(self.params):
+            self.groups.setdefault(p.dtype, []).append(k)
+        self.offsets: Dict[int, int] = {}
+        self.totals: Dict[torch.dtype, int] = {}
+        for dt, idx in self.groups.items():
+            _native.dtype_code(dt)  # raises TypeError for unsupported dtypes
+            off = 0
+            for k in idx:
+                self.offsets[k] = off
+                off += self.params[k].numel()
+            self.totals[dt] = off
+
+    def check_compatible(self, module: nn.Module) -> List[nn.Parameter]:
+        ps = list(module.parameters())
+        # The reference zips parameters() (fedavg.py:24) and silently truncates
+        # on a mismatch; equal shapes are what it assumes, so insist on them.
+        if len(ps) != len(self.params):
+            raise ValueError("models have different numbers of parameters")
+        for k, (a, b) in enumerate(zip(ps, self.params)):
+            if a.shape != b.shape or a.dtype != b.dtype:
+                raise ValueError(f"parameter {k}: shape/dtype differs from models[0]")
+        return ps
+
+    def arena_view(self, params: Sequence[torch.Tensor], dt: torch.dtype) -> Optional[torch.Tensor]:
+        """If the dtype group of `params` already is one contiguous flat buffer
+        (in layout order), return a flat view of it, else None."""
+        idx = self.groups[dt]
+        first = params[idx[0]]
+        if not first.is_contiguous():
+            return None
+        base = first.data_ptr()
+        esz = first.element_size()
+        storage = first.untyped_storage().data_ptr()
+        for k in idx:
+            p = params[k]
+            if not p.is_contiguous() or p.untyped_storage().data_ptr() != storage:
+                return None
+            if p.data_ptr() != base + self.offsets[k] * esz:
+                return None
+        total = self.totals[dt]
+        return torch.as_strided(first.detach(), (total,), (1,), first.storage_offset())
+
+
+class _Staging:
+    """Reusable device/pinned buffers keyed by (device, dtype, n, numel)."""
+
+    def __init__(self):
+        self.dev: Dict[Tuple, torch.Tensor] = {}
+        self.host: Dict[Tuple, torch.Tensor] = {}
+        # last use of a (device rows, pinned rows) pair: the next call waits on
+        # it before overwriting either buffer (a previous call may have
+        # returned with its H2D copies and kernel still queued).
+        self.last_use: Dict[Tuple, torch.cuda.Event] = {}
+
+    def acquire(self, device, dt, n, numel, stream):
+        key = (str(device), dt, n, numel)
+        ev = self.last_use.get(key)
+        if ev is not None:
+            ev.synchronize()
+        return self.device_rows(device, dt, n, numel), self.pinned_rows(dt, n, numel)
+
+    def release(self, device, dt, n, numel, stream):
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        self.last_use[(str(device), dt, n, numel)] = ev
+
+    def device_rows(self, device, dt, n, numel) -> torch.Tensor:
+        key = (str(device), dt, n, numel)
+        buf = self.dev.get(key)
+        if buf is None:
+            buf = torch.empty((n, numel), dtype=dt, device=device)
+            self.dev[key] = buf
+        return buf
+
+    def pinned_rows(self, dt, n, numel) -> torch.Tensor:
+        key = (dt, n, numel)
+        buf = self.host.get(key)
+        if buf is None:
+            buf = torch.empty((n, numel), dtype=dt, pin_memory=True)
+            self.host[key] = buf
+        return buf
+
+    def clear(self):
+        for ev in self.last_use.values():
+            ev.synchronize()
+        self.last_use.clear()
+        self.dev.clear()
+        self.host.clear()
+
+
+STAGING = _Staging()
+
+
+def _target_device(params0: Sequence[torch.Tensor], device) -> torch.device:
+    if device is not None:
+        return torch.device(device)
+    for p in params0:
+        if p.is_cuda:
+            return p.device
+    if not torch.cuda.is_available():
+        raise RuntimeError("dasklearn_amd aggregation runs on an AMD GPU; none is visible "
+                           "(there is no CPU fallback)")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, mode: int,
+                             device=None) -> Tuple[ParamLayout, Dict[torch.dtype, torch.Tensor], torch.device]:
+    """Reduce the parameters of `models` into one fresh device arena per dtype."""
+    layout = ParamLayout(models[0])
+    all_params = [layout.check_compatible(m) for m in models]
+    dev = _target_device(all_params[0], device)
+    n = len(models)
+    outs: Dict[torch.dtype, torch.Tensor] = {}
+    with torch.no_grad():
+        for dt, idx in layout.groups.items():
+            total = layout.totals[dt]
+            out = torch.empty(total, dtype=dt, device=dev)
+            outs[dt] = out
+            if total == 0:
+                continue
+            on_dev = all(all_params[i][idx[0]].device == dev for i in range(n))
+            if on_dev:
+                views = [layout.arena_view(ps, dt) for ps in all_params]
+                if all(v is not None for v in views):
+                    _native.wreduce(views, weights_f32, out, mode)
+                    continue
+                rows = [[ps[k].detach().contiguous() for k in idx] for ps in all_params]
+                outs_k = [out[layout.offsets[k]:layout.offsets[k] + layout.params[k].numel()]
+                          for k in idx]
+                _native.wreduce_tensors(rows, weights_f32, outs_k, mode)
+                continue
+            # host (or foreign-device) models: pack -> pinned -> H2D, per model
+            stream = torch.cuda.current_stream(dev)
+            dev_rows, pinned = STAGING.acquire(dev, dt, n, total, stream)
+            for i, ps in enumerate(all_params):
+                src = [ps[k].detach().reshape(-1) for k in idx]
+                if src[0].is_cuda:
+                    torch.cat([s.to(dev) for s in src], out=dev_rows[i])
+                else:
+                    torch.cat(src, out=pinned[i])
+                    with torch.cuda.stream(stream):
+                        dev_rows[i].copy_(pinned[i], non_blocking=True)
+            _native.wreduce([dev_rows[i] for i in range(n)], weights_f32, out, mode)
+            STAGING.release(dev, dt, n, total, stream)
+    return layout, outs, dev
+
+
+def module_from_arenas(model0: nn.Module, layout: ParamLayout,
+                       arenas: Dict[torch.dtype, torch.Tensor]) -> nn.Module:
+    """`copy.deepcopy(model0)` whose parameters are views of `arenas`."""
+    memo = {}
+    for dt, idx in layout.groups.items():
+        flat = arenas[dt]
+        for k in idx:
+            p = layout.params[k]
+            off = layout.offsets[k]
+            view = flat[off:off + p.numel()].view(p.shape)
+            memo[id(p)] = nn.Parameter(view, requires_grad=p.requires_grad)
+    return copy.deepcopy(model0, memo)
+
+
+def aggregate_modules(models: List[nn.Module], weights: Optional[Sequence[float]], mode: int,
+                      device=None, to_host: Optional[bool] = None) -> nn.Module:
+    """FedAvg.aggregate semantics on the GPU (see module docstring).
+
+    to_host: copy the result back to host memory (default: iff models[0]'s
+    parameters are on the host, like the reference's output)."""
+    # fedavg.py:14-17, same order of checks => same exceptions
+    if not weights:
+        weights = [float(1. / len(models)) for _ in range(len(models))]
+    else:
+        assert len(weights) == len(models)
+    model0 = models[0]  # IndexError for an empty list, as the reference
+    w32 = _native.fp32_weights(weights)
+    layout, arenas, dev = reduce_modules_to_arenas(models, w32, mode, device)
+    host_out = to_host if to_host is not None else not any(p.is_cuda for p in layout.params)
+    if host_out:
+        arenas = {dt: a.to("cpu") for dt, a in arenas.items()}  # synchronises the stream
+    return module_from_arenas(model0, layout, arenas)

@@ -1,0 +1,131 @@
+/*
+ * dlsim.h — C ABI of the MI355X-native aggregation hot path.
+ *
+ * The reference (sacs-epfl/decentralized-learning-simulator) has no native
+ * code: its hot path is the Python/PyTorch-CPU loop of
+ *   dasklearn/gradient_aggregation/fedavg.py:12-26   FedAvg.aggregate(models, weights)
+ * reached through
+ *   dasklearn/model_manager.py:41-43                  ModelManager.aggregate_trained_models
+ *   dasklearn/functions.py:89-106                     aggregate(settings, params)  (the "aggregate" task)
+ *   dasklearn/worker.py:27-31                         globals()[func_name](settings, data)
+ * Every entry point below replaces one piece of that loop; the Python host
+ * package (dasklearn_amd) binds them with ctypes, and INTEGRATION.md shows the
+ * binding a maintainer adds to the reference.
+ *
+ * Conventions
+ *   - Plain pointers and sizes only. Device buffers are caller-owned
+ *     (hipMalloc / torch CUDA tensors); host arrays (weights, pointer lists,
+ *     sizes) are read during the call and may be freed when it returns.
+ *   - Calls that take a `stream` (a hipStream_t, NULL = legacy default
+ *     stream) are stream-ordered and asynchronous: they enqueue work and
+ *     return; nothing synchronises the device.
+ *   - Return value: 0 on success, a negative DLSIM_E* code otherwise;
+ *     dlsim_last_error() gives a message (thread-local).
+ *   - No global state besides a per-thread error string.
+ */
+#ifndef DLSIM_H_
+#define DLSIM_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- element types and summation modes ---------------------------------- */
+enum dlsim_dtype {
+  DLSIM_F32 = 0,  /* IEEE binary32                                      */
+  DLSIM_BF16 = 1  /* bfloat16 (upper 16 bits of binary32), RNE rounding  */
+};
+
+enum dlsim_mode {
+  /* Bit-identical to FedAvg.aggregate (fedavg.py:20-25) on the same inputs:
+   *   acc = x0 * 0;  for i in 0..n-1: acc = acc + fl32(w_i) * x_i
+   * in that order, multiply and add rounded separately (no FMA); for bf16
+   * the product and every partial sum are rounded to bf16 (PyTorch's CPU
+   * opmath semantics). NaN payloads are not part of the contract. */
+  DLSIM_EXACT = 0,
+  /* Fused multiply-add, fp32 accumulation (bf16: one final rounding).
+   * Within n * 2^-23 relative (fp32) of EXACT; not bit-identical. */
+  DLSIM_FAST = 1
+};
+
+/* ---- error codes --------------------------------------------------------- */
+#define DLSIM_OK 0
+#define DLSIM_E_ARG (-1)      /* null pointer, n < 1, overlapping out/in, ... */
+#define DLSIM_E_DTYPE (-2)    /* dtype not in enum dlsim_dtype                */
+#define DLSIM_E_MODE (-3)     /* mode not in enum dlsim_mode                  */
+#define DLSIM_E_HIP (-100)    /* a HIP call failed: code = -100 - hipError_t  */
+
+/* Maximum inputs fused into one kernel launch; larger n is processed in
+ * passes of this many inputs that continue the running sum in `d_out`
+ * (same rounding sequence, so EXACT results do not depend on it). */
+#define DLSIM_MAX_FUSED_INPUTS 128
+
+/*
+ * dlsim_wreduce — N-way weighted element-wise reduce of flat buffers.
+ *
+ *   d_out[j] = sum_{i=0..n-1} h_weights[i] * d_inputs[i][j],  j < n_elems
+ *
+ * Replaces the N x T loop of FedAvg.aggregate (fedavg.py:20-25) for one flat
+ * parameter arena (all of a model's parameters() concatenated in order).
+ *   d_inputs   host array of n device pointers (each n_elems elements of dtype)
+ *   h_weights  host array of n fp32 weights (already rounded to fp32 — the
+ *              reference's `w * p1` converts its Python float with RNE,
+ *              fedavg.py:25); uniform 1/n is the caller's job (fedavg.py:14-15)
+ *   d_out      device buffer of n_elems; must not alias any input
+ *   stream     hipStream_t
+ * Any alignment is accepted; 16-byte-aligned buffers take the vector path.
+ */
+int dlsim_wreduce(const void* const* d_inputs, int n, const float* h_weights,
+                  void* d_out, size_t n_elems, int dtype, int mode,
+                  void* stream);
+
+/*
+ * dlsim_wreduce_tensors — the same reduce over T separate tensors per model,
+ * in one launch, without packing them into an arena first.
+ *
+ * Replaces the inner `zip(center_model.parameters(), m.parameters())` loop
+ * (fedavg.py:24-25) when the models' parameters already live on the device
+ * as separate tensors (e.g. a device-resident model cache).
+ *   d_inputs   host array of n*t device pointers, model-major:
+ *              d_inputs[i*t + k] = tensor k of model i
+ *   numels     host array of t element counts
+ *   d_outs     host array of t device pointers (outputs)
+ * Same weights, dtype and mode rules as dlsim_wreduce.
+ */
+int dlsim_wreduce_tensors(const void* const* d_inputs, int n, int t,
+                          const size_t* numels, const float* h_weights,
+                          void* const* d_outs, int dtype, int mode,
+                          void* stream);
+
+/*
+ * dlsim_shard_range — parameter-axis partition used by the sharded path.
+ *
+ * Splits [0, n_elems) into `world` contiguous slices whose boundaries are
+ * multiples of `align_elems` (except the end) and writes rank's slice to
+ * [*begin, *end). Every rank of a job must call it with the same arguments
+ * so shard boundaries agree. Host-only; no device work.
+ * (New: the reference has no multi-device path)
+ */
+int dlsim_shard_range(size_t n_elems, int world, int rank, size_t align_elems,
+                      size_t* begin, size_t* end);
+
+/*
+ * dlsim_probe_copy — streaming copy kernel (16 B/lane), used to measure the
+ * device's achievable HBM copy ceiling next to the reduce. bytes % 16 == 0.
+ */
+int dlsim_probe_copy(const void* d_src, void* d_dst, size_t bytes, void* stream);
+
+/* Message for the last failing call on this thread ("" if none). */
+const char* dlsim_last_error(void);
+
+/* ABI version: (major << 16) | minor. */
+int dlsim_version(void);
+
+#ifdef __cplusplus
+}  /* extern "C" */
+#endif
+
+#endif  /* DLSIM_H_ */

@@ -1,0 +1,151 @@
+"""TEST INFRASTRUCTURE ONLY — the checker, never the product.
+
+Python face of the CPU oracle for the aggregation hot path
+(reference: dasklearn/gradient_aggregation/fedavg.py:12-26, FedAvg.aggregate).
+
+* ``wreduce(xs, weights, dtype)`` — the plain-C restatement in
+  ``fedavg_oracle.c`` (built by ``oracle/Makefile`` into ``oracle/_build``),
+  bit-exact to the reference; pinned against tests/golden/ fixtures that were
+  produced by running the reference itself (tests/golden/make_golden.py).
+* ``reference_weights(n, weights)`` — fedavg.py:14-17 weight rules
+  (None / [] -> float(1./N); otherwise length must match) plus the fp32
+  rounding that ``w * p1`` applies (fedavg.py:25).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+import this module.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from typing import Optional, Sequence
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "liboracle.so")
+_lib = None
+
+
+def build() -> str:
+    """Compile the C oracle (idempotent)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def _load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(_LIB_PATH):
+        build()
+    lib = ctypes.CDLL(_LIB_PATH)
+    pp = ctypes.POINTER(ctypes.c_void_p)
+    for name in ("oracle_wreduce_f32", "oracle_wreduce_bf16", "oracle_wreduce_fast_f32",
+                 "oracle_wreduce_fast_bf16"):
+        fn = getattr(lib, name)
+        fn.argtypes = [pp, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+        fn.restype = ctypes.c_int
+    lib.oracle_wreduce_f32_rows.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_size_t]
+    lib.oracle_wreduce_f32_rows.restype = ctypes.c_int
+    _lib = lib
+    return lib
+
+
+def reference_weights(n: int, weights: Optional[Sequence[float]]) -> np.ndarray:
+    """fedavg.py:14-17: falsy weights -> [float(1./n)]*n, else len must be n.
+    Returned rounded to fp32 (the op converts the Python float with RNE)."""
+    if not weights:
+        weights = [float(1.0 / n) for _ in range(n)]
+    else:
+        assert len(weights) == n
+    return np.asarray([float(w) for w in weights], dtype=np.float64).astype(np.float32)
+
+
+def _as_rows(xs, np_dtype):
+    rows = [np.ascontiguousarray(x, dtype=np_dtype).reshape(-1) for x in xs]
+    p = rows[0].size
+    for r in rows:
+        if r.size != p:
+            raise ValueError("all inputs must have the same element count")
+    return rows, p
+
+
+def wreduce(xs, weights, dtype: str = "f32", mode: str = "exact") -> np.ndarray:
+    """N-way weighted reduce of flat arrays, reference rounding order.
+
+    xs: sequence of N arrays — float32 for "f32", uint16 bf16 bit patterns for
+    "bf16". weights: fp32 array-like of length N (already resolved).
+    Returns float32 (f32) or uint16 (bf16 bits).
+    """
+    lib = _load()
+    n = len(xs)
+    if n < 1:
+        raise IndexError("list index out of range")
+    w = np.ascontiguousarray(weights, dtype=np.float32)
+    if w.size != n:
+        raise AssertionError("weights/models length mismatch")
+    if dtype == "f32":
+        rows, p = _as_rows(xs, np.float32)
+        out = np.empty(p, dtype=np.float32)
+        fn = lib.oracle_wreduce_f32 if mode == "exact" else lib.oracle_wreduce_fast_f32
+    elif dtype == "bf16":
+        rows, p = _as_rows(xs, np.uint16)
+        out = np.empty(p, dtype=np.uint16)
+        fn = lib.oracle_wreduce_bf16 if mode == "exact" else lib.oracle_wreduce_fast_bf16
+    else:
+        raise ValueError(f"unsupported dtype {dtype}")
+    ptrs = (ctypes.c_void_p * n)(*[r.ctypes.data for r in rows])
+    rc = fn(ctypes.cast(ptrs, ctypes.POINTER(ctypes.c_void_p)), n, w.ctypes.data,
+            out.ctypes.data, p)
+    if rc != 0:
+        raise RuntimeError(f"oracle failed rc={rc}")
+    return out
+
+
+def wreduce_rows_f32(x: np.ndarray, weights) -> np.ndarray:
+    """Full-size fp32 fold over a (N, P) C-contiguous block (same arithmetic as
+    ``wreduce``; element loop innermost for speed)."""
+    lib = _load()
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    n, p = x.shape
+    w = np.ascontiguousarray(weights, dtype=np.float32)
+    out = np.empty(p, dtype=np.float32)
+    rc = lib.oracle_wreduce_f32_rows(x.ctypes.data, n, w.ctypes.data, out.ctypes.data, p)
+    if rc != 0:
+        raise RuntimeError(f"oracle failed rc={rc}")
+    return out
+
+
+def f32_to_bf16_bits(x: np.ndarray) -> np.ndarray:
+    """RNE fp32 -> bf16 bit patterns (NaN -> 0x7FC0), numpy restatement."""
+    u = np.ascontiguousarray(x, dtype=np.float32).view(np.uint32).astype(np.uint64)
+    nan = (u & 0x7FFFFFFF) > 0x7F800000
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
+    r[nan] = 0x7FC0
+    return r
+
+
+def bf16_bits_to_f32(h: np.ndarray) -> np.ndarray:
+    return (np.asarray(h, dtype=np.uint16).astype(np.uint32) << 16).view(np.float32)
+
+
+def same_bits(a: np.ndarray, b: np.ndarray) -> bool:
+    """Bit equality with every NaN treated as equal to every NaN (NaN payloads
+    differ between the reference's scalar/vector CPU paths and the GPU)."""
+    a = np.asarray(a)
+    b = np.asarray(b)
+    if a.shape != b.shape:
+        return False
+    if a.dtype == np.uint16:
+        fa, fb = bf16_bits_to_f32(a), bf16_bits_to_f32(b)
+        ia, ib = a, b
+    else:
+        fa, fb = a.astype(np.float32), b.astype(np.float32)
+        ia, ib = fa.view(np.uint32), fb.view(np.uint32)
+    na, nb = np.isnan(fa), np.isnan(fb)
+    if not np.array_equal(na, nb):
+        return False
+    return bool(np.array_equal(ia[~na], ib[~nb]))

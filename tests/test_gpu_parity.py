@@ -1,0 +1,240 @@
+"""HIP path vs the oracle and the reference's golden vectors (GPU).
+
+The bar: DLSIM_EXACT is bit-identical to the reference's
+FedAvg.aggregate (dasklearn/gradient_aggregation/fedavg.py:12-26) — every
+non-NaN element has the same bits, NaN positions match (NaN payloads are not
+part of the contract). DLSIM_FAST is checked against a tolerance written in
+each test.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden_paths, load_golden
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+from dasklearn_amd import _native  # noqa: E402
+
+
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    return torch.device("cuda", 0)
+
+
+def to_dev(rows, dtype):
+    if dtype == "bf16":
+        return [torch.from_numpy(np.ascontiguousarray(r).view(np.int16).copy()).view(torch.bfloat16).to(dev())
+                for r in rows]
+    return [torch.from_numpy(np.ascontiguousarray(r, dtype=np.float32)).to(dev()) for r in rows]
+
+
+def from_dev(t):
+    t = t.cpu()
+    if t.dtype == torch.bfloat16:
+        return t.view(torch.int16).numpy().view(np.uint16)
+    return t.numpy()
+
+
+def hip_reduce(rows, w, dtype, mode=_native.DLSIM_EXACT):
+    xs = to_dev(rows, dtype)
+    out = torch.empty(xs[0].numel(), dtype=xs[0].dtype, device=dev())
+    _native.wreduce(xs, w, out, mode)
+    return from_dev(out)
+
+
+# ---- golden vectors from the reference ------------------------------------------
+
+@pytest.mark.parametrize("path", golden_paths(), ids=lambda p: os.path.basename(p)[:-4])
+def test_flat_abi_matches_reference_golden(path):
+    g = load_golden(path)
+    meta = g["meta"]
+    w = orc.reference_weights(meta["n"], g["weights_arg"])
+    got = hip_reduce(list(g["inputs"]), w, meta["dtype"])
+    assert orc.same_bits(got, g["expected"]), meta["case"]
+
+
+# ---- random cases vs the oracle ----------------------------------------------------
+
+SIZES = [1, 3, 4, 5, 8, 17, 1023, 2048, 4097, 65536 + 7, 300_001]
+NS = [1, 2, 3, 7, 8, 9, 16, 17, 33, 100, 129, 200]
+
+
+def make_rows(n, p, seed, dtype):
+    rng = np.random.default_rng(seed)
+    x = (rng.standard_normal((n, p)).astype(np.float32) * np.float32(0.05))
+    if dtype == "bf16":
+        return orc.f32_to_bf16_bits(x)
+    return x
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("n", NS)
+def test_exact_vs_oracle_across_n(n, dtype):
+    p = 4097 + n  # ragged tail of every width
+    rows = make_rows(n, p, 10 + n, dtype)
+    w = orc.reference_weights(n, list(np.random.default_rng(n).dirichlet(np.ones(n))))
+    got = hip_reduce(list(rows), w, dtype)
+    assert orc.same_bits(got, orc.wreduce(list(rows), w, dtype))
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("p", SIZES)
+def test_exact_vs_oracle_across_sizes(p, dtype):
+    n = 8
+    rows = make_rows(n, p, p, dtype)
+    w = orc.reference_weights(n, None)
+    got = hip_reduce(list(rows), w, dtype)
+    assert orc.same_bits(got, orc.wreduce(list(rows), w, dtype))
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_misaligned_inputs_take_scalar_path(dtype):
+    """Views offset by one element are not 16-byte aligned: scalar kernel."""
+    n, p = 5, 10_001
+    rows = make_rows(n, p + 1, 77, dtype)
+    xs = [t[1:] for t in to_dev(list(rows), dtype)]
+    out = torch.empty(p, dtype=xs[0].dtype, device=dev())
+    w = orc.reference_weights(n, [0.3, -0.2, 0.5, 0.25, 0.15])
+    _native.wreduce(xs, w, out)
+    assert orc.same_bits(from_dev(out), orc.wreduce([r[1:] for r in rows], w, dtype))
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_output_may_alias_first_input(dtype):
+    n, p = 4, 50_003
+    rows = make_rows(n, p, 5, dtype)
+    xs = to_dev(list(rows), dtype)
+    w = orc.reference_weights(n, None)
+    _native.wreduce(xs, w, xs[0])
+    assert orc.same_bits(from_dev(xs[0]), orc.wreduce(list(rows), w, dtype))
+
+
+def test_partial_overlap_rejected():
+    buf = torch.zeros(1000, device=dev())
+    with pytest.raises(_native.DlsimError):
+        _native.wreduce([buf[0:500], buf[100:600]], orc.reference_weights(2, None), buf[50:550])
+
+
+def test_empty_tensor_is_noop():
+    x = torch.empty(0, device=dev())
+    out = torch.empty(0, device=dev())
+    _native.wreduce([x, x], orc.reference_weights(2, None), out)
+
+
+def test_unsupported_dtype_raises():
+    x = torch.zeros(16, dtype=torch.float16, device=dev())
+    with pytest.raises(TypeError):
+        _native.wreduce([x], orc.reference_weights(1, None), x)
+
+
+# ---- tensor-list entry ----------------------------------------------------------
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("n", [3, 130])
+def test_tensor_list_entry_matches_flat(n, dtype):
+    sizes = [1027, 64, 3, 517, 1, 4096]
+    p = sum(sizes)
+    rows = make_rows(n, p, 99 + n, dtype)
+    w = orc.reference_weights(n, list(np.random.default_rng(3).dirichlet(np.ones(n))))
+    flat = to_dev(list(rows), dtype)
+    by_model = []
+    for t in flat:
+        parts, off = [], 0
+        for s in sizes:
+            parts.append(t[off:off + s].clone())
+            off += s
+        by_model.append(parts)
+    outs = [torch.empty(s, dtype=flat[0].dtype, device=dev()) for s in sizes]
+    _native.wreduce_tensors(by_model, w, outs)
+    got = np.concatenate([from_dev(o) for o in outs])
+    assert orc.same_bits(got, orc.wreduce(list(rows), w, dtype))
+
+
+# ---- FAST mode: fused multiply-add, tolerance-only --------------------------------
+
+@pytest.mark.parametrize("n", [2, 8, 17, 100])
+def test_fast_mode_f32_within_tolerance(n):
+    p = 100_003
+    rows = make_rows(n, p, 1234 + n, "f32")
+    w = orc.reference_weights(n, list(np.random.default_rng(n).dirichlet(np.ones(n))))
+    got = hip_reduce(list(rows), w, "f32", _native.DLSIM_FAST)
+    exact = orc.wreduce(list(rows), w, "f32")
+    # it IS the fma chain the fast oracle computes...
+    assert orc.same_bits(got, orc.wreduce(list(rows), w, "f32", mode="fast"))
+    # ...and within n * 2^-23 of the exact fold, relative to sum |w_i x_i|
+    scale = np.abs(w[:, None] * rows).sum(axis=0)
+    assert np.all(np.abs(got - exact) <= n * 2.0 ** -23 * scale + 1e-30)
+
+
+@pytest.mark.parametrize("n", [2, 17])
+def test_fast_mode_bf16_within_tolerance(n):
+    p = 100_003
+    rows = make_rows(n, p, 4321 + n, "bf16")
+    w = orc.reference_weights(n, None)
+    got = hip_reduce(list(rows), w, "bf16", _native.DLSIM_FAST)
+    assert orc.same_bits(got, orc.wreduce(list(rows), w, "bf16", mode="fast"))
+    exact = orc.bf16_bits_to_f32(orc.wreduce(list(rows), w, "bf16"))
+    g = orc.bf16_bits_to_f32(got)
+    # one final bf16 rounding vs n per-step roundings: within (n+1) bf16 ulps
+    # (2^-8 relative) of the magnitude sum
+    scale = np.abs(w[:, None] * orc.bf16_bits_to_f32(rows)).sum(axis=0)
+    assert np.all(np.abs(g - exact) <= (n + 1) * 2.0 ** -8 * scale + 1e-30)
+
+
+# ---- full-size configurations (BASELINE.json) --------------------------------------
+
+def test_north_star_8way_11M_f32_bit_exact():
+    """8-way Dirichlet-weighted fp32 reduce of 11,181,642 params (ResNet-18/CIFAR-10)."""
+    n, p = 8, 11_181_642
+    g = torch.Generator(device="cpu").manual_seed(1234)
+    x = (torch.randn((n, p), generator=g) * 0.05).numpy()
+    w = orc.reference_weights(n, list(np.random.default_rng(7).dirichlet(np.ones(n))))
+    got = hip_reduce(list(x), w, "f32")
+    assert orc.same_bits(got, orc.wreduce_rows_f32(x, w))
+
+
+def test_cfg3_17way_11M_f32_bit_exact():
+    n, p = 17, 11_181_642
+    x = (torch.randn((n, p), generator=torch.Generator().manual_seed(5)) * 0.05).numpy()
+    w = orc.reference_weights(n, list(np.random.default_rng(7).dirichlet(np.ones(n))))
+    got = hip_reduce(list(x), w, "f32")
+    assert orc.same_bits(got, orc.wreduce_rows_f32(x, w))
+
+
+def test_cfg4_2way_125M_bf16_properties():
+    """2-way bf16 gossip merge of 125 M params with age weights [3/8, 5/8]:
+    size-independent properties at full size, bit-exact on a strided sample."""
+    p = 125_000_000
+    a = torch.randn(p, device=dev()).to(torch.bfloat16)
+    b = torch.randn(p, device=dev()).to(torch.bfloat16)
+    w = orc.reference_weights(2, [3 / 8, 5 / 8])
+    out = torch.empty_like(a)
+    _native.wreduce([a, b], w, out)
+    # property 1: one-hot weights reproduce an input exactly
+    sel = torch.empty_like(a)
+    _native.wreduce([a, b], orc.reference_weights(2, [0.0, 1.0]), sel)
+    assert torch.equal(sel, b)
+    # property 2: swapping inputs and weights == same multiset but different
+    # order: equal to the oracle on a strided sample of elements
+    idx = torch.arange(0, p, 997, device=dev())
+    rows = [from_dev(a[idx]), from_dev(b[idx])]
+    assert orc.same_bits(from_dev(out[idx]), orc.wreduce(rows, w, "bf16"))
+
+
+def test_one_hot_weights_select_input_at_full_size():
+    """Linearity/selection property at the north-star size: weights e_k return
+    model k exactly (x0*0 + ... + 1*xk + ... sums exact zeros)."""
+    n, p = 8, 11_181_642
+    xs = [torch.randn(p, device=dev()) for _ in range(n)]
+    out = torch.empty(p, device=dev())
+    for k in (0, 5, 7):
+        w = np.zeros(n, dtype=np.float32)
+        w[k] = 1.0
+        _native.wreduce(xs, w, out)
+        assert torch.equal(out, xs[k])
