@@ -33,33 +33,61 @@ int hip_fail(hipError_t e, const char* what) {
   return fail(DLSIM_E_HIP - static_cast<int>(e), "%s: %s", what, hipGetErrorString(e));
 }
 
-// Tuned launch shape (profiles/ and DESIGN.md §kernels): G inputs in flight
-// per group, VPT 16-byte vectors per lane.
-constexpr int kG = 8;
-constexpr int kVptF32 = 2;
-constexpr int kVptBF16 = 2;
+// Launch shape (tuned on MI355X with csrc/tune_wreduce.hip):
+// 4 vectors of 16 B per lane (a 16 KiB tile per stream per block), one tile
+// per block, non-temporal loads and stores. Small fan-in runs a kernel
+// specialised on n (all n*4 loads issued back to back, fewer VGPRs than the
+// grouped loop); larger n folds groups of G inputs. The specialised kernels
+// are used only while they fit in 256 VGPRs (two waves per SIMD): past that
+// the measured rate drops by up to 20% (profiles/r01_sweep_fanin_*.jsonl).
+constexpr int kVpt = 4;
 constexpr bool kNT = true;
+template <class Op> constexpr int max_fixed_fan_in() { return Op::kBytes == 4 ? 14 : 9; }
+template <class Op> constexpr int group_size() { return Op::kBytes == 4 ? 8 : 4; }
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+template <class Op, int NB, int NF>
+hipError_t launch_tiles(const dlsim::Slots<NB>& s, int n, const void* acc_in, void* out, size_t nelem,
+                        hipStream_t st) {
+  const size_t nvec = nelem / Op::E;
+  const size_t tile = static_cast<size_t>(dlsim::kBlock) * kVpt;
+  const size_t blocks = nvec / tile + 1;  // full tiles + one block for the ragged end
+  if (blocks > 0x7fffffffu) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((dlsim::k_wreduce_tiles<Op, NB, NF, group_size<Op>(), kVpt, kNT>),
+                     dim3(static_cast<unsigned>(blocks)), dim3(dlsim::kBlock), 0, st, s, n, acc_in, out,
+                     nvec, nelem);
+  return hipGetLastError();
+}
+
+template <class Op, int K>
+hipError_t launch_fixed_k(const dlsim::Slots<16>& s, int n, void* out, size_t nelem, hipStream_t st) {
+  if constexpr (K > max_fixed_fan_in<Op>()) {
+    return hipErrorInvalidValue;
+  } else {
+    if (n == K) return launch_tiles<Op, 16, K>(s, n, nullptr, out, nelem, st);
+    return launch_fixed_k<Op, K + 1>(s, n, out, nelem, st);
+  }
+}
+
+template <class Op>
+hipError_t launch_fixed(const dlsim::Slots<16>& s, int n, void* out, size_t nelem, hipStream_t st) {
+  return launch_fixed_k<Op, 1>(s, n, out, nelem, st);
+}
 
 template <class Op, int NB>
 hipError_t launch_pass(const dlsim::Slots<NB>& s, int n, const void* acc_in, void* out,
                        size_t nelem, bool vec, hipStream_t st) {
   if (vec) {
-    constexpr int VPT = (Op::kBytes == 4) ? kVptF32 : kVptBF16;
-    const size_t nvec = nelem / Op::E;
-    const size_t per_block = static_cast<size_t>(dlsim::kBlock) * VPT;
-    size_t blocks = (nvec + per_block - 1) / per_block;
-    if (blocks == 0) blocks = 1;  // tail-only
-    if (blocks > 0x7fffffffu) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((dlsim::k_wreduce_vec<Op, NB, kG, VPT, kNT>), dim3(static_cast<unsigned>(blocks)),
-                       dim3(dlsim::kBlock), 0, st, s, n, acc_in, out, nvec, nelem);
-  } else {
-    const size_t blocks = (nelem + dlsim::kBlock - 1) / dlsim::kBlock;
-    if (blocks > 0x7fffffffu) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((dlsim::k_wreduce_scalar<Op, NB>), dim3(static_cast<unsigned>(blocks)),
-                       dim3(dlsim::kBlock), 0, st, s, n, acc_in, out, nelem);
+    if constexpr (NB == 16) {
+      if (!acc_in && n <= max_fixed_fan_in<Op>()) return launch_fixed<Op>(s, n, out, nelem, st);
+    }
+    return launch_tiles<Op, NB, 0>(s, n, acc_in, out, nelem, st);
   }
+  const size_t blocks = (nelem + dlsim::kBlock - 1) / dlsim::kBlock;
+  if (blocks > 0x7fffffffu) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((dlsim::k_wreduce_scalar<Op, NB>), dim3(static_cast<unsigned>(blocks)),
+                     dim3(dlsim::kBlock), 0, st, s, n, acc_in, out, nelem);
   return hipGetLastError();
 }
 

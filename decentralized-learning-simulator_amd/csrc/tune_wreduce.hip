@@ -1,5 +1,5 @@
 // tune_wreduce.hip — standalone tuning harness for the reduce kernels.
-// Times launch-shape variants of k_wreduce_vec on rotating input sets (so
+// Times launch-shape variants of k_wreduce_tiles on rotating input sets (so
 // the 256 MiB Infinity Cache cannot serve re-reads) with hipEvents around
 // each launch, checks every variant bit-for-bit against the shipped shape,
 // and prints one line per variant. Not part of the product library.
@@ -15,6 +15,86 @@
 #include <vector>
 
 #include "wreduce_kernels.hpp"
+
+namespace dlsim {
+// Experimental bf16-exact element policies (compared against the shipped
+// BF16Exact, which rounds with v_cvt_pk_bf16_f32).
+struct BF16ExactOld {  // integer RNE with an explicit NaN branch (round-1 shape)
+  static constexpr int E = 8;
+  static constexpr int kBytes = 2;
+  __device__ static float init(float x) { return bf16_round(x * 0.0f); }
+  __device__ static float step(float acc, float w, float x) {
+    return bf16_round(acc + bf16_round(w * x));
+  }
+  __device__ static void step2(float& a0, float& a1, float w, float x0, float x1) {
+    a0 = step(a0, w, x0);
+    a1 = step(a1, w, x1);
+  }
+  __device__ static float finish(float a) { return a; }
+};
+__device__ __forceinline__ float bf16_round_nonan(float f) {  // valid when NaNs have zero low halves
+  uint32_t u = __float_as_uint(f);
+  return __uint_as_float((u + 0x7fffu + ((u >> 16) & 1u)) & 0xffff0000u);
+}
+struct BF16ExactInt {
+  static constexpr int E = 8;
+  static constexpr int kBytes = 2;
+  __device__ static float init(float x) { return x * 0.0f; }
+  __device__ static float step(float acc, float w, float x) {
+    return bf16_round_nonan(acc + bf16_round_nonan(w * x));
+  }
+  __device__ static void step2(float& a0, float& a1, float w, float x0, float x1) {
+    a0 = step(a0, w, x0);
+    a1 = step(a1, w, x1);
+  }
+  __device__ static float finish(float a) { return a; }
+};
+// ---- LDS-DMA variant (experiment, not shipped: no gain over register
+// streaming on MI355X) -------------------------------------------
+// Each wave streams its inputs global -> LDS with global_load_lds_dwordx4
+// (no VGPR destination; aux = 2 is the non-temporal policy), waits on its own
+// vmcnt, then reads its lane's 16 B back with ds_read_b128. Waves never share
+// LDS, so no barrier is needed. NF inputs, VPT vectors per lane, full tiles
+// only (the caller handles ragged ends with k_wreduce_tiles).
+template <class Op, int NF, int VPT, int AUX>
+__global__ __launch_bounds__(kBlock) void k_wreduce_lds(const Slots<128> s, void* __restrict__ out,
+                                                        size_t full_tiles) {
+  constexpr int kWaves = kBlock / 64;
+  __shared__ u32x4 lds[kWaves][NF * VPT][64];
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  constexpr size_t kTile = static_cast<size_t>(kBlock) * VPT;
+  for (size_t t = blockIdx.x; t < full_tiles; t += gridDim.x) {
+    // wave w covers vectors [t*kTile + w*64*VPT, +64*VPT): VPT contiguous KiB
+    const size_t v0 = t * kTile + static_cast<size_t>(wave) * 64 * VPT + lane;
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+#pragma unroll
+      for (int v = 0; v < VPT; ++v) {
+        const u32x4* g = static_cast<const u32x4*>(s.p[i]) + v0 + v * 64;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                         (__attribute__((address_space(3))) void*)&lds[wave][i * VPT + v][0],
+                                         16, 0, AUX);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    float a[VPT][Op::E];
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+      u32x4 r[VPT];
+#pragma unroll
+      for (int v = 0; v < VPT; ++v) r[v] = lds[wave][i * VPT + v][lane];
+      if (i == 0) init_tile<Op, VPT>(a, r, false);
+      fold_tile<Op, VPT>(a, s.w[i], r);
+    }
+#pragma unroll
+    for (int v = 0; v < VPT; ++v) st16<true>(out, v0 + v * 64, pack<Op>(a[v]));
+    // the next tile's DMA must not overwrite LDS this wave is still reading
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+}
+
+}  // namespace dlsim
 
 #define CK(x)                                                                          \
   do {                                                                                 \
@@ -44,27 +124,83 @@ __global__ void k_fill(uint32_t* p, size_t nwords, uint32_t seed, int bf16) {
 }
 
 struct Variant {
-  const char* name;
-  void (*launch)(const Slots<128>&, int, void*, size_t, size_t, hipStream_t);
+  std::string name;
+  void (*launch)(const Slots<128>&, int, void*, size_t, size_t, hipStream_t, int);
+  int gm;  // grid: 0 = one tile per block, k = k*256 blocks (grid-stride)
 };
 
-template <class Op, int G, int VPT, bool NT>
-void launch_v(const Slots<128>& s, int n, void* out, size_t nvec, size_t nelem, hipStream_t st) {
-  const size_t per = (size_t)kBlock * VPT;
-  size_t blocks = std::max<size_t>(1, (nvec + per - 1) / per);
-  hipLaunchKernelGGL((k_wreduce_vec<Op, 128, G, VPT, NT>), dim3((unsigned)blocks), dim3(kBlock), 0,
+template <class Op, int NF, int G, int VPT, bool NT>
+void launch_t(const Slots<128>& s, int n, void* out, size_t nvec, size_t nelem, hipStream_t st, int gm) {
+  const size_t tile = (size_t)kBlock * VPT;
+  const size_t full = nvec / tile;
+  size_t grid = full + 1;
+  if (gm > 0) grid = std::min<size_t>(grid, (size_t)gm * 256);
+  hipLaunchKernelGGL((k_wreduce_tiles<Op, 128, NF, G, VPT, NT>), dim3((unsigned)grid), dim3(kBlock), 0,
                      st, s, n, nullptr, out, nvec, nelem);
 }
 
+template <class Op, int NF, int G, int VPT, bool NT, bool NTS>
+void launch_ts(const Slots<128>& s, int n, void* out, size_t nvec, size_t nelem, hipStream_t st, int gm) {
+  const size_t tile = (size_t)kBlock * VPT;
+  const size_t full = nvec / tile;
+  size_t grid = full + 1;
+  if (gm > 0) grid = std::min<size_t>(grid, (size_t)gm * 256);
+  hipLaunchKernelGGL((k_wreduce_tiles<Op, 128, NF, G, VPT, NT, NTS>), dim3((unsigned)grid), dim3(kBlock), 0,
+                     st, s, n, nullptr, out, nvec, nelem);
+}
+
+// LDS-DMA body over full tiles; ragged end by the tiled kernel's last block
+// (only exact for inputs whose nvec is a multiple of the tile: the harness
+// flags any mismatch through `same`).
+template <class Op, int NF, int VPT, int AUX>
+void launch_l(const Slots<128>& s, int n, void* out, size_t nvec, size_t nelem, hipStream_t st, int gm) {
+  const size_t tile = (size_t)kBlock * VPT;
+  const size_t full = nvec / tile;
+  size_t grid = std::max<size_t>(1, full);
+  if (gm > 0) grid = std::min<size_t>(grid, (size_t)gm * 256);
+  hipLaunchKernelGGL((k_wreduce_lds<Op, NF, VPT, AUX>), dim3((unsigned)grid), dim3(kBlock), 0, st, s, out, full);
+}
+
+template <class Op, int NF>
+void add_nf(std::vector<Variant>& vs, int n) {
+  if (n != NF) return;
+  const std::string p = "NF" + std::to_string(NF);
+  vs.push_back({p + "_V1", launch_t<Op, NF, 8, 1, true>, 0});
+  vs.push_back({p + "_V2", launch_t<Op, NF, 8, 2, true>, 0});
+  vs.push_back({p + "_V4", launch_t<Op, NF, 8, 4, true>, 0});
+  vs.push_back({p + "_V2_g4", launch_t<Op, NF, 8, 2, true>, 4});
+  vs.push_back({p + "_V4_g2", launch_t<Op, NF, 8, 4, true>, 2});
+  vs.push_back({p + "_V4_g4", launch_t<Op, NF, 8, 4, true>, 4});
+  vs.push_back({p + "_V4_g8", launch_t<Op, NF, 8, 4, true>, 8});
+  vs.push_back({p + "_V2_plain", launch_t<Op, NF, 8, 2, false>, 0});
+  vs.push_back({p + "_V4_ps", launch_ts<Op, NF, 8, 4, true, false>, 0});
+  vs.push_back({p + "_V2_ps", launch_ts<Op, NF, 8, 2, true, false>, 0});
+  vs.push_back({p + "_G4V2", launch_t<Op, NF, 4, 2, true>, 0});
+  vs.push_back({p + "_lds_V1_nt", launch_l<Op, NF, 1, 2>, 0});
+  vs.push_back({p + "_lds_V2_nt", launch_l<Op, NF, 2, 2>, 0});
+  vs.push_back({p + "_lds_V2_def", launch_l<Op, NF, 2, 0>, 0});
+  vs.push_back({p + "_lds_V1_nt_g4", launch_l<Op, NF, 1, 2>, 4});
+  vs.push_back({p + "_lds_V2_nt_g2", launch_l<Op, NF, 2, 2>, 2});
+}
+
 template <class Op>
-std::vector<Variant> variants() {
-  return {
-      {"G8_V1_nt", launch_v<Op, 8, 1, true>},   {"G8_V2_nt", launch_v<Op, 8, 2, true>},
-      {"G8_V4_nt", launch_v<Op, 8, 4, true>},   {"G8_V1", launch_v<Op, 8, 1, false>},
-      {"G8_V2", launch_v<Op, 8, 2, false>},     {"G8_V4", launch_v<Op, 8, 4, false>},
-      {"G4_V2_nt", launch_v<Op, 4, 2, true>},   {"G16_V1_nt", launch_v<Op, 16, 1, true>},
-      {"G16_V2_nt", launch_v<Op, 16, 2, true>},
+std::vector<Variant> variants(int n) {
+  std::vector<Variant> vs = {
+      {"T_G8_V2", launch_t<Op, 0, 8, 2, true>, 0},
+      {"T_G8_V4", launch_t<Op, 0, 8, 4, true>, 0},
+      {"T_G8_V8", launch_t<Op, 0, 8, 8, true>, 0},
+      {"T_G8_V4_g2", launch_t<Op, 0, 8, 4, true>, 2},
+      {"T_G8_V4_g4", launch_t<Op, 0, 8, 4, true>, 4},
+      {"T_G8_V4_g8", launch_t<Op, 0, 8, 4, true>, 8},
+      {"T_G8_V2_g4", launch_t<Op, 0, 8, 2, true>, 4},
+      {"T_G4_V4", launch_t<Op, 0, 4, 4, true>, 0},
+      {"T_G16_V2", launch_t<Op, 0, 16, 2, true>, 0},
+      {"T_G8_V4_ps", launch_ts<Op, 0, 8, 4, true, false>, 0},
   };
+  add_nf<Op, 2>(vs, n);
+  add_nf<Op, 8>(vs, n);
+  add_nf<Op, 17>(vs, n);
+  return vs;
 }
 
 template <class Op>
@@ -94,22 +230,27 @@ int run(int n, size_t P, int reps, double peak_gbs) {
   for (auto& e : ev) CK(hipEventCreate(&e));
   const double alg_bytes = (double)(n + 1) * bytes;
 
-  auto vs = variants<Op>();
+  auto vs = variants<Op>(n);
   // reference output of the first (shipped-like) variant on set 0
   std::vector<char> ref(bytes), got(bytes);
-  vs[1].launch(slots[0], n, out[0], nvec, P, st);
+  vs[1].launch(slots[0], n, out[0], nvec, P, st, vs[1].gm);
   CK(hipStreamSynchronize(st));
   CK(hipMemcpy(ref.data(), out[0], bytes, hipMemcpyDeviceToHost));
+  {  // FNV-1a of the reference output: compare across element policies
+    uint64_t h = 1469598103934665603ull;
+    for (size_t i = 0; i < bytes; ++i) h = (h ^ (unsigned char)ref[i]) * 1099511628211ull;
+    printf("output_fnv1a=%016llx\n", (unsigned long long)h);
+  }
 
   // interleaved rounds (one process, same device) — rule 24 of the guide
   const int rounds = 3;
-  std::vector<std::vector<double>> med(vs.size());
+  std::vector<std::vector<double>> med(vs.size()), bat(vs.size());
   for (int r = 0; r < rounds; ++r) {
     for (size_t v = 0; v < vs.size(); ++v) {
-      for (int w = 0; w < 10; ++w) vs[v].launch(slots[w % sets], n, out[w % sets], nvec, P, st);
+      for (int w = 0; w < 10; ++w) vs[v].launch(slots[w % sets], n, out[w % sets], nvec, P, st, vs[v].gm);
       for (int k = 0; k < reps; ++k) {
         CK(hipEventRecord(ev[2 * k], st));
-        vs[v].launch(slots[k % sets], n, out[k % sets], nvec, P, st);
+        vs[v].launch(slots[k % sets], n, out[k % sets], nvec, P, st, vs[v].gm);
         CK(hipEventRecord(ev[2 * k + 1], st));
       }
       CK(hipStreamSynchronize(st));
@@ -121,19 +262,30 @@ int run(int n, size_t P, int reps, double peak_gbs) {
       }
       std::sort(t.begin(), t.end());
       med[v].push_back(t[reps / 2]);
+      // batch: one event pair around `reps` back-to-back launches
+      CK(hipEventRecord(ev[0], st));
+      for (int k = 0; k < reps; ++k) vs[v].launch(slots[k % sets], n, out[k % sets], nvec, P, st, vs[v].gm);
+      CK(hipEventRecord(ev[1], st));
+      CK(hipEventSynchronize(ev[1]));
+      float bms;
+      CK(hipEventElapsedTime(&bms, ev[0], ev[1]));
+      bat[v].push_back(bms * 1e3 / reps);
     }
   }
   for (size_t v = 0; v < vs.size(); ++v) {
-    vs[v].launch(slots[0], n, out[0], nvec, P, st);
+    vs[v].launch(slots[0], n, out[0], nvec, P, st, vs[v].gm);
     CK(hipStreamSynchronize(st));
     CK(hipMemcpy(got.data(), out[0], bytes, hipMemcpyDeviceToHost));
     // compare only the vector part (tail elements are folded by every variant identically)
-    const bool same = memcmp(ref.data(), got.data(), nvec * 16) == 0;
+    const bool same = memcmp(ref.data(), got.data(), bytes) == 0;
     std::sort(med[v].begin(), med[v].end());
+    std::sort(bat[v].begin(), bat[v].end());
     const double us = med[v][rounds / 2];
+    const double bus = bat[v][rounds / 2];
     const double gbs = alg_bytes / (us * 1e-6) / 1e9;
-    printf("variant=%-10s n=%d P=%zu bytes=%.1fMB median_us=%.2f GBps=%.0f frac=%.3f same=%d\n", vs[v].name, n,
-           P, alg_bytes / 1e6, us, gbs, gbs / peak_gbs, (int)same);
+    const double bgbs = alg_bytes / (bus * 1e-6) / 1e9;
+    printf("variant=%-16s n=%d P=%zu bytes=%.1fMB median_us=%.2f GBps=%.0f frac=%.3f batch_us=%.2f batch_GBps=%.0f bfrac=%.3f same=%d\n",
+           vs[v].name.c_str(), n, P, alg_bytes / 1e6, us, gbs, gbs / peak_gbs, bus, bgbs, bgbs / peak_gbs, (int)same);
   }
   // copy ceiling on the same footprint
   {
@@ -179,5 +331,7 @@ int main(int argc, char** argv) {
   const double peak = 8000.0;  // GB/s, MI355X HBM3E spec
   if (dt == "f32")
     return mode == "exact" ? run<F32Exact>(n, P, reps, peak) : run<F32Fast>(n, P, reps, peak);
+  if (mode == "exactold") return run<BF16ExactOld>(n, P, reps, peak);
+  if (mode == "exactint") return run<BF16ExactInt>(n, P, reps, peak);
   return mode == "exact" ? run<BF16Exact>(n, P, reps, peak) : run<BF16Fast>(n, P, reps, peak);
 }

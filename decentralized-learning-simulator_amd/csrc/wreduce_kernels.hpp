@@ -35,6 +35,8 @@ namespace dlsim {
 constexpr int kBlock = 256;  // 4 waves of 64 lanes
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
 // ---- bf16 helpers -----------------------------------------------------------
 // Round fp32 -> bf16 (returned widened back to fp32), nearest-even. A NaN
@@ -48,10 +50,21 @@ __device__ __forceinline__ float bf16_round(float f) {
   return __uint_as_float(u & 0xffff0000u);
 }
 
+// Round-to-nearest-even fp32 -> bf16 of a pair, returned widened to fp32,
+// with one v_cvt_pk_bf16_f32 (hardware RNE; NaN stays NaN).
+__device__ __forceinline__ void bf16_round2(float& a0, float& a1) {
+  const f32x2 v = {a0, a1};
+  const uint32_t u = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
+  a0 = __uint_as_float(u << 16);
+  a1 = __uint_as_float(u & 0xffff0000u);
+}
+
 // ---- element policies -------------------------------------------------------
 // E  = elements per 16-byte vector
 // init(x0): value of acc after p.mul_(0)
-// step(acc, w, x): one `c1.add_(w * p1)`
+// step(acc, w, x): one `c1.add_(w * p1)` on one element (scalar/tail path)
+// step2: the same on two adjacent elements (vector path; lets the compiler
+//        use v_pk_mul_f32 / v_pk_add_f32 and the packed bf16 convert)
 struct F32Exact {
   static constexpr int E = 4;
   static constexpr int kBytes = 4;
@@ -59,6 +72,10 @@ struct F32Exact {
   __device__ static float step(float acc, float w, float x) {
     const float p = w * x;  // rounded: contraction is off
     return acc + p;
+  }
+  __device__ static void step2(float& a0, float& a1, float w, float x0, float x1) {
+    a0 = step(a0, w, x0);
+    a1 = step(a1, w, x1);
   }
   __device__ static float finish(float a) { return a; }
 };
@@ -68,16 +85,29 @@ struct F32Fast {
   static constexpr int kBytes = 4;
   __device__ static float init(float x) { return x * 0.0f; }
   __device__ static float step(float acc, float w, float x) { return __builtin_fmaf(w, x, acc); }
+  __device__ static void step2(float& a0, float& a1, float w, float x0, float x1) {
+    a0 = step(a0, w, x0);
+    a1 = step(a1, w, x1);
+  }
   __device__ static float finish(float a) { return a; }
 };
 
+// bf16 exact: product and sum each rounded to bf16. x * 0 is +-0 or NaN,
+// already bf16-exact, so init needs no rounding.
 struct BF16Exact {
   static constexpr int E = 8;
   static constexpr int kBytes = 2;
-  __device__ static float init(float x) { return bf16_round(x * 0.0f); }
+  __device__ static float init(float x) { return x * 0.0f; }
   __device__ static float step(float acc, float w, float x) {
     const float p = bf16_round(w * x);
     return bf16_round(acc + p);
+  }
+  __device__ static void step2(float& a0, float& a1, float w, float x0, float x1) {
+    float p0 = w * x0, p1 = w * x1;
+    bf16_round2(p0, p1);
+    a0 = a0 + p0;
+    a1 = a1 + p1;
+    bf16_round2(a0, a1);
   }
   __device__ static float finish(float a) { return a; }
 };
@@ -87,6 +117,10 @@ struct BF16Fast {
   static constexpr int kBytes = 2;
   __device__ static float init(float x) { return x * 0.0f; }
   __device__ static float step(float acc, float w, float x) { return __builtin_fmaf(w, x, acc); }
+  __device__ static void step2(float& a0, float& a1, float w, float x0, float x1) {
+    a0 = step(a0, w, x0);
+    a1 = step(a1, w, x1);
+  }
   __device__ static float finish(float a) { return bf16_round(a); }
 };
 
@@ -164,66 +198,6 @@ struct Slots {
   float w[NB];
 };
 
-// One group of up to G inputs: issue every load first, then fold in order.
-// FIRST: the group starts the sum (acc from x0*0, or from acc_in).
-template <class Op, int NB, int G, int VPT, bool NT, bool FIRST>
-__device__ __forceinline__ void fold_group(const Slots<NB>& s, int i0, int cnt,
-                                           const void* acc_in, const size_t (&vi)[VPT],
-                                           const bool (&live)[VPT],
-                                           float (&a)[VPT][Op::E]) {
-  // Lanes past the end keep zeros (never stored); no value is left undefined.
-  u32x4 r[G][VPT];
-  u32x4 racc[VPT];
-#pragma unroll
-  for (int v = 0; v < VPT; ++v) racc[v] = u32x4{0u, 0u, 0u, 0u};
-  if constexpr (FIRST) {
-    if (acc_in) {
-#pragma unroll
-      for (int v = 0; v < VPT; ++v)
-        if (live[v]) racc[v] = ld16<NT>(acc_in, vi[v]);
-    }
-  }
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-#pragma unroll
-    for (int v = 0; v < VPT; ++v) r[g][v] = u32x4{0u, 0u, 0u, 0u};
-    if (g < cnt) {
-      const void* src = s.p[i0 + g];
-#pragma unroll
-      for (int v = 0; v < VPT; ++v)
-        if (live[v]) r[g][v] = ld16<NT>(src, vi[v]);
-    }
-  }
-  if constexpr (FIRST) {
-#pragma unroll
-    for (int v = 0; v < VPT; ++v) {
-      float x[Op::E];
-      if (acc_in) {
-        unpack<Op>(racc[v], x);
-#pragma unroll
-        for (int e = 0; e < Op::E; ++e) a[v][e] = x[e];
-      } else {
-        unpack<Op>(r[0][v], x);
-#pragma unroll
-        for (int e = 0; e < Op::E; ++e) a[v][e] = Op::init(x[e]);
-      }
-    }
-  }
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    if (g < cnt) {
-      const float w = s.w[i0 + g];
-#pragma unroll
-      for (int v = 0; v < VPT; ++v) {
-        float x[Op::E];
-        unpack<Op>(r[g][v], x);
-#pragma unroll
-        for (int e = 0; e < Op::E; ++e) a[v][e] = Op::step(a[v][e], w, x[e]);
-      }
-    }
-  }
-}
-
 // Scalar fold of one element over all n inputs (tail / misaligned path).
 template <class Op, int NB>
 __device__ __forceinline__ void fold_scalar(const Slots<NB>& s, int n, const void* acc_in,
@@ -243,41 +217,6 @@ __device__ __forceinline__ void fold_scalar(const Slots<NB>& s, int n, const voi
   store_elem<Op>(out, j, a);
 }
 
-// Vector kernel: thread t of block b owns 16-byte vectors
-//   b*kBlock*VPT + t + k*kBlock,  k < VPT   (coalesced per k)
-// over [0, nvec). Elements [nvec*E, nelem) — fewer than E — are folded by
-// block 0 afterwards (block 0 is dispatched first, so that latency hides
-// under the rest of the grid).
-template <class Op, int NB, int G, int VPT, bool NT>
-__global__ __launch_bounds__(kBlock) void k_wreduce_vec(const Slots<NB> s, int n,
-                                                        const void* __restrict__ acc_in,
-                                                        void* __restrict__ out, size_t nvec,
-                                                        size_t nelem) {
-  const size_t base = static_cast<size_t>(blockIdx.x) * (kBlock * VPT) + threadIdx.x;
-  size_t vi[VPT];
-  bool live[VPT];
-#pragma unroll
-  for (int v = 0; v < VPT; ++v) {
-    vi[v] = base + static_cast<size_t>(v) * kBlock;
-    live[v] = vi[v] < nvec;
-  }
-  float a[VPT][Op::E];
-  int cnt0 = n < G ? n : G;
-  fold_group<Op, NB, G, VPT, NT, true>(s, 0, cnt0, acc_in, vi, live, a);
-  for (int i0 = G; i0 < n; i0 += G) {
-    const int cnt = (n - i0) < G ? (n - i0) : G;
-    fold_group<Op, NB, G, VPT, NT, false>(s, i0, cnt, acc_in, vi, live, a);
-  }
-#pragma unroll
-  for (int v = 0; v < VPT; ++v)
-    if (live[v]) st16<NT>(out, vi[v], pack<Op>(a[v]));
-
-  if (blockIdx.x == 0) {
-    const size_t j = nvec * Op::E + threadIdx.x;
-    if (j < nelem) fold_scalar<Op, NB>(s, n, acc_in, out, j);
-  }
-}
-
 // Scalar kernel: any alignment, one element per thread.
 template <class Op, int NB>
 __global__ __launch_bounds__(kBlock) void k_wreduce_scalar(const Slots<NB> s, int n,
@@ -286,6 +225,115 @@ __global__ __launch_bounds__(kBlock) void k_wreduce_scalar(const Slots<NB> s, in
                                                            size_t nelem) {
   const size_t j = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x;
   if (j < nelem) fold_scalar<Op, NB>(s, n, acc_in, out, j);
+}
+
+// ---- tiled kernel ------------------------------------------------------------
+// A tile is kBlock*VPT 16-byte vectors; lane t of a block owns vectors
+// t + k*kBlock of the tile (coalesced 1 KiB per wave per k). Full tiles run
+// without bounds checks (no exec-mask branches around the loads); the last
+// partial tile and the < E scalar tail go to the grid's last block, which
+// holds the fewest full tiles under the grid-stride deal below.
+//
+// NF > 0: the fan-in n == NF is a compile-time constant (single pass, no
+// acc_in): every input's loads are issued back to back with no group
+// branches. NF == 0: runtime n in groups of G (first group peeled).
+template <class Op, int VPT, bool NT, bool CHECK>
+__device__ __forceinline__ void load_tile(const void* src, size_t v0, size_t nvec,
+                                          u32x4 (&r)[VPT]) {
+#pragma unroll
+  for (int v = 0; v < VPT; ++v) {
+    const size_t idx = v0 + static_cast<size_t>(v) * kBlock;
+    if constexpr (CHECK) {
+      r[v] = u32x4{0u, 0u, 0u, 0u};
+      if (idx < nvec) r[v] = ld16<NT>(src, idx);
+    } else {
+      r[v] = ld16<NT>(src, idx);
+    }
+  }
+}
+
+template <class Op, int VPT>
+__device__ __forceinline__ void fold_tile(float (&a)[VPT][Op::E], float w, const u32x4 (&r)[VPT]) {
+#pragma unroll
+  for (int v = 0; v < VPT; ++v) {
+    float x[Op::E];
+    unpack<Op>(r[v], x);
+#pragma unroll
+    for (int e = 0; e < Op::E; e += 2) Op::step2(a[v][e], a[v][e + 1], w, x[e], x[e + 1]);
+  }
+}
+
+template <class Op, int VPT>
+__device__ __forceinline__ void init_tile(float (&a)[VPT][Op::E], const u32x4 (&r)[VPT], bool from_acc) {
+#pragma unroll
+  for (int v = 0; v < VPT; ++v) {
+    float x[Op::E];
+    unpack<Op>(r[v], x);
+#pragma unroll
+    for (int e = 0; e < Op::E; ++e) a[v][e] = from_acc ? x[e] : Op::init(x[e]);
+  }
+}
+
+template <class Op, int NB, int NF, int G, int VPT, bool NT, bool CHECK, bool NTS = NT>
+__device__ __forceinline__ void reduce_tile(const Slots<NB>& s, int n, const void* acc_in,
+                                            void* out, size_t v0, size_t nvec) {
+  float a[VPT][Op::E];
+  if constexpr (NF > 0) {
+    u32x4 r[NF][VPT];
+#pragma unroll
+    for (int i = 0; i < NF; ++i) load_tile<Op, VPT, NT, CHECK>(s.p[i], v0, nvec, r[i]);
+    init_tile<Op, VPT>(a, r[0], false);
+#pragma unroll
+    for (int i = 0; i < NF; ++i) fold_tile<Op, VPT>(a, s.w[i], r[i]);
+  } else {
+    // first group: acc (if continuing a previous pass) + up to G inputs
+    {
+      u32x4 racc[VPT];
+      u32x4 r[G][VPT];
+      const int cnt = n < G ? n : G;
+      if (acc_in) load_tile<Op, VPT, NT, CHECK>(acc_in, v0, nvec, racc);
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+        if (g < cnt) load_tile<Op, VPT, NT, CHECK>(s.p[g], v0, nvec, r[g]);
+      if (acc_in) init_tile<Op, VPT>(a, racc, true);
+      else init_tile<Op, VPT>(a, r[0], false);
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+        if (g < cnt) fold_tile<Op, VPT>(a, s.w[g], r[g]);
+    }
+    for (int i0 = G; i0 < n; i0 += G) {
+      u32x4 r[G][VPT];
+      const int cnt = (n - i0) < G ? (n - i0) : G;
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+        if (g < cnt) load_tile<Op, VPT, NT, CHECK>(s.p[i0 + g], v0, nvec, r[g]);
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+        if (g < cnt) fold_tile<Op, VPT>(a, s.w[i0 + g], r[g]);
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < VPT; ++v) {
+    const size_t idx = v0 + static_cast<size_t>(v) * kBlock;
+    if (!CHECK || idx < nvec) st16<NTS>(out, idx, pack<Op>(a[v]));
+  }
+}
+
+template <class Op, int NB, int NF, int G, int VPT, bool NT, bool NTS = NT>
+__global__ __launch_bounds__(kBlock) void k_wreduce_tiles(const Slots<NB> s, int n,
+                                                          const void* __restrict__ acc_in,
+                                                          void* __restrict__ out, size_t nvec,
+                                                          size_t nelem) {
+  constexpr size_t kTile = static_cast<size_t>(kBlock) * VPT;
+  const size_t full = nvec / kTile;
+  for (size_t t = blockIdx.x; t < full; t += gridDim.x)
+    reduce_tile<Op, NB, NF, G, VPT, NT, false, NTS>(s, n, acc_in, out, t * kTile + threadIdx.x, nvec);
+  if (blockIdx.x == gridDim.x - 1) {
+    if (full * kTile < nvec)
+      reduce_tile<Op, NB, NF, G, VPT, NT, true, NTS>(s, n, acc_in, out, full * kTile + threadIdx.x, nvec);
+    const size_t j = nvec * Op::E + threadIdx.x;
+    if (j < nelem) fold_scalar<Op, NB>(s, n, acc_in, out, j);
+  }
 }
 
 // Copy probe: the achievable streaming ceiling on this device.

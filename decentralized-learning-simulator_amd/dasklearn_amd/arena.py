@@ -107,11 +107,17 @@ class _Staging:
         ev.record(stream)
         self.last_use[(str(device), dt, n, numel)] = ev
 
+    # Rows are padded to 256 B so each model's arena starts 16-byte aligned
+    # (the vector kernel's requirement); callers use rows[i, :numel].
+    @staticmethod
+    def _padded(numel):
+        return (numel + 127) // 128 * 128
+
     def device_rows(self, device, dt, n, numel) -> torch.Tensor:
         key = (str(device), dt, n, numel)
         buf = self.dev.get(key)
         if buf is None:
-            buf = torch.empty((n, numel), dtype=dt, device=device)
+            buf = torch.empty((n, self._padded(numel)), dtype=dt, device=device)[:, :numel]
             self.dev[key] = buf
         return buf
 
@@ -119,7 +125,7 @@ class _Staging:
         key = (dt, n, numel)
         buf = self.host.get(key)
         if buf is None:
-            buf = torch.empty((n, numel), dtype=dt, pin_memory=True)
+            buf = torch.empty((n, self._padded(numel)), dtype=dt, pin_memory=True)[:, :numel]
             self.host[key] = buf
         return buf
 

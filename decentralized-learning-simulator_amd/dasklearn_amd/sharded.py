@@ -1,0 +1,183 @@
+"""Parameter-axis sharding of the aggregate across the GPUs of one node.
+
+New (the reference has no multi-device path). One process
+per GPU, `torch.distributed` with the "nccl" backend (= RCCL over xGMI on
+ROCm). Every output element is independent, so the parameter axis splits into
+contiguous slices, one per rank, with boundaries from the C ABI's
+`dlsim_shard_range` (aligned to 64 elements = 256 B of fp32, so every slice
+starts 16-byte aligned and takes the vector kernel).
+
+Three entry points:
+
+* `aggregate_param_sharded` — rank r already holds slice r of every model
+  (e.g. a device-resident arena partitioned at load time): one local exact
+  reduce, no data-path collective; optionally an all-gather materialises the
+  full output. Bit-identical to the single-GPU (and reference) result.
+* `aggregate_model_sharded(exact=True)` — whole models live on different
+  ranks: an all-to-all moves slice j of every model to rank j (in global
+  model order), then the exact local reduce, then an all-gather.
+  Bit-identical: each element's N terms are still folded in reference order
+  on one GPU.
+* `aggregate_model_sharded(exact=False)` — local weighted partial sums (FAST
+  mode) + reduce-scatter + all-gather: fewer bytes on xGMI when a rank holds
+  more than one model, but a different summation order, so tolerance parity
+  only (n * 2^-23 relative in fp32).
+
+`local_reduce` defaults to the HIP kernel; tests inject the CPU oracle to run
+the collective logic on `gloo` without a GPU (test infrastructure only).
+"""
+from __future__ import annotations
+
+from typing import Callable, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import _native
+
+LocalReduce = Callable[[List[torch.Tensor], np.ndarray, torch.Tensor, int], None]
+
+
+def _hip_reduce(inputs, w32, out, mode):
+    _native.wreduce(inputs, w32, out, mode)
+
+
+class ShardedAggregator:
+
+    def __init__(self, group=None, align_elems: int = 64, local_reduce: Optional[LocalReduce] = None):
+        if not dist.is_initialized():
+            raise RuntimeError("ShardedAggregator needs torch.distributed to be initialised")
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.align = align_elems
+        self.local_reduce = local_reduce or _hip_reduce
+
+    # ---- partition --------------------------------------------------------------
+    def bounds(self, n_elems: int, rank: Optional[int] = None) -> Tuple[int, int]:
+        r = self.rank if rank is None else rank
+        return _native.shard_range(n_elems, self.world, r, self.align)
+
+    def all_bounds(self, n_elems: int) -> List[Tuple[int, int]]:
+        return [self.bounds(n_elems, r) for r in range(self.world)]
+
+    # ---- collectives ------------------------------------------------------------
+    def all_gather(self, shard: torch.Tensor, n_elems: int) -> torch.Tensor:
+        """Concatenate every rank's slice into the full vector (ragged last
+        slice handled by padding to the largest slice)."""
+        bnds = self.all_bounds(n_elems)
+        width = max(e - b for b, e in bnds)
+        padded = shard
+        if shard.numel() != width:
+            padded = torch.zeros(width, dtype=shard.dtype, device=shard.device)
+            padded[:shard.numel()].copy_(shard)
+        gathered = torch.empty(width * self.world, dtype=shard.dtype, device=shard.device)
+        dist.all_gather_into_tensor(gathered, padded, group=self.group)
+        if all(e - b == width for b, e in bnds):
+            return gathered
+        full = torch.empty(n_elems, dtype=shard.dtype, device=shard.device)
+        for r, (b, e) in enumerate(bnds):
+            full[b:e].copy_(gathered[r * width:r * width + (e - b)])
+        return full
+
+    # ---- entry points -----------------------------------------------------------
+    def aggregate_param_sharded(self, shard_inputs: Sequence[torch.Tensor], weights,
+                                n_elems: int, gather: bool = True,
+                                mode: int = _native.DLSIM_EXACT) -> torch.Tensor:
+        """shard_inputs[i] = this rank's slice (self.bounds(n_elems)) of model i."""
+        w32 = _resolve(len(shard_inputs), weights)
+        b, e = self.bounds(n_elems)
+        for x in shard_inputs:
+            if x.numel() != e - b:
+                raise ValueError(f"rank {self.rank}: shard has {x.numel()} elements, expected {e - b}")
+        out = torch.empty(e - b, dtype=shard_inputs[0].dtype, device=shard_inputs[0].device)
+        if e > b:
+            self.local_reduce(list(shard_inputs), w32, out, mode)
+        return self.all_gather(out, n_elems) if gather else out
+
+    def aggregate_model_sharded(self, local_models: Sequence[torch.Tensor], counts: Sequence[int],
+                                weights, exact: bool = True) -> torch.Tensor:
+        """local_models: this rank's whole flat models; counts[r] = how many
+        models rank r holds (global model order = rank order, then local
+        order). weights: the global list (None/[] -> uniform)."""
+        counts = list(counts)
+        if len(counts) != self.world or counts[self.rank] != len(local_models):
+            raise ValueError("counts must list every rank's model count, this rank's included")
+        n_total = sum(counts)
+        w32 = _resolve(n_total, weights)
+        ref = local_models[0] if local_models else None
+        n_elems = _agree_numel(ref, self.group)
+        dtype = ref.dtype if ref is not None else torch.float32
+        device = ref.device if ref is not None else _default_device()
+        first = sum(counts[:self.rank])
+        if exact:
+            return self._model_sharded_exact(local_models, counts, w32, n_elems, dtype, device)
+        # FAST: partial sums of local models, then sum over ranks
+        partial = torch.zeros(n_elems, dtype=torch.float32, device=device)
+        if local_models:
+            lw = w32[first:first + len(local_models)]
+            acc = torch.empty(n_elems, dtype=dtype, device=device)
+            self.local_reduce(list(local_models), lw, acc, _native.DLSIM_FAST)
+            partial.copy_(acc)
+        bnds = self.all_bounds(n_elems)
+        width = max(e - b for b, e in bnds)
+        padded = torch.zeros(width * self.world, dtype=torch.float32, device=device)
+        for r, (b, e) in enumerate(bnds):
+            padded[r * width:r * width + (e - b)].copy_(partial[b:e])
+        mine = torch.empty(width, dtype=torch.float32, device=device)
+        dist.reduce_scatter_tensor(mine, padded, op=dist.ReduceOp.SUM, group=self.group)
+        b, e = bnds[self.rank]
+        return self.all_gather(mine[:e - b].to(dtype).contiguous(), n_elems)
+
+    def _model_sharded_exact(self, local_models, counts, w32, n_elems, dtype, device):
+        bnds = self.all_bounds(n_elems)
+        lens = [e - b for b, e in bnds]
+        k = len(local_models)
+        # send: for each destination rank j, slice j of every local model
+        send = torch.empty(k * n_elems, dtype=dtype, device=device)
+        in_splits = []
+        off = 0
+        for j, (b, e) in enumerate(bnds):
+            for m in local_models:
+                send[off:off + (e - b)].copy_(m[b:e])
+                off += e - b
+            in_splits.append(k * (e - b))
+        my_len = lens[self.rank]
+        out_splits = [counts[r] * my_len for r in range(self.world)]
+        recv = torch.empty(sum(out_splits), dtype=dtype, device=device)
+        dist.all_to_all_single(recv, send, output_split_sizes=out_splits,
+                               input_split_sizes=in_splits, group=self.group)
+        rows = [recv[i * my_len:(i + 1) * my_len] for i in range(sum(counts))]
+        out = torch.empty(my_len, dtype=dtype, device=device)
+        if my_len > 0:
+            self.local_reduce(rows, w32, out, _native.DLSIM_EXACT)
+        return self.all_gather(out, n_elems)
+
+
+def _resolve(n: int, weights) -> np.ndarray:
+    # fedavg.py:14-17 rules, then the fp32 rounding of `w * p1` (fedavg.py:25)
+    if not weights:
+        weights = [float(1. / n) for _ in range(n)]
+    else:
+        assert len(weights) == n
+    return _native.fp32_weights(weights)
+
+
+def _default_device():
+    if torch.cuda.is_available():
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def _agree_numel(ref: Optional[torch.Tensor], group) -> int:
+    """Every rank must see the same model size; ranks without models learn it."""
+    dev = ref.device if ref is not None else _default_device()
+    if dist.get_backend(group) == "gloo":
+        dev = torch.device("cpu")
+    t = torch.tensor([ref.numel() if ref is not None else -1], dtype=torch.int64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    n = int(t.item())
+    if ref is not None and ref.numel() != n:
+        raise ValueError("models differ in size across ranks")
+    return n

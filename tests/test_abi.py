@@ -1,0 +1,95 @@
+"""The C ABI (include/dlsim.h) — CPU checks: the library loads, exports every
+declared symbol, host-only entry points work, and argument errors are
+reported without touching a GPU."""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+from dasklearn_amd import _native
+
+HEADER = os.path.join(ROOT, "include", "dlsim.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(dlsim_[a-z_0-9]+)\s*\(", src)))
+
+
+def test_header_matches_binding_list():
+    assert declared_functions() == sorted(_native.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _native.load()
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", _native.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (dlsim_\w+)", out))
+    assert set(declared_functions()) <= exported
+
+
+def test_library_is_gfx950_code_object():
+    data = open(_native.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data
+
+
+def test_version():
+    assert _native.version() >> 16 == 1
+
+
+@pytest.mark.parametrize("n,world", [(0, 1), (1, 1), (100, 3), (11_181_642, 8), (1000, 7), (63, 4)])
+def test_shard_range_partitions_exactly(n, world):
+    bounds = [_native.shard_range(n, world, r, 64) for r in range(world)]
+    assert bounds[0][0] == 0 and bounds[-1][1] == n
+    for (b0, e0), (b1, e1) in zip(bounds, bounds[1:]):
+        assert e0 == b1
+    for b, e in bounds:
+        assert b <= e and b % 64 == 0
+    widths = [e - b for b, e in bounds[:-1]]
+    if widths:
+        assert max(widths) - min(widths) <= 64
+
+
+def test_shard_range_rejects_bad_rank():
+    with pytest.raises(_native.DlsimError):
+        _native.shard_range(100, 2, 2, 64)
+
+
+def _raw_call(n, dtype=0, mode=0, out=ctypes.c_void_p(16)):
+    lib = _native.load()
+    ptrs = (ctypes.c_void_p * max(n, 1))(*([16] * max(n, 1)))
+    w = np.ones(max(n, 1), dtype=np.float32)
+    return lib.dlsim_wreduce(ptrs, n, w.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), out, 100,
+                             dtype, mode, None)
+
+
+def test_argument_errors_need_no_gpu():
+    lib = _native.load()
+    assert _raw_call(0) == -1
+    assert b"n must be" in lib.dlsim_last_error()
+    assert _raw_call(2, dtype=7) == -2
+    assert _raw_call(2, mode=9) == -3
+    assert _raw_call(2, out=ctypes.c_void_p(0)) == -1
+    # partially overlapping output
+    ptrs = (ctypes.c_void_p * 2)(4096, 8192)
+    w = np.ones(2, dtype=np.float32)
+    rc = lib.dlsim_wreduce(ptrs, 2, w.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                           ctypes.c_void_p(4096 + 64), 1000, 0, 0, None)
+    assert rc == -1 and b"overlap" in lib.dlsim_last_error()
+
+
+def test_zero_elements_is_a_noop():
+    lib = _native.load()
+    ptrs = (ctypes.c_void_p * 2)(16, 32)
+    w = np.ones(2, dtype=np.float32)
+    assert lib.dlsim_wreduce(ptrs, 2, w.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                             ctypes.c_void_p(64), 0, 0, 0, None) == 0

@@ -1,0 +1,126 @@
+"""Multi-process (world 2 and 3, gloo, CPU) tests of the sharded path's
+collective logic. The local reduce is the CPU oracle, injected — test
+infrastructure standing in for the GPU kernel, which tests/test_gpu_*.py
+check separately; the product default is the HIP kernel."""
+from __future__ import annotations
+
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+PATHS = [ROOT, os.path.join(ROOT, "decentralized-learning-simulator_amd"), HERE]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def oracle_reduce(inputs, w32, out, mode):
+    from oracle import oracle as orc
+    bf16 = inputs[0].dtype == torch.bfloat16
+    if bf16:
+        rows = [t.contiguous().view(torch.int16).numpy().view(np.uint16) for t in inputs]
+        res = orc.wreduce(rows, w32, "bf16", "exact" if mode == 0 else "fast")
+        out.copy_(torch.from_numpy(res.view(np.int16).copy()).view(torch.bfloat16))
+    else:
+        rows = [t.contiguous().numpy() for t in inputs]
+        out.copy_(torch.from_numpy(orc.wreduce(rows, w32, "f32", "exact" if mode == 0 else "fast")))
+
+
+def models(n, p, dtype):
+    g = torch.Generator().manual_seed(42)
+    xs = [torch.randn(p, generator=g) * 0.05 for _ in range(n)]
+    return [x.to(dtype) for x in xs]
+
+
+def _worker(rank, world, port, p, dtype_name, q):
+    for path in PATHS:
+        sys.path.insert(0, path)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from dasklearn_amd.sharded import ShardedAggregator
+        from oracle import oracle as orc
+        dtype = torch.bfloat16 if dtype_name == "bf16" else torch.float32
+        agg = ShardedAggregator(local_reduce=oracle_reduce)
+        n = 5
+        xs = models(n, p, dtype)
+        weights = [0.1, 0.3, 0.2, 0.15, 0.25]
+        w32 = orc.reference_weights(n, weights)
+        if dtype == torch.bfloat16:
+            rows = [x.view(torch.int16).numpy().view(np.uint16) for x in xs]
+            expect = torch.from_numpy(orc.wreduce(rows, w32, "bf16").view(np.int16).copy()).view(torch.bfloat16)
+        else:
+            expect = torch.from_numpy(orc.wreduce([x.numpy() for x in xs], w32, "f32"))
+
+        def same(a, b):
+            if a.dtype == torch.bfloat16:
+                return torch.equal(a.view(torch.int16), b.view(torch.int16))
+            return torch.equal(a.view(torch.int32), b.view(torch.int32))
+
+        res = {}
+        # 1) parameter-sharded: each rank holds its slice of every model
+        b, e = agg.bounds(p)
+        full = agg.aggregate_param_sharded([x[b:e].contiguous() for x in xs], weights, p)
+        res["param_sharded_exact"] = same(full, expect)
+        res["aligned_start"] = (b % 64 == 0)
+        shard_only = agg.aggregate_param_sharded([x[b:e].contiguous() for x in xs], weights, p, gather=False)
+        res["shard_only"] = same(shard_only, expect[b:e])
+        # 2) model-sharded, exact (all-to-all into slices, then the ordered fold)
+        counts = [n // world + (1 if r < n % world else 0) for r in range(world)]
+        first = sum(counts[:rank])
+        mine = xs[first:first + counts[rank]]
+        full2 = agg.aggregate_model_sharded(mine, counts, weights, exact=True)
+        res["model_sharded_exact"] = same(full2, expect)
+        # 3) model-sharded, fast (partial sums + reduce-scatter): tolerance only
+        full3 = agg.aggregate_model_sharded(mine, counts, weights, exact=False)
+        scale = sum(abs(w) * x.float().abs() for w, x in zip(w32, xs))
+        ulp = 2.0 ** -8 if dtype == torch.bfloat16 else 2.0 ** -23
+        res["model_sharded_fast_tol"] = bool(torch.all(
+            (full3.float() - expect.float()).abs() <= (n + 2) * ulp * scale + 1e-30))
+        # 4) uniform weights (None) path
+        full4 = agg.aggregate_param_sharded([x[b:e].contiguous() for x in xs], None, p)
+        w_u = orc.reference_weights(n, None)
+        if dtype == torch.bfloat16:
+            exp4 = torch.from_numpy(orc.wreduce(rows, w_u, "bf16").view(np.int16).copy()).view(torch.bfloat16)
+        else:
+            exp4 = torch.from_numpy(orc.wreduce([x.numpy() for x in xs], w_u, "f32"))
+        res["param_sharded_uniform"] = same(full4, exp4)
+        q.put((rank, res))
+    except Exception as exc:  # surface worker failures to the parent
+        import traceback
+        q.put((rank, {"error": traceback.format_exc()}))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,p,dtype", [(2, 10_003, "f32"), (3, 4_097, "f32"), (2, 5_001, "bf16"),
+                                           (3, 130, "f32")])
+def test_sharded_paths_gloo(world, p, dtype):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, p, dtype, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    results = {}
+    for _ in range(world):
+        r, res = q.get(timeout=300)
+        results[r] = res
+    for pr in procs:
+        pr.join(timeout=60)
+    for r in range(world):
+        assert "error" not in results[r], results[r].get("error")
+        assert all(results[r].values()), (r, results[r])
