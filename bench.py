@@ -42,6 +42,29 @@ METRIC = "device-resident GB/s, N-way weighted model-tensor reduce; 1/2/4/8 MI35
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 RESNET18_P = 11_181_642
 
+GNLENET_SHAPES = [(32, 3, 5, 5), (32,), (32,), (32,), (32, 32, 5, 5), (32,), (32,), (32,),
+                  (64, 32, 5, 5), (64,), (64,), (64,), (10, 576), (10,)]
+
+
+def resnet18_shapes():
+    """parameters() shapes of torchvision resnet18(num_classes=10), the
+    reference's create_model("cifar10", "resnet18") (models/__init__.py:27-29):
+    62 tensors, 11,181,642 params."""
+    shapes = [(64, 3, 7, 7), (64,), (64,)]
+    cin = 64
+    for cout, stride in ((64, 1), (128, 2), (256, 2), (512, 2)):
+        for b in range(2):
+            shapes += [(cout, cin, 3, 3), (cout,), (cout,), (cout, cout, 3, 3), (cout,), (cout,)]
+            if b == 0 and (stride != 1 or cin != cout):
+                shapes += [(cout, cin, 1, 1), (cout,), (cout,)]
+            cin = cout
+    return shapes + [(10, 512), (10,)]
+
+
+# parameter layout the CPU baseline runs on (what the reference would iterate)
+LAYOUTS = {"north_star": resnet18_shapes, "cfg3": resnet18_shapes, "cfg5": resnet18_shapes,
+           "cfg2_gnlenet": lambda: GNLENET_SHAPES}
+
 # name: (n_models, params per rank, dtype, weights, description)
 CONFIGS = {
     "north_star": (8, RESNET18_P, "f32", "dirichlet",
@@ -100,33 +123,46 @@ def pmc_traffic(config: str, mode: str):
     return best
 
 
-def cpu_baseline(n, p, dtype, weights, budget_s):
-    """The op-for-op PyTorch-CPU restatement of FedAvg.aggregate (oracle/,
-    validated bit-identical to the reference), timed on this host's cores at
-    the reference worker's 4 threads (broker.py:31, session_settings.py:52)."""
+def cpu_baseline(config, n, p, dtype, weights, budget_s):
+    """The reference's aggregate as it runs in the simulator's worker: the
+    op-for-op PyTorch-CPU restatement of FedAvg.aggregate (oracle/, validated
+    bit-identical to the reference) on N host modules with the workload's real
+    parameter layout (ResNet-18: 62 tensors), including the deepcopy of
+    models[0], at the worker's 4 threads (broker.py:31, session_settings.py:52)."""
+    from torch import nn
     from oracle import fedavg_torch
     threads = 4
     prev = torch.get_num_threads()
     torch.set_num_threads(threads)
     try:
         tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
-        g = torch.Generator().manual_seed(1234)
-        xs = [(torch.randn(p, generator=g) * 0.05).to(tdt) for _ in range(n)]
-        fedavg_torch.aggregate_flat(xs, weights)  # warm
+        shapes = LAYOUTS[config]() if config in LAYOUTS else [(p,)]
+        assert sum(int(torch.Size(sh).numel()) for sh in shapes) == p
+
+        class Shaped(nn.Module):
+            def __init__(self, seed):
+                super().__init__()
+                g = torch.Generator().manual_seed(seed)
+                self.ps = nn.ParameterList(
+                    [nn.Parameter((torch.randn(sh, generator=g) * 0.05).to(tdt)) for sh in shapes])
+
+        models = [Shaped(1234 + i) for i in range(n)]
+        fedavg_torch.aggregate_modules(models, weights)  # warm
         reps, t0 = 0, time.perf_counter()
         while True:
-            fedavg_torch.aggregate_flat(xs, weights)
+            fedavg_torch.aggregate_modules(models, weights)
             reps += 1
             el = time.perf_counter() - t0
-            if el >= budget_s or reps >= 500:
+            if el >= budget_s or reps >= 2000:
                 break
         per = el / reps
-        bytes_ = (n + 1) * p * xs[0].element_size()
+        bytes_ = (n + 1) * p * (2 if dtype == "bf16" else 4)
+        layout = f"{len(shapes)} parameter tensors" if len(shapes) > 1 else "one flat parameter"
         return {"value": round(bytes_ / per / 1e9, 3), "unit": "GB/s", "cores": threads,
                 "kind": "port",
                 "ms_per_step": round(per * 1e3, 3),
-                "sample": f"{reps} x the same {n}-way {p}-param {dtype} reduce on host tensors "
-                          f"({el:.1f} s), torch CPU ops in the reference's order at {threads} threads"}
+                "sample": f"{reps} x FedAvg.aggregate of {n} host modules ({layout}, {p} {dtype} params) "
+                          f"in {el:.1f} s: the reference's torch CPU op sequence at {threads} threads"}
     finally:
         torch.set_num_threads(prev)
 
@@ -270,7 +306,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "traffic": traffic,
-                         "kernel": "dlsim::k_wreduce_vec",
+                         "kernel": "dlsim::k_wreduce_tiles",
                          "kernel_avg_us": round(kern_avg_ms * 1e3, 2),
                          "timing": "HIP events around the K timed launches on the launch stream"},
             "copy_ceiling_GBps": round(copy_gbps, 1),
@@ -281,7 +317,7 @@ def main():
         dist.barrier()
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline:
-            result["cpu_baseline"] = cpu_baseline(n, p, dtype, weights, args.cpu_seconds)
+            result["cpu_baseline"] = cpu_baseline(args.config, n, p, dtype, weights, args.cpu_seconds)
         else:
             result["cpu_baseline"] = None
         print(json.dumps(result), flush=True)
