@@ -42,6 +42,13 @@ int hip_fail(hipError_t e, const char* what) {
 // the measured rate drops by up to 20% (profiles/r01_sweep_fanin_*.jsonl).
 constexpr int kVpt = 4;
 constexpr bool kNT = true;
+// Output stores are buffer_store_dwordx4 with sc1 (write-through): no dirty
+// output lines are left in L2 for the kernel-boundary writeback, which was
+// worth 3-4% per launch on the north star (profiles/r01_tune_store_*.log).
+// The buffer's 32-bit byte offsets cap one launch's output at 2 GiB; longer
+// outputs are split into independent launches over element ranges.
+constexpr int kStore = 16;  // sc1
+constexpr size_t kMaxLaunchOutBytes = (size_t{1} << 31) - (size_t{1} << 20);
 template <class Op> constexpr int max_fixed_fan_in() { return Op::kBytes == 4 ? 14 : 9; }
 template <class Op> constexpr int group_size() { return Op::kBytes == 4 ? 8 : 4; }
 
@@ -54,7 +61,7 @@ hipError_t launch_tiles(const dlsim::Slots<NB>& s, int n, const void* acc_in, vo
   const size_t tile = static_cast<size_t>(dlsim::kBlock) * kVpt;
   const size_t blocks = nvec / tile + 1;  // full tiles + one block for the ragged end
   if (blocks > 0x7fffffffu) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((dlsim::k_wreduce_tiles<Op, NB, NF, group_size<Op>(), kVpt, kNT>),
+  hipLaunchKernelGGL((dlsim::k_wreduce_tiles<Op, NB, NF, group_size<Op>(), kVpt, kNT, kStore>),
                      dim3(static_cast<unsigned>(blocks)), dim3(dlsim::kBlock), 0, st, s, n, acc_in, out,
                      nvec, nelem);
   return hipGetLastError();
@@ -105,10 +112,31 @@ hipError_t pass_nb(const void* const* in, const float* w, int cnt, const void* a
 }
 
 template <class Op>
+int run_range(const void* const* in, int n, const float* w, void* out, size_t nelem, bool vec,
+              hipStream_t st);
+
+// Elements are independent: an output longer than one launch's 2 GiB store
+// window is reduced as consecutive ranges (pointers offset by the range start).
+template <class Op>
 int run(const void* const* in, int n, const float* w, void* out, size_t nelem, hipStream_t st) {
   if (nelem == 0) return DLSIM_OK;
   bool vec = aligned16(out);
   for (int i = 0; i < n && vec; ++i) vec = aligned16(in[i]);
+  const size_t chunk = kMaxLaunchOutBytes / Op::kBytes;  // multiple of every tile size
+  if (!vec || nelem <= chunk) return run_range<Op>(in, n, w, out, nelem, vec, st);
+  std::vector<const void*> sub(static_cast<size_t>(n));
+  for (size_t b = 0; b < nelem; b += chunk) {
+    const size_t len = std::min(chunk, nelem - b);
+    for (int i = 0; i < n; ++i) sub[i] = static_cast<const char*>(in[i]) + b * Op::kBytes;
+    int rc = run_range<Op>(sub.data(), n, w, static_cast<char*>(out) + b * Op::kBytes, len, vec, st);
+    if (rc != DLSIM_OK) return rc;
+  }
+  return DLSIM_OK;
+}
+
+template <class Op>
+int run_range(const void* const* in, int n, const float* w, void* out, size_t nelem, bool vec,
+              hipStream_t st) {
   // Passes of <= DLSIM_MAX_FUSED_INPUTS inputs; pass k > 0 continues the sum
   // held in `out` (stored exactly: fp32, or bf16-valued in EXACT bf16).
   for (int i0 = 0; i0 < n; i0 += DLSIM_MAX_FUSED_INPUTS) {

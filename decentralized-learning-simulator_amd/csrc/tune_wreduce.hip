@@ -139,13 +139,17 @@ void launch_t(const Slots<128>& s, int n, void* out, size_t nvec, size_t nelem, 
                      st, s, n, nullptr, out, nvec, nelem);
 }
 
-template <class Op, int NF, int G, int VPT, bool NT, bool NTS>
+template <class Op, int NF, int G, int VPT, bool NT, int NTS>
 void launch_ts(const Slots<128>& s, int n, void* out, size_t nvec, size_t nelem, hipStream_t st, int gm) {
   const size_t tile = (size_t)kBlock * VPT;
   const size_t full = nvec / tile;
   size_t grid = full + 1;
+  // gm > 0: grid-stride with gm*256 blocks; gm < 0: one tile per block, at most
+  // -gm blocks per CU (occupancy capped by dynamic LDS: 160 KiB / -gm each)
+  size_t lds = 0;
   if (gm > 0) grid = std::min<size_t>(grid, (size_t)gm * 256);
-  hipLaunchKernelGGL((k_wreduce_tiles<Op, 128, NF, G, VPT, NT, NTS>), dim3((unsigned)grid), dim3(kBlock), 0,
+  if (gm < 0) lds = (160 * 1024) / (size_t)(-gm) - 512;
+  hipLaunchKernelGGL((k_wreduce_tiles<Op, 128, NF, G, VPT, NT, NTS>), dim3((unsigned)grid), dim3(kBlock), lds,
                      st, s, n, nullptr, out, nvec, nelem);
 }
 
@@ -173,8 +177,20 @@ void add_nf(std::vector<Variant>& vs, int n) {
   vs.push_back({p + "_V4_g4", launch_t<Op, NF, 8, 4, true>, 4});
   vs.push_back({p + "_V4_g8", launch_t<Op, NF, 8, 4, true>, 8});
   vs.push_back({p + "_V2_plain", launch_t<Op, NF, 8, 2, false>, 0});
-  vs.push_back({p + "_V4_ps", launch_ts<Op, NF, 8, 4, true, false>, 0});
-  vs.push_back({p + "_V2_ps", launch_ts<Op, NF, 8, 2, true, false>, 0});
+  vs.push_back({p + "_V4_ps", launch_ts<Op, NF, 8, 4, true, kStPlain>, 0});
+  vs.push_back({p + "_V2_ps", launch_ts<Op, NF, 8, 2, true, kStPlain>, 0});
+  vs.push_back({p + "_V4_sc1", launch_ts<Op, NF, 8, 4, true, 16>, 0});
+  vs.push_back({p + "_V4_sc0sc1", launch_ts<Op, NF, 8, 4, true, 17>, 0});
+  vs.push_back({p + "_V4_ntsc1", launch_ts<Op, NF, 8, 4, true, 18>, 0});
+  vs.push_back({p + "_V4_bnt", launch_ts<Op, NF, 8, 4, true, 2>, 0});
+  vs.push_back({p + "_V4_sc1_g8", launch_ts<Op, NF, 8, 4, true, 16>, 8});
+  vs.push_back({p + "_V4_sc1_occ1", launch_ts<Op, NF, 8, 4, true, 16>, -1});
+  vs.push_back({p + "_V4_sc1_occ2", launch_ts<Op, NF, 8, 4, true, 16>, -2});
+  vs.push_back({p + "_V2_sc1", launch_ts<Op, NF, 8, 2, true, 16>, 0});
+  vs.push_back({p + "_V2_sc1_occ2", launch_ts<Op, NF, 8, 2, true, 16>, -2});
+  vs.push_back({p + "_V2_sc1_occ4", launch_ts<Op, NF, 8, 2, true, 16>, -4});
+  vs.push_back({p + "_V1_sc1", launch_ts<Op, NF, 8, 1, true, 16>, 0});
+  vs.push_back({p + "_V1_sc1_occ4", launch_ts<Op, NF, 8, 1, true, 16>, -4});
   vs.push_back({p + "_G4V2", launch_t<Op, NF, 4, 2, true>, 0});
   vs.push_back({p + "_lds_V1_nt", launch_l<Op, NF, 1, 2>, 0});
   vs.push_back({p + "_lds_V2_nt", launch_l<Op, NF, 2, 2>, 0});
@@ -195,7 +211,8 @@ std::vector<Variant> variants(int n) {
       {"T_G8_V2_g4", launch_t<Op, 0, 8, 2, true>, 4},
       {"T_G4_V4", launch_t<Op, 0, 4, 4, true>, 0},
       {"T_G16_V2", launch_t<Op, 0, 16, 2, true>, 0},
-      {"T_G8_V4_ps", launch_ts<Op, 0, 8, 4, true, false>, 0},
+      {"T_G8_V4_ps", launch_ts<Op, 0, 8, 4, true, kStPlain>, 0},
+      {"T_G8_V4_sc1", launch_ts<Op, 0, 8, 4, true, 16>, 0},
   };
   add_nf<Op, 2>(vs, n);
   add_nf<Op, 8>(vs, n);

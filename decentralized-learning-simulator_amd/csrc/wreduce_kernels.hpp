@@ -189,6 +189,41 @@ __device__ __forceinline__ void st16(void* base, size_t v, const u32x4& r) {
   else *p = r;
 }
 
+// ---- output store policies ----------------------------------------------------
+// kStPlain / kStNT: global_store_dwordx4 (nt = non-temporal). Values >= 0 are
+// buffer_store_dwordx4 cache-policy bits (gfx950: sc0 = 1, nt = 2, sc1 = 16),
+// e.g. 16 = sc1 write-through: nothing of the output is left dirty in L2 at
+// the kernel boundary.
+constexpr int kStPlain = -1;
+constexpr int kStNT = -2;
+
+struct OutRef {
+  void* ptr;
+  __amdgpu_buffer_rsrc_t rsrc;
+};
+
+template <int STP>
+__device__ __forceinline__ void store_vec(const OutRef& o, size_t v, const u32x4& r) {
+  if constexpr (STP == kStPlain) {
+    st16<false>(o.ptr, v, r);
+  } else if constexpr (STP == kStNT) {
+    st16<true>(o.ptr, v, r);
+  } else {
+    __builtin_amdgcn_raw_buffer_store_b128(r, o.rsrc, static_cast<int>(v * 16), 0, STP);
+  }
+}
+
+template <int STP>
+__device__ __forceinline__ OutRef make_out(void* out, size_t nvec) {
+  OutRef o;
+  o.ptr = out;
+  if constexpr (STP >= 0) {
+    // wave-uniform descriptor from kernel arguments only (no waterfall loops)
+    o.rsrc = __builtin_amdgcn_make_buffer_rsrc(out, 0, static_cast<int>(nvec * 16), 0x00020000);
+  }
+  return o;
+}
+
 // ---- kernel arguments -------------------------------------------------------
 // Input pointers and fp32 weights travel in the kernarg segment (read with
 // scalar loads, wave-uniform), NB slots; n <= NB inputs used.
@@ -274,9 +309,9 @@ __device__ __forceinline__ void init_tile(float (&a)[VPT][Op::E], const u32x4 (&
   }
 }
 
-template <class Op, int NB, int NF, int G, int VPT, bool NT, bool CHECK, bool NTS = NT>
+template <class Op, int NB, int NF, int G, int VPT, bool NT, bool CHECK, int STP>
 __device__ __forceinline__ void reduce_tile(const Slots<NB>& s, int n, const void* acc_in,
-                                            void* out, size_t v0, size_t nvec) {
+                                            const OutRef& out, size_t v0, size_t nvec) {
   float a[VPT][Op::E];
   if constexpr (NF > 0) {
     u32x4 r[NF][VPT];
@@ -315,22 +350,25 @@ __device__ __forceinline__ void reduce_tile(const Slots<NB>& s, int n, const voi
 #pragma unroll
   for (int v = 0; v < VPT; ++v) {
     const size_t idx = v0 + static_cast<size_t>(v) * kBlock;
-    if (!CHECK || idx < nvec) st16<NTS>(out, idx, pack<Op>(a[v]));
+    if (!CHECK || idx < nvec) store_vec<STP>(out, idx, pack<Op>(a[v]));
   }
 }
 
-template <class Op, int NB, int NF, int G, int VPT, bool NT, bool NTS = NT>
+// STP: output store policy (above). Buffer-store policies need the output's
+// vector part to be < 2 GiB (32-bit byte offsets); the host checks.
+template <class Op, int NB, int NF, int G, int VPT, bool NT, int STP = (NT ? kStNT : kStPlain)>
 __global__ __launch_bounds__(kBlock) void k_wreduce_tiles(const Slots<NB> s, int n,
                                                           const void* __restrict__ acc_in,
                                                           void* __restrict__ out, size_t nvec,
                                                           size_t nelem) {
   constexpr size_t kTile = static_cast<size_t>(kBlock) * VPT;
   const size_t full = nvec / kTile;
+  const OutRef o = make_out<STP>(out, nvec);
   for (size_t t = blockIdx.x; t < full; t += gridDim.x)
-    reduce_tile<Op, NB, NF, G, VPT, NT, false, NTS>(s, n, acc_in, out, t * kTile + threadIdx.x, nvec);
+    reduce_tile<Op, NB, NF, G, VPT, NT, false, STP>(s, n, acc_in, o, t * kTile + threadIdx.x, nvec);
   if (blockIdx.x == gridDim.x - 1) {
     if (full * kTile < nvec)
-      reduce_tile<Op, NB, NF, G, VPT, NT, true, NTS>(s, n, acc_in, out, full * kTile + threadIdx.x, nvec);
+      reduce_tile<Op, NB, NF, G, VPT, NT, true, STP>(s, n, acc_in, o, full * kTile + threadIdx.x, nvec);
     const size_t j = nvec * Op::E + threadIdx.x;
     if (j < nelem) fold_scalar<Op, NB>(s, n, acc_in, out, j);
   }

@@ -238,3 +238,22 @@ def test_one_hot_weights_select_input_at_full_size():
         w[k] = 1.0
         _native.wreduce(xs, w, out)
         assert torch.equal(out, xs[k])
+
+
+def test_output_longer_than_one_launch_window():
+    """> 2 GiB of fp32 output is reduced as independent element ranges (the
+    sc1 buffer stores take 32-bit offsets): exact at the range seams."""
+    p = 600_000_000 + 13  # 2.4 GB per buffer
+    a = torch.randn(p, device=dev())
+    b = torch.randn(p, device=dev())
+    w = orc.reference_weights(2, [0.3, 0.7])
+    out = torch.empty_like(a)
+    _native.wreduce([a, b], w, out)
+    chunk = ((1 << 31) - (1 << 20)) // 4
+    idx = torch.cat([torch.arange(0, p, 9973, device=dev()),
+                     torch.arange(chunk - 300, chunk + 300, device=dev()),
+                     torch.arange(p - 300, p, device=dev())])
+    rows = [from_dev(a[idx]), from_dev(b[idx])]
+    assert orc.same_bits(from_dev(out[idx]), orc.wreduce(rows, w, "f32"))
+    del a, b, out
+    torch.cuda.empty_cache()
