@@ -356,6 +356,12 @@ __device__ __forceinline__ void reduce_tile(const Slots<NB>& s, int n, const voi
 
 // STP: output store policy (above). Buffer-store policies need the output's
 // vector part to be < 2 GiB (32-bit byte offsets); the host checks.
+//
+// Block 0 — dispatched first — folds the ragged end (the last partial tile
+// and the < E scalar tail, two dependent HBM round trips), so that latency
+// hides under the rest of the grid instead of trailing it; blocks 1.. take
+// the full tiles, one per block when the grid is full + 1 blocks, otherwise
+// grid-strided. A one-block grid does everything.
 template <class Op, int NB, int NF, int G, int VPT, bool NT, int STP = (NT ? kStNT : kStPlain)>
 __global__ __launch_bounds__(kBlock) void k_wreduce_tiles(const Slots<NB> s, int n,
                                                           const void* __restrict__ acc_in,
@@ -364,14 +370,18 @@ __global__ __launch_bounds__(kBlock) void k_wreduce_tiles(const Slots<NB> s, int
   constexpr size_t kTile = static_cast<size_t>(kBlock) * VPT;
   const size_t full = nvec / kTile;
   const OutRef o = make_out<STP>(out, nvec);
-  for (size_t t = blockIdx.x; t < full; t += gridDim.x)
-    reduce_tile<Op, NB, NF, G, VPT, NT, false, STP>(s, n, acc_in, o, t * kTile + threadIdx.x, nvec);
-  if (blockIdx.x == gridDim.x - 1) {
+  const size_t nb = gridDim.x;
+  if (blockIdx.x == 0) {
     if (full * kTile < nvec)
       reduce_tile<Op, NB, NF, G, VPT, NT, true, STP>(s, n, acc_in, o, full * kTile + threadIdx.x, nvec);
     const size_t j = nvec * Op::E + threadIdx.x;
     if (j < nelem) fold_scalar<Op, NB>(s, n, acc_in, out, j);
+    if (nb > 1) return;
   }
+  const size_t workers = nb > 1 ? nb - 1 : 1;
+  const size_t first = nb > 1 ? blockIdx.x - 1 : 0;
+  for (size_t t = first; t < full; t += workers)
+    reduce_tile<Op, NB, NF, G, VPT, NT, false, STP>(s, n, acc_in, o, t * kTile + threadIdx.x, nvec);
 }
 
 // Copy probe: the achievable streaming ceiling on this device.

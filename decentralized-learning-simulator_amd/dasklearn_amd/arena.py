@@ -24,6 +24,7 @@ the reduced arena, keeping each original's requires_grad.
 from __future__ import annotations
 
 import copy
+import time
 from collections import OrderedDict
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -152,14 +153,35 @@ def _target_device(params0: Sequence[torch.Tensor], device) -> torch.device:
     return torch.device("cuda", torch.cuda.current_device())
 
 
+class _Stages:
+    """Optional wall-clock stage breakdown (scripts/bench_host.py). When on,
+    the stream is synchronised at every stage boundary, so only use it to
+    measure."""
+
+    def __init__(self, sink: Optional[dict], stream):
+        self.sink, self.stream = sink, stream
+        self.t = time.perf_counter() if sink is not None else 0.0
+
+    def mark(self, name: str):
+        if self.sink is None:
+            return
+        self.stream.synchronize()
+        now = time.perf_counter()
+        self.sink[name] = self.sink.get(name, 0.0) + (now - self.t)
+        self.t = now
+
+
 def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, mode: int,
-                             device=None) -> Tuple[ParamLayout, Dict[torch.dtype, torch.Tensor], torch.device]:
+                             device=None, timing: Optional[dict] = None
+                             ) -> Tuple[ParamLayout, Dict[torch.dtype, torch.Tensor], torch.device]:
     """Reduce the parameters of `models` into one fresh device arena per dtype."""
     layout = ParamLayout(models[0])
     all_params = [layout.check_compatible(m) for m in models]
     dev = _target_device(all_params[0], device)
     n = len(models)
     outs: Dict[torch.dtype, torch.Tensor] = {}
+    stream = torch.cuda.current_stream(dev)
+    st = _Stages(timing, stream)
     with torch.no_grad():
         for dt, idx in layout.groups.items():
             total = layout.totals[dt]
@@ -170,17 +192,22 @@ def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, m
             on_dev = all(all_params[i][idx[0]].device == dev for i in range(n))
             if on_dev:
                 views = [layout.arena_view(ps, dt) for ps in all_params]
+                st.mark("layout")
                 if all(v is not None for v in views):
                     _native.wreduce(views, weights_f32, out, mode)
+                    st.mark("kernel")
                     continue
                 rows = [[ps[k].detach().contiguous() for k in idx] for ps in all_params]
                 outs_k = [out[layout.offsets[k]:layout.offsets[k] + layout.params[k].numel()]
                           for k in idx]
                 _native.wreduce_tensors(rows, weights_f32, outs_k, mode)
+                st.mark("kernel")
                 continue
-            # host (or foreign-device) models: pack -> pinned -> H2D, per model
-            stream = torch.cuda.current_stream(dev)
+            # host (or foreign-device) models: pack each model into pinned
+            # staging, then an async H2D copy on the current stream — the DMA of
+            # model i overlaps the packing of model i+1.
             dev_rows, pinned = STAGING.acquire(dev, dt, n, total, stream)
+            st.mark("layout")
             for i, ps in enumerate(all_params):
                 src = [ps[k].detach().reshape(-1) for k in idx]
                 if src[0].is_cuda:
@@ -189,9 +216,25 @@ def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, m
                     torch.cat(src, out=pinned[i])
                     with torch.cuda.stream(stream):
                         dev_rows[i].copy_(pinned[i], non_blocking=True)
+            st.mark("pack_h2d")
             _native.wreduce([dev_rows[i] for i in range(n)], weights_f32, out, mode)
             STAGING.release(dev, dt, n, total, stream)
+            st.mark("kernel")
     return layout, outs, dev
+
+
+def arenas_to_host(arenas: Dict[torch.dtype, torch.Tensor], stream) -> Dict[torch.dtype, torch.Tensor]:
+    """D2H into page-locked memory from torch's caching host allocator (the
+    block returns to the cache when the returned module is freed), then wait
+    for the copies: the output module may be used as soon as this returns."""
+    host = {}
+    with torch.cuda.stream(stream):
+        for dt, a in arenas.items():
+            h = torch.empty(a.numel(), dtype=dt, pin_memory=True)
+            h.copy_(a, non_blocking=True)
+            host[dt] = h
+    stream.synchronize()
+    return host
 
 
 def module_from_arenas(model0: nn.Module, layout: ParamLayout,
@@ -209,11 +252,13 @@ def module_from_arenas(model0: nn.Module, layout: ParamLayout,
 
 
 def aggregate_modules(models: List[nn.Module], weights: Optional[Sequence[float]], mode: int,
-                      device=None, to_host: Optional[bool] = None) -> nn.Module:
+                      device=None, to_host: Optional[bool] = None,
+                      timing: Optional[dict] = None) -> nn.Module:
     """FedAvg.aggregate semantics on the GPU (see module docstring).
 
     to_host: copy the result back to host memory (default: iff models[0]'s
-    parameters are on the host, like the reference's output)."""
+    parameters are on the host, like the reference's output).
+    timing: if a dict, filled with a wall-clock stage breakdown (synchronising)."""
     # fedavg.py:14-17, same order of checks => same exceptions
     if not weights:
         weights = [float(1. / len(models)) for _ in range(len(models))]
@@ -221,8 +266,13 @@ def aggregate_modules(models: List[nn.Module], weights: Optional[Sequence[float]
         assert len(weights) == len(models)
     model0 = models[0]  # IndexError for an empty list, as the reference
     w32 = _native.fp32_weights(weights)
-    layout, arenas, dev = reduce_modules_to_arenas(models, w32, mode, device)
+    layout, arenas, dev = reduce_modules_to_arenas(models, w32, mode, device, timing)
     host_out = to_host if to_host is not None else not any(p.is_cuda for p in layout.params)
+    stream = torch.cuda.current_stream(dev)
+    st = _Stages(timing, stream)
     if host_out:
-        arenas = {dt: a.to("cpu") for dt, a in arenas.items()}  # synchronises the stream
-    return module_from_arenas(model0, layout, arenas)
+        arenas = arenas_to_host(arenas, stream)
+        st.mark("d2h")
+    out = module_from_arenas(model0, layout, arenas)
+    st.mark("module")
+    return out

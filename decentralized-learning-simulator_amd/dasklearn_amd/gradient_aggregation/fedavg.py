@@ -25,8 +25,12 @@ from dasklearn_amd.gradient_aggregation import GradientAggregation
 class FedAvg(GradientAggregation):
 
     @staticmethod
-    def aggregate(models: List[nn.Module], weights: Optional[List[float]] = None) -> nn.Module:
-        return aggregate_modules(models, weights, _native.DLSIM_EXACT)
+    def aggregate(models: List[nn.Module], weights: Optional[List[float]] = None,
+                  to_host: Optional[bool] = None) -> nn.Module:
+        """to_host=None (default): the result lives where models[0] lives, as
+        in the reference; False keeps it on the GPU for a device-resident
+        aggregate -> train chain."""
+        return aggregate_modules(models, weights, _native.DLSIM_EXACT, to_host=to_host)
 
 
 class FedAvgFast(GradientAggregation):
@@ -34,5 +38,6 @@ class FedAvgFast(GradientAggregation):
     not bit-identical to the reference; within n * 2^-23 relative in fp32."""
 
     @staticmethod
-    def aggregate(models: List[nn.Module], weights: Optional[List[float]] = None) -> nn.Module:
-        return aggregate_modules(models, weights, _native.DLSIM_FAST)
+    def aggregate(models: List[nn.Module], weights: Optional[List[float]] = None,
+                  to_host: Optional[bool] = None) -> nn.Module:
+        return aggregate_modules(models, weights, _native.DLSIM_FAST, to_host=to_host)

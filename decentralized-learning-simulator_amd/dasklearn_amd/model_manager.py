@@ -38,4 +38,9 @@ class ModelManager:
 
     def aggregate_trained_models(self, weights: List[float] = None) -> Optional[nn.Module]:
         models = list(self.incoming_trained_models.values())
-        return self.get_aggregation_method().aggregate(models, weights=weights)
+        method = self.get_aggregation_method()
+        # Opt-in (not a reference setting): keep the aggregate on the GPU so a
+        # device-resident consumer skips the D2H/H2D round trip.
+        if getattr(self.settings, "aggregate_on_device", False):
+            return method.aggregate(models, weights=weights, to_host=False)
+        return method.aggregate(models, weights=weights)

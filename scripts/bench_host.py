@@ -73,6 +73,12 @@ def main():
         t = timed(lambda: FedAvg.aggregate(cpu_models, None), a.reps)
         res["host_ms"] = round(t * 1e3, 3)
         res["host_GBps"] = round(byts / t / 1e9, 2)
+        from dasklearn_amd import _native
+        from dasklearn_amd.arena import aggregate_modules
+        stages = {}
+        for _ in range(3):
+            aggregate_modules(cpu_models, None, _native.DLSIM_EXACT, timing=stages)
+        res["host_stages_ms"] = {k: round(v / 3 * 1e3, 3) for k, v in stages.items()}
         dev_models = [Shaped(shapes, i).to(dev) for i in range(n)]
         t = timed(lambda: FedAvg.aggregate(dev_models, None), a.reps)
         res["dev_list_ms"] = round(t * 1e3, 3)

@@ -172,3 +172,30 @@ def test_model_manager_and_task_function():
                                            "weights": [0.25, 0.75]})
     exp = orc.wreduce(list(g["inputs"]), orc.reference_weights(2, [0.25, 0.75]), "f32")
     assert orc.same_bits(flat_of(res[0]), exp)
+
+
+def test_device_resident_option_keeps_result_on_gpu():
+    """settings.aggregate_on_device (opt-in): host models in, GPU module out;
+    same bits as the host result."""
+    g = load_golden(os.path.join(GOLDEN, "cfg1_gnlenet_f32_n2_none.npz"))
+    models = modules_from_golden(g)
+
+    class OnDevice(Settings):
+        aggregate_on_device = True
+
+    res = functions.aggregate(OnDevice(), {"models": models, "round": 1, "peer": 0})
+    assert all(p.is_cuda for p in res[0].parameters())
+    assert orc.same_bits(flat_of(res[0]), g["expected"])
+
+
+def test_host_result_is_pinned_and_stage_timing_works():
+    from dasklearn_amd import _native
+    from dasklearn_amd.arena import aggregate_modules
+    g = load_golden(os.path.join(GOLDEN, "cfg1_gnlenet_f32_n2_none.npz"))
+    models = modules_from_golden(g)
+    stages = {}
+    out = aggregate_modules(models, None, _native.DLSIM_EXACT, timing=stages)
+    assert set(stages) >= {"layout", "pack_h2d", "kernel", "d2h", "module"}
+    p0 = next(out.parameters())
+    assert not p0.is_cuda and p0.is_pinned()
+    assert orc.same_bits(flat_of(out), g["expected"])
