@@ -91,6 +91,12 @@ def parse():
     ap.add_argument("--mode", default="exact", choices=["exact", "fast"])
     ap.add_argument("--strong", action="store_true",
                     help="strong scaling: split the config's params over ranks instead of per rank")
+    ap.add_argument("--batch", type=int, default=1,
+                    help="B independent aggregates of the config per step, in batched launches "
+                         "(dlsim_wreduce_batched; a simulated round's per-peer tasks)")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend: nccl (= RCCL over xGMI, the real path); gloo only "
+                         "to rehearse the multi-process flow on a box with fewer GPUs than ranks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="budget for the CPU baseline sample (rank 0, N=1 only)")
@@ -176,10 +182,20 @@ def main():
         if world == 1 and args.gpus != 1:
             print(f"bench.py: --gpus {args.gpus} needs torchrun with that many ranks", file=sys.stderr)
             sys.exit(2)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    if args.backend == "nccl" and world > ndev:
+        print(f"bench.py: {world} ranks but {ndev} GPUs visible", file=sys.stderr)
+        sys.exit(2)
+    local_dev = local % max(1, ndev)  # gloo rehearsal may share a GPU
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    # small control-plane tensors live where the backend can reduce them
+    cdev = dev if args.backend == "nccl" else torch.device("cpu")
 
     from dasklearn_amd import _native
 
@@ -207,10 +223,26 @@ def main():
         for i in range(n):
             x[i, :p].copy_(torch.randn(p, generator=g, device=dev) * 0.05)
         arenas.append(x)
-    outs = [torch.empty(p, dtype=tdt, device=dev) for _ in range(sets)]
-    plans = [_native.ReducePlan([arenas[s][i, :p] for i in range(n)], w32, outs[s], mode)
-             for s in range(sets)]
-    assert all(t.data_ptr() % 16 == 0 for t in plans[0]._keep[0]), "arena rows must be 16-B aligned"
+    B = max(1, args.batch)
+    if B == 1:
+        outs = [torch.empty(p, dtype=tdt, device=dev) for _ in range(sets)]
+        plans = [_native.ReducePlan([arenas[s][i, :p] for i in range(n)], w32, outs[s], mode)
+                 for s in range(sets)]
+        assert all(t.data_ptr() % 16 == 0 for t in plans[0]._keep[0]), "arena rows must be 16-B aligned"
+    else:
+        # B tasks per step, each with its own N input models (rows of a bigger
+        # arena block) and output; sets rotate as above
+        blocks = []
+        for s in range(sets):
+            x = torch.empty((B, n, p_pad), dtype=tdt, device=dev)
+            x.copy_(arenas[s].unsqueeze(0).expand(B, n, p_pad))
+            x.add_(torch.randn((B, 1, 1), generator=g, device=dev).to(tdt) * 0.01)
+            blocks.append(x)
+        del arenas
+        outs_b = [torch.empty((B, p_pad), dtype=tdt, device=dev) for _ in range(sets)]
+        plans = [_native.BatchPlan([([blocks[s][b, i, :p] for i in range(n)], w32, outs_b[s][b, :p])
+                                    for b in range(B)], mode) for s in range(sets)]
+        outs = [o[0, :p] for o in outs_b]
     stream = torch.cuda.current_stream(dev)
 
     for k in range(args.warmup):
@@ -238,9 +270,9 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_avg_ms = ev0.elapsed_time(ev1) / K
 
-    bytes_per_launch = (n + 1) * p * esz
-    el_t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    tot_b = torch.tensor([bytes_per_launch * K], dtype=torch.float64, device=dev)
+    bytes_per_launch = (n + 1) * p * esz * B
+    el_t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
+    tot_b = torch.tensor([bytes_per_launch * K], dtype=torch.float64, device=cdev)
     if world > 1:
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
         dist.all_reduce(tot_b, op=dist.ReduceOp.SUM)
@@ -249,7 +281,7 @@ def main():
     value = total_bytes / max_el / 1e9
 
     # copy ceiling on this device (same footprint as one step), reported beside
-    cb = (bytes_per_launch // 2) & ~15
+    cb = min(bytes_per_launch // 2, 1 << 30) & ~15
     src = torch.empty(cb, dtype=torch.uint8, device=dev).fill_(1)
     dst = torch.empty_like(src)
     for _ in range(5):
@@ -265,22 +297,24 @@ def main():
 
     allgather = None
     if world > 1:
-        full = torch.empty(p * world, dtype=tdt, device=dev)
+        shard = outs[0] if args.backend == "nccl" else outs[0].cpu()
+        full = torch.empty(p * world, dtype=tdt, device=shard.device)
         for _ in range(3):
-            dist.all_gather_into_tensor(full, outs[0])
+            dist.all_gather_into_tensor(full, shard)
         torch.cuda.synchronize(dev)
         dist.barrier()
         a0 = time.perf_counter()
         reps = 10
         for _ in range(reps):
-            dist.all_gather_into_tensor(full, outs[0])
+            dist.all_gather_into_tensor(full, shard)
         torch.cuda.synchronize(dev)
         ag_ms = (time.perf_counter() - a0) / reps * 1e3
-        agt = torch.tensor([ag_ms], dtype=torch.float64, device=dev)
+        agt = torch.tensor([ag_ms], dtype=torch.float64, device=cdev)
         dist.all_reduce(agt, op=dist.ReduceOp.MAX)
         allgather = {"ms": round(float(agt.item()), 4),
                      "bytes_out_per_rank": p * esz * world,
-                     "note": "RCCL all_gather_into_tensor of the reduced shards (not in value)"}
+                     "note": ("RCCL" if args.backend == "nccl" else "gloo (rehearsal)")
+                             + " all_gather_into_tensor of the reduced shards (not in value)"}
 
     result = None
     if rank == 0:
@@ -300,13 +334,15 @@ def main():
             "dtype": dtype,
             "data": "synthetic: torch.randn*0.05 on device, 3 rotating input sets; "
                     f"{wkind} weights",
-            "config": {"workload": args.config + ": " + desc, "n_models": n, "params_per_rank": p,
+            "config": {"workload": args.config + ": " + desc + (f" x {B} tasks per launch" if B > 1 else ""),
+                       "backend": args.backend if world > 1 else None,
+                       "n_models": n, "params_per_rank": p, "tasks_per_step": B,
                        "mode": args.mode, "parallelism": f"param-shard x{world}",
                        "bytes_per_step_per_rank": bytes_per_launch},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "traffic": traffic,
-                         "kernel": "dlsim::k_wreduce_tiles",
+                         "kernel": "dlsim::k_wreduce_tiles" if B == 1 else "dlsim::k_wreduce_batch",
                          "kernel_avg_us": round(kern_avg_ms * 1e3, 2),
                          "timing": "HIP events around the K timed launches on the launch stream"},
             "copy_ceiling_GBps": round(copy_gbps, 1),

@@ -101,34 +101,37 @@ hipError_t launch_pass(const dlsim::Slots<NB>& s, int n, const void* acc_in, voi
 // Packs up to NB inputs into kernel arguments and launches one pass.
 template <class Op, int NB>
 hipError_t pass_nb(const void* const* in, const float* w, int cnt, const void* acc_in, void* out,
-                   size_t nelem, bool vec, hipStream_t st) {
+                   size_t nelem, bool vec, float div, hipStream_t st) {
   dlsim::Slots<NB> s;
   std::memset(&s, 0, sizeof(s));
   for (int i = 0; i < cnt; ++i) {
     s.p[i] = in[i];
-    s.w[i] = w[i];
+    s.w[i] = w ? w[i] : 1.0f;
   }
+  s.div = div;
   return launch_pass<Op, NB>(s, cnt, acc_in, out, nelem, vec, st);
 }
 
 template <class Op>
 int run_range(const void* const* in, int n, const float* w, void* out, size_t nelem, bool vec,
-              hipStream_t st);
+              float div, hipStream_t st);
 
 // Elements are independent: an output longer than one launch's 2 GiB store
 // window is reduced as consecutive ranges (pointers offset by the range start).
+// div: final divisor (the mean policies; 1 for the weighted reduce).
 template <class Op>
-int run(const void* const* in, int n, const float* w, void* out, size_t nelem, hipStream_t st) {
+int run(const void* const* in, int n, const float* w, void* out, size_t nelem, hipStream_t st,
+        float div = 1.0f) {
   if (nelem == 0) return DLSIM_OK;
   bool vec = aligned16(out);
   for (int i = 0; i < n && vec; ++i) vec = aligned16(in[i]);
   const size_t chunk = kMaxLaunchOutBytes / Op::kBytes;  // multiple of every tile size
-  if (!vec || nelem <= chunk) return run_range<Op>(in, n, w, out, nelem, vec, st);
+  if (!vec || nelem <= chunk) return run_range<Op>(in, n, w, out, nelem, vec, div, st);
   std::vector<const void*> sub(static_cast<size_t>(n));
   for (size_t b = 0; b < nelem; b += chunk) {
     const size_t len = std::min(chunk, nelem - b);
     for (int i = 0; i < n; ++i) sub[i] = static_cast<const char*>(in[i]) + b * Op::kBytes;
-    int rc = run_range<Op>(sub.data(), n, w, static_cast<char*>(out) + b * Op::kBytes, len, vec, st);
+    int rc = run_range<Op>(sub.data(), n, w, static_cast<char*>(out) + b * Op::kBytes, len, vec, div, st);
     if (rc != DLSIM_OK) return rc;
   }
   return DLSIM_OK;
@@ -136,17 +139,131 @@ int run(const void* const* in, int n, const float* w, void* out, size_t nelem, h
 
 template <class Op>
 int run_range(const void* const* in, int n, const float* w, void* out, size_t nelem, bool vec,
-              hipStream_t st) {
+              float div, hipStream_t st) {
   // Passes of <= DLSIM_MAX_FUSED_INPUTS inputs; pass k > 0 continues the sum
-  // held in `out` (stored exactly: fp32, or bf16-valued in EXACT bf16).
+  // held in `out` (stored exactly: fp32, or bf16-valued in EXACT bf16); only
+  // the last pass applies the divisor.
   for (int i0 = 0; i0 < n; i0 += DLSIM_MAX_FUSED_INPUTS) {
     const int cnt = std::min(DLSIM_MAX_FUSED_INPUTS, n - i0);
     const void* acc_in = (i0 == 0) ? nullptr : out;
+    const float* wp = w ? w + i0 : nullptr;
+    const float d = (i0 + cnt >= n) ? div : 1.0f;
     hipError_t e = (cnt <= 16)
-                       ? pass_nb<Op, 16>(in + i0, w + i0, cnt, acc_in, out, nelem, vec, st)
-                       : pass_nb<Op, DLSIM_MAX_FUSED_INPUTS>(in + i0, w + i0, cnt, acc_in, out,
-                                                             nelem, vec, st);
+                       ? pass_nb<Op, 16>(in + i0, wp, cnt, acc_in, out, nelem, vec, d, st)
+                       : pass_nb<Op, DLSIM_MAX_FUSED_INPUTS>(in + i0, wp, cnt, acc_in, out,
+                                                             nelem, vec, d, st);
     if (e != hipSuccess) return hip_fail(e, "kernel launch");
+  }
+  return DLSIM_OK;
+}
+
+// ---- batched launches ---------------------------------------------------------
+template <class Op, int NF>
+hipError_t launch_batch_nf(const dlsim::BatchSlots& s, unsigned blocks, hipStream_t st) {
+  hipLaunchKernelGGL((dlsim::k_wreduce_batch<Op, NF, group_size<Op>(), kVpt, kNT, kStore>), dim3(blocks),
+                     dim3(dlsim::kBlock), 0, st, s);
+  return hipGetLastError();
+}
+
+template <class Op, int K>
+hipError_t launch_batch_fixed(const dlsim::BatchSlots& s, int n, unsigned blocks, hipStream_t st) {
+  if constexpr (K > max_fixed_fan_in<Op>()) {
+    return launch_batch_nf<Op, 0>(s, blocks, st);
+  } else {
+    if (n == K) return launch_batch_nf<Op, K>(s, blocks, st);
+    return launch_batch_fixed<Op, K + 1>(s, n, blocks, st);
+  }
+}
+
+// Fill and launch BatchSlots with tasks [t0, t1); all tasks vector-eligible.
+template <class Op>
+hipError_t launch_batch(const int* fan_in, const size_t* in_off, const void* const* in, const float* w,
+                        void* const* outs, const size_t* nelem, int t0, int t1, hipStream_t st) {
+  dlsim::BatchSlots s;
+  std::memset(&s, 0, sizeof(s));
+  const size_t tile = static_cast<size_t>(dlsim::kBlock) * kVpt;
+  uint32_t blocks = 0;
+  int ptrs = 0;
+  bool uniform = true;
+  for (int t = t0; t < t1; ++t) {
+    const int k = t - t0;
+    const size_t nvec = nelem[t] / Op::E;
+    s.out[k] = outs[t];
+    s.nvec[k] = nvec;
+    s.nelem[k] = nelem[t];
+    s.block_start[k] = blocks;
+    s.ptr_off[k] = static_cast<uint16_t>(ptrs);
+    s.fan_in[k] = static_cast<uint16_t>(fan_in[t]);
+    for (int i = 0; i < fan_in[t]; ++i) {
+      s.p[ptrs + i] = in[in_off[t] + i];
+      s.w[ptrs + i] = w[in_off[t] + i];
+    }
+    ptrs += fan_in[t];
+    blocks += static_cast<uint32_t>(nvec / tile + 1);
+    uniform = uniform && fan_in[t] == fan_in[t0];
+  }
+  s.ntasks = t1 - t0;
+  s.block_start[t1 - t0] = blocks;
+  if (uniform) return launch_batch_fixed<Op, 1>(s, fan_in[t0], blocks, st);
+  return launch_batch_nf<Op, 0>(s, blocks, st);
+}
+
+template <class Op>
+int run_batched(int b, const int* fan_in, const void* const* in, const float* w, void* const* outs,
+                const size_t* nelem, hipStream_t st) {
+  std::vector<size_t> off(static_cast<size_t>(b) + 1, 0);
+  for (int t = 0; t < b; ++t) off[t + 1] = off[t] + static_cast<size_t>(fan_in[t]);
+  const size_t tile = static_cast<size_t>(dlsim::kBlock) * kVpt;
+  auto batchable = [&](int t) {
+    if (nelem[t] == 0 || fan_in[t] > 16) return false;
+    if (nelem[t] * Op::kBytes > kMaxLaunchOutBytes) return false;
+    if (!aligned16(outs[t])) return false;
+    for (int i = 0; i < fan_in[t]; ++i)
+      if (!aligned16(in[off[t] + i])) return false;
+    return true;
+  };
+  // Tasks that cannot ride in a batch (large fan-in, misaligned, > 2 GiB) go alone.
+  std::vector<int> group;
+  for (int t = 0; t < b; ++t) {
+    if (batchable(t)) {
+      group.push_back(t);
+      continue;
+    }
+    if (nelem[t] == 0) continue;
+    int rc = run<Op>(in + off[t], fan_in[t], w + off[t], outs[t], nelem[t], st);
+    if (rc != DLSIM_OK) return rc;
+  }
+  // Pack the rest greedily into kernel-argument batches, in task order.
+  std::vector<const void*> ins;
+  std::vector<float> ws;
+  std::vector<void*> os;
+  std::vector<size_t> ne, ioff;
+  std::vector<int> fi;
+  for (int t : group) {
+    ioff.push_back(ins.size());
+    for (int i = 0; i < fan_in[t]; ++i) {
+      ins.push_back(in[off[t] + i]);
+      ws.push_back(w[off[t] + i]);
+    }
+    os.push_back(outs[t]);
+    ne.push_back(nelem[t]);
+    fi.push_back(fan_in[t]);
+  }
+  const int g = static_cast<int>(group.size());
+  int t0 = 0;
+  while (t0 < g) {
+    int t1 = t0, ptrs = 0;
+    uint64_t blocks = 0;
+    while (t1 < g && t1 - t0 < dlsim::kBatchMaxTasks && ptrs + fi[t1] <= dlsim::kBatchMaxPtrs &&
+           blocks + ne[t1] / Op::E / tile + 1 < 0x7fffffffull) {
+      ptrs += fi[t1];
+      blocks += ne[t1] / Op::E / tile + 1;
+      ++t1;
+    }
+    hipError_t e = launch_batch<Op>(fi.data(), ioff.data(), ins.data(), ws.data(), os.data(), ne.data(), t0,
+                                    t1, st);
+    if (e != hipSuccess) return hip_fail(e, "batched kernel launch");
+    t0 = t1;
   }
   return DLSIM_OK;
 }
@@ -154,11 +271,11 @@ int run_range(const void* const* in, int n, const float* w, void* out, size_t ne
 size_t elem_bytes(int dtype) { return dtype == DLSIM_BF16 ? 2 : 4; }
 
 int check_args(const void* const* in, int n, const float* w, const void* out, size_t nelem,
-               int dtype, int mode) {
+               int dtype, int mode, bool need_w = true) {
   if (dtype != DLSIM_F32 && dtype != DLSIM_BF16) return fail(DLSIM_E_DTYPE, "unsupported dtype %d", dtype);
   if (mode != DLSIM_EXACT && mode != DLSIM_FAST) return fail(DLSIM_E_MODE, "unsupported mode %d", mode);
   if (n < 1) return fail(DLSIM_E_ARG, "n must be >= 1 (got %d)", n);
-  if (!in || !w) return fail(DLSIM_E_ARG, "null inputs or weights array");
+  if (!in || (need_w && !w)) return fail(DLSIM_E_ARG, "null inputs or weights array");
   if (nelem == 0) return DLSIM_OK;
   if (!out) return fail(DLSIM_E_ARG, "null output pointer");
   const size_t bytes = nelem * elem_bytes(dtype);
@@ -230,6 +347,40 @@ int dlsim_wreduce_tensors(const void* const* d_inputs, int n, int t, const size_
     }
   }
   return DLSIM_OK;
+}
+
+int dlsim_wreduce_batched(int b, const int* fan_in, const void* const* d_inputs,
+                          const float* h_weights, void* const* d_outs, const size_t* n_elems,
+                          int dtype, int mode, void* stream) {
+  g_err.clear();
+  if (b < 0) return fail(DLSIM_E_ARG, "b must be >= 0 (got %d)", b);
+  if (b == 0) return DLSIM_OK;
+  if (!fan_in || !d_inputs || !h_weights || !d_outs || !n_elems) return fail(DLSIM_E_ARG, "null array argument");
+  size_t off = 0;
+  for (int t = 0; t < b; ++t) {
+    int rc = check_args(d_inputs + off, fan_in[t], h_weights + off, d_outs[t], n_elems[t], dtype, mode);
+    if (rc != DLSIM_OK) return fail(rc, "task %d: %s", t, g_err.c_str());
+    off += static_cast<size_t>(fan_in[t]);
+  }
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (dtype == DLSIM_F32)
+    return mode == DLSIM_EXACT
+               ? run_batched<dlsim::F32Exact>(b, fan_in, d_inputs, h_weights, d_outs, n_elems, st)
+               : run_batched<dlsim::F32Fast>(b, fan_in, d_inputs, h_weights, d_outs, n_elems, st);
+  return mode == DLSIM_EXACT
+             ? run_batched<dlsim::BF16Exact>(b, fan_in, d_inputs, h_weights, d_outs, n_elems, st)
+             : run_batched<dlsim::BF16Fast>(b, fan_in, d_inputs, h_weights, d_outs, n_elems, st);
+}
+
+int dlsim_mean(const void* const* d_inputs, int n, void* d_out, size_t n_elems, int dtype,
+               void* stream) {
+  g_err.clear();
+  int rc = check_args(d_inputs, n, nullptr, d_out, n_elems, dtype, DLSIM_EXACT, false);
+  if (rc != DLSIM_OK) return rc;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const float div = static_cast<float>(n);
+  return dtype == DLSIM_F32 ? run<dlsim::F32Mean>(d_inputs, n, nullptr, d_out, n_elems, st, div)
+                            : run<dlsim::BF16Mean>(d_inputs, n, nullptr, d_out, n_elems, st, div);
 }
 
 int dlsim_shard_range(size_t n_elems, int world, int rank, size_t align_elems, size_t* begin,

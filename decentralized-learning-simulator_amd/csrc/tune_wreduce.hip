@@ -30,7 +30,7 @@ struct BF16ExactOld {  // integer RNE with an explicit NaN branch (round-1 shape
     a0 = step(a0, w, x0);
     a1 = step(a1, w, x1);
   }
-  __device__ static float finish(float a) { return a; }
+  __device__ static float finish(float a, float) { return a; }
 };
 __device__ __forceinline__ float bf16_round_nonan(float f) {  // valid when NaNs have zero low halves
   uint32_t u = __float_as_uint(f);
@@ -47,7 +47,7 @@ struct BF16ExactInt {
     a0 = step(a0, w, x0);
     a1 = step(a1, w, x1);
   }
-  __device__ static float finish(float a) { return a; }
+  __device__ static float finish(float a, float) { return a; }
 };
 // ---- LDS-DMA variant (experiment, not shipped: no gain over register
 // streaming on MI355X) -------------------------------------------
@@ -88,7 +88,7 @@ __global__ __launch_bounds__(kBlock) void k_wreduce_lds(const Slots<128> s, void
       fold_tile<Op, VPT>(a, s.w[i], r);
     }
 #pragma unroll
-    for (int v = 0; v < VPT; ++v) st16<true>(out, v0 + v * 64, pack<Op>(a[v]));
+    for (int v = 0; v < VPT; ++v) st16<true>(out, v0 + v * 64, pack<Op>(a[v], s.div));
     // the next tile's DMA must not overwrite LDS this wave is still reading
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }

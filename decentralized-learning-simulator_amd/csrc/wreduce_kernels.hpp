@@ -77,7 +77,7 @@ struct F32Exact {
     a0 = step(a0, w, x0);
     a1 = step(a1, w, x1);
   }
-  __device__ static float finish(float a) { return a; }
+  __device__ static float finish(float a, float) { return a; }
 };
 
 struct F32Fast {
@@ -89,7 +89,7 @@ struct F32Fast {
     a0 = step(a0, w, x0);
     a1 = step(a1, w, x1);
   }
-  __device__ static float finish(float a) { return a; }
+  __device__ static float finish(float a, float) { return a; }
 };
 
 // bf16 exact: product and sum each rounded to bf16. x * 0 is +-0 or NaN,
@@ -109,7 +109,7 @@ struct BF16Exact {
     a1 = a1 + p1;
     bf16_round2(a0, a1);
   }
-  __device__ static float finish(float a) { return a; }
+  __device__ static float finish(float a, float) { return a; }
 };
 
 struct BF16Fast {
@@ -121,7 +121,39 @@ struct BF16Fast {
     a0 = step(a0, w, x0);
     a1 = step(a1, w, x1);
   }
-  __device__ static float finish(float a) { return bf16_round(a); }
+  __device__ static float finish(float a, float) { return bf16_round(a); }
+};
+
+// Mean of the inputs (ChunkManager.reconstruct_model, chunk_manager.py:38-40:
+// torch.mean(torch.stack(chunks), dim=0) = sum over dim 0, then div_(n)):
+// acc starts at +0 (the reduction's identity), adds every input in order,
+// then one division by n (weights unused). fp32 matches PyTorch's CPU
+// reduction bit for bit while that reduction is sequential (n <= 4);
+// beyond, PyTorch's order depends on sizes and threads.
+// bf16: the sum is accumulated in fp32 and rounded to bf16 (the bf16 sum
+// tensor), then divided and rounded again (div_ on bf16).
+struct F32Mean {
+  static constexpr int E = 4;
+  static constexpr int kBytes = 4;
+  __device__ static float init(float) { return 0.0f; }
+  __device__ static float step(float acc, float, float x) { return acc + x; }
+  __device__ static void step2(float& a0, float& a1, float, float x0, float x1) {
+    a0 = a0 + x0;
+    a1 = a1 + x1;
+  }
+  __device__ static float finish(float a, float div) { return a / div; }
+};
+
+struct BF16Mean {
+  static constexpr int E = 8;
+  static constexpr int kBytes = 2;
+  __device__ static float init(float) { return 0.0f; }
+  __device__ static float step(float acc, float, float x) { return acc + x; }
+  __device__ static void step2(float& a0, float& a1, float, float x0, float x1) {
+    a0 = a0 + x0;
+    a1 = a1 + x1;
+  }
+  __device__ static float finish(float a, float div) { return bf16_round(bf16_round(a) / div); }
 };
 
 // ---- 16-byte vector <-> E floats --------------------------------------------
@@ -140,16 +172,16 @@ __device__ __forceinline__ void unpack(const u32x4& r, float (&x)[Op::E]) {
 }
 
 template <class Op>
-__device__ __forceinline__ u32x4 pack(const float (&a)[Op::E]) {
+__device__ __forceinline__ u32x4 pack(const float (&a)[Op::E], float div) {
   u32x4 r;
   if constexpr (Op::kBytes == 4) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) r[e] = __float_as_uint(Op::finish(a[e]));
+    for (int e = 0; e < 4; ++e) r[e] = __float_as_uint(Op::finish(a[e], div));
   } else {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const uint32_t lo = __float_as_uint(Op::finish(a[2 * e])) >> 16;
-      const uint32_t hi = __float_as_uint(Op::finish(a[2 * e + 1])) & 0xffff0000u;
+      const uint32_t lo = __float_as_uint(Op::finish(a[2 * e], div)) >> 16;
+      const uint32_t hi = __float_as_uint(Op::finish(a[2 * e + 1], div)) & 0xffff0000u;
       r[e] = lo | hi;
     }
   }
@@ -167,11 +199,11 @@ __device__ __forceinline__ float load_elem(const void* p, size_t j) {
 }
 
 template <class Op>
-__device__ __forceinline__ void store_elem(void* p, size_t j, float a) {
+__device__ __forceinline__ void store_elem(void* p, size_t j, float a, float div) {
   if constexpr (Op::kBytes == 4) {
-    static_cast<float*>(p)[j] = Op::finish(a);
+    static_cast<float*>(p)[j] = Op::finish(a, div);
   } else {
-    static_cast<uint16_t*>(p)[j] = static_cast<uint16_t>(__float_as_uint(Op::finish(a)) >> 16);
+    static_cast<uint16_t*>(p)[j] = static_cast<uint16_t>(__float_as_uint(Op::finish(a, div)) >> 16);
   }
 }
 
@@ -231,25 +263,29 @@ template <int NB>
 struct Slots {
   const void* p[NB];
   float w[NB];
+  float div;  // final divisor of the mean policies (1 elsewhere / between passes)
+  __device__ const void* ptr(int i) const { return p[i]; }
+  __device__ float wt(int i) const { return w[i]; }
+  __device__ float divisor() const { return div; }
 };
 
 // Scalar fold of one element over all n inputs (tail / misaligned path).
-template <class Op, int NB>
-__device__ __forceinline__ void fold_scalar(const Slots<NB>& s, int n, const void* acc_in,
+template <class Op, class S>
+__device__ __forceinline__ void fold_scalar(const S& s, int n, const void* acc_in,
                                             void* out, size_t j) {
-  float a = acc_in ? load_elem<Op>(acc_in, j) : Op::init(load_elem<Op>(s.p[0], j));
+  float a = acc_in ? load_elem<Op>(acc_in, j) : Op::init(load_elem<Op>(s.ptr(0), j));
   int i = 0;
   // Loads of a chunk of 8 inputs are independent of the running sum; the
   // unrolled chunk lets them issue together.
   for (; i + 8 <= n; i += 8) {
     float x[8];
 #pragma unroll
-    for (int g = 0; g < 8; ++g) x[g] = load_elem<Op>(s.p[i + g], j);
+    for (int g = 0; g < 8; ++g) x[g] = load_elem<Op>(s.ptr(i + g), j);
 #pragma unroll
-    for (int g = 0; g < 8; ++g) a = Op::step(a, s.w[i + g], x[g]);
+    for (int g = 0; g < 8; ++g) a = Op::step(a, s.wt(i + g), x[g]);
   }
-  for (; i < n; ++i) a = Op::step(a, s.w[i], load_elem<Op>(s.p[i], j));
-  store_elem<Op>(out, j, a);
+  for (; i < n; ++i) a = Op::step(a, s.wt(i), load_elem<Op>(s.ptr(i), j));
+  store_elem<Op>(out, j, a, s.divisor());
 }
 
 // Scalar kernel: any alignment, one element per thread.
@@ -259,7 +295,7 @@ __global__ __launch_bounds__(kBlock) void k_wreduce_scalar(const Slots<NB> s, in
                                                            void* __restrict__ out,
                                                            size_t nelem) {
   const size_t j = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x;
-  if (j < nelem) fold_scalar<Op, NB>(s, n, acc_in, out, j);
+  if (j < nelem) fold_scalar<Op, Slots<NB>>(s, n, acc_in, out, j);
 }
 
 // ---- tiled kernel ------------------------------------------------------------
@@ -309,17 +345,17 @@ __device__ __forceinline__ void init_tile(float (&a)[VPT][Op::E], const u32x4 (&
   }
 }
 
-template <class Op, int NB, int NF, int G, int VPT, bool NT, bool CHECK, int STP>
-__device__ __forceinline__ void reduce_tile(const Slots<NB>& s, int n, const void* acc_in,
+template <class Op, class S, int NF, int G, int VPT, bool NT, bool CHECK, int STP>
+__device__ __forceinline__ void reduce_tile(const S& s, int n, const void* acc_in,
                                             const OutRef& out, size_t v0, size_t nvec) {
   float a[VPT][Op::E];
   if constexpr (NF > 0) {
     u32x4 r[NF][VPT];
 #pragma unroll
-    for (int i = 0; i < NF; ++i) load_tile<Op, VPT, NT, CHECK>(s.p[i], v0, nvec, r[i]);
+    for (int i = 0; i < NF; ++i) load_tile<Op, VPT, NT, CHECK>(s.ptr(i), v0, nvec, r[i]);
     init_tile<Op, VPT>(a, r[0], false);
 #pragma unroll
-    for (int i = 0; i < NF; ++i) fold_tile<Op, VPT>(a, s.w[i], r[i]);
+    for (int i = 0; i < NF; ++i) fold_tile<Op, VPT>(a, s.wt(i), r[i]);
   } else {
     // first group: acc (if continuing a previous pass) + up to G inputs
     {
@@ -329,28 +365,28 @@ __device__ __forceinline__ void reduce_tile(const Slots<NB>& s, int n, const voi
       if (acc_in) load_tile<Op, VPT, NT, CHECK>(acc_in, v0, nvec, racc);
 #pragma unroll
       for (int g = 0; g < G; ++g)
-        if (g < cnt) load_tile<Op, VPT, NT, CHECK>(s.p[g], v0, nvec, r[g]);
+        if (g < cnt) load_tile<Op, VPT, NT, CHECK>(s.ptr(g), v0, nvec, r[g]);
       if (acc_in) init_tile<Op, VPT>(a, racc, true);
       else init_tile<Op, VPT>(a, r[0], false);
 #pragma unroll
       for (int g = 0; g < G; ++g)
-        if (g < cnt) fold_tile<Op, VPT>(a, s.w[g], r[g]);
+        if (g < cnt) fold_tile<Op, VPT>(a, s.wt(g), r[g]);
     }
     for (int i0 = G; i0 < n; i0 += G) {
       u32x4 r[G][VPT];
       const int cnt = (n - i0) < G ? (n - i0) : G;
 #pragma unroll
       for (int g = 0; g < G; ++g)
-        if (g < cnt) load_tile<Op, VPT, NT, CHECK>(s.p[i0 + g], v0, nvec, r[g]);
+        if (g < cnt) load_tile<Op, VPT, NT, CHECK>(s.ptr(i0 + g), v0, nvec, r[g]);
 #pragma unroll
       for (int g = 0; g < G; ++g)
-        if (g < cnt) fold_tile<Op, VPT>(a, s.w[i0 + g], r[g]);
+        if (g < cnt) fold_tile<Op, VPT>(a, s.wt(i0 + g), r[g]);
     }
   }
 #pragma unroll
   for (int v = 0; v < VPT; ++v) {
     const size_t idx = v0 + static_cast<size_t>(v) * kBlock;
-    if (!CHECK || idx < nvec) store_vec<STP>(out, idx, pack<Op>(a[v]));
+    if (!CHECK || idx < nvec) store_vec<STP>(out, idx, pack<Op>(a[v], s.divisor()));
   }
 }
 
@@ -373,15 +409,68 @@ __global__ __launch_bounds__(kBlock) void k_wreduce_tiles(const Slots<NB> s, int
   const size_t nb = gridDim.x;
   if (blockIdx.x == 0) {
     if (full * kTile < nvec)
-      reduce_tile<Op, NB, NF, G, VPT, NT, true, STP>(s, n, acc_in, o, full * kTile + threadIdx.x, nvec);
+      reduce_tile<Op, Slots<NB>, NF, G, VPT, NT, true, STP>(s, n, acc_in, o, full * kTile + threadIdx.x, nvec);
     const size_t j = nvec * Op::E + threadIdx.x;
-    if (j < nelem) fold_scalar<Op, NB>(s, n, acc_in, out, j);
+    if (j < nelem) fold_scalar<Op, Slots<NB>>(s, n, acc_in, out, j);
     if (nb > 1) return;
   }
   const size_t workers = nb > 1 ? nb - 1 : 1;
   const size_t first = nb > 1 ? blockIdx.x - 1 : 0;
   for (size_t t = first; t < full; t += workers)
-    reduce_tile<Op, NB, NF, G, VPT, NT, false, STP>(s, n, acc_in, o, t * kTile + threadIdx.x, nvec);
+    reduce_tile<Op, Slots<NB>, NF, G, VPT, NT, false, STP>(s, n, acc_in, o, t * kTile + threadIdx.x, nvec);
+}
+
+// ---- batched launch: many independent aggregates in one grid -----------------
+// The aggregate tasks of one simulated round (every peer's neighbour mix) are
+// independent; small models (GNLeNet: 3 MB per task) are launch-bound when
+// each is its own kernel. One grid covers every task: task t owns blocks
+// [block_start[t], block_start[t+1]); its first block folds the task's ragged
+// end, the others one full tile each. Descriptors travel as kernel arguments
+// (read with scalar loads); the host splits larger batches.
+constexpr int kBatchMaxTasks = 32;
+constexpr int kBatchMaxPtrs = 192;
+
+struct BatchSlots {
+  const void* p[kBatchMaxPtrs];
+  float w[kBatchMaxPtrs];
+  void* out[kBatchMaxTasks];
+  size_t nvec[kBatchMaxTasks];
+  size_t nelem[kBatchMaxTasks];
+  uint32_t block_start[kBatchMaxTasks + 1];
+  uint16_t ptr_off[kBatchMaxTasks];
+  uint16_t fan_in[kBatchMaxTasks];
+  int ntasks;
+};
+
+// One task's view of the batch (same accessor interface as Slots).
+struct TaskArgs {
+  const BatchSlots& b;
+  int off;
+  __device__ const void* ptr(int i) const { return b.p[off + i]; }
+  __device__ float wt(int i) const { return b.w[off + i]; }
+  __device__ float divisor() const { return 1.0f; }
+};
+
+template <class Op, int NF, int G, int VPT, bool NT, int STP>
+__global__ __launch_bounds__(kBlock) void k_wreduce_batch(const BatchSlots s) {
+  const uint32_t bid = blockIdx.x;
+  int t = 0;
+  while (t + 1 < s.ntasks && bid >= s.block_start[t + 1]) ++t;  // wave-uniform scan
+  const TaskArgs a{s, s.ptr_off[t]};
+  const int n = NF > 0 ? NF : s.fan_in[t];
+  const size_t nvec = s.nvec[t];
+  constexpr size_t kTile = static_cast<size_t>(kBlock) * VPT;
+  const size_t full = nvec / kTile;
+  const OutRef o = make_out<STP>(s.out[t], nvec);
+  const uint32_t local = bid - s.block_start[t];
+  if (local == 0) {
+    if (full * kTile < nvec)
+      reduce_tile<Op, TaskArgs, NF, G, VPT, NT, true, STP>(a, n, nullptr, o, full * kTile + threadIdx.x, nvec);
+    const size_t j = nvec * Op::E + threadIdx.x;
+    if (j < s.nelem[t]) fold_scalar<Op, TaskArgs>(a, n, nullptr, s.out[t], j);
+    return;
+  }
+  reduce_tile<Op, TaskArgs, NF, G, VPT, NT, false, STP>(a, n, nullptr, o, (local - 1) * kTile + threadIdx.x, nvec);
 }
 
 // Copy probe: the achievable streaming ceiling on this device.

@@ -26,6 +26,8 @@ MAX_FUSED_INPUTS = 128
 EXPORTS = (
     "dlsim_wreduce",
     "dlsim_wreduce_tensors",
+    "dlsim_wreduce_batched",
+    "dlsim_mean",
     "dlsim_shard_range",
     "dlsim_probe_copy",
     "dlsim_last_error",
@@ -65,6 +67,12 @@ def load() -> ctypes.CDLL:
                                               ctypes.POINTER(ctypes.c_float), ctypes.POINTER(vp),
                                               i, i, vp]
         lib.dlsim_wreduce_tensors.restype = i
+        lib.dlsim_wreduce_batched.argtypes = [i, ctypes.POINTER(i), ctypes.POINTER(vp),
+                                              ctypes.POINTER(ctypes.c_float), ctypes.POINTER(vp),
+                                              ctypes.POINTER(sz), i, i, vp]
+        lib.dlsim_wreduce_batched.restype = i
+        lib.dlsim_mean.argtypes = [ctypes.POINTER(vp), i, vp, sz, i, vp]
+        lib.dlsim_mean.restype = i
         lib.dlsim_shard_range.argtypes = [sz, i, i, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)]
         lib.dlsim_shard_range.restype = i
         lib.dlsim_probe_copy.argtypes = [vp, vp, sz, vp]
@@ -156,6 +164,87 @@ class ReducePlan:
 def wreduce(inputs, weights_f32, out, mode: int = DLSIM_EXACT, stream=None):
     """out = sum_i w_i * inputs[i] on the device (flat tensors), stream-ordered."""
     ReducePlan(inputs, weights_f32, out, mode).launch(stream)
+    return out
+
+
+class BatchPlan:
+    """A prepared `dlsim_wreduce_batched` call (arrays built once)."""
+
+    def __init__(self, tasks, mode: int = DLSIM_EXACT):
+        self.b = len(tasks)
+        out0 = tasks[0][2]
+        self.device, self.mode, self.dtype = out0.device, mode, dtype_code(out0.dtype)
+        fan, ptrs, ws, outs, numels = [], [], [], [], []
+        for inputs, w32, out in tasks:
+            fan.append(len(inputs))
+            ptrs.extend(t.data_ptr() for t in inputs)
+            ws.extend(np.asarray(w32, dtype=np.float32).tolist())
+            outs.append(out.data_ptr())
+            numels.append(out.numel())
+        self._keep = tasks
+        self._fan = (ctypes.c_int * self.b)(*fan)
+        self._ptrs = (ctypes.c_void_p * len(ptrs))(*ptrs)
+        self._w = (ctypes.c_float * len(ws))(*ws)
+        self._outs = (ctypes.c_void_p * self.b)(*outs)
+        self._num = (ctypes.c_size_t * self.b)(*numels)
+        self._lib = load()
+
+    def launch(self, stream=None) -> None:
+        _check("dlsim_wreduce_batched",
+               self._lib.dlsim_wreduce_batched(self.b, self._fan, self._ptrs, self._w, self._outs,
+                                               self._num, self.dtype, self.mode,
+                                               _stream_handle(self.device, stream)))
+
+
+def wreduce_batched(tasks, mode: int = DLSIM_EXACT, stream=None):
+    """tasks: sequence of (inputs, weights_f32, out) — independent reduces,
+    launched together (dlsim_wreduce_batched). Returns the outs."""
+    lib = load()
+    b = len(tasks)
+    if b == 0:
+        return []
+    dt = dtype_code(tasks[0][2].dtype)
+    fan, ptrs, ws, outs, numels = [], [], [], [], []
+    for inputs, w32, out in tasks:
+        if len(inputs) < 1:
+            raise IndexError("list index out of range")
+        if len(w32) != len(inputs):
+            raise AssertionError("weights/models length mismatch")
+        for t in list(inputs) + [out]:
+            if not t.is_cuda or t.dtype != out.dtype or t.numel() != out.numel() or not t.is_contiguous():
+                raise ValueError("each task: contiguous device tensors of one dtype and size")
+        if out.dtype != tasks[0][2].dtype or out.device != tasks[0][2].device:
+            raise ValueError("all tasks of a batch share dtype and device")
+        fan.append(len(inputs))
+        ptrs.extend(t.data_ptr() for t in inputs)
+        ws.extend(np.asarray(w32, dtype=np.float32).tolist())
+        outs.append(out.data_ptr())
+        numels.append(out.numel())
+    c_fan = (ctypes.c_int * b)(*fan)
+    c_ptrs = (ctypes.c_void_p * len(ptrs))(*ptrs)
+    c_w = (ctypes.c_float * len(ws))(*ws)
+    c_outs = (ctypes.c_void_p * b)(*outs)
+    c_num = (ctypes.c_size_t * b)(*numels)
+    _check("dlsim_wreduce_batched",
+           lib.dlsim_wreduce_batched(b, c_fan, c_ptrs, c_w, c_outs, c_num, dt, mode,
+                                     _stream_handle(tasks[0][2].device, stream)))
+    return [t[2] for t in tasks]
+
+
+def mean(inputs, out, stream=None):
+    """out = (sum_i inputs[i]) / n on the device (flat tensors), stream-ordered:
+    torch.mean(torch.stack(inputs), 0) semantics (dlsim_mean)."""
+    lib = load()
+    n = len(inputs)
+    if n < 1:
+        raise IndexError("list index out of range")
+    dt = dtype_code(out.dtype)
+    for t in list(inputs) + [out]:
+        if not t.is_cuda or t.dtype != out.dtype or t.numel() != out.numel() or not t.is_contiguous():
+            raise ValueError("inputs and output must be contiguous device tensors of one dtype and size")
+    ptrs = (ctypes.c_void_p * n)(*[t.data_ptr() for t in inputs])
+    _check("dlsim_mean", lib.dlsim_mean(ptrs, n, out.data_ptr(), out.numel(), dt,
+                                        _stream_handle(out.device, stream)))
     return out
 
 

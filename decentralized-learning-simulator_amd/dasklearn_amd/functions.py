@@ -19,7 +19,25 @@ from dasklearn_amd.model_manager import ModelManager
 
 logger = logging.getLogger(__name__)
 
-__all__ = ["aggregate"]
+__all__ = ["aggregate", "chunk", "reconstruct_from_chunks"]
+
+# The reference builds the model to reconstruct into from its model zoo
+# (functions.py:144, dasklearn.models.create_model). Out of scope here, so it
+# is looked up lazily when the package runs inside the reference, and can be
+# replaced (tests do) by assigning `model_factory`.
+model_factory = None
+
+
+def _create_model(settings):
+    global model_factory
+    if model_factory is None:
+        try:
+            from dasklearn.models import create_model  # the reference's model zoo
+        except ImportError as exc:  # pragma: no cover - outside the reference
+            raise ImportError("reconstruct_from_chunks needs dasklearn.models.create_model "
+                              "or dasklearn_amd.functions.model_factory") from exc
+        model_factory = create_model
+    return model_factory(settings.dataset, architecture=settings.model)
 
 
 def aggregate(settings, params: Dict) -> List[nn.Module]:
@@ -40,3 +58,18 @@ def aggregate(settings, params: Dict) -> List[nn.Module]:
     agg_model = model_manager.aggregate_trained_models(weights)
     logger.debug("Model aggregation took %f s.", time.time() - start_time)
     return [agg_model]
+
+
+def chunk(settings, params: Dict) -> List:
+    """functions.py:136-140: split a model's flat state_dict into n chunks."""
+    from dasklearn_amd.chunk_manager import ChunkManager
+    return ChunkManager.chunk_model(params["model"], params["n"])
+
+
+def reconstruct_from_chunks(settings, params: Dict) -> List[nn.Module]:
+    """functions.py:142-146: average every chunk index over its contributors
+    (on the GPU) and load the result into a fresh model."""
+    from dasklearn_amd.chunk_manager import ChunkManager
+    model = _create_model(settings)
+    model = ChunkManager.reconstruct_model(params["chunks"], model)
+    return [model]

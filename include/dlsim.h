@@ -101,6 +101,40 @@ int dlsim_wreduce_tensors(const void* const* d_inputs, int n, int t,
                           void* stream);
 
 /*
+ * dlsim_wreduce_batched — b independent weighted reduces (e.g. the aggregate
+ * tasks of one simulated round, one per peer) in as few kernel launches as
+ * possible.
+ *
+ * Task t has fan_in[t] inputs: d_inputs[o_t .. o_t + fan_in[t]) with weights
+ * h_weights[o_t ..], o_t = fan_in[0] + ... + fan_in[t-1]; it writes
+ * n_elems[t] elements to d_outs[t]. Every task follows dlsim_wreduce's rules
+ * and rounding (results are bit-identical to b separate dlsim_wreduce calls).
+ * Replaces b separate `aggregate` tasks scheduled by the broker
+ * (broker.py:261-275 -> functions.py:89-106); up to 32 tasks / 192 inputs
+ * share one launch, tasks with fan-in > 16 run alone.
+ */
+int dlsim_wreduce_batched(int b, const int* fan_in, const void* const* d_inputs,
+                          const float* h_weights, void* const* d_outs, const size_t* n_elems,
+                          int dtype, int mode, void* stream);
+
+/*
+ * dlsim_mean — element-wise mean of n flat buffers (no weights).
+ *
+ *   d_out[j] = (0 + d_inputs[0][j] + ... + d_inputs[n-1][j]) / n
+ *
+ * Replaces `torch.mean(torch.stack(chunks_at_idx), dim=0)` of
+ * ChunkManager.reconstruct_model (simulation/conflux/chunk_manager.py:38-40),
+ * which PyTorch computes as a sum over dim 0 followed by div_(n): the sum is
+ * folded in input order from +0 and divided once (IEEE division). bf16: the
+ * fp32 sum is rounded to bf16, then divided and rounded again. Bit-identical
+ * to the reference while PyTorch's CPU dim-0 reduction is sequential (n <= 4);
+ * for larger n PyTorch's order depends on sizes and thread count, so parity
+ * is a tolerance. Same buffer and stream rules as dlsim_wreduce.
+ */
+int dlsim_mean(const void* const* d_inputs, int n, void* d_out, size_t n_elems, int dtype,
+               void* stream);
+
+/*
  * dlsim_shard_range — parameter-axis partition used by the sharded path.
  *
  * Splits [0, n_elems) into `world` contiguous slices whose boundaries are

@@ -111,3 +111,28 @@ int oracle_wreduce_fast_bf16(const uint16_t* const* in, int n, const float* w, u
   }
   return 0;
 }
+
+/* Mean of n rows, as PyTorch's CPU `torch.mean(torch.stack(xs), 0)` computes
+ * it while its dim-0 reduction is sequential (n <= 4): acc = +0, acc += x_i
+ * in order, then one IEEE division by n (sum followed by div_).
+ * Restates simulation/conflux/chunk_manager.py:38-40 for the chunked path.
+ * bf16: the fp32 sum is rounded to bf16, then divided and rounded again. */
+int oracle_mean_f32(const float* const* in, int n, float* out, size_t p) {
+  if (n < 1 || !in || !out) return -1;
+  for (size_t j = 0; j < p; ++j) {
+    float acc = 0.0f;
+    for (int i = 0; i < n; ++i) acc = acc + in[i][j];
+    out[j] = acc / (float)n;
+  }
+  return 0;
+}
+
+int oracle_mean_bf16(const uint16_t* const* in, int n, uint16_t* out, size_t p) {
+  if (n < 1 || !in || !out) return -1;
+  for (size_t j = 0; j < p; ++j) {
+    float acc = 0.0f;
+    for (int i = 0; i < n; ++i) acc = acc + oracle_bf16_to_f32(in[i][j]);
+    out[j] = oracle_f32_to_bf16(bf16r(acc) / (float)n);
+  }
+  return 0;
+}

@@ -47,6 +47,10 @@ def _load():
         fn = getattr(lib, name)
         fn.argtypes = [pp, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
         fn.restype = ctypes.c_int
+    for name in ("oracle_mean_f32", "oracle_mean_bf16"):
+        fn = getattr(lib, name)
+        fn.argtypes = [pp, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t]
+        fn.restype = ctypes.c_int
     lib.oracle_wreduce_f32_rows.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                                             ctypes.c_void_p, ctypes.c_size_t]
     lib.oracle_wreduce_f32_rows.restype = ctypes.c_int
@@ -102,6 +106,27 @@ def wreduce(xs, weights, dtype: str = "f32", mode: str = "exact") -> np.ndarray:
             out.ctypes.data, p)
     if rc != 0:
         raise RuntimeError(f"oracle failed rc={rc}")
+    return out
+
+
+def mean(xs, dtype: str = "f32") -> np.ndarray:
+    """Sequential mean (sum from +0, one division): torch.mean(torch.stack(xs), 0)
+    while PyTorch's dim-0 reduction is sequential (n <= 4)."""
+    lib = _load()
+    n = len(xs)
+    if n < 1:
+        raise IndexError("list index out of range")
+    if dtype == "f32":
+        rows, p = _as_rows(xs, np.float32)
+        out = np.empty(p, dtype=np.float32)
+        fn = lib.oracle_mean_f32
+    else:
+        rows, p = _as_rows(xs, np.uint16)
+        out = np.empty(p, dtype=np.uint16)
+        fn = lib.oracle_mean_bf16
+    ptrs = (ctypes.c_void_p * n)(*[r.ctypes.data for r in rows])
+    if fn(ctypes.cast(ptrs, ctypes.POINTER(ctypes.c_void_p)), n, out.ctypes.data, p) != 0:
+        raise RuntimeError("oracle mean failed")
     return out
 
 

@@ -91,6 +91,23 @@ def main():
         t = timed(lambda: fedavg_torch.aggregate_modules(cpu_models, None), a.reps, sync=False)
         res["cpu_ref_4t_ms"] = round(t * 1e3, 3)
         res["cpu_ref_4t_GBps"] = round(byts / t / 1e9, 2)
+        if n == 8:  # wire format vs the reference's pickle, one model's state_dict
+            import pickle
+            from dasklearn_amd import wire
+            sd = cpu_models[0].state_dict()
+            nbytes = P * 4
+            t = timed(lambda: pickle.dumps(sd), a.reps, sync=False)
+            blob = pickle.dumps(sd)
+            res["pickle_dumps_GBps"] = round(nbytes / t / 1e9, 2)
+            t = timed(lambda: pickle.loads(blob), a.reps, sync=False)
+            res["pickle_loads_GBps"] = round(nbytes / t / 1e9, 2)
+            t = timed(lambda: wire.encode_state_dict(sd), a.reps, sync=False)
+            buf = wire.encode_state_dict(sd)
+            res["dlsw_encode_GBps"] = round(nbytes / t / 1e9, 2)
+            t = timed(lambda: wire.decode_state_dict(buf), a.reps, sync=False)
+            res["dlsw_decode_host_GBps"] = round(nbytes / t / 1e9, 2)
+            t = timed(lambda: wire.decode_state_dict(buf, dev), a.reps)
+            res["dlsw_decode_device_GBps"] = round(nbytes / t / 1e9, 2)
         print(json.dumps(res), flush=True)
 
 

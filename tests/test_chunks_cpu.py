@@ -1,0 +1,85 @@
+"""Chunked-model path (Conflux/Shatter), CPU side: the oracle's sequential
+mean and the chunking data movement against fixtures produced by the
+reference's own ChunkManager (tests/golden/make_golden_chunks.py;
+dasklearn/simulation/conflux/chunk_manager.py:13-53)."""
+from __future__ import annotations
+
+import glob
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+from torch import nn
+
+from conftest import GOLDEN
+from oracle import oracle as orc
+from dasklearn_amd.chunk_manager import ChunkManager
+
+CHUNK_FIXTURES = sorted(glob.glob(os.path.join(GOLDEN, "chunks", "*.npz")))
+
+
+def load(path):
+    with np.load(path, allow_pickle=False) as z:
+        d = {k: z[k] for k in z.files}
+    d["meta"] = json.loads(str(d["meta"]))
+    return d
+
+
+class Net(nn.Module):
+    def __init__(self, shapes):
+        super().__init__()
+        self.ps = nn.ParameterList([nn.Parameter(torch.zeros(*s)) for s in shapes])
+
+
+def model_from_flat(shapes, flat):
+    m = Net(shapes)
+    off = 0
+    with torch.no_grad():
+        for p in m.parameters():
+            p.copy_(torch.from_numpy(flat[off:off + p.numel()].copy()).view_as(p))
+            off += p.numel()
+    return m
+
+
+@pytest.mark.parametrize("path", CHUNK_FIXTURES, ids=lambda p: os.path.basename(p)[:-4])
+def test_chunking_matches_reference(path):
+    d = load(path)
+    k, counts = d["meta"]["num_chunks"], d["meta"]["counts"]
+    for p in range(max(counts)):
+        chunks = ChunkManager.chunk_model(model_from_flat(d["meta"]["shapes"], d[f"flat_{p}"]), k)
+        assert len(chunks) == k
+        for c in range(k):
+            if p < counts[c]:
+                assert np.array_equal(chunks[c].numpy(), d[f"chunks_{c}"][p])
+
+
+@pytest.mark.parametrize("path", CHUNK_FIXTURES, ids=lambda p: os.path.basename(p)[:-4])
+def test_oracle_mean_vs_reference(path):
+    """Bit-exact where PyTorch's dim-0 sum is sequential (<= 4 contributors);
+    within m * 2^-23 of mean|x| otherwise."""
+    d = load(path)
+    k, counts = d["meta"]["num_chunks"], d["meta"]["counts"]
+    got = np.concatenate([orc.mean(list(d[f"chunks_{c}"])) for c in range(k)])
+    off = 0
+    for c in range(k):
+        L = d[f"chunks_{c}"].shape[1]
+        g, e = got[off:off + L], d["expected"][off:off + L]
+        if counts[c] <= 4:
+            assert orc.same_bits(g, e), (c, counts[c])
+        else:
+            scale = np.abs(d[f"chunks_{c}"]).mean(axis=0)
+            assert np.all(np.abs(g - e) <= counts[c] * 2.0 ** -23 * scale + 1e-30), (c, counts[c])
+        off += L
+
+
+def test_reconstruct_asserts_on_empty_chunk_index():
+    with pytest.raises(AssertionError, match="No chunks received at index 1"):
+        ChunkManager.reconstruct_model([[torch.zeros(3)], []], Net([[6]]))
+
+
+def test_chunk_remainder_goes_to_last_chunk():
+    m = Net([[10], [3]])
+    chunks = ChunkManager.chunk_model(m, 4)  # 13 = 3+3+3+4
+    assert [c.numel() for c in chunks] == [3, 3, 3, 4]

