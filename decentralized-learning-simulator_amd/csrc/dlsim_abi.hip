@@ -268,6 +268,113 @@ int run_batched(int b, const int* fan_in, const void* const* in, const float* w,
   return DLSIM_OK;
 }
 
+// ---- descriptor-table batches ---------------------------------------------------
+struct TableLayout {
+  size_t tasks_off, map_off, ptrs_off, w_off, bytes;
+  uint32_t nblocks;
+};
+
+size_t round8(size_t x) { return (x + 7) / 8 * 8; }
+
+template <class Op>
+uint32_t task_blocks(size_t nelem) {
+  const size_t tile = static_cast<size_t>(dlsim::kBlock) * kVpt;
+  return static_cast<uint32_t>(nelem / Op::E / tile + 1);
+}
+
+template <class Op>
+bool table_layout(int b, const int* fan_in, const size_t* nelem, TableLayout* L) {
+  uint64_t blocks = 0, ptrs = 0;
+  for (int t = 0; t < b; ++t) {
+    blocks += task_blocks<Op>(nelem[t]);
+    ptrs += static_cast<uint64_t>(fan_in[t]);
+  }
+  if (blocks >= 0x7fffffffull) return false;
+  L->nblocks = static_cast<uint32_t>(blocks);
+  L->tasks_off = round8(sizeof(dlsim::BatchTableHeader));
+  L->map_off = round8(L->tasks_off + sizeof(dlsim::BatchTaskDesc) * static_cast<size_t>(b));
+  L->ptrs_off = round8(L->map_off + sizeof(uint32_t) * static_cast<size_t>(blocks));
+  L->w_off = round8(L->ptrs_off + sizeof(void*) * static_cast<size_t>(ptrs));
+  L->bytes = round8(L->w_off + sizeof(float) * static_cast<size_t>(ptrs));
+  return true;
+}
+
+template <class Op>
+int table_fill(int b, const int* fan_in, const void* const* in, const float* w, void* const* outs,
+               const size_t* nelem, void* h_table, size_t bytes) {
+  TableLayout L;
+  if (!table_layout<Op>(b, fan_in, nelem, &L)) return fail(DLSIM_E_ARG, "batch too large");
+  if (bytes < L.bytes) return fail(DLSIM_E_ARG, "table buffer too small (%zu < %zu)", bytes, L.bytes);
+  unsigned char* base = static_cast<unsigned char*>(h_table);
+  std::memset(base, 0, L.bytes);
+  auto* h = reinterpret_cast<dlsim::BatchTableHeader*>(base);
+  auto* tasks = reinterpret_cast<dlsim::BatchTaskDesc*>(base + L.tasks_off);
+  auto* map = reinterpret_cast<uint32_t*>(base + L.map_off);
+  auto* ptrs = reinterpret_cast<const void**>(base + L.ptrs_off);
+  auto* ws = reinterpret_cast<float*>(base + L.w_off);
+  h->ntasks = static_cast<uint32_t>(b);
+  h->nblocks = L.nblocks;
+  h->tasks_off = L.tasks_off;
+  h->map_off = L.map_off;
+  h->ptrs_off = L.ptrs_off;
+  h->w_off = L.w_off;
+  uint32_t blk = 0, off = 0;
+  bool uniform = true;
+  for (int t = 0; t < b; ++t) {
+    const size_t total = nelem[t] * Op::kBytes;
+    if (fan_in[t] > DLSIM_MAX_FUSED_INPUTS || total > kMaxLaunchOutBytes || !aligned16(outs[t]))
+      return fail(DLSIM_E_ARG, "task %d cannot be table-batched (fan-in <= %d, 16-B aligned, < 2 GiB)", t,
+                  DLSIM_MAX_FUSED_INPUTS);
+    const uint32_t nb = task_blocks<Op>(nelem[t]);
+    tasks[t].out = outs[t];
+    tasks[t].nvec = nelem[t] / Op::E;
+    tasks[t].nelem = nelem[t];
+    tasks[t].block_start = blk;
+    tasks[t].ptr_off = off;
+    tasks[t].fan_in = static_cast<uint32_t>(fan_in[t]);
+    for (uint32_t k = 0; k < nb; ++k) map[blk + k] = static_cast<uint32_t>(t);
+    for (int i = 0; i < fan_in[t]; ++i) {
+      if (!aligned16(in[off + i]))
+        return fail(DLSIM_E_ARG, "task %d input %d is not 16-byte aligned", t, i);
+      ptrs[off + i] = in[off + i];
+      ws[off + i] = w[off + i];
+    }
+    blk += nb;
+    off += static_cast<uint32_t>(fan_in[t]);
+    uniform = uniform && fan_in[t] == fan_in[0];
+  }
+  h->uniform_fan_in = uniform ? static_cast<uint32_t>(fan_in[0]) : 0u;
+  return DLSIM_OK;
+}
+
+template <class Op, int NF>
+hipError_t launch_table_nf(const void* d_table, uint32_t blocks, hipStream_t st) {
+  hipLaunchKernelGGL((dlsim::k_wreduce_batch_table<Op, NF, group_size<Op>(), kVpt, kNT, kStore>),
+                     dim3(blocks), dim3(dlsim::kBlock), 0, st, static_cast<const unsigned char*>(d_table));
+  return hipGetLastError();
+}
+
+template <class Op, int K>
+hipError_t launch_table_fixed(const void* d_table, int n, uint32_t blocks, hipStream_t st) {
+  if constexpr (K > max_fixed_fan_in<Op>()) {
+    return launch_table_nf<Op, 0>(d_table, blocks, st);
+  } else {
+    if (n == K) return launch_table_nf<Op, K>(d_table, blocks, st);
+    return launch_table_fixed<Op, K + 1>(d_table, n, blocks, st);
+  }
+}
+
+template <class Op>
+int table_launch(const void* h_table, const void* d_table, hipStream_t st) {
+  const auto* h = static_cast<const dlsim::BatchTableHeader*>(h_table);
+  if (h->ntasks == 0) return DLSIM_OK;
+  hipError_t e = h->uniform_fan_in ? launch_table_fixed<Op, 1>(d_table, static_cast<int>(h->uniform_fan_in),
+                                                               h->nblocks, st)
+                                   : launch_table_nf<Op, 0>(d_table, h->nblocks, st);
+  if (e != hipSuccess) return hip_fail(e, "table batch launch");
+  return DLSIM_OK;
+}
+
 size_t elem_bytes(int dtype) { return dtype == DLSIM_BF16 ? 2 : 4; }
 
 int check_args(const void* const* in, int n, const float* w, const void* out, size_t nelem,
@@ -370,6 +477,51 @@ int dlsim_wreduce_batched(int b, const int* fan_in, const void* const* d_inputs,
   return mode == DLSIM_EXACT
              ? run_batched<dlsim::BF16Exact>(b, fan_in, d_inputs, h_weights, d_outs, n_elems, st)
              : run_batched<dlsim::BF16Fast>(b, fan_in, d_inputs, h_weights, d_outs, n_elems, st);
+}
+
+int dlsim_batch_table_bytes(int b, const int* fan_in, const size_t* n_elems, int dtype, size_t* bytes) {
+  g_err.clear();
+  if (b < 0 || (b > 0 && (!fan_in || !n_elems)) || !bytes) return fail(DLSIM_E_ARG, "bad arguments");
+  if (dtype != DLSIM_F32 && dtype != DLSIM_BF16) return fail(DLSIM_E_DTYPE, "unsupported dtype %d", dtype);
+  for (int t = 0; t < b; ++t)
+    if (fan_in[t] < 1) return fail(DLSIM_E_ARG, "task %d: fan-in must be >= 1", t);
+  TableLayout L;
+  const bool ok = dtype == DLSIM_F32 ? table_layout<dlsim::F32Exact>(b, fan_in, n_elems, &L)
+                                     : table_layout<dlsim::BF16Exact>(b, fan_in, n_elems, &L);
+  if (!ok) return fail(DLSIM_E_ARG, "batch too large");
+  *bytes = L.bytes;
+  return DLSIM_OK;
+}
+
+int dlsim_batch_table_fill(int b, const int* fan_in, const void* const* d_inputs, const float* h_weights,
+                           void* const* d_outs, const size_t* n_elems, int dtype, void* h_table,
+                           size_t table_bytes) {
+  g_err.clear();
+  if (b < 0 || !h_table) return fail(DLSIM_E_ARG, "bad arguments");
+  if (b > 0 && (!fan_in || !d_inputs || !h_weights || !d_outs || !n_elems))
+    return fail(DLSIM_E_ARG, "null array argument");
+  size_t off = 0;
+  for (int t = 0; t < b; ++t) {
+    int rc = check_args(d_inputs + off, fan_in[t], h_weights + off, d_outs[t], n_elems[t], dtype, DLSIM_EXACT);
+    if (rc != DLSIM_OK) return fail(rc, "task %d: %s", t, g_err.c_str());
+    off += static_cast<size_t>(fan_in[t]);
+  }
+  return dtype == DLSIM_F32
+             ? table_fill<dlsim::F32Exact>(b, fan_in, d_inputs, h_weights, d_outs, n_elems, h_table, table_bytes)
+             : table_fill<dlsim::BF16Exact>(b, fan_in, d_inputs, h_weights, d_outs, n_elems, h_table, table_bytes);
+}
+
+int dlsim_batch_table_launch(const void* h_table, const void* d_table, int dtype, int mode, void* stream) {
+  g_err.clear();
+  if (!h_table || !d_table) return fail(DLSIM_E_ARG, "null table");
+  if (dtype != DLSIM_F32 && dtype != DLSIM_BF16) return fail(DLSIM_E_DTYPE, "unsupported dtype %d", dtype);
+  if (mode != DLSIM_EXACT && mode != DLSIM_FAST) return fail(DLSIM_E_MODE, "unsupported mode %d", mode);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (dtype == DLSIM_F32)
+    return mode == DLSIM_EXACT ? table_launch<dlsim::F32Exact>(h_table, d_table, st)
+                               : table_launch<dlsim::F32Fast>(h_table, d_table, st);
+  return mode == DLSIM_EXACT ? table_launch<dlsim::BF16Exact>(h_table, d_table, st)
+                             : table_launch<dlsim::BF16Fast>(h_table, d_table, st);
 }
 
 int dlsim_mean(const void* const* d_inputs, int n, void* d_out, size_t n_elems, int dtype,

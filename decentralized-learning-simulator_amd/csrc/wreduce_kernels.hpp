@@ -473,6 +473,64 @@ __global__ __launch_bounds__(kBlock) void k_wreduce_batch(const BatchSlots s) {
   reduce_tile<Op, TaskArgs, NF, G, VPT, NT, false, STP>(a, n, nullptr, o, (local - 1) * kTile + threadIdx.x, nvec);
 }
 
+// ---- batched launch from a device descriptor table ----------------------------
+// Same work as k_wreduce_batch for any number of tasks: the descriptors live
+// in a device buffer the caller uploads (dlsim_batch_table_*), each block
+// finds its task with one read of a block -> task map (scalar loads, the
+// index is wave-uniform).
+struct BatchTableHeader {
+  uint32_t ntasks;
+  uint32_t nblocks;
+  uint32_t uniform_fan_in;  // fan-in shared by every task, or 0
+  uint32_t reserved;
+  uint64_t tasks_off;       // byte offsets from the table base
+  uint64_t map_off;
+  uint64_t ptrs_off;
+  uint64_t w_off;
+};
+
+struct BatchTaskDesc {
+  void* out;
+  uint64_t nvec;
+  uint64_t nelem;
+  uint32_t block_start;
+  uint32_t ptr_off;
+  uint32_t fan_in;
+  uint32_t reserved;
+};
+
+struct TableArgs {
+  const void* const* p;
+  const float* w;
+  __device__ const void* ptr(int i) const { return p[i]; }
+  __device__ float wt(int i) const { return w[i]; }
+  __device__ float divisor() const { return 1.0f; }
+};
+
+template <class Op, int NF, int G, int VPT, bool NT, int STP>
+__global__ __launch_bounds__(kBlock) void k_wreduce_batch_table(const unsigned char* __restrict__ table) {
+  const BatchTableHeader* h = reinterpret_cast<const BatchTableHeader*>(table);
+  const uint32_t* map = reinterpret_cast<const uint32_t*>(table + h->map_off);
+  const uint32_t t = map[blockIdx.x];
+  const BatchTaskDesc d = reinterpret_cast<const BatchTaskDesc*>(table + h->tasks_off)[t];
+  const TableArgs a{reinterpret_cast<const void* const*>(table + h->ptrs_off) + d.ptr_off,
+                    reinterpret_cast<const float*>(table + h->w_off) + d.ptr_off};
+  const int n = NF > 0 ? NF : static_cast<int>(d.fan_in);
+  const size_t nvec = d.nvec;
+  constexpr size_t kTile = static_cast<size_t>(kBlock) * VPT;
+  const size_t full = nvec / kTile;
+  const OutRef o = make_out<STP>(d.out, nvec);
+  const uint32_t local = blockIdx.x - d.block_start;
+  if (local == 0) {
+    if (full * kTile < nvec)
+      reduce_tile<Op, TableArgs, NF, G, VPT, NT, true, STP>(a, n, nullptr, o, full * kTile + threadIdx.x, nvec);
+    const size_t j = nvec * Op::E + threadIdx.x;
+    if (j < d.nelem) fold_scalar<Op, TableArgs>(a, n, nullptr, d.out, j);
+    return;
+  }
+  reduce_tile<Op, TableArgs, NF, G, VPT, NT, false, STP>(a, n, nullptr, o, (local - 1) * kTile + threadIdx.x, nvec);
+}
+
 // Copy probe: the achievable streaming ceiling on this device.
 template <int VPT>
 __global__ __launch_bounds__(kBlock) void k_copy16(const u32x4* __restrict__ src,

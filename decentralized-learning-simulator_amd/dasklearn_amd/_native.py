@@ -27,6 +27,9 @@ EXPORTS = (
     "dlsim_wreduce",
     "dlsim_wreduce_tensors",
     "dlsim_wreduce_batched",
+    "dlsim_batch_table_bytes",
+    "dlsim_batch_table_fill",
+    "dlsim_batch_table_launch",
     "dlsim_mean",
     "dlsim_shard_range",
     "dlsim_probe_copy",
@@ -71,6 +74,15 @@ def load() -> ctypes.CDLL:
                                               ctypes.POINTER(ctypes.c_float), ctypes.POINTER(vp),
                                               ctypes.POINTER(sz), i, i, vp]
         lib.dlsim_wreduce_batched.restype = i
+        lib.dlsim_batch_table_bytes.argtypes = [i, ctypes.POINTER(i), ctypes.POINTER(sz), i,
+                                                ctypes.POINTER(sz)]
+        lib.dlsim_batch_table_bytes.restype = i
+        lib.dlsim_batch_table_fill.argtypes = [i, ctypes.POINTER(i), ctypes.POINTER(vp),
+                                               ctypes.POINTER(ctypes.c_float), ctypes.POINTER(vp),
+                                               ctypes.POINTER(sz), i, vp, sz]
+        lib.dlsim_batch_table_fill.restype = i
+        lib.dlsim_batch_table_launch.argtypes = [vp, vp, i, i, vp]
+        lib.dlsim_batch_table_launch.restype = i
         lib.dlsim_mean.argtypes = [ctypes.POINTER(vp), i, vp, sz, i, vp]
         lib.dlsim_mean.restype = i
         lib.dlsim_shard_range.argtypes = [sz, i, i, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)]
@@ -168,32 +180,49 @@ def wreduce(inputs, weights_f32, out, mode: int = DLSIM_EXACT, stream=None):
 
 
 class BatchPlan:
-    """A prepared `dlsim_wreduce_batched` call (arrays built once)."""
+    """A prepared batch (one simulated round's aggregate tasks): the descriptor
+    table is built once on the host, uploaded once to a device buffer, and
+    every `launch()` is one kernel over all tasks (dlsim_batch_table_*)."""
 
     def __init__(self, tasks, mode: int = DLSIM_EXACT):
+        import torch
         self.b = len(tasks)
         out0 = tasks[0][2]
         self.device, self.mode, self.dtype = out0.device, mode, dtype_code(out0.dtype)
         fan, ptrs, ws, outs, numels = [], [], [], [], []
         for inputs, w32, out in tasks:
+            if len(w32) != len(inputs):
+                raise AssertionError("weights/models length mismatch")
+            for t in list(inputs) + [out]:
+                if not t.is_cuda or t.dtype != out0.dtype or t.numel() != out.numel() \
+                        or not t.is_contiguous() or t.device != self.device:
+                    raise ValueError("each task: contiguous device tensors of one dtype, size and device")
             fan.append(len(inputs))
             ptrs.extend(t.data_ptr() for t in inputs)
             ws.extend(np.asarray(w32, dtype=np.float32).tolist())
             outs.append(out.data_ptr())
             numels.append(out.numel())
+        lib = load()
+        c_fan = (ctypes.c_int * self.b)(*fan)
+        c_num = (ctypes.c_size_t * self.b)(*numels)
+        nbytes = ctypes.c_size_t(0)
+        _check("dlsim_batch_table_bytes",
+               lib.dlsim_batch_table_bytes(self.b, c_fan, c_num, self.dtype, ctypes.byref(nbytes)))
+        self._h = torch.empty(nbytes.value, dtype=torch.uint8, pin_memory=True)
+        _check("dlsim_batch_table_fill",
+               lib.dlsim_batch_table_fill(self.b, c_fan, (ctypes.c_void_p * len(ptrs))(*ptrs),
+                                          (ctypes.c_float * len(ws))(*ws),
+                                          (ctypes.c_void_p * self.b)(*outs), c_num, self.dtype,
+                                          self._h.data_ptr(), nbytes.value))
+        self._d = self._h.to(self.device, non_blocking=True)
+        torch.cuda.current_stream(self.device).synchronize()  # table resident before any stream uses it
         self._keep = tasks
-        self._fan = (ctypes.c_int * self.b)(*fan)
-        self._ptrs = (ctypes.c_void_p * len(ptrs))(*ptrs)
-        self._w = (ctypes.c_float * len(ws))(*ws)
-        self._outs = (ctypes.c_void_p * self.b)(*outs)
-        self._num = (ctypes.c_size_t * self.b)(*numels)
-        self._lib = load()
+        self._lib = lib
 
     def launch(self, stream=None) -> None:
-        _check("dlsim_wreduce_batched",
-               self._lib.dlsim_wreduce_batched(self.b, self._fan, self._ptrs, self._w, self._outs,
-                                               self._num, self.dtype, self.mode,
-                                               _stream_handle(self.device, stream)))
+        _check("dlsim_batch_table_launch",
+               self._lib.dlsim_batch_table_launch(self._h.data_ptr(), self._d.data_ptr(), self.dtype,
+                                                  self.mode, _stream_handle(self.device, stream)))
 
 
 def wreduce_batched(tasks, mode: int = DLSIM_EXACT, stream=None):

@@ -17,7 +17,10 @@ Layout ("DLSW", version 1):
     b"DLSW" | u32 version | u32 header_len | header (UTF-8 JSON) | pad to 64 B | payload
     header = {"entries": [{"name", "dtype", "shape", "offset", "nbytes"}...],
               "payload_bytes": N}
-Every entry's offset is 64-byte aligned within the payload.
+The payload starts 64-byte aligned; entries are packed densely at their
+natural alignment (the element size), so a parameters-only state_dict of one
+dtype decodes into exactly the flat arena the GPU aggregate reduces in one
+launch (dasklearn_amd/arena.py `arena_view`).
 """
 from __future__ import annotations
 
@@ -40,8 +43,8 @@ _DTYPES = {
 _NAMES = {v: k for k, v in _DTYPES.items()}
 
 
-def _round(x: int) -> int:
-    return (x + ALIGN - 1) // ALIGN * ALIGN
+def _round(x: int, a: int = ALIGN) -> int:
+    return (x + a - 1) // a * a
 
 
 def _layout(sd: Dict[str, torch.Tensor]):
@@ -49,11 +52,12 @@ def _layout(sd: Dict[str, torch.Tensor]):
     for name, t in sd.items():
         if t.dtype not in _NAMES:
             raise TypeError(f"{name}: unsupported dtype {t.dtype}")
+        off = _round(off, t.element_size())
         nbytes = t.numel() * t.element_size()
         entries.append({"name": name, "dtype": _NAMES[t.dtype], "shape": list(t.shape),
                         "offset": off, "nbytes": nbytes})
-        off = _round(off + nbytes)
-    return entries, off
+        off += nbytes
+    return entries, _round(off)
 
 
 def encode_state_dict(sd: Dict[str, torch.Tensor]) -> bytearray:

@@ -118,6 +118,31 @@ int dlsim_wreduce_batched(int b, const int* fan_in, const void* const* d_inputs,
                           int dtype, int mode, void* stream);
 
 /*
+ * Descriptor-table batches: any number of tasks per launch.
+ *
+ * The kernel-argument form above carries at most 32 tasks / 192 inputs per
+ * launch. For a whole round (hundreds of peers) the task descriptors go to a
+ * caller-owned device buffer instead:
+ *   dlsim_batch_table_bytes   size of the table for these tasks
+ *   dlsim_batch_table_fill    write it into caller host memory h_table
+ *                             (every task: fan-in <= 128, 16-B aligned
+ *                             buffers, output < 2 GiB; else DLSIM_E_ARG)
+ *   (caller copies h_table to d_table, e.g. hipMemcpyAsync on `stream`)
+ *   dlsim_batch_table_launch  one launch over every task; reads the grid size
+ *                             from h_table and the descriptors from d_table
+ * A filled table can be launched again as long as the buffers it names are
+ * alive (a prepared round; graph-capturable: no allocation, no sync).
+ * Results are bit-identical to separate dlsim_wreduce calls.
+ */
+int dlsim_batch_table_bytes(int b, const int* fan_in, const size_t* n_elems, int dtype,
+                            size_t* bytes);
+int dlsim_batch_table_fill(int b, const int* fan_in, const void* const* d_inputs,
+                           const float* h_weights, void* const* d_outs, const size_t* n_elems,
+                           int dtype, void* h_table, size_t table_bytes);
+int dlsim_batch_table_launch(const void* h_table, const void* d_table, int dtype, int mode,
+                             void* stream);
+
+/*
  * dlsim_mean — element-wise mean of n flat buffers (no weights).
  *
  *   d_out[j] = (0 + d_inputs[0][j] + ... + d_inputs[n-1][j]) / n

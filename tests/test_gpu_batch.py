@@ -94,3 +94,37 @@ def test_module_level_batch_matches_per_task():
 def _cpu(m):
     import copy
     return copy.deepcopy(m).cpu()
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_table_plan_whole_round(dtype):
+    """100 peers x fan-in 8 (one D-PSGD round of GNLeNet-sized tasks) in one
+    table launch, launched twice (the table is reusable)."""
+    rng = np.random.default_rng(7)
+    tasks = [make_task(rng, 8, 85_354, dtype) for _ in range(100)]
+    plan = _native.BatchPlan([(t[0], t[2], t[3]) for t in tasks])
+    for _ in range(2):
+        for t in tasks:
+            t[3].zero_()
+        plan.launch()
+        for ins, host, w, out in tasks:
+            got = out.cpu()
+            got = got.view(torch.int16).numpy().view(np.uint16) if dtype == "bf16" else got.numpy()
+            assert orc.same_bits(got, orc.wreduce(host, w, dtype))
+
+
+def test_table_plan_mixed_fan_in_up_to_128():
+    rng = np.random.default_rng(8)
+    tasks = [make_task(rng, n, p, "f32") for n, p in [(1, 7), (17, 3000), (40, 70_001), (128, 4097),
+                                                        (2, 1), (9, 100_000)]]
+    plan = _native.BatchPlan([(t[0], t[2], t[3]) for t in tasks], _native.DLSIM_EXACT)
+    plan.launch()
+    for ins, host, w, out in tasks:
+        assert orc.same_bits(out.cpu().numpy(), orc.wreduce(host, w, "f32"))
+
+
+def test_table_plan_rejects_misaligned_task():
+    rng = np.random.default_rng(9)
+    t = make_task(rng, 3, 1000, "f32", misalign=True)
+    with pytest.raises(_native.DlsimError):
+        _native.BatchPlan([(t[0], t[2], t[3])])

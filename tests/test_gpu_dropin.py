@@ -202,27 +202,24 @@ def test_host_result_is_pinned_and_stage_timing_works():
 
 
 def test_wire_decode_to_device_feeds_aggregate_without_packing():
-    """DLSW-decoded device state -> module whose parameters are one arena ->
-    the aggregate reads it in place (arena_view) and matches the oracle."""
+    """DLSW-decoded device state of a parameters-only model is one dense arena:
+    installed as the parameters, the aggregate reads it in place (arena_view,
+    one launch) and matches the oracle."""
     from dasklearn_amd import wire
     from dasklearn_amd.arena import ParamLayout
     torch.manual_seed(5)
-    models = [nn.Sequential(nn.Linear(33, 17), nn.Linear(17, 5)) for _ in range(3)]
+    make = lambda: nn.Sequential(nn.Linear(33, 17), nn.Linear(17, 5))  # noqa: E731
+    models = [make() for _ in range(3)]
     dev_models = []
     for m in models:
         sd = wire.decode_state_dict(wire.serialize_model(m), torch.device("cuda", 0))
-        shell = nn.Sequential(nn.Linear(33, 17), nn.Linear(17, 5))
-        for (name, _), mod_name in zip(shell.named_parameters(), sd):
-            pass
-        # install the decoded tensors as the parameters themselves (no copy)
-        with torch.no_grad():
-            for name, p in list(shell.named_parameters()):
-                mod, attr = name.rsplit(".", 1)
-                setattr(shell.get_submodule(mod), attr, nn.Parameter(sd[name]))
+        shell = make()
+        for name, _ in list(shell.named_parameters()):
+            mod, attr = name.rsplit(".", 1)
+            setattr(shell.get_submodule(mod), attr, nn.Parameter(sd[name]))
         dev_models.append(shell)
     lay = ParamLayout(dev_models[0])
-    # parameters-only state dict: contiguous in order with 64-B aligned gaps,
-    # so it is NOT one dense arena — the tensor-list path takes it
+    assert all(lay.arena_view(list(m.parameters()), torch.float32) is not None for m in dev_models)
     out = FedAvg.aggregate(dev_models, None)
     ref = fedavg_torch.aggregate_modules(models, None)
     assert orc.same_bits(flat_of(out), flat_of(ref))
