@@ -297,8 +297,15 @@ def main():
 
     allgather = None
     if world > 1:
-        shard = outs[0] if args.backend == "nccl" else outs[0].cpu()
-        full = torch.empty(p * world, dtype=tdt, device=shard.device)
+        # slices can differ by one 64-element unit under --strong: pad to the widest
+        width = p
+        if args.strong:
+            width = max(e - b for b, e in (_native.shard_range(p_cfg, world, r, 64) for r in range(world)))
+        shard = torch.zeros(width, dtype=tdt, device=dev)
+        shard[:p].copy_(outs[0])
+        if args.backend != "nccl":
+            shard = shard.cpu()
+        full = torch.empty(width * world, dtype=tdt, device=shard.device)
         for _ in range(3):
             dist.all_gather_into_tensor(full, shard)
         torch.cuda.synchronize(dev)
@@ -312,14 +319,15 @@ def main():
         agt = torch.tensor([ag_ms], dtype=torch.float64, device=cdev)
         dist.all_reduce(agt, op=dist.ReduceOp.MAX)
         allgather = {"ms": round(float(agt.item()), 4),
-                     "bytes_out_per_rank": p * esz * world,
+                     "bytes_out_per_rank": width * esz * world,
                      "note": ("RCCL" if args.backend == "nccl" else "gloo (rehearsal)")
                              + " all_gather_into_tensor of the reduced shards (not in value)"}
 
     result = None
     if rank == 0:
         achieved = bytes_per_launch / (kern_avg_ms * 1e-3) / 1e9
-        traffic = pmc_traffic(args.config, args.mode)
+        # PMC bytes were profiled for the plain single-task, per-rank-shard run
+        traffic = pmc_traffic(args.config, args.mode) if (B == 1 and not args.strong) else None
         result = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -334,7 +342,8 @@ def main():
             "dtype": dtype,
             "data": "synthetic: torch.randn*0.05 on device, 3 rotating input sets; "
                     f"{wkind} weights",
-            "config": {"workload": args.config + ": " + desc + (f" x {B} tasks per launch" if B > 1 else ""),
+            "config": {"workload": args.config + ": " + desc + (f" x {B} tasks per launch" if B > 1 else "")
+                       + (f" (strong scaling: {p_cfg} params split over {world} ranks)" if args.strong and world > 1 else ""),
                        "backend": args.backend if world > 1 else None,
                        "n_models": n, "params_per_rank": p, "tasks_per_step": B,
                        "mode": args.mode, "parallelism": f"param-shard x{world}",

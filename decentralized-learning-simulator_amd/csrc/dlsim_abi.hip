@@ -427,33 +427,29 @@ int dlsim_wreduce_tensors(const void* const* d_inputs, int n, int t, const size_
   if (t < 0) return fail(DLSIM_E_ARG, "t must be >= 0 (got %d)", t);
   if (t > 0 && (!d_inputs || !numels || !d_outs)) return fail(DLSIM_E_ARG, "null array argument");
   if (n < 1) return fail(DLSIM_E_ARG, "n must be >= 1 (got %d)", n);
-  const void* col[DLSIM_MAX_FUSED_INPUTS];
+  if (!h_weights) return fail(DLSIM_E_ARG, "null weights array");
+  // Tensor k of every model is one task of fan-in n; the T tasks run as a
+  // batch (a handful of launches instead of one per tensor).
+  std::vector<const void*> ins(static_cast<size_t>(n) * t);
+  std::vector<float> ws(static_cast<size_t>(n) * t);
+  std::vector<int> fan(static_cast<size_t>(t), n);
   for (int k = 0; k < t; ++k) {
-    // Gather tensor k of every model; n may exceed the stack column, so go
-    // in slices that continue the sum like the flat path's passes.
-    for (int i0 = 0; i0 < n; i0 += DLSIM_MAX_FUSED_INPUTS) {
-      const int cnt = std::min(DLSIM_MAX_FUSED_INPUTS, n - i0);
-      for (int i = 0; i < cnt; ++i) col[i] = d_inputs[static_cast<size_t>(i0 + i) * t + k];
-      int rc = check_args(col, cnt, h_weights + i0, d_outs[k], numels[k], dtype, mode);
-      if (rc != DLSIM_OK) return rc;
+    for (int i = 0; i < n; ++i) {
+      ins[static_cast<size_t>(k) * n + i] = d_inputs[static_cast<size_t>(i) * t + k];
+      ws[static_cast<size_t>(k) * n + i] = h_weights[i];
     }
+    int rc = check_args(&ins[static_cast<size_t>(k) * n], n, h_weights, d_outs[k], numels[k], dtype, mode);
+    if (rc != DLSIM_OK) return fail(rc, "tensor %d: %s", k, g_err.c_str());
   }
-  for (int k = 0; k < t; ++k) {
-    if (numels[k] == 0) continue;
-    if (n <= DLSIM_MAX_FUSED_INPUTS) {
-      for (int i = 0; i < n; ++i) col[i] = d_inputs[static_cast<size_t>(i) * t + k];
-      int rc = dispatch(col, n, h_weights, d_outs[k], numels[k], dtype, mode,
-                        static_cast<hipStream_t>(stream));
-      if (rc != DLSIM_OK) return rc;
-    } else {
-      std::vector<const void*> full(static_cast<size_t>(n));
-      for (int i = 0; i < n; ++i) full[i] = d_inputs[static_cast<size_t>(i) * t + k];
-      int rc = dispatch(full.data(), n, h_weights, d_outs[k], numels[k], dtype, mode,
-                        static_cast<hipStream_t>(stream));
-      if (rc != DLSIM_OK) return rc;
-    }
-  }
-  return DLSIM_OK;
+  if (t == 0) return DLSIM_OK;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (dtype == DLSIM_F32)
+    return mode == DLSIM_EXACT
+               ? run_batched<dlsim::F32Exact>(t, fan.data(), ins.data(), ws.data(), d_outs, numels, st)
+               : run_batched<dlsim::F32Fast>(t, fan.data(), ins.data(), ws.data(), d_outs, numels, st);
+  return mode == DLSIM_EXACT
+             ? run_batched<dlsim::BF16Exact>(t, fan.data(), ins.data(), ws.data(), d_outs, numels, st)
+             : run_batched<dlsim::BF16Fast>(t, fan.data(), ins.data(), ws.data(), d_outs, numels, st);
 }
 
 int dlsim_wreduce_batched(int b, const int* fan_in, const void* const* d_inputs,

@@ -84,7 +84,8 @@ int dlsim_wreduce(const void* const* d_inputs, int n, const float* h_weights,
 
 /*
  * dlsim_wreduce_tensors — the same reduce over T separate tensors per model,
- * in one launch, without packing them into an arena first.
+ * without packing them into an arena first: tensor k of every model is one
+ * task of a batch (dlsim_wreduce_batched), so T tensors take a few launches.
  *
  * Replaces the inner `zip(center_model.parameters(), m.parameters())` loop
  * (fedavg.py:24-25) when the models' parameters already live on the device
