@@ -48,6 +48,12 @@ constexpr bool kNT = true;
 // The buffer's 32-bit byte offsets cap one launch's output at 2 GiB; longer
 // outputs are split into independent launches over element ranges.
 constexpr int kStore = 16;  // sc1
+// Per element type (profiles/r01_tune_*): fp32 takes sc1 write-through stores
+// and the wave-contiguous lane map (each wave sweeps 4 KiB per stream, +1.3%
+// on the north star); bf16, whose output is a third of the traffic in the
+// 2-way merge, keeps non-temporal stores (+2% there) and the block map.
+template <class Op> constexpr int store_policy() { return Op::kBytes == 4 ? kStore : dlsim::kStNT; }
+template <class Op> constexpr bool wave_map() { return Op::kBytes == 4; }
 constexpr size_t kMaxLaunchOutBytes = (size_t{1} << 31) - (size_t{1} << 20);
 template <class Op> constexpr int max_fixed_fan_in() { return Op::kBytes == 4 ? 14 : 9; }
 template <class Op> constexpr int group_size() { return Op::kBytes == 4 ? 8 : 4; }
@@ -61,7 +67,8 @@ hipError_t launch_tiles(const dlsim::Slots<NB>& s, int n, const void* acc_in, vo
   const size_t tile = static_cast<size_t>(dlsim::kBlock) * kVpt;
   const size_t blocks = nvec / tile + 1;  // full tiles + one block for the ragged end
   if (blocks > 0x7fffffffu) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((dlsim::k_wreduce_tiles<Op, NB, NF, group_size<Op>(), kVpt, kNT, kStore>),
+  hipLaunchKernelGGL((dlsim::k_wreduce_tiles<Op, NB, NF, group_size<Op>(), kVpt, kNT, store_policy<Op>(),
+                                             wave_map<Op>()>),
                      dim3(static_cast<unsigned>(blocks)), dim3(dlsim::kBlock), 0, st, s, n, acc_in, out,
                      nvec, nelem);
   return hipGetLastError();
@@ -160,7 +167,7 @@ int run_range(const void* const* in, int n, const float* w, void* out, size_t ne
 // ---- batched launches ---------------------------------------------------------
 template <class Op, int NF>
 hipError_t launch_batch_nf(const dlsim::BatchSlots& s, unsigned blocks, hipStream_t st) {
-  hipLaunchKernelGGL((dlsim::k_wreduce_batch<Op, NF, group_size<Op>(), kVpt, kNT, kStore>), dim3(blocks),
+  hipLaunchKernelGGL((dlsim::k_wreduce_batch<Op, NF, group_size<Op>(), kVpt, kNT, store_policy<Op>()>), dim3(blocks),
                      dim3(dlsim::kBlock), 0, st, s);
   return hipGetLastError();
 }
@@ -349,7 +356,7 @@ int table_fill(int b, const int* fan_in, const void* const* in, const float* w, 
 
 template <class Op, int NF>
 hipError_t launch_table_nf(const void* d_table, uint32_t blocks, hipStream_t st) {
-  hipLaunchKernelGGL((dlsim::k_wreduce_batch_table<Op, NF, group_size<Op>(), kVpt, kNT, kStore>),
+  hipLaunchKernelGGL((dlsim::k_wreduce_batch_table<Op, NF, group_size<Op>(), kVpt, kNT, store_policy<Op>()>),
                      dim3(blocks), dim3(dlsim::kBlock), 0, st, static_cast<const unsigned char*>(d_table));
   return hipGetLastError();
 }

@@ -139,7 +139,7 @@ void launch_t(const Slots<128>& s, int n, void* out, size_t nvec, size_t nelem, 
                      st, s, n, nullptr, out, nvec, nelem);
 }
 
-template <class Op, int NF, int G, int VPT, bool NT, int NTS>
+template <class Op, int NF, int G, int VPT, int NT, int NTS, bool WM = false>
 void launch_ts(const Slots<128>& s, int n, void* out, size_t nvec, size_t nelem, hipStream_t st, int gm) {
   const size_t tile = (size_t)kBlock * VPT;
   const size_t full = nvec / tile;
@@ -149,7 +149,7 @@ void launch_ts(const Slots<128>& s, int n, void* out, size_t nvec, size_t nelem,
   size_t lds = 0;
   if (gm > 0) grid = std::min<size_t>(grid, (size_t)gm * 256);
   if (gm < 0) lds = (160 * 1024) / (size_t)(-gm) - 512;
-  hipLaunchKernelGGL((k_wreduce_tiles<Op, 128, NF, G, VPT, NT, NTS>), dim3((unsigned)grid), dim3(kBlock), lds,
+  hipLaunchKernelGGL((k_wreduce_tiles<Op, 128, NF, G, VPT, NT, NTS, WM>), dim3((unsigned)grid), dim3(kBlock), lds,
                      st, s, n, nullptr, out, nvec, nelem);
 }
 
@@ -184,6 +184,12 @@ void add_nf(std::vector<Variant>& vs, int n) {
   vs.push_back({p + "_V4_ntsc1", launch_ts<Op, NF, 8, 4, true, 18>, 0});
   vs.push_back({p + "_V4_bnt", launch_ts<Op, NF, 8, 4, true, 2>, 0});
   vs.push_back({p + "_V4_sc1_g8", launch_ts<Op, NF, 8, 4, true, 16>, 8});
+  vs.push_back({p + "_V4_sc1_wave", launch_ts<Op, NF, 8, 4, 1, 16, true>, 0});
+  vs.push_back({p + "_V4_sc1_bld", launch_ts<Op, NF, 8, 4, kLdBuffer + 0, 16>, 0});
+  vs.push_back({p + "_V4_sc1_bnt", launch_ts<Op, NF, 8, 4, kLdBuffer + 2, 16>, 0});
+  vs.push_back({p + "_V4_sc1_bsc1nt", launch_ts<Op, NF, 8, 4, kLdBuffer + 18, 16>, 0});
+  vs.push_back({p + "_V4_sc1_bsc01nt", launch_ts<Op, NF, 8, 4, kLdBuffer + 19, 16>, 0});
+  vs.push_back({p + "_V4_sc1_bsc1", launch_ts<Op, NF, 8, 4, kLdBuffer + 16, 16>, 0});
   vs.push_back({p + "_V4_sc1_occ1", launch_ts<Op, NF, 8, 4, true, 16>, -1});
   vs.push_back({p + "_V4_sc1_occ2", launch_ts<Op, NF, 8, 4, true, 16>, -2});
   vs.push_back({p + "_V2_sc1", launch_ts<Op, NF, 8, 2, true, 16>, 0});

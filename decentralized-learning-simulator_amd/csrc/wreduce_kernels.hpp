@@ -207,11 +207,24 @@ __device__ __forceinline__ void store_elem(void* p, size_t j, float a, float div
   }
 }
 
-template <bool NT>
+// Load policies: 0 = plain global_load, 1 = global_load ... nt; values
+// >= kLdBuffer are buffer_load_dwordx4 with cache-policy bits (LDP - kLdBuffer:
+// sc0 = 1, nt = 2, sc1 = 16). Buffer loads use 32-bit byte offsets: one launch
+// reads < 2 GiB per input (the host splits longer ranges).
+constexpr int kLdBuffer = 100;
+
+template <int LDP>
 __device__ __forceinline__ u32x4 ld16(const void* base, size_t v) {
-  const u32x4* p = static_cast<const u32x4*>(base) + v;
-  if constexpr (NT) return __builtin_nontemporal_load(p);
-  else return *p;
+  if constexpr (LDP >= kLdBuffer) {
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(v * 16), 0,
+                                                                           LDP - kLdBuffer));
+  } else {
+    const u32x4* p = static_cast<const u32x4*>(base) + v;
+    if constexpr (LDP == 1) return __builtin_nontemporal_load(p);
+    else return *p;
+  }
 }
 
 template <bool NT>
@@ -308,12 +321,12 @@ __global__ __launch_bounds__(kBlock) void k_wreduce_scalar(const Slots<NB> s, in
 // NF > 0: the fan-in n == NF is a compile-time constant (single pass, no
 // acc_in): every input's loads are issued back to back with no group
 // branches. NF == 0: runtime n in groups of G (first group peeled).
-template <class Op, int VPT, bool NT, bool CHECK>
+template <class Op, int VPT, int NT, bool CHECK, int VS = kBlock>
 __device__ __forceinline__ void load_tile(const void* src, size_t v0, size_t nvec,
                                           u32x4 (&r)[VPT]) {
 #pragma unroll
   for (int v = 0; v < VPT; ++v) {
-    const size_t idx = v0 + static_cast<size_t>(v) * kBlock;
+    const size_t idx = v0 + static_cast<size_t>(v) * VS;
     if constexpr (CHECK) {
       r[v] = u32x4{0u, 0u, 0u, 0u};
       if (idx < nvec) r[v] = ld16<NT>(src, idx);
@@ -345,14 +358,14 @@ __device__ __forceinline__ void init_tile(float (&a)[VPT][Op::E], const u32x4 (&
   }
 }
 
-template <class Op, class S, int NF, int G, int VPT, bool NT, bool CHECK, int STP>
+template <class Op, class S, int NF, int G, int VPT, int NT, bool CHECK, int STP, int VS = kBlock>
 __device__ __forceinline__ void reduce_tile(const S& s, int n, const void* acc_in,
                                             const OutRef& out, size_t v0, size_t nvec) {
   float a[VPT][Op::E];
   if constexpr (NF > 0) {
     u32x4 r[NF][VPT];
 #pragma unroll
-    for (int i = 0; i < NF; ++i) load_tile<Op, VPT, NT, CHECK>(s.ptr(i), v0, nvec, r[i]);
+    for (int i = 0; i < NF; ++i) load_tile<Op, VPT, NT, CHECK, VS>(s.ptr(i), v0, nvec, r[i]);
     init_tile<Op, VPT>(a, r[0], false);
 #pragma unroll
     for (int i = 0; i < NF; ++i) fold_tile<Op, VPT>(a, s.wt(i), r[i]);
@@ -362,10 +375,10 @@ __device__ __forceinline__ void reduce_tile(const S& s, int n, const void* acc_i
       u32x4 racc[VPT];
       u32x4 r[G][VPT];
       const int cnt = n < G ? n : G;
-      if (acc_in) load_tile<Op, VPT, NT, CHECK>(acc_in, v0, nvec, racc);
+      if (acc_in) load_tile<Op, VPT, NT, CHECK, VS>(acc_in, v0, nvec, racc);
 #pragma unroll
       for (int g = 0; g < G; ++g)
-        if (g < cnt) load_tile<Op, VPT, NT, CHECK>(s.ptr(g), v0, nvec, r[g]);
+        if (g < cnt) load_tile<Op, VPT, NT, CHECK, VS>(s.ptr(g), v0, nvec, r[g]);
       if (acc_in) init_tile<Op, VPT>(a, racc, true);
       else init_tile<Op, VPT>(a, r[0], false);
 #pragma unroll
@@ -377,7 +390,7 @@ __device__ __forceinline__ void reduce_tile(const S& s, int n, const void* acc_i
       const int cnt = (n - i0) < G ? (n - i0) : G;
 #pragma unroll
       for (int g = 0; g < G; ++g)
-        if (g < cnt) load_tile<Op, VPT, NT, CHECK>(s.ptr(i0 + g), v0, nvec, r[g]);
+        if (g < cnt) load_tile<Op, VPT, NT, CHECK, VS>(s.ptr(i0 + g), v0, nvec, r[g]);
 #pragma unroll
       for (int g = 0; g < G; ++g)
         if (g < cnt) fold_tile<Op, VPT>(a, s.wt(i0 + g), r[g]);
@@ -385,7 +398,7 @@ __device__ __forceinline__ void reduce_tile(const S& s, int n, const void* acc_i
   }
 #pragma unroll
   for (int v = 0; v < VPT; ++v) {
-    const size_t idx = v0 + static_cast<size_t>(v) * kBlock;
+    const size_t idx = v0 + static_cast<size_t>(v) * VS;
     if (!CHECK || idx < nvec) store_vec<STP>(out, idx, pack<Op>(a[v], s.divisor()));
   }
 }
@@ -398,7 +411,10 @@ __device__ __forceinline__ void reduce_tile(const S& s, int n, const void* acc_i
 // hides under the rest of the grid instead of trailing it; blocks 1.. take
 // the full tiles, one per block when the grid is full + 1 blocks, otherwise
 // grid-strided. A one-block grid does everything.
-template <class Op, int NB, int NF, int G, int VPT, bool NT, int STP = (NT ? kStNT : kStPlain)>
+// WAVEMAP: lane l of wave w reads vectors w*64*VPT + l + k*64 of a tile (each
+// wave sweeps VPT contiguous KiB per stream) instead of l' + k*kBlock.
+template <class Op, int NB, int NF, int G, int VPT, int NT, int STP = (NT ? kStNT : kStPlain),
+          bool WAVEMAP = false>
 __global__ __launch_bounds__(kBlock) void k_wreduce_tiles(const Slots<NB> s, int n,
                                                           const void* __restrict__ acc_in,
                                                           void* __restrict__ out, size_t nvec,
@@ -416,8 +432,14 @@ __global__ __launch_bounds__(kBlock) void k_wreduce_tiles(const Slots<NB> s, int
   }
   const size_t workers = nb > 1 ? nb - 1 : 1;
   const size_t first = nb > 1 ? blockIdx.x - 1 : 0;
-  for (size_t t = first; t < full; t += workers)
-    reduce_tile<Op, Slots<NB>, NF, G, VPT, NT, false, STP>(s, n, acc_in, o, t * kTile + threadIdx.x, nvec);
+  if constexpr (WAVEMAP) {
+    const size_t lane_off = (threadIdx.x >> 6) * 64 * VPT + (threadIdx.x & 63);
+    for (size_t t = first; t < full; t += workers)
+      reduce_tile<Op, Slots<NB>, NF, G, VPT, NT, false, STP, 64>(s, n, acc_in, o, t * kTile + lane_off, nvec);
+  } else {
+    for (size_t t = first; t < full; t += workers)
+      reduce_tile<Op, Slots<NB>, NF, G, VPT, NT, false, STP>(s, n, acc_in, o, t * kTile + threadIdx.x, nvec);
+  }
 }
 
 // ---- batched launch: many independent aggregates in one grid -----------------
@@ -451,7 +473,7 @@ struct TaskArgs {
   __device__ float divisor() const { return 1.0f; }
 };
 
-template <class Op, int NF, int G, int VPT, bool NT, int STP>
+template <class Op, int NF, int G, int VPT, int NT, int STP>
 __global__ __launch_bounds__(kBlock) void k_wreduce_batch(const BatchSlots s) {
   const uint32_t bid = blockIdx.x;
   int t = 0;
@@ -507,7 +529,7 @@ struct TableArgs {
   __device__ float divisor() const { return 1.0f; }
 };
 
-template <class Op, int NF, int G, int VPT, bool NT, int STP>
+template <class Op, int NF, int G, int VPT, int NT, int STP>
 __global__ __launch_bounds__(kBlock) void k_wreduce_batch_table(const unsigned char* __restrict__ table) {
   const BatchTableHeader* h = reinterpret_cast<const BatchTableHeader*>(table);
   const uint32_t* map = reinterpret_cast<const uint32_t*>(table + h->map_off);
