@@ -46,23 +46,29 @@ class ParamLayout:
             self.groups.setdefault(p.dtype, []).append(k)
         self.offsets: Dict[int, int] = {}
         self.totals: Dict[torch.dtype, int] = {}
+        self._group_offsets: Dict[torch.dtype, List[int]] = {}
         for dt, idx in self.groups.items():
             _native.dtype_code(dt)  # raises TypeError for unsupported dtypes
             off = 0
+            offs = []
             for k in idx:
                 self.offsets[k] = off
+                offs.append(off)
                 off += self.params[k].numel()
             self.totals[dt] = off
+            self._group_offsets[dt] = offs
+        self._signature = [(p.shape, p.dtype) for p in self.params]
 
     def check_compatible(self, module: nn.Module) -> List[nn.Parameter]:
         ps = list(module.parameters())
         # The reference zips parameters() (fedavg.py:24) and silently truncates
         # on a mismatch; equal shapes are what it assumes, so insist on them.
-        if len(ps) != len(self.params):
-            raise ValueError("models have different numbers of parameters")
-        for k, (a, b) in enumerate(zip(ps, self.params)):
-            if a.shape != b.shape or a.dtype != b.dtype:
-                raise ValueError(f"parameter {k}: shape/dtype differs from models[0]")
+        if [(p.shape, p.dtype) for p in ps] != self._signature:
+            if len(ps) != len(self.params):
+                raise ValueError("models have different numbers of parameters")
+            for k, (a, b) in enumerate(zip(ps, self.params)):
+                if a.shape != b.shape or a.dtype != b.dtype:
+                    raise ValueError(f"parameter {k}: shape/dtype differs from models[0]")
         return ps
 
     def arena_view(self, params: Sequence[torch.Tensor], dt: torch.dtype) -> Optional[torch.Tensor]:
@@ -70,17 +76,16 @@ class ParamLayout:
         (in layout order), return a flat view of it, else None."""
         idx = self.groups[dt]
         first = params[idx[0]]
-        if not first.is_contiguous():
-            return None
         base = first.data_ptr()
         esz = first.element_size()
+        if [params[k].data_ptr() - base for k in idx] != [o * esz for o in self._group_offsets[dt]]:
+            return None
+        # one storage (adjacent separate allocations are not an arena) and
+        # contiguous tensors (a transposed view could start at the right place)
         storage = first.untyped_storage().data_ptr()
-        for k in idx:
-            p = params[k]
-            if not p.is_contiguous() or p.untyped_storage().data_ptr() != storage:
-                return None
-            if p.data_ptr() != base + self.offsets[k] * esz:
-                return None
+        if any(params[k].untyped_storage().data_ptr() != storage or not params[k].is_contiguous()
+               for k in idx):
+            return None
         total = self.totals[dt]
         return torch.as_strided(first.detach(), (total,), (1,), first.storage_offset())
 

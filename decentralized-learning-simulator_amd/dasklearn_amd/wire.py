@@ -60,21 +60,29 @@ def _layout(sd: Dict[str, torch.Tensor]):
     return entries, _round(off)
 
 
-def encode_state_dict(sd: Dict[str, torch.Tensor]) -> bytearray:
-    """state_dict (host or device tensors) -> DLSW bytes."""
+def encode_state_dict(sd: Dict[str, torch.Tensor]):
+    """state_dict (host or device tensors) -> DLSW bytes, as a uint8 numpy
+    array (buffer protocol: send it, write it, or hand it to decode_state_dict).
+    The buffer is written once: no zero-fill, one copy per tensor."""
     entries, payload = _layout(sd)
     header = json.dumps({"entries": entries, "payload_bytes": payload}).encode()
     pre = MAGIC + struct.pack("<II", VERSION, len(header)) + header
     start = _round(len(pre))
-    buf = bytearray(start + payload)
-    buf[:len(pre)] = pre
-    body = torch.frombuffer(buf, dtype=torch.uint8, offset=start, count=payload) if payload else None
+    buf = torch.empty(start + payload, dtype=torch.uint8)
+    buf[:len(pre)].copy_(torch.frombuffer(bytearray(pre), dtype=torch.uint8))
+    buf[len(pre):start].zero_()
+    body = buf[start:]
+    end = 0
     for e, t in zip(entries, sd.values()):
+        if e["offset"] > end:
+            body[end:e["offset"]].zero_()  # alignment padding
+        end = e["offset"] + e["nbytes"]
         if e["nbytes"] == 0:
             continue
         src = t.detach().contiguous().reshape(-1).view(torch.uint8)
-        body[e["offset"]:e["offset"] + e["nbytes"]].copy_(src)  # D2H when t is on the GPU
-    return buf
+        body[e["offset"]:end].copy_(src)  # D2H when t is on the GPU
+    body[end:].zero_()
+    return buf.numpy()
 
 
 def _parse(buf):
@@ -107,7 +115,7 @@ def decode_state_dict(buf, device: Optional[torch.device] = None) -> "OrderedDic
     return out
 
 
-def serialize_model(model: torch.nn.Module) -> bytearray:
+def serialize_model(model: torch.nn.Module):
     """DLSW counterpart of the reference's serialize_model (models/__init__.py:9-10)."""
     return encode_state_dict(model.state_dict())
 

@@ -134,3 +134,56 @@ def test_dpsgd_replay_bit_identical(n, rounds):
         b = exp[f"agg_{p}_{rounds}"][0]
         assert all(not q.is_cuda for q in a.parameters())
         assert orc.same_bits(flat(a), flat(b)), (n, p)
+
+
+def oracle_reconstruct(settings, params):
+    """The reference's reconstruct arithmetic (chunk_manager.py:38-53) with
+    torch CPU ops: per chunk index torch.mean(torch.stack(...)), cat, copy."""
+    chunks = params["chunks"]
+    means = [torch.mean(torch.stack(list(cs)), dim=0) for cs in chunks]
+    flat = torch.cat(means)
+    model = Shaped(GNLENET)
+    off = 0
+    with torch.no_grad():
+        for t in model.state_dict().values():
+            t.copy_(flat[off:off + t.numel()].view(t.shape))
+            off += t.numel()
+    return [model]
+
+
+def test_conflux_style_chunk_replay_bit_identical():
+    """4 peers, k = 4 chunks: every peer chunks its trained model; chunk c of
+    peer p goes to peers p+1 and p+2; each peer reconstructs from its own and
+    the received chunks (3 contributors per index: PyTorch's mean is
+    sequential there, so the GPU path must match bit for bit)."""
+    ns = {}
+    exec("from dasklearn_amd.functions import *", ns)
+    n, k, rounds = 4, 4, 2
+    torch.manual_seed(11)
+    init = Shaped(GNLENET)
+    with torch.no_grad():
+        for p in init.parameters():
+            p.copy_(torch.randn(p.shape) * 0.05)
+
+    def run(reconstruct):
+        models = {p: init for p in range(n)}
+        for r in range(1, rounds + 1):
+            trained = {p: synthetic_train(Settings(), {"model": models[p], "round": r, "peer": p})[0]
+                       for p in range(n)}
+            chunked = {p: ns["chunk"](Settings(), {"model": trained[p], "n": k}) for p in range(n)}
+            for p in range(n):
+                got = [[chunked[p][c]] + [chunked[(p - d) % n][c] for d in (1, 2)] for c in range(k)]
+                models[p] = reconstruct(Settings(), {"chunks": got, "round": r, "peer": p})[0]
+        return models
+
+    import dasklearn_amd.functions as fn
+    old = fn.model_factory
+    fn.model_factory = lambda dataset, architecture=None: Shaped(GNLENET)
+    try:
+        Settings.dataset, Settings.model = "cifar10", "gnlenet"
+        got = run(ns["reconstruct_from_chunks"])
+    finally:
+        fn.model_factory = old
+    exp = run(oracle_reconstruct)
+    for p in range(n):
+        assert orc.same_bits(flat(got[p]), flat(exp[p])), p

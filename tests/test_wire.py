@@ -68,7 +68,7 @@ def test_rejects_foreign_buffers():
     with pytest.raises(ValueError):
         wire.decode_state_dict(bytearray(pickle.dumps({"a": 1})))
     buf = wire.serialize_model(nn.Linear(2, 2))
-    buf[4] = 9  # version
+    buf[4] = 9  # version (little-endian u32 at byte 4)
     with pytest.raises(ValueError):
         wire.decode_state_dict(buf)
 
@@ -76,3 +76,11 @@ def test_rejects_foreign_buffers():
 def test_unsupported_dtype():
     with pytest.raises(TypeError):
         wire.encode_state_dict({"c": torch.zeros(2, dtype=torch.complex64)})
+
+
+def test_encoded_bytes_are_deterministic():
+    torch.manual_seed(1)
+    m = WithBN()
+    a = bytes(wire.serialize_model(m))
+    b = bytes(wire.serialize_model(m))
+    assert a == b  # padding is zeroed, nothing uninitialised leaks
