@@ -165,44 +165,19 @@ void launch_l(const Slots<128>& s, int n, void* out, size_t nvec, size_t nelem, 
   hipLaunchKernelGGL((k_wreduce_lds<Op, NF, VPT, AUX>), dim3((unsigned)grid), dim3(kBlock), 0, st, s, out, full);
 }
 
+// Representative shapes (the full round-1 sweep is in profiles/r01_tune_*):
+// the shipped fp32 shape (wave map + sc1), the block map, nt stores, buffer
+// nt loads and the LDS-DMA experiment.
 template <class Op, int NF>
 void add_nf(std::vector<Variant>& vs, int n) {
   if (n != NF) return;
   const std::string p = "NF" + std::to_string(NF);
-  vs.push_back({p + "_V1", launch_t<Op, NF, 8, 1, true>, 0});
-  vs.push_back({p + "_V2", launch_t<Op, NF, 8, 2, true>, 0});
   vs.push_back({p + "_V4", launch_t<Op, NF, 8, 4, true>, 0});
-  vs.push_back({p + "_V2_g4", launch_t<Op, NF, 8, 2, true>, 4});
-  vs.push_back({p + "_V4_g2", launch_t<Op, NF, 8, 4, true>, 2});
-  vs.push_back({p + "_V4_g4", launch_t<Op, NF, 8, 4, true>, 4});
-  vs.push_back({p + "_V4_g8", launch_t<Op, NF, 8, 4, true>, 8});
-  vs.push_back({p + "_V2_plain", launch_t<Op, NF, 8, 2, false>, 0});
-  vs.push_back({p + "_V4_ps", launch_ts<Op, NF, 8, 4, true, kStPlain>, 0});
-  vs.push_back({p + "_V2_ps", launch_ts<Op, NF, 8, 2, true, kStPlain>, 0});
-  vs.push_back({p + "_V4_sc1", launch_ts<Op, NF, 8, 4, true, 16>, 0});
-  vs.push_back({p + "_V4_sc0sc1", launch_ts<Op, NF, 8, 4, true, 17>, 0});
-  vs.push_back({p + "_V4_ntsc1", launch_ts<Op, NF, 8, 4, true, 18>, 0});
-  vs.push_back({p + "_V4_bnt", launch_ts<Op, NF, 8, 4, true, 2>, 0});
-  vs.push_back({p + "_V4_sc1_g8", launch_ts<Op, NF, 8, 4, true, 16>, 8});
+  vs.push_back({p + "_V4_sc1", launch_ts<Op, NF, 8, 4, 1, 16>, 0});
   vs.push_back({p + "_V4_sc1_wave", launch_ts<Op, NF, 8, 4, 1, 16, true>, 0});
-  vs.push_back({p + "_V4_sc1_bld", launch_ts<Op, NF, 8, 4, kLdBuffer + 0, 16>, 0});
   vs.push_back({p + "_V4_sc1_bnt", launch_ts<Op, NF, 8, 4, kLdBuffer + 2, 16>, 0});
-  vs.push_back({p + "_V4_sc1_bsc1nt", launch_ts<Op, NF, 8, 4, kLdBuffer + 18, 16>, 0});
-  vs.push_back({p + "_V4_sc1_bsc01nt", launch_ts<Op, NF, 8, 4, kLdBuffer + 19, 16>, 0});
-  vs.push_back({p + "_V4_sc1_bsc1", launch_ts<Op, NF, 8, 4, kLdBuffer + 16, 16>, 0});
-  vs.push_back({p + "_V4_sc1_occ1", launch_ts<Op, NF, 8, 4, true, 16>, -1});
-  vs.push_back({p + "_V4_sc1_occ2", launch_ts<Op, NF, 8, 4, true, 16>, -2});
-  vs.push_back({p + "_V2_sc1", launch_ts<Op, NF, 8, 2, true, 16>, 0});
-  vs.push_back({p + "_V2_sc1_occ2", launch_ts<Op, NF, 8, 2, true, 16>, -2});
-  vs.push_back({p + "_V2_sc1_occ4", launch_ts<Op, NF, 8, 2, true, 16>, -4});
-  vs.push_back({p + "_V1_sc1", launch_ts<Op, NF, 8, 1, true, 16>, 0});
-  vs.push_back({p + "_V1_sc1_occ4", launch_ts<Op, NF, 8, 1, true, 16>, -4});
-  vs.push_back({p + "_G4V2", launch_t<Op, NF, 4, 2, true>, 0});
-  vs.push_back({p + "_lds_V1_nt", launch_l<Op, NF, 1, 2>, 0});
+  vs.push_back({p + "_V2_sc1", launch_ts<Op, NF, 8, 2, 1, 16>, 0});
   vs.push_back({p + "_lds_V2_nt", launch_l<Op, NF, 2, 2>, 0});
-  vs.push_back({p + "_lds_V2_def", launch_l<Op, NF, 2, 0>, 0});
-  vs.push_back({p + "_lds_V1_nt_g4", launch_l<Op, NF, 1, 2>, 4});
-  vs.push_back({p + "_lds_V2_nt_g2", launch_l<Op, NF, 2, 2>, 2});
 }
 
 template <class Op>
@@ -210,15 +185,7 @@ std::vector<Variant> variants(int n) {
   std::vector<Variant> vs = {
       {"T_G8_V2", launch_t<Op, 0, 8, 2, true>, 0},
       {"T_G8_V4", launch_t<Op, 0, 8, 4, true>, 0},
-      {"T_G8_V8", launch_t<Op, 0, 8, 8, true>, 0},
-      {"T_G8_V4_g2", launch_t<Op, 0, 8, 4, true>, 2},
-      {"T_G8_V4_g4", launch_t<Op, 0, 8, 4, true>, 4},
-      {"T_G8_V4_g8", launch_t<Op, 0, 8, 4, true>, 8},
-      {"T_G8_V2_g4", launch_t<Op, 0, 8, 2, true>, 4},
-      {"T_G4_V4", launch_t<Op, 0, 4, 4, true>, 0},
-      {"T_G16_V2", launch_t<Op, 0, 16, 2, true>, 0},
-      {"T_G8_V4_ps", launch_ts<Op, 0, 8, 4, true, kStPlain>, 0},
-      {"T_G8_V4_sc1", launch_ts<Op, 0, 8, 4, true, 16>, 0},
+      {"T_G8_V4_sc1", launch_ts<Op, 0, 8, 4, 1, 16>, 0},
   };
   add_nf<Op, 2>(vs, n);
   add_nf<Op, 8>(vs, n);
