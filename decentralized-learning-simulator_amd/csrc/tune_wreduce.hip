@@ -94,6 +94,21 @@ __global__ __launch_bounds__(kBlock) void k_wreduce_lds(const Slots<128> s, void
   }
 }
 
+// Block-size experiment: wave-contiguous map (stride 64 per vector) with
+// BLOCK threads per workgroup; tile = BLOCK * VPT vectors; block 0 takes the
+// ragged end (none for tile-multiple P) like the shipped kernel.
+template <class Op, int NF, int VPT, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_tiles_block(const Slots<128> s, int n, void* __restrict__ out,
+                                                       size_t nvec) {
+  constexpr size_t kT = static_cast<size_t>(BLOCK) * VPT;
+  const size_t full = nvec / kT;
+  const OutRef o = make_out<16>(out, nvec);
+  if (blockIdx.x == 0) return;  // tile-multiple sizes only in this experiment
+  const size_t t = blockIdx.x - 1;
+  if (t >= full) return;
+  const size_t lane_off = (threadIdx.x >> 6) * 64 * VPT + (threadIdx.x & 63);
+  reduce_tile<Op, Slots<128>, NF, 8, VPT, 1, false, 16, 64>(s, n, nullptr, o, t * kT + lane_off, nvec);
+}
 }  // namespace dlsim
 
 #define CK(x)                                                                          \
@@ -168,6 +183,13 @@ void launch_l(const Slots<128>& s, int n, void* out, size_t nvec, size_t nelem, 
 // Representative shapes (the full round-1 sweep is in profiles/r01_tune_*):
 // the shipped fp32 shape (wave map + sc1), the block map, nt stores, buffer
 // nt loads and the LDS-DMA experiment.
+template <class Op, int NF, int VPT, int BLOCK>
+void launch_b(const Slots<128>& s, int n, void* out, size_t nvec, size_t, hipStream_t st, int) {
+  const size_t full = nvec / ((size_t)BLOCK * VPT);
+  hipLaunchKernelGGL((k_tiles_block<Op, NF, VPT, BLOCK>), dim3((unsigned)(full + 1)), dim3(BLOCK), 0, st, s, n,
+                     out, nvec);
+}
+
 template <class Op, int NF>
 void add_nf(std::vector<Variant>& vs, int n) {
   if (n != NF) return;
@@ -178,6 +200,12 @@ void add_nf(std::vector<Variant>& vs, int n) {
   vs.push_back({p + "_V4_sc1_bnt", launch_ts<Op, NF, 8, 4, kLdBuffer + 2, 16>, 0});
   vs.push_back({p + "_V2_sc1", launch_ts<Op, NF, 8, 2, 1, 16>, 0});
   vs.push_back({p + "_lds_V2_nt", launch_l<Op, NF, 2, 2>, 0});
+  vs.push_back({p + "_B128_V4", launch_b<Op, NF, 4, 128>, 0});
+  vs.push_back({p + "_B256_V4", launch_b<Op, NF, 4, 256>, 0});
+  vs.push_back({p + "_B512_V4", launch_b<Op, NF, 4, 512>, 0});
+  vs.push_back({p + "_B1024_V4", launch_b<Op, NF, 4, 1024>, 0});
+  vs.push_back({p + "_B512_V2", launch_b<Op, NF, 2, 512>, 0});
+  vs.push_back({p + "_B64_V4", launch_b<Op, NF, 4, 64>, 0});
 }
 
 template <class Op>

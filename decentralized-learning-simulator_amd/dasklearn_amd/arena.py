@@ -281,3 +281,21 @@ def aggregate_modules(models: List[nn.Module], weights: Optional[Sequence[float]
     out = module_from_arenas(model0, layout, arenas)
     st.mark("module")
     return out
+
+
+def to_device_arena(model: nn.Module, device=None) -> nn.Module:
+    """A copy of `model` (deepcopy semantics) whose parameters are views of one
+    device arena per dtype — the form the aggregate reads in place. A plain
+    copy (not a 1-way reduce: x*0 + 1*x is not the identity for inf/NaN)."""
+    layout = ParamLayout(model)
+    dev = _target_device(layout.params, device)
+    arenas = {}
+    with torch.no_grad():
+        for dt, idx in layout.groups.items():
+            flat = torch.empty(layout.totals[dt], dtype=dt, device=dev)
+            for k in idx:
+                off = layout.offsets[k]
+                p = layout.params[k]
+                flat[off:off + p.numel()].copy_(p.detach().reshape(-1), non_blocking=True)
+            arenas[dt] = flat
+    return module_from_arenas(model, layout, arenas)
