@@ -129,48 +129,69 @@ def pmc_traffic(config: str, mode: str):
     return best
 
 
+def _host_threads() -> int:
+    """Host cores this process may use: the affinity set, capped by
+    OMP_NUM_THREADS (the GPU box sets it to the job's CPU share)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(omp))) if omp and omp.isdigit() else n
+
+
 def cpu_baseline(config, n, p, dtype, weights, budget_s):
     """The reference's aggregate as it runs in the simulator's worker: the
     op-for-op PyTorch-CPU restatement of FedAvg.aggregate (oracle/, validated
     bit-identical to the reference) on N host modules with the workload's real
     parameter layout (ResNet-18: 62 tensors), including the deepcopy of
-    models[0], at the worker's 4 threads (broker.py:31, session_settings.py:52)."""
+    models[0], at the worker's 4 threads (broker.py:31, session_settings.py:52).
+    A second, shorter sample at every host core this job may use goes under
+    "all_cores" (SURVEY.md §8d asks for both)."""
     from torch import nn
     from oracle import fedavg_torch
+    tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
+    shapes = LAYOUTS[config]() if config in LAYOUTS else [(p,)]
+    assert sum(int(torch.Size(sh).numel()) for sh in shapes) == p
+
+    class Shaped(nn.Module):
+        def __init__(self, seed):
+            super().__init__()
+            g = torch.Generator().manual_seed(seed)
+            self.ps = nn.ParameterList(
+                [nn.Parameter((torch.randn(sh, generator=g) * 0.05).to(tdt)) for sh in shapes])
+
+    models = [Shaped(1234 + i) for i in range(n)]
+    bytes_ = (n + 1) * p * (2 if dtype == "bf16" else 4)
+
+    def timed(threads, budget):
+        prev = torch.get_num_threads()
+        torch.set_num_threads(threads)
+        try:
+            fedavg_torch.aggregate_modules(models, weights)  # warm
+            reps, t0 = 0, time.perf_counter()
+            while True:
+                fedavg_torch.aggregate_modules(models, weights)
+                reps += 1
+                el = time.perf_counter() - t0
+                if el >= budget or reps >= 2000:
+                    return reps, el
+        finally:
+            torch.set_num_threads(prev)
+
     threads = 4
-    prev = torch.get_num_threads()
-    torch.set_num_threads(threads)
-    try:
-        tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
-        shapes = LAYOUTS[config]() if config in LAYOUTS else [(p,)]
-        assert sum(int(torch.Size(sh).numel()) for sh in shapes) == p
-
-        class Shaped(nn.Module):
-            def __init__(self, seed):
-                super().__init__()
-                g = torch.Generator().manual_seed(seed)
-                self.ps = nn.ParameterList(
-                    [nn.Parameter((torch.randn(sh, generator=g) * 0.05).to(tdt)) for sh in shapes])
-
-        models = [Shaped(1234 + i) for i in range(n)]
-        fedavg_torch.aggregate_modules(models, weights)  # warm
-        reps, t0 = 0, time.perf_counter()
-        while True:
-            fedavg_torch.aggregate_modules(models, weights)
-            reps += 1
-            el = time.perf_counter() - t0
-            if el >= budget_s or reps >= 2000:
-                break
-        per = el / reps
-        bytes_ = (n + 1) * p * (2 if dtype == "bf16" else 4)
-        layout = f"{len(shapes)} parameter tensors" if len(shapes) > 1 else "one flat parameter"
-        return {"value": round(bytes_ / per / 1e9, 3), "unit": "GB/s", "cores": threads,
-                "kind": "port",
-                "ms_per_step": round(per * 1e3, 3),
-                "sample": f"{reps} x FedAvg.aggregate of {n} host modules ({layout}, {p} {dtype} params) "
-                          f"in {el:.1f} s: the reference's torch CPU op sequence at {threads} threads"}
-    finally:
-        torch.set_num_threads(prev)
+    reps, el = timed(threads, budget_s)
+    per = el / reps
+    layout = f"{len(shapes)} parameter tensors" if len(shapes) > 1 else "one flat parameter"
+    out = {"value": round(bytes_ / per / 1e9, 3), "unit": "GB/s", "cores": threads,
+           "kind": "port",
+           "ms_per_step": round(per * 1e3, 3),
+           "sample": f"{reps} x FedAvg.aggregate of {n} host modules ({layout}, {p} {dtype} params) "
+                     f"in {el:.1f} s: the reference's torch CPU op sequence at {threads} threads"}
+    all_t = _host_threads()
+    if all_t != threads:
+        reps2, el2 = timed(all_t, budget_s / 2)
+        out["all_cores"] = {"value": round(bytes_ * reps2 / el2 / 1e9, 3), "unit": "GB/s", "cores": all_t,
+                            "ms_per_step": round(el2 / reps2 * 1e3, 3),
+                            "sample": f"{reps2} x the same aggregate in {el2:.1f} s at {all_t} threads"}
+    return out
 
 
 def main():

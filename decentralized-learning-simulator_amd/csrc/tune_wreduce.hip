@@ -228,7 +228,22 @@ int run(int n, size_t P, int reps, double peak_gbs) {
   const size_t nvec = P / Op::E;
   std::vector<void*> in((size_t)sets * n);
   std::vector<void*> out(sets);
-  for (auto& p : in) CK(hipMalloc(&p, bytes + 256));
+  // Input layout experiment: DLSIM_TUNE_STAGGER unset = one hipMalloc per
+  // input; set to S (bytes, multiple of 256) = all inputs rows of one arena,
+  // row stride = bytes rounded up to 256 B, plus S more per row (S = 0 is the
+  // bench's (n, p_pad) layout).
+  const char* stg = getenv("DLSIM_TUNE_STAGGER");
+  void* arena = nullptr;
+  if (stg) {
+    const size_t stagger = strtoull(stg, nullptr, 10) & ~(size_t)255;
+    const size_t stride = ((bytes + 255) & ~(size_t)255) + stagger;
+    CK(hipMalloc(&arena, stride * in.size() + 256));
+    for (size_t k = 0; k < in.size(); ++k) in[k] = (char*)arena + k * stride;
+    printf("layout=arena stride=%zu stagger=%zu\n", stride, stagger);
+  } else {
+    for (auto& p : in) CK(hipMalloc(&p, bytes + 256));
+    printf("layout=separate\n");
+  }
   for (auto& p : out) CK(hipMalloc(&p, bytes + 256));
   for (size_t k = 0; k < in.size(); ++k)
     hipLaunchKernelGGL(k_fill, dim3(2048), dim3(256), 0, 0, (uint32_t*)in[k], bytes / 4,
@@ -249,6 +264,17 @@ int run(int n, size_t P, int reps, double peak_gbs) {
   const double alg_bytes = (double)(n + 1) * bytes;
 
   auto vs = variants<Op>(n);
+  if (const char* only = getenv("DLSIM_TUNE_ONLY")) {  // comma-separated exact names
+    const std::string keep = std::string(",") + only + ",";
+    std::vector<Variant> sel;
+    for (auto& v : vs)
+      if (keep.find("," + v.name + ",") != std::string::npos) sel.push_back(v);
+    if (sel.size() < 2) {
+      fprintf(stderr, "DLSIM_TUNE_ONLY must keep at least 2 variants\n");
+      return 1;
+    }
+    vs = sel;
+  }
   // reference output of the first (shipped-like) variant on set 0
   std::vector<char> ref(bytes), got(bytes);
   vs[1].launch(slots[0], n, out[0], nvec, P, st, vs[1].gm);
@@ -331,7 +357,9 @@ int run(int n, size_t P, int reps, double peak_gbs) {
     CK(hipFree(a));
     CK(hipFree(b));
   }
-  for (auto& p : in) CK(hipFree(p));
+  if (arena) CK(hipFree(arena));
+  else
+    for (auto& p : in) CK(hipFree(p));
   for (auto& p : out) CK(hipFree(p));
   return 0;
 }
