@@ -237,8 +237,10 @@ def main():
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     arenas = []
     # rows padded to 256 B so every model's arena starts 16-byte aligned
-    # (the vector kernel's requirement; unaligned rows would take the scalar path)
-    p_pad = (p + 63) // 64 * 64
+    # (the vector kernel's requirement; unaligned rows would take the scalar
+    # path), at the staging arena's stride (4 KiB more at power-of-two strides)
+    from dasklearn_amd.arena import row_stride
+    p_pad = row_stride(p, esz)
     for s in range(sets):
         x = torch.empty((n, p_pad), dtype=tdt, device=dev)
         for i in range(n):

@@ -286,18 +286,20 @@ struct Slots {
 template <class Op, class S>
 __device__ __forceinline__ void fold_scalar(const S& s, int n, const void* acc_in,
                                             void* out, size_t j) {
-  float a = acc_in ? load_elem<Op>(acc_in, j) : Op::init(load_elem<Op>(s.ptr(0), j));
-  int i = 0;
-  // Loads of a chunk of 8 inputs are independent of the running sum; the
-  // unrolled chunk lets them issue together.
-  for (; i + 8 <= n; i += 8) {
+  // Every load of a chunk of 8 inputs (and the pass accumulator) issues
+  // before its first use: one HBM round trip per chunk, not one per input.
+  // The first input doubles as the x0*0 seed (n >= 1).
+  const float acc0 = acc_in ? load_elem<Op>(acc_in, j) : 0.0f;
+  float a = 0.0f;
+  for (int i = 0; i < n; i += 8) {
     float x[8];
 #pragma unroll
-    for (int g = 0; g < 8; ++g) x[g] = load_elem<Op>(s.ptr(i + g), j);
+    for (int g = 0; g < 8; ++g) x[g] = (i + g < n) ? load_elem<Op>(s.ptr(i + g), j) : 0.0f;
+    if (i == 0) a = acc_in ? acc0 : Op::init(x[0]);
 #pragma unroll
-    for (int g = 0; g < 8; ++g) a = Op::step(a, s.wt(i + g), x[g]);
+    for (int g = 0; g < 8; ++g)
+      if (i + g < n) a = Op::step(a, s.wt(i + g), x[g]);
   }
-  for (; i < n; ++i) a = Op::step(a, s.wt(i), load_elem<Op>(s.ptr(i), j));
   store_elem<Op>(out, j, a, s.divisor());
 }
 
@@ -406,11 +408,12 @@ __device__ __forceinline__ void reduce_tile(const S& s, int n, const void* acc_i
 // STP: output store policy (above). Buffer-store policies need the output's
 // vector part to be < 2 GiB (32-bit byte offsets); the host checks.
 //
-// Block 0 — dispatched first — folds the ragged end (the last partial tile
-// and the < E scalar tail, two dependent HBM round trips), so that latency
-// hides under the rest of the grid instead of trailing it; blocks 1.. take
-// the full tiles, one per block when the grid is full + 1 blocks, otherwise
-// grid-strided. A one-block grid does everything.
+// Block 0 — dispatched first — folds the ragged end (the last partial tile,
+// then the < E scalar tail), so that latency hides under the rest of the
+// grid instead of trailing it; blocks 1.. take the full tiles, one per block
+// when the grid is full + 1 blocks, otherwise grid-strided. A one-block grid
+// does everything. (Splitting the two ragged parts over blocks 0 and 1 was
+// measured and did not pay: profiles/r01_tune_ragged.log.)
 // WAVEMAP: lane l of wave w reads vectors w*64*VPT + l + k*64 of a tile (each
 // wave sweeps VPT contiguous KiB per stream) instead of l' + k*kBlock.
 template <class Op, int NB, int NF, int G, int VPT, int NT, int STP = (NT ? kStNT : kStPlain),

@@ -240,8 +240,9 @@ def wreduce_batched(tasks, mode: int = DLSIM_EXACT, stream=None):
         if len(w32) != len(inputs):
             raise AssertionError("weights/models length mismatch")
         for t in list(inputs) + [out]:
-            if not t.is_cuda or t.dtype != out.dtype or t.numel() != out.numel() or not t.is_contiguous():
-                raise ValueError("each task: contiguous device tensors of one dtype and size")
+            if not t.is_cuda or t.dtype != out.dtype or t.numel() != out.numel() or not t.is_contiguous() \
+                    or t.device != out.device:
+                raise ValueError("each task: contiguous device tensors of one dtype, size and device")
         if out.dtype != tasks[0][2].dtype or out.device != tasks[0][2].device:
             raise ValueError("all tasks of a batch share dtype and device")
         fan.append(len(inputs))
@@ -269,8 +270,10 @@ def mean(inputs, out, stream=None):
         raise IndexError("list index out of range")
     dt = dtype_code(out.dtype)
     for t in list(inputs) + [out]:
-        if not t.is_cuda or t.dtype != out.dtype or t.numel() != out.numel() or not t.is_contiguous():
-            raise ValueError("inputs and output must be contiguous device tensors of one dtype and size")
+        if not t.is_cuda or t.dtype != out.dtype or t.numel() != out.numel() or not t.is_contiguous() \
+                or t.device != out.device:
+            raise ValueError("inputs and output must be contiguous tensors of one dtype and size "
+                             "on one device")
     ptrs = (ctypes.c_void_p * n)(*[t.data_ptr() for t in inputs])
     _check("dlsim_mean", lib.dlsim_mean(ptrs, n, out.data_ptr(), out.numel(), dt,
                                         _stream_handle(out.device, stream)))
@@ -291,7 +294,8 @@ def wreduce_tensors(inputs_by_model, weights_f32, outs, mode: int = DLSIM_EXACT,
             raise ValueError("every model must have the same number of tensors")
         for k, x in enumerate(row):
             if not x.is_cuda or not x.is_contiguous() or x.dtype != outs[k].dtype \
-                    or x.numel() != outs[k].numel():
+                    or x.numel() != outs[k].numel() or x.device != outs[k].device \
+                    or outs[k].device != outs[0].device:
                 raise ValueError(f"tensor {k}: device/contiguity/dtype/size mismatch")
             flat.append(x.data_ptr())
     ptrs = (ctypes.c_void_p * len(flat))(*flat)

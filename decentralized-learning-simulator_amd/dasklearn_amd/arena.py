@@ -90,6 +90,22 @@ class ParamLayout:
         return torch.as_strided(first.detach(), (total,), (1,), first.storage_offset())
 
 
+def row_stride(numel: int, elem_bytes: int) -> int:
+    """Elements between consecutive model rows of a staging arena: `numel`
+    rounded up to 256 B (every row 16-byte aligned for the vector kernel),
+    plus 4 KiB when that leaves a stride that is a multiple of 64 KiB. Rows
+    at power-of-two strides contend for the same HBM channels: 8 x 8 M fp32
+    rows run at 0.75 of peak at a 32 MiB stride and 0.80 with 4 KiB added
+    (profiles/r01_tune_pow2.log); other strides are left alone (the 11 M
+    ResNet-18 rows measured the same with any stagger,
+    profiles/r01_tune_layout.log)."""
+    per256 = 256 // elem_bytes
+    padded = (numel + per256 - 1) // per256 * per256
+    if (padded * elem_bytes) % 65536 == 0:
+        padded += 4096 // elem_bytes
+    return padded
+
+
 class _Staging:
     """Reusable device/pinned buffers keyed by (device, dtype, n, numel)."""
 
@@ -113,17 +129,17 @@ class _Staging:
         ev.record(stream)
         self.last_use[(str(device), dt, n, numel)] = ev
 
-    # Rows are padded to 256 B so each model's arena starts 16-byte aligned
-    # (the vector kernel's requirement); callers use rows[i, :numel].
+    # Rows start 16-byte aligned (the vector kernel's requirement) at an HBM
+    # friendly stride (row_stride); callers use rows[i, :numel].
     @staticmethod
-    def _padded(numel):
-        return (numel + 127) // 128 * 128
+    def _padded(numel, dt):
+        return row_stride(numel, torch.empty((), dtype=dt).element_size())
 
     def device_rows(self, device, dt, n, numel) -> torch.Tensor:
         key = (str(device), dt, n, numel)
         buf = self.dev.get(key)
         if buf is None:
-            buf = torch.empty((n, self._padded(numel)), dtype=dt, device=device)[:, :numel]
+            buf = torch.empty((n, self._padded(numel, dt)), dtype=dt, device=device)[:, :numel]
             self.dev[key] = buf
         return buf
 
@@ -131,7 +147,7 @@ class _Staging:
         key = (dt, n, numel)
         buf = self.host.get(key)
         if buf is None:
-            buf = torch.empty((n, self._padded(numel)), dtype=dt, pin_memory=True)[:, :numel]
+            buf = torch.empty((n, self._padded(numel, dt)), dtype=dt, pin_memory=True)[:, :numel]
             self.host[key] = buf
         return buf
 

@@ -121,3 +121,18 @@ def test_task_function_is_star_exported():
     ns = {}
     exec("from dasklearn_amd.functions import *", ns)
     assert ns["aggregate"] is functions.aggregate
+
+
+@pytest.mark.parametrize("numel,esz,expect", [
+    (11_181_642, 4, 11_181_696),        # ResNet-18 fp32: 256 B padding only
+    (125_000_000, 2, 125_000_064),      # cfg4 bf16: 256 B padding, not a 64 KiB multiple
+    (1 << 20, 4, (1 << 20) + 1024),     # 4 MiB stride -> +4 KiB
+    (1 << 23, 2, (1 << 23) + 2048),
+    (85_354, 4, 85_376),
+    (1, 4, 64),
+])
+def test_staging_row_stride(numel, esz, expect):
+    s = arena.row_stride(numel, esz)
+    assert s == expect
+    assert (s * esz) % 256 == 0 and s >= numel
+    assert (s * esz) % 65536 != 0
