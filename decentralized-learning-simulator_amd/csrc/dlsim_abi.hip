@@ -52,26 +52,59 @@ constexpr int kStore = 16;  // sc1
 // and the wave-contiguous lane map (each wave sweeps 4 KiB per stream, +1.3%
 // on the north star); bf16, whose output is a third of the traffic in the
 // 2-way merge, keeps non-temporal stores (+2% there) and the block map.
+// These are the policies of the grouped (runtime fan-in) kernel and of the
+// batched kernels.
 template <class Op> constexpr int store_policy() { return Op::kBytes == 4 ? kStore : dlsim::kStNT; }
 template <class Op> constexpr bool wave_map() { return Op::kBytes == 4; }
 constexpr size_t kMaxLaunchOutBytes = (size_t{1} << 31) - (size_t{1} << 20);
 template <class Op> constexpr int max_fixed_fan_in() { return Op::kBytes == 4 ? 14 : 9; }
 template <class Op> constexpr int group_size() { return Op::kBytes == 4 ? 8 : 4; }
 
+// Launch shape of the fixed fan-in kernels, chosen by the per-stream size
+// (size sweep: profiles/r01_tune_shape_sweep.log, arena rows as in bench.py):
+//   fp32  < 5 M elements   : block map, sc1 stores   (1-4% over the wave map at 1-4 M)
+//   fp32 >= 5 M            : wave map,  sc1 stores   (~1% at 6-11 M)
+//   bf16  < 48 M elements  : VPT 1, wave map, sc1    (+7-12% at 4-33 M for n = 2)
+//   bf16 >= 48 M           : VPT 4, block map, nt    (+1.5-2.5% at 64-125 M)
+struct Shape {
+  int vpt;
+  int store;
+  bool wave;
+};
+template <class Op, bool Small> constexpr Shape fixed_shape() {
+  if constexpr (Op::kBytes == 4) return Small ? Shape{4, kStore, false} : Shape{4, kStore, true};
+  else return Small ? Shape{1, kStore, true} : Shape{4, dlsim::kStNT, false};
+}
+template <class Op> constexpr size_t small_shape_below() { return Op::kBytes == 4 ? 5000000 : 48000000; }
+
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+template <class Op, int NB, int NF, int VPT, int STP, bool WAVE>
+hipError_t launch_shape(const dlsim::Slots<NB>& s, int n, const void* acc_in, void* out, size_t nelem,
+                        hipStream_t st) {
+  const size_t nvec = nelem / Op::E;
+  const size_t tile = static_cast<size_t>(dlsim::kBlock) * VPT;
+  const size_t blocks = nvec / tile + 1;  // full tiles + one block for the ragged end
+  if (blocks > 0x7fffffffu) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((dlsim::k_wreduce_tiles<Op, NB, NF, group_size<Op>(), VPT, kNT, STP, WAVE>),
+                     dim3(static_cast<unsigned>(blocks)), dim3(dlsim::kBlock), 0, st, s, n, acc_in, out,
+                     nvec, nelem);
+  return hipGetLastError();
+}
 
 template <class Op, int NB, int NF>
 hipError_t launch_tiles(const dlsim::Slots<NB>& s, int n, const void* acc_in, void* out, size_t nelem,
                         hipStream_t st) {
-  const size_t nvec = nelem / Op::E;
-  const size_t tile = static_cast<size_t>(dlsim::kBlock) * kVpt;
-  const size_t blocks = nvec / tile + 1;  // full tiles + one block for the ragged end
-  if (blocks > 0x7fffffffu) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((dlsim::k_wreduce_tiles<Op, NB, NF, group_size<Op>(), kVpt, kNT, store_policy<Op>(),
-                                             wave_map<Op>()>),
-                     dim3(static_cast<unsigned>(blocks)), dim3(dlsim::kBlock), 0, st, s, n, acc_in, out,
-                     nvec, nelem);
-  return hipGetLastError();
+  if constexpr (NF > 0) {
+    if (nelem < small_shape_below<Op>()) {
+      constexpr Shape k = fixed_shape<Op, true>();
+      return launch_shape<Op, NB, NF, k.vpt, k.store, k.wave>(s, n, acc_in, out, nelem, st);
+    }
+    constexpr Shape k = fixed_shape<Op, false>();
+    return launch_shape<Op, NB, NF, k.vpt, k.store, k.wave>(s, n, acc_in, out, nelem, st);
+  } else {
+    return launch_shape<Op, NB, 0, kVpt, store_policy<Op>(), wave_map<Op>()>(s, n, acc_in, out, nelem, st);
+  }
 }
 
 template <class Op, int K>

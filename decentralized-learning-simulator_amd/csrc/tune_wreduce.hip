@@ -109,6 +109,23 @@ __global__ __launch_bounds__(BLOCK) void k_tiles_block(const Slots<128> s, int n
   const size_t lane_off = (threadIdx.x >> 6) * 64 * VPT + (threadIdx.x & 63);
   reduce_tile<Op, Slots<128>, NF, 8, VPT, 1, false, 16, 64>(s, n, nullptr, o, t * kT + lane_off, nvec);
 }
+
+// XCD-aware tile map experiment: workgroups are dispatched round-robin over
+// the 8 XCDs, so block k+1 runs on XCD (k+1) % 8; this map gives each XCD one
+// contiguous 1/8 of the tiles (its own L2 / TLB footprint) instead of every
+// 8th tile. Tile-multiple sizes only; grid = 8 * per + 1.
+template <class Op, int NF, int VPT>
+__global__ __launch_bounds__(kBlock) void k_tiles_xcd(const Slots<128> s, int n, void* __restrict__ out,
+                                                      size_t nvec, size_t per) {
+  constexpr size_t kT = static_cast<size_t>(kBlock) * VPT;
+  const OutRef o = make_out<16>(out, nvec);
+  if (blockIdx.x == 0) return;
+  const size_t k = blockIdx.x - 1;
+  const size_t t = (k & 7) * per + (k >> 3);
+  if (t >= nvec / kT) return;
+  const size_t lane_off = (threadIdx.x >> 6) * 64 * VPT + (threadIdx.x & 63);
+  reduce_tile<Op, Slots<128>, NF, 8, VPT, 1, false, 16, 64>(s, n, nullptr, o, t * kT + lane_off, nvec);
+}
 }  // namespace dlsim
 
 #define CK(x)                                                                          \
@@ -190,6 +207,14 @@ void launch_b(const Slots<128>& s, int n, void* out, size_t nvec, size_t, hipStr
                      out, nvec);
 }
 
+template <class Op, int NF, int VPT>
+void launch_x(const Slots<128>& s, int n, void* out, size_t nvec, size_t, hipStream_t st, int) {
+  const size_t full = nvec / ((size_t)kBlock * VPT);
+  const size_t per = (full + 7) / 8;
+  hipLaunchKernelGGL((k_tiles_xcd<Op, NF, VPT>), dim3((unsigned)(8 * per + 1)), dim3(kBlock), 0, st, s, n, out,
+                     nvec, per);
+}
+
 template <class Op, int NF>
 void add_nf(std::vector<Variant>& vs, int n) {
   if (n != NF) return;
@@ -206,6 +231,10 @@ void add_nf(std::vector<Variant>& vs, int n) {
   vs.push_back({p + "_B1024_V4", launch_b<Op, NF, 4, 1024>, 0});
   vs.push_back({p + "_B512_V2", launch_b<Op, NF, 2, 512>, 0});
   vs.push_back({p + "_B64_V4", launch_b<Op, NF, 4, 64>, 0});
+  vs.push_back({p + "_V2_sc1_wave", launch_ts<Op, NF, 8, 2, 1, 16, true>, 0});
+  vs.push_back({p + "_V1_sc1_wave", launch_ts<Op, NF, 8, 1, 1, 16, true>, 0});
+  vs.push_back({p + "_xcd_V4", launch_x<Op, NF, 4>, 0});
+  vs.push_back({p + "_xcd_V2", launch_x<Op, NF, 2>, 0});
 }
 
 template <class Op>

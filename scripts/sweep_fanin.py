@@ -29,7 +29,7 @@ def run_case(n, p, dtype, mode, reps, dev):
     outs = [torch.empty(p, dtype=tdt, device=dev) for _ in range(sets)]
     w = _native.fp32_weights(np.random.default_rng(n).dirichlet(np.ones(n)))
     plans = [_native.ReducePlan([xs[s][i, :p] for i in range(n)], w, outs[s], mode) for s in range(sets)]
-    for k in range(6):
+    for k in range(20):
         plans[k % sets].launch()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
@@ -48,7 +48,7 @@ def run_case(n, p, dtype, mode, reps, dev):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--p", type=int, default=11_181_642)
-    ap.add_argument("--reps", type=int, default=30)
+    ap.add_argument("--reps", type=int, default=100)
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     ns = list(range(1, 21)) + [24, 33, 64, 100, 128, 129]

@@ -227,6 +227,24 @@ def test_cfg4_2way_125M_bf16_properties():
     assert orc.same_bits(from_dev(out[idx]), orc.wreduce(rows, w, "bf16"))
 
 
+@pytest.mark.parametrize("dtype,p", [("f32", 4_999_997), ("f32", 5_000_003),
+                                     ("bf16", 47_999_993), ("bf16", 48_000_007)])
+@pytest.mark.parametrize("n", [2, 8])
+def test_launch_shapes_either_side_of_the_size_switch(dtype, p, n):
+    """The fixed fan-in kernels change launch shape by size (dlsim_abi.hip
+    fixed_shape: fp32 block/wave map at 5 M elements, bf16 VPT 1 sc1 / VPT 4 nt
+    at 48 M): both shapes bit-exact against the oracle over every element."""
+    g = torch.Generator(device=dev()).manual_seed(p + n)
+    tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
+    xs = [(torch.randn(p, generator=g, device=dev()) * 0.05).to(tdt) for _ in range(n)]
+    w = orc.reference_weights(n, list(np.random.default_rng(n).dirichlet(np.ones(n))))
+    out = torch.empty_like(xs[0])
+    _native.wreduce(xs, w, out)
+    assert orc.same_bits(from_dev(out), orc.wreduce([from_dev(x) for x in xs], w, dtype))
+    del xs, out
+    torch.cuda.empty_cache()
+
+
 def test_one_hot_weights_select_input_at_full_size():
     """Linearity/selection property at the north-star size: weights e_k return
     model k exactly (x0*0 + ... + 1*xk + ... sums exact zeros)."""

@@ -1,0 +1,82 @@
+"""The sharded path on the real backend: a world-1 "nccl" (= RCCL) process
+group on the GPU box's one MI355X, with the HIP kernel as the local reduce.
+
+World 1 is the most RCCL allows on one device (it rejects two ranks on the
+same GPU); the multi-rank collective logic is covered by
+tests/test_sharded_gloo.py and the 8-GPU run belongs to the driver. What this
+adds: every collective the sharded entry points issue (all-gather,
+all-to-all, reduce-scatter, the size all-reduce) runs through RCCL on device
+tensors, and the results match the C oracle (exact paths bit for bit)."""
+from __future__ import annotations
+
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+@pytest.fixture(scope="module")
+def rccl_world1():
+    assert torch.cuda.is_available()
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    yield
+    dist.destroy_process_group()
+
+
+def _expect(xs, w32, dtype):
+    from oracle import oracle as orc
+    if dtype == torch.bfloat16:
+        rows = [x.cpu().view(torch.int16).numpy().view(np.uint16) for x in xs]
+        return torch.from_numpy(orc.wreduce(rows, w32, "bf16").view(np.int16).copy()).view(torch.bfloat16)
+    return torch.from_numpy(orc.wreduce([x.cpu().numpy() for x in xs], w32, "f32"))
+
+
+def _same(a, b):
+    a, b = a.cpu(), b.cpu()
+    if a.dtype == torch.bfloat16:
+        return torch.equal(a.view(torch.int16), b.view(torch.int16))
+    return torch.equal(a.view(torch.int32), b.view(torch.int32))
+
+
+@pytest.mark.parametrize("n,p,dtype", [(5, 100_003, torch.float32), (8, 1_048_577, torch.float32),
+                                       (3, 50_001, torch.bfloat16)])
+def test_sharded_entry_points_rccl(rccl_world1, n, p, dtype):
+    from dasklearn_amd.sharded import ShardedAggregator
+    from oracle import oracle as orc
+
+    assert dist.get_backend() == "nccl"
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(11 + n)
+    xs = [(torch.randn(p, generator=g, device=dev) * 0.05).to(dtype) for _ in range(n)]
+    weights = [float(w) for w in np.random.default_rng(n).dirichlet(np.ones(n))]
+    w32 = orc.reference_weights(n, weights)
+    expect = _expect(xs, w32, dtype)
+
+    agg = ShardedAggregator()  # HIP kernel as the local reduce
+    b, e = agg.bounds(p)
+    assert (b, e) == (0, p)
+    assert _same(agg.aggregate_param_sharded([x[b:e] for x in xs], weights, p), expect)
+    assert _same(agg.aggregate_param_sharded([x[b:e] for x in xs], weights, p, gather=False), expect)
+    # whole models on "different ranks" (all on rank 0 here): all-to-all, exact fold, all-gather
+    assert _same(agg.aggregate_model_sharded(xs, [n], weights, exact=True), expect)
+    # FAST: partial sums + reduce-scatter + all-gather, tolerance only
+    fast = agg.aggregate_model_sharded(xs, [n], weights, exact=False).cpu().float()
+    scale = sum(abs(float(w)) * x.cpu().float().abs() for w, x in zip(w32, xs))
+    ulp = 2.0 ** -8 if dtype == torch.bfloat16 else 2.0 ** -23
+    assert torch.all((fast - expect.float()).abs() <= (n + 2) * ulp * scale + 1e-30)
+    # uniform weights (fedavg.py:14-15)
+    assert _same(agg.aggregate_param_sharded(xs, None, p), _expect(xs, orc.reference_weights(n, None), dtype))
