@@ -25,6 +25,7 @@ from __future__ import annotations
 
 import copy
 import time
+import weakref
 from collections import OrderedDict
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -58,6 +59,17 @@ class ParamLayout:
             self.totals[dt] = off
             self._group_offsets[dt] = offs
         self._signature = [(p.shape, p.dtype) for p in self.params]
+        # per dtype group: element counts and shapes for splitting an arena
+        self.split_sizes = {dt: [self.params[k].numel() for k in idx] for dt, idx in self.groups.items()}
+        self.split_shapes = {dt: [None if self.params[k].dim() == 1 else self.params[k].shape for k in idx]
+                             for dt, idx in self.groups.items()}
+
+    def rebind(self, params: List[nn.Parameter]) -> "ParamLayout":
+        """The same layout over another module's parameters (same signature,
+        which the caller guarantees): no recomputation."""
+        other = copy.copy(self)
+        other.params = params
+        return other
 
     def check_compatible(self, module: nn.Module) -> List[nn.Parameter]:
         ps = list(module.parameters())
@@ -196,8 +208,7 @@ def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, m
                              device=None, timing: Optional[dict] = None
                              ) -> Tuple[ParamLayout, Dict[torch.dtype, torch.Tensor], torch.device]:
     """Reduce the parameters of `models` into one fresh device arena per dtype."""
-    layout = ParamLayout(models[0])
-    all_params = [layout.check_compatible(m) for m in models]
+    layout, all_params, in_views = input_arenas(models)
     dev = _target_device(all_params[0], device)
     n = len(models)
     outs: Dict[torch.dtype, torch.Tensor] = {}
@@ -212,9 +223,9 @@ def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, m
                 continue
             on_dev = all(all_params[i][idx[0]].device == dev for i in range(n))
             if on_dev:
-                views = [layout.arena_view(ps, dt) for ps in all_params]
+                views = in_views[dt]
                 st.mark("layout")
-                if all(v is not None for v in views):
+                if views is not None:
                     _native.wreduce(views, weights_f32, out, mode)
                     st.mark("kernel")
                     continue
@@ -258,18 +269,137 @@ def arenas_to_host(arenas: Dict[torch.dtype, torch.Tensor], stream) -> Dict[torc
     return host
 
 
+# Atomic attribute types a module clone may share (deepcopy returns them as is).
+_ATOMIC = (type(None), bool, int, float, complex, str, bytes, torch.dtype, torch.device, torch.layout,
+           torch.memory_format)
+
+
+def _plain_module_class(cls) -> bool:
+    """Classes whose copy.deepcopy is nn.Module's default reduce/getstate/
+    setstate round trip, which _clone_module restates without the generic
+    __reduce_ex__ machinery."""
+    return (cls.__reduce_ex__ is object.__reduce_ex__ and cls.__reduce__ is object.__reduce__
+            and getattr(cls, "__deepcopy__", None) is None and cls.__getstate__ is nn.Module.__getstate__)
+
+
+def _clone_module(m: nn.Module, memo: dict) -> nn.Module:
+    """copy.deepcopy(m, memo) for a module tree, ~5x faster for plain modules.
+
+    deepcopy of an nn.Module is: state = Module.__getstate__() (the __dict__
+    minus _compiled_call_impl), deep-copied with the shared memo, then
+    cls.__new__(cls).__setstate__(state). That is what this does, taking
+    parameters from the memo (the arena views module_from_arenas installs),
+    recursing into `_modules` directly, and sharing atomic values and fresh
+    empty hook containers without a generic round trip. Anything else (buffers,
+    non-empty containers, custom attributes) goes through copy.deepcopy with
+    the same memo; classes with their own reduce/deepcopy/getstate take
+    copy.deepcopy whole."""
+    got = memo.get(id(m))
+    if got is not None:
+        return got
+    cls = type(m)
+    if not _plain_module_class(cls):
+        return copy.deepcopy(m, memo)
+    new = cls.__new__(cls)
+    memo[id(m)] = new
+    state = {}
+    for k, v in m.__dict__.items():
+        if k == "_compiled_call_impl":
+            continue
+        tv = type(v)
+        if k == "_modules":
+            state[k] = tv((name, None if c is None else _clone_module(c, memo)) for name, c in v.items())
+        elif k == "_parameters":
+            state[k] = tv((name, None if q is None else (memo[id(q)] if id(q) in memo else copy.deepcopy(q, memo)))
+                          for name, q in v.items())
+        elif tv in _ATOMIC:
+            state[k] = v
+        elif (tv is dict or tv is OrderedDict or tv is set) and not v:
+            state[k] = tv()
+        else:
+            state[k] = copy.deepcopy(v, memo)
+    new.__setstate__(state)
+    return new
+
+
+class _ArenaEntry:
+    __slots__ = ("layout", "arenas", "ptrs")
+
+    def __init__(self, layout, arenas, ptrs):
+        self.layout, self.arenas, self.ptrs = layout, arenas, ptrs
+
+
+# Modules whose parameters this package installed as views of flat arenas
+# (module_from_arenas): their layout and arenas, so later aggregates skip the
+# layout/contiguity checks. Weak keys: an entry lives as long as its module.
+_ARENAS: "weakref.WeakKeyDictionary[nn.Module, _ArenaEntry]" = weakref.WeakKeyDictionary()
+
+
+def registered_arenas(module: nn.Module, params: Optional[List[nn.Parameter]] = None):
+    """(layout over `module`'s parameters, {dtype: flat arena}) if `module` was
+    built by module_from_arenas and its parameters still are those views
+    (same count, shapes and addresses: a parameter re-assigned or re-pointed
+    since, e.g. `p.data = t`, invalidates the entry); else None."""
+    try:
+        e = _ARENAS.get(module)
+    except TypeError:
+        return None
+    if e is None:
+        return None
+    ps = list(module.parameters()) if params is None else params
+    if len(ps) != len(e.ptrs):
+        return None
+    for q, (ptr, shape) in zip(ps, e.ptrs):
+        if q.data_ptr() != ptr or q.shape != shape:
+            return None
+    return e.layout.rebind(ps), e.arenas
+
+
 def module_from_arenas(model0: nn.Module, layout: ParamLayout,
                        arenas: Dict[torch.dtype, torch.Tensor]) -> nn.Module:
-    """`copy.deepcopy(model0)` whose parameters are views of `arenas`."""
+    """`copy.deepcopy(model0)` whose parameters are views of `arenas`
+    (registered, so a later aggregate reads the arenas without checks)."""
     memo = {}
+    new_params = [None] * len(layout.params)
     for dt, idx in layout.groups.items():
-        flat = arenas[dt]
-        for k in idx:
+        parts = torch.split(arenas[dt], layout.split_sizes[dt])  # one call for the group
+        for k, part, shape in zip(idx, parts, layout.split_shapes[dt]):
             p = layout.params[k]
-            off = layout.offsets[k]
-            view = flat[off:off + p.numel()].view(p.shape)
-            memo[id(p)] = nn.Parameter(view, requires_grad=p.requires_grad)
-    return copy.deepcopy(model0, memo)
+            q = nn.Parameter(part if shape is None else part.view(shape), requires_grad=p.requires_grad)
+            memo[id(p)] = q
+            new_params[k] = q
+    out = _clone_module(model0, memo)
+    # The clone maps every parameter of model0 to its view one to one and keeps
+    # the module/parameter order, so parameters() of `out` is new_params.
+    _ARENAS[out] = _ArenaEntry(layout.rebind([]), dict(arenas),
+                               tuple((q.data_ptr(), q.shape) for q in new_params))
+    return out
+
+
+def input_arenas(models: Sequence[nn.Module]):
+    """Layout of models[0], every model's parameter list, and per dtype the
+    flat arena view of every model — or None for a dtype where some model is
+    not an arena (separate storages, host memory, ...). Registered arenas
+    (module_from_arenas outputs) skip the layout and contiguity checks."""
+    reg0 = registered_arenas(models[0])
+    layout = reg0[0] if reg0 is not None else ParamLayout(models[0])
+    all_params, views = [], {dt: [] for dt in layout.groups}
+    for i, m in enumerate(models):
+        reg = reg0 if i == 0 else registered_arenas(m)
+        if reg is not None and (reg[0]._signature is layout._signature or reg[0]._signature == layout._signature):
+            ps = reg[0].params
+            all_params.append(ps)
+            for dt in layout.groups:
+                if views[dt] is not None:
+                    views[dt].append(reg[1][dt])
+            continue
+        ps = layout.check_compatible(m)
+        all_params.append(ps)
+        for dt in layout.groups:
+            if views[dt] is not None:
+                v = layout.arena_view(ps, dt)
+                views[dt] = None if v is None else views[dt] + [v]
+    return layout, all_params, views
 
 
 def aggregate_modules(models: List[nn.Module], weights: Optional[Sequence[float]], mode: int,

@@ -17,7 +17,7 @@ import torch
 from torch import nn
 
 from . import _native
-from .arena import ParamLayout, aggregate_modules, arenas_to_host, module_from_arenas
+from .arena import aggregate_modules, input_arenas, module_from_arenas
 
 
 def _resolve(models, weights):
@@ -38,38 +38,51 @@ def aggregate_batch(tasks: Sequence[Tuple[List[nn.Module], Optional[Sequence[flo
     task goes through the single-task path. Output placement follows
     FedAvg.aggregate (where models[0] lives)."""
     results: List[Optional[nn.Module]] = [None] * len(tasks)
-    batched = []  # (task index, layout, views per dtype, w32, host_out)
+    prepared, where = [], []
     for ti, (models, weights) in enumerate(tasks):
         w32 = _resolve(models, weights)
         model0 = models[0]  # IndexError for an empty task, as the reference
-        layout = ParamLayout(model0)
-        params = [layout.check_compatible(m) for m in models]
-        views = {}
-        ok = all(p.is_cuda for ps in params for p in ps) and len(layout.groups) > 0
-        if ok:
-            dev = params[0][0].device
-            for dt in layout.groups:
-                vs = [layout.arena_view(ps, dt) for ps in params]
-                if any(v is None for v in vs) or any(v.device != dev for v in vs):
-                    ok = False
-                    break
-                views[dt] = vs
-        if not ok:
+        layout, _, views = input_arenas(models)
+        if _device_views(views) is None:
             results[ti] = aggregate_modules(models, weights, mode)
             continue
-        batched.append((ti, layout, views, w32))
-    # one batched call per dtype present; outputs are fresh arenas per task
+        prepared.append((model0, layout, views, w32))
+        where.append(ti)
+    for ti, out in zip(where, aggregate_arena_tasks(prepared, mode)):
+        results[ti] = out
+    return results
+
+
+def _device_views(views) -> Optional[torch.device]:
+    """The one CUDA device every flat view lives on, or None."""
+    dev = None
+    if not views:
+        return None
+    for vs in views.values():
+        if vs is None:
+            return None
+        for v in vs:
+            if not v.is_cuda or (dev is not None and v.device != dev):
+                return None
+            dev = v.device
+    return dev
+
+
+def aggregate_arena_tasks(prepared, mode: int = _native.DLSIM_EXACT) -> List[nn.Module]:
+    """prepared: [(model0, layout of model0, {dtype: [flat arena per model]},
+    fp32 weights)] with every arena on one device -> one module per task
+    (deepcopy(model0) semantics, parameters views of a fresh output arena),
+    all tasks of a dtype and device in batched launches."""
     by_dtype = {}
-    outs = {}
-    for ti, layout, views, w32 in batched:
-        dev = next(iter(views.values()))[0].device
-        outs[ti] = {}
+    outs = []
+    for model0, layout, views, w32 in prepared:
+        o = {}
         for dt, vs in views.items():
+            dev = vs[0].device
             out = torch.empty(layout.totals[dt], dtype=dt, device=dev)
-            outs[ti][dt] = out
+            o[dt] = out
             by_dtype.setdefault((dt, dev), []).append((vs, w32, out))
+        outs.append(o)
     for (dt, dev), group in by_dtype.items():
         _native.wreduce_batched(group, mode, torch.cuda.current_stream(dev))
-    for ti, layout, views, w32 in batched:
-        results[ti] = module_from_arenas(tasks[ti][0][0], layout, outs[ti])
-    return results
+    return [module_from_arenas(model0, layout, o) for (model0, layout, _, _), o in zip(prepared, outs)]

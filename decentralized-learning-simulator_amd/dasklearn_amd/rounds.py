@@ -11,21 +11,25 @@ whose inputs are ready runs in the wave; the aggregate tasks of a wave go to
 `aggregate_batch` together (descriptor-table launches), other tasks (train,
 test, ...) are called through the function table like the worker does.
 
-Models that reach an aggregate are uploaded once each into a device arena
-(`to_device_arena`), so an aggregate -> train -> aggregate chain never
-crosses PCIe when the train function works on the device. Results are
-bit-identical to running the same tasks one by one with FedAvg.aggregate.
+Models that reach an aggregate are resolved once per wave to one flat device
+arena each: aggregate outputs are registered arenas (read in place), other
+device arenas are read in place, anything else is copied once into a fresh
+arena (one concatenation, no module built). So an aggregate -> train ->
+aggregate chain never crosses PCIe when the train function works on the
+device. Results are bit-identical to running the same tasks one by one with
+FedAvg.aggregate.
 """
 from __future__ import annotations
 
+import time
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import torch
 from torch import nn
 
 from . import _native
-from .arena import ParamLayout, to_device_arena
-from .batch import aggregate_batch
+from .arena import _target_device, input_arenas
+from .batch import _device_views, _resolve, aggregate_arena_tasks
 
 Task = Tuple[str, str, dict]  # (task_name, func_name, data with placeholders)
 
@@ -49,14 +53,18 @@ def _refs(v, out):
 class RoundExecutor:
 
     def __init__(self, funcs: Dict[str, Callable], settings, device=None,
-                 mode: int = _native.DLSIM_EXACT):
+                 mode: int = _native.DLSIM_EXACT, timing: bool = False):
+        """timing: accumulate wall seconds per kind of wave work in
+        `self.stats` ("aggregate", "other"); the stream is synchronised after
+        every batched aggregate so its kernels count (measurement only)."""
+        self.timing = timing
+        self.stats: Dict[str, float] = {"aggregate": 0.0, "other": 0.0, "aggregate_tasks": 0}
         self.funcs = dict(funcs)
         self.settings = settings
         self.device = device
         self.mode = mode
         self.results: Dict[str, list] = {}
         self.waves: List[List[str]] = []
-        self._resident: Dict[int, nn.Module] = {}
 
     def _resolve(self, v):
         if _is_ref(v):
@@ -67,17 +75,42 @@ class RoundExecutor:
             return {k: self._resolve(x) for k, x in v.items()}
         return v
 
-    def _resident_model(self, m: nn.Module) -> nn.Module:
-        """Device-arena form of `m` (uploaded once per object)."""
-        layout = ParamLayout(m)
-        params = layout.params
-        if params and all(p.is_cuda for p in params) and all(
-                layout.arena_view(params, dt) is not None for dt in layout.groups):
-            return m
-        key = id(m)
-        if key not in self._resident:
-            self._resident[key] = to_device_arena(m, self.device)
-        return self._resident[key]
+    def _arena_of(self, m: nn.Module, cache: dict):
+        """(layout over m's parameters, {dtype: flat device arena}) for one
+        model, once per wave (`cache` keeps the model alive, so its id cannot
+        be reused while the entry exists)."""
+        hit = cache.get(id(m))
+        if hit is not None and hit[0] is m:
+            return hit[1], hit[2]
+        layout, params, views = input_arenas([m])
+        dev = _device_views(views)
+        if dev is not None and (self.device is None or dev == torch.device(self.device)):
+            arenas = {dt: vs[0] for dt, vs in views.items()}
+        else:
+            dev = _target_device(params[0], self.device)
+            with torch.no_grad():
+                arenas = {dt: torch.cat([params[0][k].detach().reshape(-1).to(dev, non_blocking=True) for k in idx])
+                          for dt, idx in layout.groups.items()}
+        cache[id(m)] = (m, layout, arenas)
+        return layout, arenas
+
+    def _aggregate_wave(self, aggs) -> List[nn.Module]:
+        cache: dict = {}
+        prepared = []
+        for name, _, data in aggs:
+            d = self._resolve(data)
+            models = d["models"]
+            w32 = _resolve(models, d.get("weights"))  # fedavg.py:14-17 rules and exceptions
+            ents = [self._arena_of(m, cache) for m in models]
+            layout0 = ents[0][0]
+            sig = layout0._signature
+            for i in range(1, len(ents)):
+                lay = ents[i][0]
+                if lay._signature is not sig and lay._signature != sig:
+                    layout0.check_compatible(models[i])  # raises the shape/dtype error
+            views = {dt: [a[dt] for _, a in ents] for dt in layout0.groups}
+            prepared.append((models[0], layout0, views, w32))
+        return aggregate_arena_tasks(prepared, self.mode)
 
     def run(self, tasks: Sequence[Task], seed: Optional[Dict[str, list]] = None) -> Dict[str, list]:
         """Execute `tasks`; `seed` pre-populates results (e.g. initial models).
@@ -94,21 +127,27 @@ class RoundExecutor:
                                   if r not in self.results and r not in names})
                 raise RuntimeError(f"unresolvable task inputs: {missing[:5]}")
             aggs = [t for t in ready if t[1] == "aggregate"]
+            t0 = time.perf_counter()
             for name, func, data in ready:
                 if func == "aggregate":
                     continue
                 res = self.funcs[func](self.settings, self._resolve(data))
                 assert isinstance(res, (list, tuple))  # broker.py:282-283
                 self.results[name] = list(res)
+            if self.timing and torch.cuda.is_available():
+                torch.cuda.synchronize()
+            t1 = time.perf_counter()
             if aggs:
-                batch = []
-                for name, _, data in aggs:
-                    d = self._resolve(data)
-                    models = [self._resident_model(m) for m in d["models"]]
-                    batch.append((models, d.get("weights")))
-                outs = aggregate_batch(batch, self.mode)
+                outs = self._aggregate_wave(aggs)
                 for (name, _, _), out in zip(aggs, outs):
                     self.results[name] = [out]
+                if self.timing:
+                    torch.cuda.synchronize()
+            if self.timing:
+                t2 = time.perf_counter()
+                self.stats["other"] += t1 - t0
+                self.stats["aggregate"] += t2 - t1
+                self.stats["aggregate_tasks"] += len(aggs)
             done = {t[0] for t in ready}
             self.waves.append(sorted(done))
             pending = [t for t in pending if t[0] not in done]

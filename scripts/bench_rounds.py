@@ -1,0 +1,170 @@
+"""Wall time of the aggregate work of simulated D-PSGD rounds (SURVEY.md §8f
+row 4): the reference's DAG shape (every peer trains, then aggregates its k
+ring neighbours' models and its own, dasklearn/simulation/dpsgd/client.py:
+142-151; fan-in k+1 with k = floor(log2 n)), GNLeNet-shaped models.
+
+Three ways of running the same aggregate tasks:
+  batched     RoundExecutor: each wave's aggregates in batched launches over
+              device-resident arenas (dasklearn_amd/rounds.py)
+  sequential  one functions.aggregate call per task, as the reference worker
+              does (worker.py:27-31), models on the device
+  cpu_ref     the reference's FedAvg.aggregate op sequence (oracle restatement)
+              per task on host models at the worker's 4 threads (broker.py:31)
+The train task is a synthetic device-side perturbation (the real one needs
+network datasets; out of scope) and is not counted.
+
+    python scripts/bench_rounds.py [--peers 100] [--rounds 4]
+"""
+from __future__ import annotations
+
+import argparse
+import copy
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "decentralized-learning-simulator_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import torch  # noqa: E402
+from torch import nn  # noqa: E402
+
+GNLENET = [(32, 3, 5, 5), (32,), (32,), (32,), (32, 32, 5, 5), (32,), (32,), (32,), (64, 32, 5, 5),
+           (64,), (64,), (64,), (10, 576), (10,)]
+
+
+class Shaped(nn.Module):
+    def __init__(self, shapes):
+        super().__init__()
+        self.ps = nn.ParameterList([nn.Parameter(torch.randn(*s) * 0.05) for s in shapes])
+
+
+class Settings:
+    from dasklearn_amd.gradient_aggregation import GradientAggregationMethod
+    gradient_aggregation = GradientAggregationMethod.FEDAVG
+
+
+def ring(n, k):
+    nb = {}
+    for p in range(n):
+        s = set()
+        for d in range(1, k // 2 + 1):
+            s.add((p + d) % n)
+            s.add((p - d) % n)
+        if k % 2:
+            s.add((p + k // 2 + 1) % n)
+        s.discard(p)
+        nb[p] = sorted(s)
+    return nb
+
+
+def dag(n, rounds):
+    k = min(max(1, math.floor(math.log2(n))), n - 1)
+    nb = ring(n, k)
+    tasks = []
+    for r in range(1, rounds + 1):
+        for p in range(n):
+            model = ("init", 0) if r == 1 else (f"agg_{p}_{r - 1}", 0)
+            tasks.append((f"train_{p}_{r}", "train", {"model": model, "round": r, "peer": p}))
+        for p in range(n):
+            models = [(f"train_{q}_{r}", 0) for q in nb[p]] + [(f"train_{p}_{r}", 0)]
+            tasks.append((f"agg_{p}_{r}", "aggregate", {"models": models, "round": r, "peer": p}))
+    return tasks, k + 1
+
+
+def train(settings, params):
+    out = copy.deepcopy(params["model"])
+    with torch.no_grad():
+        for p in out.parameters():
+            p.add_(1e-3 * (params["peer"] + 1))
+    return [out]
+
+
+def resolve(results, v):
+    if isinstance(v, tuple) and len(v) == 2 and isinstance(v[0], str):
+        return results[v[0]][v[1]]
+    if isinstance(v, list):
+        return [resolve(results, x) for x in v]
+    return v
+
+
+def sequential(tasks, agg_fn, init, sync):
+    """The worker's one-task-at-a-time loop; only aggregate calls are timed."""
+    results = {"init": [init]}
+    t_agg, n_agg = 0.0, 0
+    for name, f, data in tasks:
+        d = {k: resolve(results, v) for k, v in data.items()}
+        if f == "aggregate":
+            sync()
+            t0 = time.perf_counter()
+            results[name] = agg_fn(Settings(), d)
+            sync()
+            t_agg += time.perf_counter() - t0
+            n_agg += 1
+        else:
+            results[name] = train(Settings(), d)
+    return t_agg, n_agg
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--peers", type=int, default=100)
+    ap.add_argument("--rounds", type=int, default=4)
+    ap.add_argument("--cpu-rounds", type=int, default=2)
+    ap.add_argument("--profile", default=None, help="cProfile the batched run into this file")
+    a = ap.parse_args()
+    from dasklearn_amd.functions import aggregate
+    from dasklearn_amd.rounds import RoundExecutor
+    from oracle import fedavg_torch
+
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    init_h = Shaped(GNLENET)
+    init_d = copy.deepcopy(init_h).to(dev)
+    tasks, fan = dag(a.peers, a.rounds)
+    p = sum(int(torch.Size(s).numel()) for s in GNLENET)
+    task_bytes = (fan + 1) * p * 4
+    sync = torch.cuda.synchronize
+
+    # warm-up (library load, allocator, kernels)
+    wt, _ = dag(min(a.peers, 8), 1)
+    RoundExecutor({"train": train}, Settings()).run(wt, seed={"init": [init_d]})
+    sequential(wt, aggregate, init_d, sync)
+
+    ex = RoundExecutor({"train": train}, Settings(), timing=True)
+    if a.profile:
+        import cProfile
+        import pstats
+        prof = cProfile.Profile()
+        prof.enable()
+        ex.run(tasks, seed={"init": [init_d]})
+        prof.disable()
+        with open(a.profile, "w") as f:
+            pstats.Stats(prof, stream=f).sort_stats("cumulative").print_stats(40)
+    else:
+        ex.run(tasks, seed={"init": [init_d]})
+    bt, bn = ex.stats["aggregate"], ex.stats["aggregate_tasks"]
+    st, sn = sequential(tasks, aggregate, init_d, sync)
+
+    def cpu_agg(settings, d):
+        return [fedavg_torch.aggregate_modules(d["models"], d.get("weights"))]
+
+    torch.set_num_threads(4)
+    ctasks, _ = dag(a.peers, a.cpu_rounds)
+    ct, cn = sequential(ctasks, cpu_agg, init_h, lambda: None)
+
+    def line(kind, t, n):
+        return {"kind": kind, "peers": a.peers, "fan_in": fan, "tasks": n, "params": p,
+                "ms_per_round": round(t / n * a.peers * 1e3, 3), "us_per_task": round(t / n * 1e6, 1),
+                "GBps_algorithmic": round(task_bytes * n / t / 1e9, 2)}
+
+    for l in (line("batched", bt, bn), line("sequential", st, sn), line("cpu_ref_4threads", ct, cn)):
+        print(json.dumps(l), flush=True)
+
+
+if __name__ == "__main__":
+    main()

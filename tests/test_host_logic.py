@@ -95,6 +95,101 @@ def test_module_from_arenas_has_deepcopy_semantics():
     assert all(torch.all(p != 2.0) for p in m.parameters())  # original untouched
 
 
+class _Tied(nn.Module):
+    """Weight tying, a shared submodule, a hook and a non-module attribute."""
+
+    def __init__(self):
+        super().__init__()
+        self.emb = nn.Linear(6, 6, bias=False)
+        self.head = nn.Linear(6, 6)
+        self.head.weight = self.emb.weight
+        self.block = nn.Sequential(nn.Conv2d(2, 3, 3, padding=1), nn.GroupNorm(1, 3))
+        self.again = self.block  # the same submodule twice
+        self.table = [torch.ones(2), {"x": (1, 2)}]
+        self.register_buffer("steps", torch.tensor(5))
+        self.register_forward_hook(lambda mod, i, o: None)
+
+
+class _CustomCopy(nn.Linear):
+    def __deepcopy__(self, memo):  # classes with their own deepcopy keep it
+        new = nn.Linear(self.in_features, self.out_features)
+        memo[id(self)] = new
+        new.marker = "custom"
+        return new
+
+
+def _structure(m):
+    return [(name, type(mod).__name__, sorted(k for k in mod.__dict__ if k != "_compiled_call_impl"))
+            for name, mod in m.named_modules(remove_duplicate=False)]
+
+
+@pytest.mark.parametrize("make", [lambda: _Tied(),
+                                  lambda: nn.Sequential(nn.Conv2d(3, 4, 3), nn.BatchNorm2d(4), nn.ReLU(),
+                                                        nn.Flatten(), nn.Linear(4, 2)),
+                                  lambda: nn.ModuleDict({"a": nn.Linear(2, 2), "b": nn.ParameterList(
+                                      [nn.Parameter(torch.ones(3)), nn.Parameter(torch.zeros(2, 2))])})])
+def test_fast_clone_matches_deepcopy(make):
+    """module_from_arenas clones model0 without copy.deepcopy's generic
+    machinery (arena._clone_module); the result must look exactly like
+    copy.deepcopy(model0) with the parameters replaced."""
+    import copy
+    m = make()
+    lay = arena.ParamLayout(m)
+    flat = torch.arange(lay.totals[torch.float32], dtype=torch.float32)
+    out = arena.module_from_arenas(m, lay, {torch.float32: flat})
+    ref = copy.deepcopy(m)
+    assert _structure(out) == _structure(ref)
+    assert [n for n, _ in out.named_parameters()] == [n for n, _ in ref.named_parameters()]
+    assert [n for n, _ in out.named_buffers()] == [n for n, _ in ref.named_buffers()]
+    for (n, b), (_, b0) in zip(out.named_buffers(), m.named_buffers()):
+        assert torch.equal(b, b0) and b.data_ptr() != b0.data_ptr(), n
+    got = torch.cat([p.detach().reshape(-1) for p in out.parameters()])
+    assert torch.equal(got, flat)  # parameters are the arena, in order
+    assert all(a.data_ptr() != b.data_ptr() for a, b in zip(out.parameters(), m.parameters()))
+    if isinstance(m, _Tied):
+        assert out.head.weight is out.emb.weight and out.again is out.block
+        assert out.table is not m.table and torch.equal(out.table[0], m.table[0])
+        assert len(out._forward_hooks) == 1 and out._forward_hooks is not m._forward_hooks
+        x = torch.randn(1, 2, 4, 4)
+        assert torch.equal(out.block(x), out.again(x))
+    assert arena.registered_arenas(out) is not None
+
+
+def test_fast_clone_respects_custom_deepcopy():
+    m = nn.Sequential(_CustomCopy(3, 2))
+    lay = arena.ParamLayout(m)
+    out = arena.module_from_arenas(m, lay, {torch.float32: torch.zeros(lay.totals[torch.float32])})
+    assert out[0].marker == "custom"
+
+
+def test_registered_arenas_invalidated_by_reassignment():
+    m = nn.Sequential(nn.Linear(4, 3), nn.Linear(3, 2))
+    lay = arena.ParamLayout(m)
+    flat = torch.zeros(lay.totals[torch.float32])
+    out = arena.module_from_arenas(m, lay, {torch.float32: flat})
+    reg = arena.registered_arenas(out)
+    assert reg is not None and reg[1][torch.float32] is flat
+    assert [p is q for p, q in zip(reg[0].params, out.parameters())] == [True] * 4
+    out[1].bias.data = torch.ones(2)  # re-pointed: no longer the arena
+    assert arena.registered_arenas(out) is None
+    out2 = arena.module_from_arenas(m, lay, {torch.float32: flat.clone()})
+    out2[0].weight = nn.Parameter(torch.ones(3, 4))  # replaced
+    assert arena.registered_arenas(out2) is None
+    assert arena.registered_arenas(m) is None  # never registered
+
+
+def test_input_arenas_mixes_registered_and_plain():
+    m = nn.Sequential(nn.Linear(4, 3), nn.Linear(3, 2))
+    lay = arena.ParamLayout(m)
+    a = arena.module_from_arenas(m, lay, {torch.float32: torch.zeros(lay.totals[torch.float32])})
+    layout, params, views = arena.input_arenas([a, m, a])
+    assert views[torch.float32] is None  # m is not an arena
+    layout, params, views = arena.input_arenas([a, a])
+    assert [v.data_ptr() for v in views[torch.float32]] == [a[0].weight.data_ptr()] * 2
+    with pytest.raises(ValueError):
+        arena.input_arenas([a, nn.Sequential(nn.Linear(4, 3), nn.Linear(3, 3))])
+
+
 def test_model_manager_first_model_per_peer_wins():
     mm = ModelManager(None, object(), 0)
     a, b = nn.Linear(1, 1), nn.Linear(1, 1)
