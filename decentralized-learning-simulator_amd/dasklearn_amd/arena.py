@@ -204,22 +204,124 @@ class _Stages:
         self.t = now
 
 
+_SIDE_STREAMS: Dict[torch.device, Tuple[torch.cuda.Stream, torch.cuda.Stream]] = {}
+
+
+def _side_streams(dev: torch.device):
+    """(H2D stream, D2H stream) of a device: copies in both directions run
+    beside the reduce kernels on the caller's stream (PCIe is full duplex and
+    each direction has its own DMA engine)."""
+    ss = _SIDE_STREAMS.get(dev)
+    if ss is None:
+        ss = (torch.cuda.Stream(dev), torch.cuda.Stream(dev))
+        _SIDE_STREAMS[dev] = ss
+    return ss
+
+
+# Host pipeline chunking: about this many bytes of each model per chunk, at
+# most this many chunks, boundaries on multiples of this many elements (keeps
+# every chunk of a 256-B aligned staging row 16-B aligned for the vector kernel).
+PIPELINE_CHUNK_BYTES = 16 << 20
+PIPELINE_MAX_CHUNKS = 8
+_CHUNK_ALIGN = 1024
+
+
+def _chunk_plan(layout: ParamLayout, dt: torch.dtype, esz: int):
+    """[(c0, c1, [(j, a, b)])]: element ranges of the dtype group's arena and,
+    per range, the pieces [a, b) of group tensor j that fill it in order."""
+    total = layout.totals[dt]
+    k = max(1, min(PIPELINE_MAX_CHUNKS, round(total * esz / PIPELINE_CHUNK_BYTES)))
+    bounds = [0]
+    for c in range(1, k):
+        b = (total * c // k) // _CHUNK_ALIGN * _CHUNK_ALIGN
+        if b > bounds[-1]:
+            bounds.append(b)
+    bounds.append(total)
+    offs, sizes = layout._group_offsets[dt], layout.split_sizes[dt]
+    plan = []
+    for c0, c1 in zip(bounds, bounds[1:]):
+        pieces = []
+        for j, (off, sz) in enumerate(zip(offs, sizes)):
+            a, b = max(c0, off), min(c1, off + sz)
+            if a < b:
+                pieces.append((j, a - off, b - off))
+        plan.append((c0, c1, pieces))
+    return plan
+
+
+def _host_pipeline(all_params, idx, layout, dt, dev, out, weights_f32, mode, stream, want_host):
+    """Host models -> device reduce (-> host result), pipelined over chunks of
+    the parameter axis: chunk c of every model is packed into pinned staging
+    (CPU) and copied H2D on the H2D stream while chunk c-1 is reduced on the
+    caller's stream and chunk c-2's result goes back on the D2H stream. Bytes
+    and results are those of the unchunked path (elements are independent);
+    what changes is that the kernel and the D2H hide under the H2D stream.
+    Returns the pinned host result (want_host, more than one chunk) or None
+    (the result is in `out` on the device, queued on `stream`)."""
+    n = len(all_params)
+    total = layout.totals[dt]
+    dev_rows, pinned = STAGING.acquire(dev, dt, n, total, stream)
+    plan = _chunk_plan(layout, dt, out.element_size())
+    if len(plan) == 1:
+        # one chunk: no side streams (their events cost more than they hide
+        # for small models) — pack model i while model i-1's H2D runs
+        for i, ps in enumerate(all_params):
+            torch.cat([ps[k].detach().reshape(-1) for k in idx], out=pinned[i])
+            dev_rows[i].copy_(pinned[i], non_blocking=True)
+        _native.wreduce([dev_rows[i] for i in range(n)], weights_f32, out, mode, stream)
+        STAGING.release(dev, dt, n, total, stream)
+        return None
+    h2d, d2h = _side_streams(dev)
+    h2d.wait_stream(stream)
+    host = torch.empty(total, dtype=dt, pin_memory=True) if want_host else None
+    sizes = layout.split_sizes[dt]
+    flats = [[ps[k].detach().reshape(-1) for k in idx] for ps in all_params]
+    for c0, c1, pieces in plan:
+        for i in range(n):
+            fl = flats[i]
+            src = [fl[j] if (a == 0 and b == sizes[j]) else fl[j][a:b] for j, a, b in pieces]
+            dst = pinned[i, c0:c1]
+            torch.cat(src, out=dst)
+            with torch.cuda.stream(h2d):
+                dev_rows[i, c0:c1].copy_(dst, non_blocking=True)
+        stream.wait_stream(h2d)
+        _native.wreduce([dev_rows[i, c0:c1] for i in range(n)], weights_f32, out[c0:c1], mode, stream)
+        if host is not None:
+            d2h.wait_stream(stream)
+            with torch.cuda.stream(d2h):
+                host[c0:c1].copy_(out[c0:c1], non_blocking=True)
+    STAGING.release(dev, dt, n, total, stream)
+    if host is not None:
+        out.record_stream(d2h)
+        stream.wait_stream(d2h)
+    return host
+
+
 def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, mode: int,
-                             device=None, timing: Optional[dict] = None
-                             ) -> Tuple[ParamLayout, Dict[torch.dtype, torch.Tensor], torch.device]:
-    """Reduce the parameters of `models` into one fresh device arena per dtype."""
+                             device=None, timing: Optional[dict] = None, host_out: bool = False
+                             ) -> Tuple[ParamLayout, Dict[torch.dtype, torch.Tensor], torch.device, bool]:
+    """Reduce the parameters of `models` into one fresh arena per dtype.
+
+    Returns (layout, arenas, device, on_host). With host_out, host models take
+    the chunked pipeline and come back already in pinned host memory
+    (on_host True, copies complete); otherwise the arenas are on the device."""
     layout, all_params, in_views = input_arenas(models)
     dev = _target_device(all_params[0], device)
     n = len(models)
     outs: Dict[torch.dtype, torch.Tensor] = {}
     stream = torch.cuda.current_stream(dev)
     st = _Stages(timing, stream)
+    host_models = all(not all_params[i][idx[0]].is_cuda
+                      for idx in layout.groups.values() for i in range(n))
+    piped = host_out and host_models and len(layout.groups) > 0
     with torch.no_grad():
         for dt, idx in layout.groups.items():
             total = layout.totals[dt]
             out = torch.empty(total, dtype=dt, device=dev)
             outs[dt] = out
             if total == 0:
+                if piped:
+                    outs[dt] = torch.empty(0, dtype=dt)
                 continue
             on_dev = all(all_params[i][idx[0]].device == dev for i in range(n))
             if on_dev:
@@ -235,24 +337,31 @@ def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, m
                 _native.wreduce_tensors(rows, weights_f32, outs_k, mode)
                 st.mark("kernel")
                 continue
-            # host (or foreign-device) models: pack each model into pinned
-            # staging, then an async H2D copy on the current stream — the DMA of
-            # model i overlaps the packing of model i+1.
-            dev_rows, pinned = STAGING.acquire(dev, dt, n, total, stream)
+            if not any(all_params[i][idx[0]].is_cuda for i in range(n)):
+                # host models (the reference's case): chunked pack / H2D /
+                # reduce (/ D2H) pipeline
+                st.mark("layout")
+                h = _host_pipeline(all_params, idx, layout, dt, dev, out, weights_f32, mode, stream, piped)
+                if h is not None:
+                    outs[dt] = h
+                st.mark("pipeline")
+                continue
+            # models on another GPU: gather onto this one, then reduce
+            dev_rows, _ = STAGING.acquire(dev, dt, n, total, stream)
             st.mark("layout")
             for i, ps in enumerate(all_params):
-                src = [ps[k].detach().reshape(-1) for k in idx]
-                if src[0].is_cuda:
-                    torch.cat([s.to(dev) for s in src], out=dev_rows[i])
-                else:
-                    torch.cat(src, out=pinned[i])
-                    with torch.cuda.stream(stream):
-                        dev_rows[i].copy_(pinned[i], non_blocking=True)
-            st.mark("pack_h2d")
+                torch.cat([ps[k].detach().reshape(-1).to(dev) for k in idx], out=dev_rows[i])
             _native.wreduce([dev_rows[i] for i in range(n)], weights_f32, out, mode)
             STAGING.release(dev, dt, n, total, stream)
             st.mark("kernel")
-    return layout, outs, dev
+    if piped:
+        left = {dt: a for dt, a in outs.items() if a.is_cuda}
+        if left:  # single-chunk groups: their D2H now
+            outs.update(arenas_to_host(left, stream))
+            st.mark("d2h")
+        else:
+            stream.synchronize()
+    return layout, outs, dev, piped
 
 
 def arenas_to_host(arenas: Dict[torch.dtype, torch.Tensor], stream) -> Dict[torch.dtype, torch.Tensor]:
@@ -417,11 +526,11 @@ def aggregate_modules(models: List[nn.Module], weights: Optional[Sequence[float]
         assert len(weights) == len(models)
     model0 = models[0]  # IndexError for an empty list, as the reference
     w32 = _native.fp32_weights(weights)
-    layout, arenas, dev = reduce_modules_to_arenas(models, w32, mode, device, timing)
-    host_out = to_host if to_host is not None else not any(p.is_cuda for p in layout.params)
+    host_out = to_host if to_host is not None else not any(p.is_cuda for p in model0.parameters())
+    layout, arenas, dev, on_host = reduce_modules_to_arenas(models, w32, mode, device, timing, host_out)
     stream = torch.cuda.current_stream(dev)
     st = _Stages(timing, stream)
-    if host_out:
+    if host_out and not on_host:
         arenas = arenas_to_host(arenas, stream)
         st.mark("d2h")
     out = module_from_arenas(model0, layout, arenas)

@@ -7,6 +7,8 @@ goes back as one. This measures, for N ResNet-18/CIFAR-10-shaped models
 
   host      FedAvg.aggregate(cpu models) -> cpu module (pack into pinned
             staging, H2D, kernel, D2H): the PCIe-inclusive rate
+  host_shm  the same with the models' storages in shared memory (torch-mp
+            file_system strategy, how models reach the reference's worker)
   dev_list  CUDA models with separate parameter tensors (tensor-list ABI)
   dev_arena CUDA models whose parameters are views of one arena (one launch)
   cpu_ref   the reference's own op sequence on the CPU (oracle restatement),
@@ -79,6 +81,16 @@ def main():
         for _ in range(3):
             aggregate_modules(cpu_models, None, _native.DLSIM_EXACT, timing=stages)
         res["host_stages_ms"] = {k: round(v / 3 * 1e3, 3) for k, v in stages.items()}
+        # shm-backed host models, as they reach the reference's worker through
+        # torch.multiprocessing's file_system strategy (worker.py:6)
+        import copy
+        import torch.multiprocessing as tmp
+        tmp.set_sharing_strategy("file_system")
+        shm_models = [copy.deepcopy(m).share_memory() for m in cpu_models]
+        t = timed(lambda: FedAvg.aggregate(shm_models, None), a.reps)
+        res["host_shm_ms"] = round(t * 1e3, 3)
+        res["host_shm_GBps"] = round(byts / t / 1e9, 2)
+        del shm_models
         dev_models = [Shaped(shapes, i).to(dev) for i in range(n)]
         t = timed(lambda: FedAvg.aggregate(dev_models, None), a.reps)
         res["dev_list_ms"] = round(t * 1e3, 3)

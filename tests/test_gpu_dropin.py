@@ -195,7 +195,7 @@ def test_host_result_is_pinned_and_stage_timing_works():
     models = modules_from_golden(g)
     stages = {}
     out = aggregate_modules(models, None, _native.DLSIM_EXACT, timing=stages)
-    assert set(stages) >= {"layout", "pack_h2d", "kernel", "d2h", "module"}
+    assert set(stages) >= {"layout", "pipeline", "d2h", "module"}
     p0 = next(out.parameters())
     assert not p0.is_cuda and p0.is_pinned()
     assert orc.same_bits(flat_of(out), g["expected"])
@@ -223,3 +223,76 @@ def test_wire_decode_to_device_feeds_aggregate_without_packing():
     out = FedAvg.aggregate(dev_models, None)
     ref = fedavg_torch.aggregate_modules(models, None)
     assert orc.same_bits(flat_of(out), flat_of(ref))
+
+
+# ---- chunked host pipeline (arena._host_pipeline) ------------------------------------
+
+class Mixed(nn.Module):
+    """fp32 and bf16 parameter groups, interleaved (two arenas)."""
+
+    def __init__(self, seed):
+        super().__init__()
+        g = torch.Generator().manual_seed(seed)
+        self.a = nn.Parameter(torch.randn(300, 37, generator=g) * 0.05)
+        self.b = nn.Parameter((torch.randn(1001, generator=g) * 0.05).to(torch.bfloat16))
+        self.c = nn.Parameter(torch.randn(4097, generator=g) * 0.05)
+        self.d = nn.Parameter((torch.randn(64, 65, generator=g) * 0.05).to(torch.bfloat16))
+        self.e = nn.Parameter(torch.randn(3, generator=g))
+
+
+def _expected_by_dtype(models, weights):
+    w = orc.reference_weights(len(models), weights)
+    out = {}
+    for dt, code in ((torch.float32, "f32"), (torch.bfloat16, "bf16")):
+        rows = []
+        for m in models:
+            ps = [p.detach().reshape(-1) for p in m.parameters() if p.dtype == dt]
+            t = torch.cat(ps)
+            rows.append(t.view(torch.int16).numpy().view(np.uint16) if dt == torch.bfloat16 else t.numpy())
+        out[dt] = orc.wreduce(rows, w, code)
+    return out
+
+
+@pytest.mark.parametrize("chunk_bytes", [None, 4096, 50_000])
+@pytest.mark.parametrize("to_host", [None, False])
+def test_host_pipeline_chunks_are_exact(monkeypatch, chunk_bytes, to_host):
+    """Host modules go through the chunked pack/H2D/reduce/D2H pipeline; chunk
+    boundaries split tensors (forced small chunks) and both dtype groups:
+    bit-identical to the oracle, on the host (default) or on the device."""
+    from dasklearn_amd import arena
+    if chunk_bytes is not None:
+        monkeypatch.setattr(arena, "PIPELINE_CHUNK_BYTES", chunk_bytes)
+    models = [Mixed(s) for s in range(5)]
+    weights = [0.1, 0.3, 0.2, 0.15, 0.25]
+    out = FedAvg.aggregate(models, weights, to_host=to_host)
+    assert all(p.is_cuda == (to_host is False) for p in out.parameters())
+    exp = _expected_by_dtype(models, weights)
+    for dt in (torch.float32, torch.bfloat16):
+        t = torch.cat([p.detach().reshape(-1).cpu() for p in out.parameters() if p.dtype == dt])
+        got = t.view(torch.int16).numpy().view(np.uint16) if dt == torch.bfloat16 else t.numpy()
+        assert orc.same_bits(got, exp[dt]), (dt, chunk_bytes)
+
+
+def test_host_pipeline_resnet18_shapes_multi_chunk():
+    """8 host ResNet-18/CIFAR-10-shaped models (62 tensors, 44.7 MB each, 5
+    pipeline chunks): the host path of the north-star workload, bit-exact;
+    a second call reuses the staging buffers."""
+    import sys
+    sys.path.insert(0, GOLDEN)
+    from inputs import resnet18_cifar10_shapes
+    from dasklearn_amd import arena
+    assert len(arena._chunk_plan(arena.ParamLayout(Ragged(resnet18_cifar10_shapes())), torch.float32, 4)) > 1
+    models = []
+    for i in range(8):
+        m = Ragged(resnet18_cifar10_shapes())
+        g = torch.Generator().manual_seed(50 + i)
+        with torch.no_grad():
+            for p in m.parameters():
+                p.copy_(torch.randn(p.shape, generator=g) * 0.05)
+        models.append(m)
+    w = list(np.random.default_rng(7).dirichlet(np.ones(8)))
+    exp = orc.wreduce_rows_f32(np.stack([flat_of(m) for m in models]), orc.reference_weights(8, w))
+    for _ in range(2):
+        out = FedAvg.aggregate(models, w)
+        assert all(p.is_pinned() for p in out.parameters())
+        assert orc.same_bits(flat_of(out), exp)
