@@ -216,9 +216,11 @@ hipError_t launch_batch_fixed(const dlsim::BatchSlots& s, int n, unsigned blocks
 }
 
 // Fill and launch BatchSlots with tasks [t0, t1); all tasks vector-eligible.
+// divs: per-task final divisor (the mean policies), nullptr = 1.
 template <class Op>
 hipError_t launch_batch(const int* fan_in, const size_t* in_off, const void* const* in, const float* w,
-                        void* const* outs, const size_t* nelem, int t0, int t1, hipStream_t st) {
+                        const float* divs, void* const* outs, const size_t* nelem, int t0, int t1,
+                        hipStream_t st) {
   dlsim::BatchSlots s;
   std::memset(&s, 0, sizeof(s));
   const size_t tile = static_cast<size_t>(dlsim::kBlock) * kVpt;
@@ -234,6 +236,7 @@ hipError_t launch_batch(const int* fan_in, const size_t* in_off, const void* con
     s.block_start[k] = blocks;
     s.ptr_off[k] = static_cast<uint16_t>(ptrs);
     s.fan_in[k] = static_cast<uint16_t>(fan_in[t]);
+    s.div[k] = divs ? divs[t] : 1.0f;
     for (int i = 0; i < fan_in[t]; ++i) {
       s.p[ptrs + i] = in[in_off[t] + i];
       s.w[ptrs + i] = w[in_off[t] + i];
@@ -250,7 +253,7 @@ hipError_t launch_batch(const int* fan_in, const size_t* in_off, const void* con
 
 template <class Op>
 int run_batched(int b, const int* fan_in, const void* const* in, const float* w, void* const* outs,
-                const size_t* nelem, hipStream_t st) {
+                const size_t* nelem, hipStream_t st, const float* divs = nullptr) {
   std::vector<size_t> off(static_cast<size_t>(b) + 1, 0);
   for (int t = 0; t < b; ++t) off[t + 1] = off[t] + static_cast<size_t>(fan_in[t]);
   const size_t tile = static_cast<size_t>(dlsim::kBlock) * kVpt;
@@ -270,12 +273,12 @@ int run_batched(int b, const int* fan_in, const void* const* in, const float* w,
       continue;
     }
     if (nelem[t] == 0) continue;
-    int rc = run<Op>(in + off[t], fan_in[t], w + off[t], outs[t], nelem[t], st);
+    int rc = run<Op>(in + off[t], fan_in[t], w + off[t], outs[t], nelem[t], st, divs ? divs[t] : 1.0f);
     if (rc != DLSIM_OK) return rc;
   }
   // Pack the rest greedily into kernel-argument batches, in task order.
   std::vector<const void*> ins;
-  std::vector<float> ws;
+  std::vector<float> ws, dv;
   std::vector<void*> os;
   std::vector<size_t> ne, ioff;
   std::vector<int> fi;
@@ -288,6 +291,7 @@ int run_batched(int b, const int* fan_in, const void* const* in, const float* w,
     os.push_back(outs[t]);
     ne.push_back(nelem[t]);
     fi.push_back(fan_in[t]);
+    dv.push_back(divs ? divs[t] : 1.0f);
   }
   const int g = static_cast<int>(group.size());
   int t0 = 0;
@@ -300,8 +304,8 @@ int run_batched(int b, const int* fan_in, const void* const* in, const float* w,
       blocks += ne[t1] / Op::E / tile + 1;
       ++t1;
     }
-    hipError_t e = launch_batch<Op>(fi.data(), ioff.data(), ins.data(), ws.data(), os.data(), ne.data(), t0,
-                                    t1, st);
+    hipError_t e = launch_batch<Op>(fi.data(), ioff.data(), ins.data(), ws.data(), dv.data(), os.data(),
+                                    ne.data(), t0, t1, st);
     if (e != hipSuccess) return hip_fail(e, "batched kernel launch");
     t0 = t1;
   }
@@ -569,6 +573,27 @@ int dlsim_mean(const void* const* d_inputs, int n, void* d_out, size_t n_elems, 
   const float div = static_cast<float>(n);
   return dtype == DLSIM_F32 ? run<dlsim::F32Mean>(d_inputs, n, nullptr, d_out, n_elems, st, div)
                             : run<dlsim::BF16Mean>(d_inputs, n, nullptr, d_out, n_elems, st, div);
+}
+
+int dlsim_mean_batched(int b, const int* fan_in, const void* const* d_inputs, void* const* d_outs,
+                       const size_t* n_elems, int dtype, void* stream) {
+  g_err.clear();
+  if (b < 0) return fail(DLSIM_E_ARG, "b must be >= 0 (got %d)", b);
+  if (b == 0) return DLSIM_OK;
+  if (!fan_in || !d_inputs || !d_outs || !n_elems) return fail(DLSIM_E_ARG, "null array argument");
+  size_t off = 0;
+  std::vector<float> divs(static_cast<size_t>(b));
+  for (int t = 0; t < b; ++t) {
+    int rc = check_args(d_inputs + off, fan_in[t], nullptr, d_outs[t], n_elems[t], dtype, DLSIM_EXACT, false);
+    if (rc != DLSIM_OK) return fail(rc, "task %d: %s", t, g_err.c_str());
+    off += static_cast<size_t>(fan_in[t]);
+    divs[t] = static_cast<float>(fan_in[t]);
+  }
+  const std::vector<float> ones(off, 1.0f);  // unused by the mean policies
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  return dtype == DLSIM_F32
+             ? run_batched<dlsim::F32Mean>(b, fan_in, d_inputs, ones.data(), d_outs, n_elems, st, divs.data())
+             : run_batched<dlsim::BF16Mean>(b, fan_in, d_inputs, ones.data(), d_outs, n_elems, st, divs.data());
 }
 
 int dlsim_shard_range(size_t n_elems, int world, int rank, size_t align_elems, size_t* begin,

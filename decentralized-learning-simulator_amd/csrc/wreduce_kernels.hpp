@@ -461,6 +461,7 @@ struct BatchSlots {
   void* out[kBatchMaxTasks];
   size_t nvec[kBatchMaxTasks];
   size_t nelem[kBatchMaxTasks];
+  float div[kBatchMaxTasks];  // final divisor per task (mean policies; 1 for the reduce)
   uint32_t block_start[kBatchMaxTasks + 1];
   uint16_t ptr_off[kBatchMaxTasks];
   uint16_t fan_in[kBatchMaxTasks];
@@ -471,9 +472,10 @@ struct BatchSlots {
 struct TaskArgs {
   const BatchSlots& b;
   int off;
+  float d;
   __device__ const void* ptr(int i) const { return b.p[off + i]; }
   __device__ float wt(int i) const { return b.w[off + i]; }
-  __device__ float divisor() const { return 1.0f; }
+  __device__ float divisor() const { return d; }
 };
 
 template <class Op, int NF, int G, int VPT, int NT, int STP>
@@ -481,7 +483,7 @@ __global__ __launch_bounds__(kBlock) void k_wreduce_batch(const BatchSlots s) {
   const uint32_t bid = blockIdx.x;
   int t = 0;
   while (t + 1 < s.ntasks && bid >= s.block_start[t + 1]) ++t;  // wave-uniform scan
-  const TaskArgs a{s, s.ptr_off[t]};
+  const TaskArgs a{s, s.ptr_off[t], s.div[t]};
   const int n = NF > 0 ? NF : s.fan_in[t];
   const size_t nvec = s.nvec[t];
   constexpr size_t kTile = static_cast<size_t>(kBlock) * VPT;

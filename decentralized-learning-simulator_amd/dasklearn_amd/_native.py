@@ -31,6 +31,7 @@ EXPORTS = (
     "dlsim_batch_table_fill",
     "dlsim_batch_table_launch",
     "dlsim_mean",
+    "dlsim_mean_batched",
     "dlsim_shard_range",
     "dlsim_probe_copy",
     "dlsim_last_error",
@@ -85,6 +86,9 @@ def load() -> ctypes.CDLL:
         lib.dlsim_batch_table_launch.restype = i
         lib.dlsim_mean.argtypes = [ctypes.POINTER(vp), i, vp, sz, i, vp]
         lib.dlsim_mean.restype = i
+        lib.dlsim_mean_batched.argtypes = [i, ctypes.POINTER(i), ctypes.POINTER(vp), ctypes.POINTER(vp),
+                                           ctypes.POINTER(sz), i, vp]
+        lib.dlsim_mean_batched.restype = i
         lib.dlsim_shard_range.argtypes = [sz, i, i, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)]
         lib.dlsim_shard_range.restype = i
         lib.dlsim_probe_copy.argtypes = [vp, vp, sz, vp]
@@ -278,6 +282,35 @@ def mean(inputs, out, stream=None):
     _check("dlsim_mean", lib.dlsim_mean(ptrs, n, out.data_ptr(), out.numel(), dt,
                                         _stream_handle(out.device, stream)))
     return out
+
+
+def mean_batched(tasks, stream=None):
+    """tasks: sequence of (inputs, out) — independent means (e.g. every chunk
+    index of a reconstruction), launched together (dlsim_mean_batched).
+    Returns the outs."""
+    lib = load()
+    b = len(tasks)
+    if b == 0:
+        return []
+    out0 = tasks[0][1]
+    dt = dtype_code(out0.dtype)
+    fan, ptrs, outs, numels = [], [], [], []
+    for inputs, out in tasks:
+        if len(inputs) < 1:
+            raise IndexError("list index out of range")
+        for t in list(inputs) + [out]:
+            if not t.is_cuda or t.dtype != out0.dtype or t.numel() != out.numel() or not t.is_contiguous() \
+                    or t.device != out0.device:
+                raise ValueError("each task: contiguous device tensors of one dtype and size; one device")
+        fan.append(len(inputs))
+        ptrs.extend(t.data_ptr() for t in inputs)
+        outs.append(out.data_ptr())
+        numels.append(out.numel())
+    _check("dlsim_mean_batched",
+           lib.dlsim_mean_batched(b, (ctypes.c_int * b)(*fan), (ctypes.c_void_p * len(ptrs))(*ptrs),
+                                  (ctypes.c_void_p * b)(*outs), (ctypes.c_size_t * b)(*numels), dt,
+                                  _stream_handle(out0.device, stream)))
+    return [t[1] for t in tasks]
 
 
 def wreduce_tensors(inputs_by_model, weights_f32, outs, mode: int = DLSIM_EXACT, stream=None):

@@ -11,8 +11,9 @@ functions.py:142-146). That average is a second N-way reduce of the hot path
   state_dict and slices of it) and are restated with the same tensor ops, on
   whatever device the model lives.
 * `reconstruct_model`: per chunk index, `torch.mean(torch.stack(chunks), 0)`
-  (chunk_manager.py:38-40) becomes one `dlsim_mean` launch over the chunks —
-  sum in input order from +0, one division by the contributor count. That is
+  (chunk_manager.py:38-40) becomes one task of a `dlsim_mean_batched` launch
+  (every chunk index of the reconstruction in one launch) — sum in input order
+  from +0, one division by the contributor count. That is
   bit-identical to the reference while PyTorch's CPU dim-0 reduction is
   sequential (<= 4 contributors per chunk); with more contributors PyTorch
   switches to a size- and thread-dependent order, so parity is a tolerance
@@ -51,34 +52,83 @@ class ChunkManager:
     def mean_chunks(chunks_at_idx: List[torch.Tensor], device=None) -> torch.Tensor:
         """torch.mean(torch.stack(chunks_at_idx), dim=0) on the GPU; the result
         lives where the first chunk lives."""
-        first = chunks_at_idx[0]
-        for c in chunks_at_idx:
-            if c.shape != first.shape or c.dtype != first.dtype:
-                raise RuntimeError("stack expects each tensor to be equal size")
-        dev = _target_device([first], device)
-        src = [c.reshape(-1) for c in chunks_at_idx]
+        return ChunkManager.mean_chunk_indices([chunks_at_idx], device)[0]
+
+    @staticmethod
+    def mean_chunk_indices(chunks: List[List[torch.Tensor]], device=None) -> List[torch.Tensor]:
+        """[torch.mean(torch.stack(cs), dim=0) for cs in chunks], every chunk
+        index in one batched launch per dtype (dlsim_mean_batched). Device
+        chunks are read in place; host chunks (the reference's case) are staged
+        into one pinned buffer, copied with one H2D, and the means come back
+        with one D2H. Each result lives where its first chunk lives."""
+        for cs in chunks:
+            first = cs[0]
+            for c in cs:
+                if c.shape != first.shape or c.dtype != first.dtype:
+                    raise RuntimeError("stack expects each tensor to be equal size")
+        dev = _target_device([cs[0] for cs in chunks], device)
+        results: List[torch.Tensor] = [None] * len(chunks)
         with torch.no_grad():
-            if first.is_cuda and all(c.device == dev for c in src):
-                rows = [c.contiguous() for c in src]
-            else:
-                stage = torch.empty((len(src), first.numel()), dtype=first.dtype, pin_memory=True)
-                for i, c in enumerate(src):
-                    stage[i].copy_(c)
-                dev_rows = stage.to(dev, non_blocking=True)
-                rows = [dev_rows[i] for i in range(len(src))]
-            out = torch.empty(first.numel(), dtype=first.dtype, device=dev)
-            if out.numel():
-                _native.mean(rows, out)
-            if not first.is_cuda:
-                out = out.cpu()
-        return out.view(first.shape)
+            by_dtype = {}
+            for ci, cs in enumerate(chunks):
+                by_dtype.setdefault(cs[0].dtype, []).append(ci)
+            for dt, idxs in by_dtype.items():
+                on_dev = all(c.is_cuda and c.device == dev for ci in idxs for c in chunks[ci])
+                if on_dev:
+                    tasks = []
+                    for ci in idxs:
+                        rows = [c.reshape(-1).contiguous() for c in chunks[ci]]
+                        tasks.append((rows, torch.empty(rows[0].numel(), dtype=dt, device=dev)))
+                    _native.mean_batched([t for t in tasks if t[1].numel()])
+                    for ci, (_, out) in zip(idxs, tasks):
+                        results[ci] = out.view(chunks[ci][0].shape)
+                    continue
+                # host (or mixed) chunks: rows at 256-B aligned offsets of one
+                # pinned staging buffer, outputs likewise in one device buffer
+                esz = torch.empty((), dtype=dt).element_size()
+                al = 256 // esz
+                rnd = lambda k: (k + al - 1) // al * al  # noqa: E731
+                in_off, out_off, n_in, n_out = [], [], 0, 0
+                for ci in idxs:
+                    k = chunks[ci][0].numel()
+                    offs = []
+                    for _ in chunks[ci]:
+                        offs.append(n_in)
+                        n_in += rnd(k)
+                    in_off.append(offs)
+                    out_off.append(n_out)
+                    n_out += rnd(k)
+                stage = torch.empty(max(n_in, 1), dtype=dt, pin_memory=True)
+                d_in = torch.empty(max(n_in, 1), dtype=dt, device=dev)
+                for ci, offs in zip(idxs, in_off):
+                    for c, o in zip(chunks[ci], offs):
+                        k = c.numel()
+                        stage[o:o + k].copy_(c.reshape(-1))
+                        # this row's DMA overlaps the staging of the next one
+                        d_in[o:o + k].copy_(stage[o:o + k], non_blocking=True)
+                d_out = torch.empty(max(n_out, 1), dtype=dt, device=dev)
+                tasks = []
+                for ci, offs, o in zip(idxs, in_off, out_off):
+                    k = chunks[ci][0].numel()
+                    if k:
+                        tasks.append(([d_in[x:x + k] for x in offs], d_out[o:o + k]))
+                _native.mean_batched(tasks)
+                host = torch.empty(max(n_out, 1), dtype=dt, pin_memory=True)
+                host.copy_(d_out, non_blocking=True)
+                torch.cuda.current_stream(dev).synchronize()
+                for ci, o in zip(idxs, out_off):
+                    first = chunks[ci][0]
+                    src = host if not first.is_cuda else d_out
+                    results[ci] = src[o:o + first.numel()].view(first.shape)
+        return results
 
     @staticmethod
     def reconstruct_model(chunks: List[List[torch.Tensor]], model: nn.Module) -> nn.Module:
         for idx in range(len(chunks)):
             assert chunks[idx], "No chunks received at index %d!" % idx
-        for chunk_idx, chunks_at_idx in enumerate(chunks):
-            chunks[chunk_idx] = ChunkManager.mean_chunks(chunks_at_idx)
+        means = ChunkManager.mean_chunk_indices(chunks)  # one launch for every index
+        for chunk_idx in range(len(chunks)):
+            chunks[chunk_idx] = means[chunk_idx]
         flat_params = torch.cat(chunks)
         pointer = 0
         with torch.no_grad():

@@ -161,6 +161,19 @@ int dlsim_mean(const void* const* d_inputs, int n, void* d_out, size_t n_elems, 
                void* stream);
 
 /*
+ * dlsim_mean_batched — b independent dlsim_mean calls in as few launches as
+ * possible (the kernel-argument batches of dlsim_wreduce_batched, with a
+ * per-task divisor): task t averages fan_in[t] buffers d_inputs[o_t ..
+ * o_t + fan_in[t]) into d_outs[t] (n_elems[t] elements), o_t the prefix sum
+ * of fan_in. Replaces the per-chunk-index loop of
+ * ChunkManager.reconstruct_model (simulation/conflux/chunk_manager.py:38-40):
+ * every chunk index of one reconstruction (or of many) in one launch.
+ * Results are bit-identical to b separate dlsim_mean calls.
+ */
+int dlsim_mean_batched(int b, const int* fan_in, const void* const* d_inputs, void* const* d_outs,
+                       const size_t* n_elems, int dtype, void* stream);
+
+/*
  * dlsim_shard_range — parameter-axis partition used by the sharded path.
  *
  * Splits [0, n_elems) into `world` contiguous slices whose boundaries are

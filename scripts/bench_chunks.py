@@ -1,0 +1,133 @@
+"""Chunked-model reconstruction: the mean of every chunk
+index over its contributors, as Conflux's `reconstruct_from_chunks` task does
+(dasklearn/functions.py:142-146 -> simulation/conflux/chunk_manager.py:38-53),
+for a ResNet-18/CIFAR-10-sized flat model (11,181,642 fp32), k = 10 chunks
+(ConfluxSettings.chunks_in_sample default, conflux/settings.py:11) and m
+contributors per index (success_fraction 1: the sample size).
+
+  kernel      dlsim_mean_batched over device-resident chunks, every index in
+              one launch: HIP events over back-to-back launches, algorithmic
+              bytes (m + 1) * P * 4 per reconstruction
+  device      ChunkManager.reconstruct_model on device chunks (wall)
+  host        the same on host chunks (PCIe-inclusive wall; the reference's case)
+  cpu_ref     the reference's arithmetic on the CPU: per index
+              torch.mean(torch.stack(chunks), 0), then cat + copy, 4 threads
+
+    python scripts/bench_chunks.py
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "decentralized-learning-simulator_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import torch  # noqa: E402
+from torch import nn  # noqa: E402
+
+from dasklearn_amd import _native  # noqa: E402
+from dasklearn_amd.chunk_manager import ChunkManager  # noqa: E402
+
+P = 11_181_642
+
+
+class Flat(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.w = nn.Parameter(torch.zeros(P))
+
+
+def med(f, reps=10, sync=True):
+    f()
+    if sync:
+        torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        f()
+        if sync:
+            torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+def cpu_reconstruct(chunks, model):
+    means = [torch.mean(torch.stack(cs), dim=0) for cs in chunks]
+    flat = torch.cat(means)
+    with torch.no_grad():
+        off = 0
+        for t in model.state_dict().values():
+            t.copy_(flat[off:off + t.numel()].view(t.shape))
+            off += t.numel()
+    return model
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    k = 10
+    for m in (4, 10):
+        g = torch.Generator().manual_seed(m)
+        flats = [torch.randn(P, generator=g) * 0.05 for _ in range(m)]
+        host_chunks = [ChunkManager.chunk_model(_wrap(f), k) for f in flats]  # [model][index]
+        by_index = [[host_chunks[i][c] for i in range(m)] for c in range(k)]
+        dflats = [f.to(dev) for f in flats]
+        dev_chunks = [ChunkManager.chunk_model(_wrap(f), k) for f in dflats]
+        dev_by_index = [[dev_chunks[i][c] for i in range(m)] for c in range(k)]
+        byts = (m + 1) * P * 4
+        res = {"k": k, "m": m, "params": P, "bytes": byts}
+        # kernel only: one batched launch per reconstruction, 3 rotating output sets
+        outs = [[torch.empty(cs[0].numel(), device=dev) for cs in dev_by_index] for _ in range(3)]
+        tasks = [[(cs, o) for cs, o in zip(dev_by_index, outs[s])] for s in range(3)]
+        for s in range(3):
+            _native.mean_batched(tasks[s])
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = 50
+        torch.cuda.synchronize()
+        e0.record()
+        for r in range(reps):
+            _native.mean_batched(tasks[r % 3])
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / reps
+        res["kernel_us"] = round(us, 2)
+        res["kernel_GBps"] = round(byts / us / 1e3, 1)
+        res["kernel_frac_of_8TBps"] = round(byts / us / 1e3 / 8000.0, 4)
+        # per-index launches (the unbatched form) for comparison
+        torch.cuda.synchronize()
+        e0.record()
+        for r in range(reps):
+            for cs, o in tasks[r % 3]:
+                _native.mean(cs, o)
+        e1.record()
+        torch.cuda.synchronize()
+        res["per_index_launches_us"] = round(e0.elapsed_time(e1) * 1e3 / reps, 2)
+        tgt_d = Flat().to(dev)
+        res["device_ms"] = round(med(lambda: ChunkManager.reconstruct_model([list(c) for c in dev_by_index],
+                                                                           tgt_d)) * 1e3, 3)
+        tgt_h = Flat()
+        res["host_ms"] = round(med(lambda: ChunkManager.reconstruct_model([list(c) for c in by_index],
+                                                                         tgt_h)) * 1e3, 3)
+        res["host_GBps"] = round(byts / (res["host_ms"] * 1e-3) / 1e9, 2)
+        torch.set_num_threads(4)
+        tgt_c = Flat()
+        res["cpu_ref_4t_ms"] = round(med(lambda: cpu_reconstruct([list(c) for c in by_index], tgt_c),
+                                         reps=5, sync=False) * 1e3, 3)
+        res["cpu_ref_4t_GBps"] = round(byts / (res["cpu_ref_4t_ms"] * 1e-3) / 1e9, 2)
+        print(json.dumps(res), flush=True)
+        del dflats, dev_chunks, dev_by_index, outs, tasks
+
+
+def _wrap(flat):
+    m = Flat()
+    m.w = nn.Parameter(flat, requires_grad=False)
+    return m
+
+
+if __name__ == "__main__":
+    main()

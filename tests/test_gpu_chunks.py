@@ -92,3 +92,49 @@ def test_reconstruct_task_function_uses_factory():
         assert orc.same_bits(got, d["expected"])
     chunked = functions.chunk(S(), {"model": res[0], "n": 3})
     assert len(chunked) == 3 and sum(c.numel() for c in chunked) == got.size
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_mean_batched_equals_separate_means(dtype):
+    """dlsim_mean_batched: 40 tasks (two kernel-argument batches), fan-in 1..20
+    (the > 16 ones run alone), ragged sizes: each task bit-identical to the
+    oracle mean (n <= 128: one pass)."""
+    rng = np.random.default_rng(3)
+    tasks, exp = [], []
+    for t in range(40):
+        n = 1 + (t * 7) % 20
+        p = 1 + int(rng.integers(1, 5000))
+        x = rng.standard_normal((n, p)).astype(np.float32)
+        rows = orc.f32_to_bf16_bits(x) if dtype == "bf16" else x
+        if dtype == "bf16":
+            xs = [torch.from_numpy(r.view(np.int16).copy()).view(torch.bfloat16).to(dev()) for r in rows]
+        else:
+            xs = [torch.from_numpy(r.copy()).to(dev()) for r in rows]
+        tasks.append((xs, torch.empty(p, dtype=xs[0].dtype, device=dev())))
+        exp.append(orc.mean(list(rows), dtype))
+    _native.mean_batched(tasks)
+    for (_, out), e in zip(tasks, exp):
+        got = out.cpu()
+        got = got.view(torch.int16).numpy().view(np.uint16) if dtype == "bf16" else got.numpy()
+        assert orc.same_bits(got, e)
+
+
+@pytest.mark.parametrize("where", ["host", "device"])
+def test_mean_chunk_indices_one_launch_per_dtype(where):
+    """Every chunk index of a reconstruction in one batched launch, host chunks
+    through one staging buffer: same bits as one dlsim_mean per index; results
+    live where their first chunk lives."""
+    rng = np.random.default_rng(9)
+    chunks = []
+    for c in range(10):
+        p = 777 + 13 * c
+        dt = torch.bfloat16 if c % 3 == 2 else torch.float32
+        cs = [torch.from_numpy(rng.standard_normal(p).astype(np.float32)).to(dt) for _ in range(1 + c % 6)]
+        chunks.append([t.to(dev()) for t in cs] if where == "device" else cs)
+    means = ChunkManager.mean_chunk_indices(chunks)
+    for cs, m in zip(chunks, means):
+        assert m.is_cuda == (where == "device") and m.dtype == cs[0].dtype and m.shape == cs[0].shape
+        ref = torch.empty(cs[0].numel(), dtype=cs[0].dtype, device=dev())
+        _native.mean([t.to(dev()).reshape(-1) for t in cs], ref)
+        assert torch.equal(m.cpu().view(torch.int16 if m.dtype == torch.bfloat16 else torch.int32),
+                           ref.cpu().view(torch.int16 if m.dtype == torch.bfloat16 else torch.int32))
