@@ -9,7 +9,8 @@ contributors per index (success_fraction 1: the sample size).
               one launch: HIP events over back-to-back launches, algorithmic
               bytes (m + 1) * P * 4 per reconstruction
   device      ChunkManager.reconstruct_model on device chunks (wall)
-  host        the same on host chunks (PCIe-inclusive wall; the reference's case)
+  host        the same on host chunks (PCIe-inclusive wall; the reference's case),
+              at the box's default threads and at the worker's 4
   cpu_ref     the reference's arithmetic on the CPU: per index
               torch.mean(torch.stack(chunks), 0), then cat + copy, 4 threads
 
@@ -114,11 +115,15 @@ def main():
         res["host_ms"] = round(med(lambda: ChunkManager.reconstruct_model([list(c) for c in by_index],
                                                                          tgt_h)) * 1e3, 3)
         res["host_GBps"] = round(byts / (res["host_ms"] * 1e-3) / 1e9, 2)
+        nt = torch.get_num_threads()
         torch.set_num_threads(4)
+        res["host_4t_ms"] = round(med(lambda: ChunkManager.reconstruct_model([list(c) for c in by_index],
+                                                                            tgt_h)) * 1e3, 3)
         tgt_c = Flat()
         res["cpu_ref_4t_ms"] = round(med(lambda: cpu_reconstruct([list(c) for c in by_index], tgt_c),
                                          reps=5, sync=False) * 1e3, 3)
         res["cpu_ref_4t_GBps"] = round(byts / (res["cpu_ref_4t_ms"] * 1e-3) / 1e9, 2)
+        torch.set_num_threads(nt)
         print(json.dumps(res), flush=True)
         del dflats, dev_chunks, dev_by_index, outs, tasks
 

@@ -83,3 +83,18 @@ def test_chunk_remainder_goes_to_last_chunk():
     m = Net([[10], [3]])
     chunks = ChunkManager.chunk_model(m, 4)  # 13 = 3+3+3+4
     assert [c.numel() for c in chunks] == [3, 3, 3, 4]
+
+
+def test_span_is_a_cat_only_for_back_to_back_views():
+    """reconstruct_model skips torch.cat when the chunk means already lie back
+    to back in one buffer (chunk_manager._span); anything else still cats."""
+    from dasklearn_amd.chunk_manager import _span
+    buf = torch.arange(20.0)
+    views = [buf[0:4], buf[4:12], buf[12:19]]
+    s = _span(views)
+    assert s is not None and torch.equal(s, torch.cat(views)) and s.data_ptr() == buf.data_ptr()
+    assert _span([buf[0:4], buf[5:8]]) is None  # gap
+    assert _span([buf[4:8], buf[0:4]]) is None  # out of order
+    assert _span([buf[0:4], torch.arange(4.0)]) is None  # other storage
+    assert _span([buf[0:8:2]]) is None  # strided
+    assert _span([buf.view(4, 5)]) is None  # not flat
