@@ -25,6 +25,7 @@
  */
 #include <math.h>
 #include <stddef.h>
+#include <stdlib.h>
 #include <stdint.h>
 #include <string.h>
 
@@ -116,7 +117,8 @@ int oracle_wreduce_fast_bf16(const uint16_t* const* in, int n, const float* w, u
  * it while its dim-0 reduction is sequential (n <= 4): acc = +0, acc += x_i
  * in order, then one IEEE division by n (sum followed by div_).
  * Restates simulation/conflux/chunk_manager.py:38-40 for the chunked path.
- * bf16: the fp32 sum is rounded to bf16, then divided and rounded again. */
+ * bf16: the fp32 sum is divided in fp32 and rounded to bf16 once (mean_out
+ * on CPU sums a bf16 input in fp32, divides, then casts back). */
 int oracle_mean_f32(const float* const* in, int n, float* out, size_t p) {
   if (n < 1 || !in || !out) return -1;
   for (size_t j = 0; j < p; ++j) {
@@ -132,7 +134,147 @@ int oracle_mean_bf16(const uint16_t* const* in, int n, uint16_t* out, size_t p) 
   for (size_t j = 0; j < p; ++j) {
     float acc = 0.0f;
     for (int i = 0; i < n; ++i) acc = acc + oracle_bf16_to_f32(in[i][j]);
-    out[j] = oracle_f32_to_bf16(bf16r(acc) / (float)n);
+    out[j] = oracle_f32_to_bf16(acc / (float)n);
   }
   return 0;
+}
+
+/* ---- torch.mean(torch.stack(rows), 0) in PyTorch's own CPU order ----------
+ *
+ * The reference's chunk mean (simulation/conflux/chunk_manager.py:40) runs on
+ * the worker's CPU at settings.torch_threads intra-op threads (broker.py:31,
+ * session_settings.py:52). On CPU, mean = sum over dim 0 then div_ (fp32; a
+ * bf16 input is summed in fp32, divided, and rounded once). The sum is ATen's
+ * cascade_sum (SumKernel.cpp), whose order per output column is:
+ *
+ *  - columns are split over T threads by parallel_dim_reduction
+ *    (TensorIteratorReduce.cpp): only when m*n >= 32768 (GRAIN_SIZE) and
+ *    T > 1; T' = min(T, n) ranges of ceil(n/T') columns, both ends rounded
+ *    down to 32 columns (128 B), the final end kept;
+ *  - within a range of s1 columns, vectorized_outer_sum (s1 >= 8, the float
+ *    vector width of the AVX2 kernel, which AVX512 machines also run for sum)
+ *    folds whole 32-column blocks with multi_row_sum ("cascade" below) and the
+ *    rest with row_sum ("ilp"); for s1 < 8, scalar_outer_sum folds groups of
+ *    4 columns with multi_row_sum and the rest with row_sum;
+ *  - n == 1 (a one-element chunk) is an inner reduction: vectorized_inner_sum
+ *    ("inner") for m >= 8, row_sum otherwise.
+ *
+ * Every rule above was checked against torch.mean on this image for
+ * T in {1,2,3,4,8}, m in 1..513, n in 1..1,118,166 (tests/test_chunk_mean_order.py).
+ * All chunk-internal ranges have 32-multiple lengths, so the only non-cascade
+ * columns are the last < 32 columns of the final range: ilp_begin below. */
+
+static int ceil_log2_i64(long long x) {
+  if (x <= 2) return 1;
+  int b = 0;
+  unsigned long long v = (unsigned long long)(x - 1);
+  while (v) { ++b; v >>= 1; }
+  return b;
+}
+
+/* multi_row_sum over S values x[0], x[st], x[2 st], ...: 4 accumulator levels,
+ * 2^lp values per level-0 block. */
+static float cascade_sum(const float* x, long long S, long long st) {
+  int lp = ceil_log2_i64(S) / 4;
+  if (lp < 4) lp = 4;
+  const long long step = 1LL << lp, mask = step - 1;
+  float a[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  long long i = 0;
+  while (i + step <= S) {
+    for (long long j = 0; j < step; ++j, ++i) a[0] = a[0] + x[i * st];
+    for (int l = 1; l < 4; ++l) {
+      a[l] = a[l] + a[l - 1];
+      a[l - 1] = 0.0f;
+      if ((i & (mask << (l * lp))) != 0) break;
+    }
+  }
+  for (; i < S; ++i) a[0] = a[0] + x[i * st];
+  for (int l = 1; l < 4; ++l) a[0] = a[0] + a[l];
+  return a[0];
+}
+
+/* row_sum: 4 interleaved cascades (ILP), the remainder into the first, then
+ * ((p0 + p1) + p2) + p3. */
+static float ilp_sum(const float* x, long long len, long long st) {
+  const long long s = len / 4;
+  float p[4];
+  for (int k = 0; k < 4; ++k) p[k] = cascade_sum(x + k * st, s, 4 * st);
+  for (long long i = 4 * s; i < len; ++i) p[0] = p[0] + x[i * st];
+  return ((p[0] + p[1]) + p[2]) + p[3];
+}
+
+/* vectorized_inner_sum over a contiguous run of m values (8 lanes). */
+static float inner_sum(const float* x, long long m) {
+  const long long vs = m / 8;
+  float fin = 0.0f;
+  for (long long k = vs * 8; k < m; ++k) fin = fin + x[k];
+  for (int l = 0; l < 8; ++l) fin = fin + ilp_sum(x + l, vs, 8);
+  return fin;
+}
+
+size_t oracle_chunk_mean_ilp_begin(int m, size_t n, int threads) {
+  if (n == 0) return 0;
+  if (n == 1) return 0;
+  size_t b = 0, e = n;
+  if (!((unsigned long long)m * n < 32768ULL || threads <= 1)) {
+    const size_t tp = (size_t)threads < n ? (size_t)threads : n;
+    const size_t cs = (n + tp - 1) / tp;
+    for (size_t t = 0; t < tp; ++t) {
+      size_t tb = t * cs;
+      if (tb >= n) break;
+      size_t te = tb + cs < n ? tb + cs : n;
+      tb -= tb % 32;
+      if (te != n) te -= te % 32;
+      if (tb < te) { b = tb; e = te; }
+    }
+  }
+  const size_t s1 = e - b;
+  const size_t main = s1 >= 8 ? s1 / 32 * 32 : s1 / 4 * 4;
+  return b + main;
+}
+
+int oracle_chunk_mean_f32(const float* const* in, int m, float* out, size_t n, int threads) {
+  if (m < 1 || !in || !out) return -1;
+  const size_t cb = 4096;
+  float* col = (float*)malloc(sizeof(float) * (size_t)m * cb);
+  if (!col) return -2;
+  const size_t ib = oracle_chunk_mean_ilp_begin(m, n, threads);
+  for (size_t j0 = 0; j0 < n; j0 += cb) {
+    const size_t c = n - j0 < cb ? n - j0 : cb;
+    for (size_t j = 0; j < c; ++j)
+      for (int i = 0; i < m; ++i) col[j * (size_t)m + i] = in[i][j0 + j];
+    for (size_t j = 0; j < c; ++j) {
+      const float* x = col + j * (size_t)m;
+      const size_t g = j0 + j;
+      float s;
+      if (n == 1) s = m >= 8 ? inner_sum(x, m) : ilp_sum(x, m, 1);
+      else if (g < ib) s = cascade_sum(x, m, 1);
+      else s = ilp_sum(x, m, 1);
+      out[g] = s / (float)m;
+    }
+  }
+  free(col);
+  return 0;
+}
+
+int oracle_chunk_mean_bf16(const uint16_t* const* in, int m, uint16_t* out, size_t n, int threads) {
+  if (m < 1 || !in || !out) return -1;
+  float* tmp = (float*)malloc(sizeof(float) * (n ? n : 1));
+  float** rows = (float**)malloc(sizeof(float*) * (size_t)m);
+  if (!tmp || !rows) { free(tmp); free(rows); return -2; }
+  int rc = 0;
+  /* widen each row to fp32 (the sum_out(Float) input cast), then the fp32 order */
+  for (int i = 0; i < m && rc == 0; ++i) {
+    rows[i] = (float*)malloc(sizeof(float) * (n ? n : 1));
+    if (!rows[i]) { rc = -2; for (int k = 0; k < i; ++k) free(rows[k]); break; }
+    for (size_t j = 0; j < n; ++j) rows[i][j] = oracle_bf16_to_f32(in[i][j]);
+  }
+  if (rc == 0) {
+    rc = oracle_chunk_mean_f32((const float* const*)rows, m, tmp, n, threads);
+    for (size_t j = 0; j < n && rc == 0; ++j) out[j] = oracle_f32_to_bf16(tmp[j]);
+    for (int i = 0; i < m; ++i) free(rows[i]);
+  }
+  free(tmp);
+  free(rows);
+  return rc;
 }

@@ -51,6 +51,12 @@ def _load():
         fn = getattr(lib, name)
         fn.argtypes = [pp, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t]
         fn.restype = ctypes.c_int
+    for name in ("oracle_chunk_mean_f32", "oracle_chunk_mean_bf16"):
+        fn = getattr(lib, name)
+        fn.argtypes = [pp, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        fn.restype = ctypes.c_int
+    lib.oracle_chunk_mean_ilp_begin.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int]
+    lib.oracle_chunk_mean_ilp_begin.restype = ctypes.c_size_t
     lib.oracle_wreduce_f32_rows.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                                             ctypes.c_void_p, ctypes.c_size_t]
     lib.oracle_wreduce_f32_rows.restype = ctypes.c_int
@@ -110,8 +116,9 @@ def wreduce(xs, weights, dtype: str = "f32", mode: str = "exact") -> np.ndarray:
 
 
 def mean(xs, dtype: str = "f32") -> np.ndarray:
-    """Sequential mean (sum from +0, one division): torch.mean(torch.stack(xs), 0)
-    while PyTorch's dim-0 reduction is sequential (n <= 4)."""
+    """Sequential mean (sum from +0, one division; bf16 rounded once):
+    torch.mean(torch.stack(xs), 0) while PyTorch's CPU dim-0 reduction is
+    sequential (see chunk_mean for its exact order)."""
     lib = _load()
     n = len(xs)
     if n < 1:
@@ -128,6 +135,34 @@ def mean(xs, dtype: str = "f32") -> np.ndarray:
     if fn(ctypes.cast(ptrs, ctypes.POINTER(ctypes.c_void_p)), n, out.ctypes.data, p) != 0:
         raise RuntimeError("oracle mean failed")
     return out
+
+
+def chunk_mean(xs, dtype: str = "f32", threads: int = 4) -> np.ndarray:
+    """torch.mean(torch.stack(xs), 0) exactly as PyTorch's CPU kernels compute
+    it at `threads` intra-op threads (simulation/conflux/chunk_manager.py:40
+    under broker.py:31's torch.set_num_threads(settings.torch_threads)):
+    ATen's cascade_sum column order, then one division (fedavg_oracle.c)."""
+    lib = _load()
+    n = len(xs)
+    if n < 1:
+        raise IndexError("list index out of range")
+    if dtype == "f32":
+        rows, p = _as_rows(xs, np.float32)
+        out = np.empty(p, dtype=np.float32)
+        fn = lib.oracle_chunk_mean_f32
+    else:
+        rows, p = _as_rows(xs, np.uint16)
+        out = np.empty(p, dtype=np.uint16)
+        fn = lib.oracle_chunk_mean_bf16
+    ptrs = (ctypes.c_void_p * n)(*[r.ctypes.data for r in rows])
+    if fn(ctypes.cast(ptrs, ctypes.POINTER(ctypes.c_void_p)), n, out.ctypes.data, p, threads) != 0:
+        raise RuntimeError("oracle chunk mean failed")
+    return out
+
+
+def chunk_mean_ilp_begin(m: int, n: int, threads: int) -> int:
+    """First column that PyTorch's CPU sum folds in row_sum (ILP) order."""
+    return int(_load().oracle_chunk_mean_ilp_begin(m, n, threads))
 
 
 def wreduce_rows_f32(x: np.ndarray, weights) -> np.ndarray:

@@ -98,3 +98,15 @@ def test_span_is_a_cat_only_for_back_to_back_views():
     assert _span([buf[0:4], torch.arange(4.0)]) is None  # other storage
     assert _span([buf[0:8:2]]) is None  # strided
     assert _span([buf.view(4, 5)]) is None  # not flat
+
+
+@pytest.mark.parametrize("path", CHUNK_FIXTURES, ids=lambda p: os.path.basename(p)[:-4])
+def test_chunk_mean_oracle_bit_exact_vs_reference(path):
+    """The order-exact restatement (oracle.chunk_mean: ATen's cascade_sum
+    column order at the fixture's torch_threads) reproduces every chunk mean
+    the reference's ChunkManager produced, for every contributor count."""
+    d = load(path)
+    k, counts = d["meta"]["num_chunks"], d["meta"]["counts"]
+    got = np.concatenate([orc.chunk_mean(list(d[f"chunks_{c}"]), "f32", d["meta"]["torch_threads"])
+                          for c in range(k)])
+    assert orc.same_bits(got, d["expected"])
