@@ -1,0 +1,341 @@
+// chunk_mean_kernels.hpp — gfx950 kernels for the chunk mean of the chunked
+// algorithms (Conflux/Shatter): torch.mean(torch.stack(chunks), dim=0) per
+// chunk index (reference simulation/conflux/chunk_manager.py:38-40), computed
+// in PyTorch's own CPU summation order so the result is bit-identical to the
+// reference's worker at settings.torch_threads threads (broker.py:31).
+//
+// PyTorch's CPU mean is a sum over dim 0 followed by one division (a bf16
+// input is summed in fp32, divided, and rounded once). The sum is ATen's
+// cascade_sum; the host (dlsim_abi.hip, chunk_mean_ilp_begin) classifies the
+// columns of a chunk into two orders, restated in oracle/fedavg_oracle.c and
+// pinned against torch.mean (tests/test_chunk_mean_order.py):
+//
+//   cascade  columns [0, ilp_begin): multi_row_sum — rows folded in order
+//            into a level-0 accumulator from +0; after every 16 rows the
+//            level-0 sum is added into level 1 (and level 1 into level 2
+//            every 256 rows, ...); at the end level 0 + level 1 + ...
+//   ilp      columns [ilp_begin, n) (< 32 of them): row_sum — four
+//            interleaved cascades over rows k, k+4, k+8, ... (k = 0..3), the
+//            m mod 4 remaining rows added to the first, then
+//            ((p0 + p1) + p2) + p3;
+//   inner    a one-element chunk with m >= 8 (vectorized_inner_sum): eight
+//            lanes l, each the ilp order over rows l, l+8, ...; the m mod 8
+//            remaining rows summed from +0, then the eight lanes added in turn.
+//
+// Layout of the work: every chunk index is one task of a batched grid (the
+// kernel-argument batches of k_wreduce_batch). The cascade columns stream in
+// tiles of 256 lanes x VPT 16-byte vectors, one lane folding its elements'
+// m terms in registers in row order (no cross-lane step: the order is per
+// element). Block 0 of a task — dispatched first — takes the task's ragged
+// end: the partial tile, then the < 40 scalar columns (the cascade columns
+// past the last whole vector and the ilp/inner columns), whose rows it stages
+// through LDS 64 at a time so one thread per column folds them at LDS speed.
+#pragma once
+
+#include "wreduce_kernels.hpp"
+
+#pragma clang fp contract(off)
+
+namespace dlsim {
+
+constexpr int kCmMaxTasks = 32;
+constexpr int kCmMaxPtrs = 192;
+constexpr int kCmTailRows = 64;  // rows staged per LDS round in block 0
+constexpr int kCmTailCols = 64;  // scalar columns of a task (< E + 32)
+
+enum : uint8_t { kCmVec = 1, kCmInner = 2 };
+
+struct ChunkMeanSlots {
+  const void* p[kCmMaxPtrs];
+  void* out[kCmMaxTasks];
+  size_t nelem[kCmMaxTasks];
+  size_t ilp_begin[kCmMaxTasks];
+  uint32_t block_start[kCmMaxTasks + 1];
+  uint16_t ptr_off[kCmMaxTasks];
+  uint16_t m[kCmMaxTasks];
+  uint8_t flags[kCmMaxTasks];
+  int ntasks;
+};
+
+struct PtrArgs {
+  const void* const* p;
+  __device__ const void* ptr(int i) const { return p[i]; }
+};
+
+// One element's cascade (multi_row_sum with 16-value blocks and 4 levels).
+struct CascadeSum {
+  float a[4];
+  __device__ void init() { a[0] = a[1] = a[2] = a[3] = 0.0f; }
+  // value number i (0-based) of the sequence, in order
+  __device__ void add(long long i, float x) {
+    a[0] = a[0] + x;
+    if (((i + 1) & 15) == 0) flush(i + 1);
+  }
+  __device__ void flush(long long i) {
+#pragma unroll
+    for (int l = 1; l < 4; ++l) {
+      a[l] = a[l] + a[l - 1];
+      a[l - 1] = 0.0f;
+      if ((i & (15LL << (4 * l))) != 0) break;
+    }
+  }
+  __device__ float result() const { return ((a[0] + a[1]) + a[2]) + a[3]; }
+};
+
+// One element's row_sum (ilp) order over a sequence of `len` values.
+struct IlpSum {
+  float a[4][4];  // [level][k]
+  float p[4];
+  long long s;    // values per interleaved cascade (len / 4)
+  bool done;
+  __device__ void init(long long len) {
+    s = len / 4;
+    done = false;
+#pragma unroll
+    for (int l = 0; l < 4; ++l)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) a[l][k] = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) p[k] = 0.0f;
+  }
+  __device__ void add(long long idx, float x) {
+    if (idx < 4 * s) {
+      const int k = static_cast<int>(idx & 3);
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk)  // constant indices: the state stays in VGPRs
+        if (kk == k) a[0][kk] = a[0][kk] + x;
+      const long long i = (idx >> 2) + 1;  // groups of 4 completed
+      if (k == 3 && (i & 15) == 0) {
+#pragma unroll
+        for (int l = 1; l < 4; ++l) {
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) {
+            a[l][kk] = a[l][kk] + a[l - 1][kk];
+            a[l - 1][kk] = 0.0f;
+          }
+          if ((i & (15LL << (4 * l))) != 0) break;
+        }
+      }
+    } else {
+      if (!done) finish();
+      p[0] = p[0] + x;
+    }
+  }
+  __device__ void finish() {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) p[k] = ((a[0][k] + a[1][k]) + a[2][k]) + a[3][k];
+    done = true;
+  }
+  __device__ float result() {
+    if (!done) finish();
+    return ((p[0] + p[1]) + p[2]) + p[3];
+  }
+};
+
+// Raw 16-byte slot of E elements from a buffer of unknown alignment (scalar
+// loads; elements at or past `lim` read as 0).
+template <class Op>
+__device__ __forceinline__ u32x4 ld_slot_scalar(const void* base, size_t v, size_t lim) {
+  u32x4 r = {0u, 0u, 0u, 0u};
+  const size_t j0 = v * Op::E;
+  if constexpr (Op::kBytes == 4) {
+    const uint32_t* q = static_cast<const uint32_t*>(base);
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (j0 + e < lim) r[e] = q[j0 + e];
+  } else {
+    const uint16_t* q = static_cast<const uint16_t*>(base);
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if (j0 + e < lim) r[e >> 1] |= static_cast<uint32_t>(q[j0 + e]) << (16 * (e & 1));
+  }
+  return r;
+}
+
+// Cascade fold of m rows for the VPT slots v0 + k*kBlock of one lane.
+// LV: accumulator levels in use (2 while m < 256, else 4).
+// VEC: 16-B aligned task (vector loads, buffer stores); else scalar access.
+template <class Op, class A, int VPT, int LV, bool VEC, bool CHECK>
+__device__ __forceinline__ void cm_tile(const A& a, int m, const OutRef& o, size_t v0, size_t nvec,
+                                        size_t ncol, float div) {
+  float acc[LV][VPT][Op::E];
+#pragma unroll
+  for (int l = 0; l < LV; ++l)
+#pragma unroll
+    for (int v = 0; v < VPT; ++v)
+#pragma unroll
+      for (int e = 0; e < Op::E; ++e) acc[l][v][e] = 0.0f;
+  for (int i0 = 0; i0 < m; i0 += 16) {
+    const int cnt = m - i0 < 16 ? m - i0 : 16;
+#pragma unroll
+    for (int h = 0; h < 16; h += 8) {
+      if (h < cnt) {
+        u32x4 r[8][VPT];
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+          if (h + g < cnt) {
+            const void* src = a.ptr(i0 + h + g);
+#pragma unroll
+            for (int v = 0; v < VPT; ++v) {
+              const size_t idx = v0 + static_cast<size_t>(v) * kBlock;
+              if constexpr (VEC) {
+                if (!CHECK || idx < nvec) r[g][v] = ld16<1>(src, idx);
+                else r[g][v] = u32x4{0u, 0u, 0u, 0u};
+              } else {
+                r[g][v] = (!CHECK || idx < nvec) ? ld_slot_scalar<Op>(src, idx, ncol) : u32x4{0u, 0u, 0u, 0u};
+              }
+            }
+          }
+        }
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+          if (h + g < cnt) {
+#pragma unroll
+            for (int v = 0; v < VPT; ++v) {
+              float x[Op::E];
+              unpack<Op>(r[g][v], x);
+#pragma unroll
+              for (int e = 0; e < Op::E; ++e) acc[0][v][e] = acc[0][v][e] + x[e];
+            }
+          }
+        }
+      }
+    }
+    if (cnt == 16) {
+      const int i = i0 + 16;
+#pragma unroll
+      for (int l = 1; l < LV; ++l) {
+#pragma unroll
+        for (int v = 0; v < VPT; ++v)
+#pragma unroll
+          for (int e = 0; e < Op::E; ++e) {
+            acc[l][v][e] = acc[l][v][e] + acc[l - 1][v][e];
+            acc[l - 1][v][e] = 0.0f;
+          }
+        if ((i & (15 << (4 * l))) != 0) break;
+      }
+    }
+  }
+#pragma unroll
+  for (int l = 1; l < LV; ++l)
+#pragma unroll
+    for (int v = 0; v < VPT; ++v)
+#pragma unroll
+      for (int e = 0; e < Op::E; ++e) acc[0][v][e] = acc[0][v][e] + acc[l][v][e];
+#pragma unroll
+  for (int v = 0; v < VPT; ++v) {
+    const size_t idx = v0 + static_cast<size_t>(v) * kBlock;
+    if (CHECK && idx >= nvec) continue;
+    if constexpr (VEC) {
+      store_vec<Op::kBytes == 4 ? 16 : kStNT>(o, idx, pack<Op>(acc[0][v], div));
+    } else {
+#pragma unroll
+      for (int e = 0; e < Op::E; ++e) {
+        const size_t j = idx * Op::E + e;
+        if (j < ncol) store_elem<Op>(o.ptr, j, acc[0][v][e], div);
+      }
+    }
+  }
+}
+
+// Block 0 of a task: the scalar columns [c0, n) — cascade order below
+// ilp_begin, ilp order from it (or the inner order for a one-element chunk) —
+// staged through LDS kCmTailRows rows at a time.
+template <class Op, class A>
+__device__ __forceinline__ void cm_scalar_cols(const A& a, int m, void* out, size_t c0, size_t n,
+                                               size_t ilp_begin, bool inner, float div) {
+  __shared__ float st[kCmTailRows][kCmTailCols];
+  const int W = static_cast<int>(n - c0);  // block-uniform, <= kCmTailCols
+  const int tid = threadIdx.x;
+  const size_t col = c0 + static_cast<size_t>(tid);
+  const bool is_ilp = col >= ilp_begin;
+  const long long vs = m / 8;  // inner: 8-lane vectors
+  CascadeSum cs;
+  IlpSum il;
+  cs.init();
+  il.init(inner ? vs : m);
+  float fin = 0.0f;  // inner: the m mod 8 trailing rows, from +0
+  for (int r0 = 0; r0 < m; r0 += kCmTailRows) {
+    const int rc = m - r0 < kCmTailRows ? m - r0 : kCmTailRows;
+    for (int idx = tid; idx < rc * W; idx += kBlock) {
+      const int row = idx / W, c = idx - row * W;
+      st[row][c] = load_elem<Op>(a.ptr(r0 + row), c0 + static_cast<size_t>(c));
+    }
+    __syncthreads();
+    if (!inner) {
+      if (tid < W) {
+        for (int rr = 0; rr < rc; ++rr) {
+          const float x = st[rr][tid];
+          if (is_ilp) il.add(r0 + rr, x);
+          else cs.add(r0 + rr, x);
+        }
+      }
+    } else if (tid < 8) {
+      for (int rr = 0; rr < rc; ++rr) {
+        const long long i = r0 + rr;
+        if (i < 8 * vs && (i & 7) == tid) il.add(i >> 3, st[rr][0]);
+        if (tid == 0 && i >= 8 * vs) fin = fin + st[rr][0];
+      }
+    }
+    __syncthreads();
+  }
+  if (!inner) {
+    if (tid < W) store_elem<Op>(out, col, is_ilp ? il.result() : cs.result(), div);
+    return;
+  }
+  if (tid < 8) st[0][tid] = il.result();
+  __syncthreads();
+  if (tid == 0) {
+#pragma unroll
+    for (int l = 0; l < 8; ++l) fin = fin + st[0][l];
+    store_elem<Op>(out, 0, fin, div);
+  }
+}
+
+// One task's share of the grid: local block 0 does the ragged end, local
+// block b >= 1 the full tile b - 1 of the cascade columns.
+template <class Op, class A, int VPT, int LV>
+__device__ __forceinline__ void cm_task(const A& a, int m, void* out, size_t n, size_t ilp_begin,
+                                        uint8_t flags, uint32_t local) {
+  const float div = static_cast<float>(m);
+  const size_t nvec = ilp_begin / Op::E;  // whole vectors of cascade columns
+  constexpr size_t kTile = static_cast<size_t>(kBlock) * VPT;
+  const size_t full = nvec / kTile;
+  const bool vec = (flags & kCmVec) != 0;
+  const OutRef o = make_out<Op::kBytes == 4 ? 16 : kStNT>(out, vec ? nvec : 0);
+  if (local == 0) {
+    if (full * kTile < nvec) {
+      if (vec) cm_tile<Op, A, VPT, LV, true, true>(a, m, o, full * kTile + threadIdx.x, nvec, ilp_begin, div);
+      else cm_tile<Op, A, VPT, LV, false, true>(a, m, o, full * kTile + threadIdx.x, nvec, ilp_begin, div);
+    }
+    const size_t c0 = nvec * Op::E;
+    if (c0 < n) cm_scalar_cols<Op, A>(a, m, out, c0, n, ilp_begin, (flags & kCmInner) != 0, div);
+    return;
+  }
+  const size_t v0 = static_cast<size_t>(local - 1) * kTile + threadIdx.x;
+  if (vec) cm_tile<Op, A, VPT, LV, true, false>(a, m, o, v0, nvec, ilp_begin, div);
+  else cm_tile<Op, A, VPT, LV, false, false>(a, m, o, v0, nvec, ilp_begin, div);
+}
+
+// Kernel-argument batch: up to kCmMaxTasks tasks, kCmMaxPtrs inputs (so
+// m < 256 and two accumulator levels suffice).
+template <class Op, int VPT>
+__global__ __launch_bounds__(kBlock) void k_chunk_mean_batch(const ChunkMeanSlots s) {
+  const uint32_t bid = blockIdx.x;
+  int t = 0;
+  while (t + 1 < s.ntasks && bid >= s.block_start[t + 1]) ++t;  // wave-uniform scan
+  const PtrArgs a{s.p + s.ptr_off[t]};
+  cm_task<Op, PtrArgs, VPT, 2>(a, s.m[t], s.out[t], s.nelem[t], s.ilp_begin[t], s.flags[t],
+                               bid - s.block_start[t]);
+}
+
+// One task whose input pointers live in device memory (any m).
+template <class Op, int VPT>
+__global__ __launch_bounds__(kBlock) void k_chunk_mean_table(const void* const* __restrict__ ptrs, int m,
+                                                             void* out, size_t n, size_t ilp_begin,
+                                                             uint8_t flags) {
+  const PtrArgs a{ptrs};
+  cm_task<Op, PtrArgs, VPT, 4>(a, m, out, n, ilp_begin, flags, blockIdx.x);
+}
+
+}  // namespace dlsim

@@ -13,6 +13,7 @@
 
 #include "dlsim.h"
 #include "wreduce_kernels.hpp"
+#include "chunk_mean_kernels.hpp"
 
 namespace {
 
@@ -451,6 +452,112 @@ int dispatch(const void* const* in, int n, const float* w, void* out, size_t nel
                              : run<dlsim::BF16Fast>(in, n, w, out, nelem, st);
 }
 
+// ---- chunk mean in PyTorch's CPU order (chunk_mean_kernels.hpp) --------------
+// First column that ATen's cascade_sum folds in row_sum (ilp) order, for an
+// [m, n] fp32 reduction over dim 0 at `threads` intra-op threads
+// (parallel_dim_reduction's column split, 32-column rounding; the 8-wide
+// vectorized_outer_sum blocks of 32 columns; scalar_outer_sum's groups of 4
+// under 8 columns). n == 1 is the inner reduction (all "ilp"/inner).
+size_t chunk_mean_ilp_begin(int m, size_t n, int threads) {
+  if (n <= 1) return 0;
+  size_t b = 0, e = n;
+  if (!(static_cast<unsigned long long>(m) * n < 32768ULL || threads <= 1)) {
+    const size_t tp = static_cast<size_t>(threads) < n ? static_cast<size_t>(threads) : n;
+    const size_t cs = (n + tp - 1) / tp;
+    for (size_t t = 0; t < tp; ++t) {
+      size_t tb = t * cs;
+      if (tb >= n) break;
+      size_t te = tb + cs < n ? tb + cs : n;
+      tb -= tb % 32;
+      if (te != n) te -= te % 32;
+      if (tb < te) {
+        b = tb;
+        e = te;
+      }
+    }
+  }
+  const size_t s1 = e - b;
+  return b + (s1 >= 8 ? s1 / 32 * 32 : s1 / 4 * 4);
+}
+
+constexpr int kCmVpt = 2;
+
+template <class Op>
+int run_chunk_mean(int b, const int* fan_in, const void* const* in, void* const* outs, const size_t* nelem,
+                   int threads, hipStream_t st) {
+  constexpr size_t tile = static_cast<size_t>(dlsim::kBlock) * kCmVpt;
+  std::vector<size_t> off(static_cast<size_t>(b) + 1, 0);
+  for (int t = 0; t < b; ++t) off[t + 1] = off[t] + static_cast<size_t>(fan_in[t]);
+  auto task_flags = [&](int t) {
+    bool vec = aligned16(outs[t]);
+    for (int i = 0; i < fan_in[t] && vec; ++i) vec = aligned16(in[off[t] + i]);
+    uint8_t f = vec ? dlsim::kCmVec : 0;
+    if (nelem[t] == 1 && fan_in[t] >= 8) f |= dlsim::kCmInner;
+    return f;
+  };
+  auto task_blocks = [&](int t, size_t ib) { return ib / Op::E / tile + 1; };
+  dlsim::ChunkMeanSlots s;
+  std::memset(&s, 0, sizeof(s));
+  int nt = 0, np = 0;
+  size_t blocks = 0;
+  auto flush = [&]() -> int {
+    if (nt == 0) return DLSIM_OK;
+    s.ntasks = nt;
+    s.block_start[nt] = static_cast<uint32_t>(blocks);
+    hipLaunchKernelGGL((dlsim::k_chunk_mean_batch<Op, kCmVpt>), dim3(static_cast<unsigned>(blocks)),
+                       dim3(dlsim::kBlock), 0, st, s);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "chunk mean batch launch");
+    std::memset(&s, 0, sizeof(s));
+    nt = np = 0;
+    blocks = 0;
+    return DLSIM_OK;
+  };
+  for (int t = 0; t < b; ++t) {
+    const size_t n = nelem[t];
+    if (n == 0) continue;
+    const int m = fan_in[t];
+    const size_t ib = chunk_mean_ilp_begin(m, n, threads);
+    const uint8_t flags = task_flags(t);
+    const size_t tb = task_blocks(t, ib);
+    if (m > dlsim::kCmMaxPtrs) {
+      // input pointers through a stream-ordered device array (any m)
+      void* d = nullptr;
+      const size_t bytes = static_cast<size_t>(m) * sizeof(void*);
+      hipError_t e = hipMallocAsync(&d, bytes, st);
+      if (e != hipSuccess) return hip_fail(e, "chunk mean pointer table alloc");
+      // pageable source: the copy is staged before the call returns
+      e = hipMemcpyAsync(d, in + off[t], bytes, hipMemcpyHostToDevice, st);
+      if (e == hipSuccess) {
+        hipLaunchKernelGGL((dlsim::k_chunk_mean_table<Op, kCmVpt>), dim3(static_cast<unsigned>(tb)),
+                           dim3(dlsim::kBlock), 0, st, static_cast<const void* const*>(d), m, outs[t], n, ib,
+                           flags);
+        e = hipGetLastError();
+      }
+      hipError_t e2 = hipFreeAsync(d, st);
+      if (e != hipSuccess) return hip_fail(e, "chunk mean table launch");
+      if (e2 != hipSuccess) return hip_fail(e2, "chunk mean pointer table free");
+      continue;
+    }
+    if (nt == dlsim::kCmMaxTasks || np + m > dlsim::kCmMaxPtrs || blocks + tb > 0x7fffffffu) {
+      int rc = flush();
+      if (rc != DLSIM_OK) return rc;
+    }
+    s.block_start[nt] = static_cast<uint32_t>(blocks);
+    s.ptr_off[nt] = static_cast<uint16_t>(np);
+    s.m[nt] = static_cast<uint16_t>(m);
+    s.out[nt] = outs[t];
+    s.nelem[nt] = n;
+    s.ilp_begin[nt] = ib;
+    s.flags[nt] = flags;
+    for (int i = 0; i < m; ++i) s.p[np + i] = in[off[t] + i];
+    np += m;
+    blocks += tb;
+    ++nt;
+  }
+  return flush();
+}
+
 }  // namespace
 
 extern "C" {
@@ -594,6 +701,32 @@ int dlsim_mean_batched(int b, const int* fan_in, const void* const* d_inputs, vo
   return dtype == DLSIM_F32
              ? run_batched<dlsim::F32Mean>(b, fan_in, d_inputs, ones.data(), d_outs, n_elems, st, divs.data())
              : run_batched<dlsim::BF16Mean>(b, fan_in, d_inputs, ones.data(), d_outs, n_elems, st, divs.data());
+}
+
+size_t dlsim_chunk_mean_ilp_begin(int m, size_t n_elems, int cpu_threads) {
+  return chunk_mean_ilp_begin(m, n_elems, cpu_threads);
+}
+
+int dlsim_chunk_mean_batched(int b, const int* fan_in, const void* const* d_inputs, void* const* d_outs,
+                             const size_t* n_elems, int dtype, int cpu_threads, void* stream) {
+  g_err.clear();
+  if (b < 0) return fail(DLSIM_E_ARG, "b must be >= 0 (got %d)", b);
+  if (b == 0) return DLSIM_OK;
+  if (!fan_in || !d_inputs || !d_outs || !n_elems) return fail(DLSIM_E_ARG, "null array argument");
+  if (cpu_threads < 1) return fail(DLSIM_E_ARG, "cpu_threads must be >= 1 (got %d)", cpu_threads);
+  size_t off = 0;
+  for (int t = 0; t < b; ++t) {
+    int rc = check_args(d_inputs + off, fan_in[t], nullptr, d_outs[t], n_elems[t], dtype, DLSIM_EXACT, false);
+    if (rc != DLSIM_OK) return fail(rc, "task %d: %s", t, g_err.c_str());
+    if (fan_in[t] > 65535) return fail(DLSIM_E_ARG, "task %d: fan-in %d > 65535", t, fan_in[t]);
+    if (n_elems[t] * elem_bytes(dtype) >= kMaxLaunchOutBytes)
+      return fail(DLSIM_E_ARG, "task %d: chunk of %zu elements is >= 2 GiB", t, n_elems[t]);
+    off += static_cast<size_t>(fan_in[t]);
+  }
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  return dtype == DLSIM_F32
+             ? run_chunk_mean<dlsim::F32Mean>(b, fan_in, d_inputs, d_outs, n_elems, cpu_threads, st)
+             : run_chunk_mean<dlsim::BF16Mean>(b, fan_in, d_inputs, d_outs, n_elems, cpu_threads, st);
 }
 
 int dlsim_shard_range(size_t n_elems, int world, int rank, size_t align_elems, size_t* begin,

@@ -124,14 +124,13 @@ struct BF16Fast {
   __device__ static float finish(float a, float) { return bf16_round(a); }
 };
 
-// Mean of the inputs (ChunkManager.reconstruct_model, chunk_manager.py:38-40:
-// torch.mean(torch.stack(chunks), dim=0) = sum over dim 0, then div_(n)):
-// acc starts at +0 (the reduction's identity), adds every input in order,
-// then one division by n (weights unused). fp32 matches PyTorch's CPU
-// reduction bit for bit while that reduction is sequential (n <= 4);
-// beyond, PyTorch's order depends on sizes and threads.
-// bf16: the sum is accumulated in fp32 and rounded to bf16 (the bf16 sum
-// tensor), then divided and rounded again (div_ on bf16).
+// Mean of the inputs in input order (dlsim_mean): acc starts at +0 (the
+// reduction's identity), adds every input in order, then one division by n
+// (weights unused). bf16: the sum is accumulated in fp32, divided in fp32 and
+// rounded once (PyTorch's CPU mean of a bf16 tensor sums in fp32, divides,
+// and casts back). PyTorch's own CPU order for torch.mean(torch.stack(...),
+// 0) — what ChunkManager.reconstruct_model (chunk_manager.py:38-40) needs —
+// is chunk_mean_kernels.hpp; these policies also carry its element format.
 struct F32Mean {
   static constexpr int E = 4;
   static constexpr int kBytes = 4;
@@ -153,7 +152,7 @@ struct BF16Mean {
     a0 = a0 + x0;
     a1 = a1 + x1;
   }
-  __device__ static float finish(float a, float div) { return bf16_round(bf16_round(a) / div); }
+  __device__ static float finish(float a, float div) { return bf16_round(a / div); }
 };
 
 // ---- 16-byte vector <-> E floats --------------------------------------------

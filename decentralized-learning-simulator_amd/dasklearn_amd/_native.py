@@ -32,6 +32,8 @@ EXPORTS = (
     "dlsim_batch_table_launch",
     "dlsim_mean",
     "dlsim_mean_batched",
+    "dlsim_chunk_mean_batched",
+    "dlsim_chunk_mean_ilp_begin",
     "dlsim_shard_range",
     "dlsim_probe_copy",
     "dlsim_last_error",
@@ -89,6 +91,11 @@ def load() -> ctypes.CDLL:
         lib.dlsim_mean_batched.argtypes = [i, ctypes.POINTER(i), ctypes.POINTER(vp), ctypes.POINTER(vp),
                                            ctypes.POINTER(sz), i, vp]
         lib.dlsim_mean_batched.restype = i
+        lib.dlsim_chunk_mean_batched.argtypes = [i, ctypes.POINTER(i), ctypes.POINTER(vp), ctypes.POINTER(vp),
+                                                 ctypes.POINTER(sz), i, i, vp]
+        lib.dlsim_chunk_mean_batched.restype = i
+        lib.dlsim_chunk_mean_ilp_begin.argtypes = [i, sz, i]
+        lib.dlsim_chunk_mean_ilp_begin.restype = sz
         lib.dlsim_shard_range.argtypes = [sz, i, i, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)]
         lib.dlsim_shard_range.restype = i
         lib.dlsim_probe_copy.argtypes = [vp, vp, sz, vp]
@@ -311,6 +318,45 @@ def mean_batched(tasks, stream=None):
                                   (ctypes.c_void_p * b)(*outs), (ctypes.c_size_t * b)(*numels), dt,
                                   _stream_handle(out0.device, stream)))
     return [t[1] for t in tasks]
+
+
+def chunk_mean_batched(tasks, threads=None, stream=None):
+    """tasks: sequence of (inputs, out) — for each, out = the reference's CPU
+    torch.mean(torch.stack(inputs), 0) bit for bit, at `threads` intra-op
+    threads (default torch.get_num_threads(): the worker's
+    settings.torch_threads, broker.py:31), all in few launches
+    (dlsim_chunk_mean_batched). Returns the outs."""
+    lib = load()
+    b = len(tasks)
+    if b == 0:
+        return []
+    if threads is None:
+        import torch
+        threads = torch.get_num_threads()
+    out0 = tasks[0][1]
+    dt = dtype_code(out0.dtype)
+    fan, ptrs, outs, numels = [], [], [], []
+    for inputs, out in tasks:
+        if len(inputs) < 1:
+            raise IndexError("list index out of range")
+        for t in list(inputs) + [out]:
+            if not t.is_cuda or t.dtype != out0.dtype or t.numel() != out.numel() or not t.is_contiguous() \
+                    or t.device != out0.device:
+                raise ValueError("each task: contiguous device tensors of one dtype and size; one device")
+        fan.append(len(inputs))
+        ptrs.extend(t.data_ptr() for t in inputs)
+        outs.append(out.data_ptr())
+        numels.append(out.numel())
+    _check("dlsim_chunk_mean_batched",
+           lib.dlsim_chunk_mean_batched(b, (ctypes.c_int * b)(*fan), (ctypes.c_void_p * len(ptrs))(*ptrs),
+                                        (ctypes.c_void_p * b)(*outs), (ctypes.c_size_t * b)(*numels), dt,
+                                        int(threads), _stream_handle(out0.device, stream)))
+    return [t[1] for t in tasks]
+
+
+def chunk_mean_ilp_begin(m: int, n: int, threads: int) -> int:
+    """Host rule of dlsim_chunk_mean_batched (no GPU needed)."""
+    return int(load().dlsim_chunk_mean_ilp_begin(m, n, threads))
 
 
 def wreduce_tensors(inputs_by_model, weights_f32, outs, mode: int = DLSIM_EXACT, stream=None):

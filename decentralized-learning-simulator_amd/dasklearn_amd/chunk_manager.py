@@ -5,19 +5,20 @@ state_dict into k chunks (`chunk` task, functions.py:136-140), send chunk c to
 some peers, and rebuild a model from the received chunks by averaging each
 chunk index over its contributors (`reconstruct_from_chunks` task,
 functions.py:142-146). That average is a second N-way reduce of the hot path
-(SURVEY.md §8f row 2); here it runs on the GPU through `dlsim_mean`.
+(SURVEY.md §8f row 2); here it runs on the GPU through `dlsim_chunk_mean_batched`.
 
 * `chunk_model` / `get_flat_params` are pure data movement (a torch.cat of the
   state_dict and slices of it) and are restated with the same tensor ops, on
   whatever device the model lives.
 * `reconstruct_model`: per chunk index, `torch.mean(torch.stack(chunks), 0)`
-  (chunk_manager.py:38-40) becomes one task of a `dlsim_mean_batched` launch
-  (every chunk index of the reconstruction in one launch) — sum in input order
-  from +0, one division by the contributor count. That is
-  bit-identical to the reference while PyTorch's CPU dim-0 reduction is
-  sequential (<= 4 contributors per chunk); with more contributors PyTorch
-  switches to a size- and thread-dependent order, so parity is a tolerance
-  (m * 2^-23 relative to the mean of |x|; tests/test_gpu_chunks.py).
+  (chunk_manager.py:38-40) becomes one task of a `dlsim_chunk_mean_batched`
+  launch (every chunk index of the reconstruction in one launch), computed in
+  PyTorch's own CPU summation order (ATen's cascade_sum column classes at the
+  calling process's torch.get_num_threads(), which in the worker is
+  settings.torch_threads, broker.py:31) and divided once: bit-identical to the
+  reference for every contributor count (tests/test_gpu_chunks.py against the
+  reference's fixtures; the order itself is pinned against torch.mean in
+  tests/test_chunk_mean_order.py).
   As in the reference, `chunks[c]` is replaced in place by its mean and the
   result is copied into `model.state_dict()` (parameters and buffers).
 """
@@ -57,7 +58,7 @@ class ChunkManager:
     @staticmethod
     def mean_chunk_indices(chunks: List[List[torch.Tensor]], device=None) -> List[torch.Tensor]:
         """[torch.mean(torch.stack(cs), dim=0) for cs in chunks], every chunk
-        index in one batched launch per dtype (dlsim_mean_batched). Device
+        index in one batched launch per dtype (dlsim_chunk_mean_batched). Device
         chunks are read in place; host chunks (the reference's case) are staged
         into one pinned buffer, copied with one H2D, and the means come back
         with one D2H. Each result lives where its first chunk lives."""
@@ -94,7 +95,7 @@ class ChunkManager:
                         results[ci] = out.view(chunks[ci][0].shape)
                         if k:
                             tasks.append(([c.reshape(-1).contiguous() for c in chunks[ci]], out))
-                    _native.mean_batched(tasks)
+                    _native.chunk_mean_batched(tasks)
                     continue
                 # host (or mixed) chunks: rows at 256-B aligned offsets of one
                 # pinned staging buffer, outputs in one device buffer
@@ -119,7 +120,7 @@ class ChunkManager:
                     k = chunks[ci][0].numel()
                     if k:
                         tasks.append(([d_in[x:x + k] for x in offs], d_out[o:o + k]))
-                _native.mean_batched(tasks)
+                _native.chunk_mean_batched(tasks)
                 host = torch.empty(max(n_out, 1), dtype=dt, pin_memory=True)
                 host.copy_(d_out, non_blocking=True)
                 torch.cuda.current_stream(dev).synchronize()

@@ -174,6 +174,30 @@ int dlsim_mean_batched(int b, const int* fan_in, const void* const* d_inputs, vo
                        const size_t* n_elems, int dtype, void* stream);
 
 /*
+ * dlsim_chunk_mean_batched — b chunk means, each bit-identical to the
+ * reference's CPU `torch.mean(torch.stack(chunks), dim=0)`
+ * (simulation/conflux/chunk_manager.py:38-40) as PyTorch computes it at
+ * `cpu_threads` intra-op threads (the worker's settings.torch_threads,
+ * broker.py:31; torch.get_num_threads() in the calling process). Task t
+ * averages fan_in[t] buffers d_inputs[o_t .. o_t + fan_in[t]) (o_t the prefix
+ * sum of fan_in) into d_outs[t] (n_elems[t] elements, < 2 GiB). The order is
+ * ATen's cascade_sum (chunk_mean_kernels.hpp); bf16 chunks are summed in
+ * fp32, divided and rounded once. Any fan-in up to 65535: up to 192 inputs
+ * per launch travel as kernel arguments, larger ones through a stream-ordered
+ * device array (hipMallocAsync / hipFreeAsync on `stream`).
+ * Replaces the per-index loop of ChunkManager.reconstruct_model.
+ */
+int dlsim_chunk_mean_batched(int b, const int* fan_in, const void* const* d_inputs, void* const* d_outs,
+                             const size_t* n_elems, int dtype, int cpu_threads, void* stream);
+
+/*
+ * dlsim_chunk_mean_ilp_begin — the first column of an [m, n_elems] chunk
+ * stack that PyTorch's CPU sum folds in its row_sum order at cpu_threads
+ * threads (host logic, no GPU; exposed for tests).
+ */
+size_t dlsim_chunk_mean_ilp_begin(int m, size_t n_elems, int cpu_threads);
+
+/*
  * dlsim_shard_range — parameter-axis partition used by the sharded path.
  *
  * Splits [0, n_elems) into `world` contiguous slices whose boundaries are

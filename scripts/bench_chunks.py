@@ -5,9 +5,11 @@ for a ResNet-18/CIFAR-10-sized flat model (11,181,642 fp32), k = 10 chunks
 (ConfluxSettings.chunks_in_sample default, conflux/settings.py:11) and m
 contributors per index (success_fraction 1: the sample size).
 
-  kernel      dlsim_mean_batched over device-resident chunks, every index in
-              one launch: HIP events over back-to-back launches, algorithmic
-              bytes (m + 1) * P * 4 per reconstruction
+  kernel      dlsim_chunk_mean_batched (PyTorch's CPU order, the product path)
+              over device-resident chunks, every index in one launch: HIP
+              events over back-to-back launches, algorithmic bytes
+              (m + 1) * P * 4 per reconstruction; seq_kernel: the same with
+              dlsim_mean_batched (input order), for comparison
   device      ChunkManager.reconstruct_model on device chunks (wall)
   host        the same on host chunks (PCIe-inclusive wall; the reference's case),
               at the box's default threads and at the worker's 4
@@ -85,26 +87,28 @@ def main():
         # kernel only: one batched launch per reconstruction, 3 rotating output sets
         outs = [[torch.empty(cs[0].numel(), device=dev) for cs in dev_by_index] for _ in range(3)]
         tasks = [[(cs, o) for cs, o in zip(dev_by_index, outs[s])] for s in range(3)]
-        for s in range(3):
-            _native.mean_batched(tasks[s])
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         reps = 50
-        torch.cuda.synchronize()
-        e0.record()
-        for r in range(reps):
-            _native.mean_batched(tasks[r % 3])
-        e1.record()
-        torch.cuda.synchronize()
-        us = e0.elapsed_time(e1) * 1e3 / reps
-        res["kernel_us"] = round(us, 2)
-        res["kernel_GBps"] = round(byts / us / 1e3, 1)
-        res["kernel_frac_of_8TBps"] = round(byts / us / 1e3 / 8000.0, 4)
+        for key, fn in (("kernel", lambda ts: _native.chunk_mean_batched(ts, threads=4)),
+                        ("seq_kernel", _native.mean_batched)):
+            for s in range(3):
+                fn(tasks[s])
+            torch.cuda.synchronize()
+            e0.record()
+            for r in range(reps):
+                fn(tasks[r % 3])
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / reps
+            res[key + "_us"] = round(us, 2)
+            res[key + "_GBps"] = round(byts / us / 1e3, 1)
+            res[key + "_frac_of_8TBps"] = round(byts / us / 1e3 / 8000.0, 4)
         # per-index launches (the unbatched form) for comparison
         torch.cuda.synchronize()
         e0.record()
         for r in range(reps):
             for cs, o in tasks[r % 3]:
-                _native.mean(cs, o)
+                _native.chunk_mean_batched([(cs, o)], threads=4)
         e1.record()
         torch.cuda.synchronize()
         res["per_index_launches_us"] = round(e0.elapsed_time(e1) * 1e3 / reps, 2)

@@ -95,3 +95,16 @@ def test_short_final_range_matches_torch():
     rng = np.random.default_rng(11)
     x = _rows(rng, 400, 101, "f32")
     assert orc.same_bits(orc.chunk_mean(list(x), "f32", 20), _torch_mean(x, 20, "f32"))
+
+
+def test_abi_ilp_begin_matches_oracle():
+    """The product's host rule (dlsim_chunk_mean_ilp_begin, csrc/dlsim_abi.hip)
+    and the oracle's agree everywhere the column split can land."""
+    from dasklearn_amd import _native
+    rng = np.random.default_rng(0)
+    cases = [(m, n, t) for m in (1, 4, 17, 400, 1000) for n in (0, 1, 2, 7, 8, 31, 32, 33, 37, 101, 1000, 40001)
+             for t in (1, 2, 3, 4, 8, 20)]
+    cases += [(int(rng.integers(1, 3000)), int(rng.integers(1, 200000)), int(rng.integers(1, 64)))
+              for _ in range(300)]
+    for m, n, t in cases:
+        assert _native.chunk_mean_ilp_begin(m, n, t) == orc.chunk_mean_ilp_begin(m, n, t), (m, n, t)

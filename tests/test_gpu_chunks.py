@@ -1,5 +1,6 @@
-"""Chunked-model path on the GPU: dlsim_mean and ChunkManager.reconstruct_model
-against the reference's ChunkManager fixtures and the oracle."""
+"""Chunked-model path on the GPU: dlsim_chunk_mean_batched (PyTorch's CPU
+order), dlsim_mean (input order) and ChunkManager.reconstruct_model against
+the reference's ChunkManager fixtures and the oracle."""
 from __future__ import annotations
 
 import os
@@ -56,20 +57,17 @@ def test_reconstruct_matches_reference(path, where):
     target = Net(d["meta"]["shapes"])
     if where == "device":
         target = target.to(dev())
-    out = ChunkManager.reconstruct_model(chunks, target)
+    prev = torch.get_num_threads()
+    torch.set_num_threads(d["meta"]["torch_threads"])  # the reference worker's threads
+    try:
+        out = ChunkManager.reconstruct_model(chunks, target)
+    finally:
+        torch.set_num_threads(prev)
     assert out is target
     assert all(torch.is_tensor(c) for c in chunks)  # replaced in place by the means
     got = ChunkManager.get_flat_params(out).cpu().numpy()
-    off = 0
-    for c in range(k):
-        L = d[f"chunks_{c}"].shape[1]
-        g, e = got[off:off + L], d["expected"][off:off + L]
-        if counts[c] <= 4:
-            assert orc.same_bits(g, e), (c, counts[c])
-        else:
-            scale = np.abs(d[f"chunks_{c}"]).mean(axis=0)
-            assert np.all(np.abs(g - e) <= counts[c] * 2.0 ** -23 * scale + 1e-30)
-        off += L
+    # bit-exact for every contributor count (PyTorch's CPU order)
+    assert orc.same_bits(got, d["expected"]), counts
 
 
 def test_reconstruct_task_function_uses_factory():
@@ -122,8 +120,8 @@ def test_mean_batched_equals_separate_means(dtype):
 @pytest.mark.parametrize("where", ["host", "device"])
 def test_mean_chunk_indices_one_launch_per_dtype(where):
     """Every chunk index of a reconstruction in one batched launch, host chunks
-    through one staging buffer: same bits as one dlsim_mean per index; results
-    live where their first chunk lives."""
+    through one staging buffer: same bits as one dlsim_chunk_mean_batched call
+    per index; results live where their first chunk lives."""
     rng = np.random.default_rng(9)
     chunks = []
     for c in range(10):
@@ -135,6 +133,96 @@ def test_mean_chunk_indices_one_launch_per_dtype(where):
     for cs, m in zip(chunks, means):
         assert m.is_cuda == (where == "device") and m.dtype == cs[0].dtype and m.shape == cs[0].shape
         ref = torch.empty(cs[0].numel(), dtype=cs[0].dtype, device=dev())
-        _native.mean([t.to(dev()).reshape(-1) for t in cs], ref)
+        _native.chunk_mean_batched([([t.to(dev()).reshape(-1) for t in cs], ref)])
         assert torch.equal(m.cpu().view(torch.int16 if m.dtype == torch.bfloat16 else torch.int32),
                            ref.cpu().view(torch.int16 if m.dtype == torch.bfloat16 else torch.int32))
+
+
+def _rows_t(rng, m, n, dtype, offset=0):
+    """m rows of n elements as device tensors, `offset` elements into their
+    buffers (offset 1: not 16-byte aligned)."""
+    x = (rng.standard_normal((m, n)) * np.exp(rng.standard_normal((m, n)) * 2)).astype(np.float32)
+    rows = orc.f32_to_bf16_bits(x) if dtype == "bf16" else x
+    ts = []
+    for r in rows:
+        h = torch.from_numpy(r.view(np.int16).copy()).view(torch.bfloat16) if dtype == "bf16" \
+            else torch.from_numpy(r.copy())
+        buf = torch.empty(n + offset, dtype=h.dtype, device=dev())
+        buf[offset:].copy_(h)
+        ts.append(buf[offset:])
+    return rows, ts
+
+
+def _bits(t):
+    t = t.cpu()
+    return t.view(torch.int16).numpy().view(np.uint16) if t.dtype == torch.bfloat16 else t.numpy()
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("threads", [1, 4, 8])
+def test_chunk_mean_matches_torch_order(dtype, threads):
+    """Every (m, n) class of PyTorch's CPU sum order — cascade blocks, the
+    < 32-column ilp tail, the < 8-column scalar groups, the one-element inner
+    reduction, the level-1 flush at 16 rows — in batches that cross the
+    32-task / 192-input launch limits: each task bit-identical to the
+    order-exact oracle (pinned against torch.mean on the CPU)."""
+    rng = np.random.default_rng(threads * 10 + (dtype == "bf16"))
+    tasks, exp = [], []
+    for m in (1, 2, 3, 4, 5, 8, 9, 16, 17, 18, 33, 100):
+        for n in (1, 2, 3, 5, 7, 8, 9, 31, 33, 65, 1000, 4099, 40001):
+            rows, ts = _rows_t(rng, m, n, dtype)
+            tasks.append((ts, torch.empty(n, dtype=ts[0].dtype, device=dev())))
+            exp.append(orc.chunk_mean(list(rows), dtype, threads))
+    _native.chunk_mean_batched(tasks, threads=threads)
+    for (ts, out), e in zip(tasks, exp):
+        assert orc.same_bits(_bits(out), e), (len(ts), out.numel())
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_chunk_mean_unaligned_and_aliased(dtype):
+    """Rows one element into their buffers (scalar path), and the output
+    aliasing input 0."""
+    rng = np.random.default_rng(5)
+    for m, n in ((3, 4099), (7, 40001), (20, 100)):
+        rows, ts = _rows_t(rng, m, n, dtype, offset=1)
+        out = torch.empty(n + 1, dtype=ts[0].dtype, device=dev())[1:]
+        _native.chunk_mean_batched([(ts, out)], threads=4)
+        e = orc.chunk_mean(list(rows), dtype, 4)
+        assert orc.same_bits(_bits(out), e)
+        _native.chunk_mean_batched([(ts, ts[0])], threads=4)
+        assert orc.same_bits(_bits(ts[0]), e)
+
+
+@pytest.mark.parametrize("m", [193, 256, 300])
+def test_chunk_mean_large_fan_in(m):
+    """More inputs than a kernel-argument batch holds: the device pointer
+    array path, with the level-2 flush of the cascade at 256 rows."""
+    rng = np.random.default_rng(m)
+    for n in (1, 9, 5000):
+        rows, ts = _rows_t(rng, m, n, "f32")
+        out = torch.empty(n, device=dev())
+        _native.chunk_mean_batched([(ts, out)], threads=4)
+        assert orc.same_bits(_bits(out), orc.chunk_mean(list(rows), "f32", 4)), n
+
+
+def test_chunk_mean_resnet18_chunks_full_size():
+    """k = 10 chunks of a ResNet-18-sized flat model (11,181,642 fp32), 12
+    contributors each, worker threads 4: every element bit-identical."""
+    P, k, m = 11_181_642, 10, 12
+    g = torch.Generator(device=dev()).manual_seed(3)
+    flats = [torch.randn(P, generator=g, device=dev()) * 0.05 for _ in range(m)]
+    size = P // k
+    bounds = [(c * size, (c + 1) * size if c < k - 1 else P) for c in range(k)]
+    tasks = [([f[b:e] for f in flats], torch.empty(e - b, device=dev())) for b, e in bounds]
+    _native.chunk_mean_batched(tasks, threads=4)
+    host = [f.cpu().numpy() for f in flats]
+    for (b, e), (_, out) in zip(bounds, tasks):
+        assert orc.same_bits(out.cpu().numpy(), orc.chunk_mean([h[b:e] for h in host], "f32", 4))
+
+
+def test_chunk_mean_errors():
+    x = torch.zeros(8, device=dev())
+    with pytest.raises(IndexError):
+        _native.chunk_mean_batched([([], x)])
+    with pytest.raises(RuntimeError, match="cpu_threads"):
+        _native.chunk_mean_batched([([x], torch.empty(8, device=dev()))], threads=0)
