@@ -480,7 +480,7 @@ size_t chunk_mean_ilp_begin(int m, size_t n, int threads) {
   return b + (s1 >= 8 ? s1 / 32 * 32 : s1 / 4 * 4);
 }
 
-constexpr int kCmVpt = 2;
+constexpr int kCmVpt = 4;
 
 template <class Op>
 int run_chunk_mean(int b, const int* fan_in, const void* const* in, void* const* outs, const size_t* nelem,
