@@ -215,6 +215,46 @@ void launch_x(const Slots<128>& s, int n, void* out, size_t nvec, size_t, hipStr
                      nvec, per);
 }
 
+// Two tile sizes in one grid: the first ~gm percent of the vectors in big
+// tiles (VB vectors per lane), the rest in small tiles (VSM) dispatched last,
+// so the blocks still running at the end of the launch are short (a finer
+// tail). Wave map + sc1 stores as the shipped fp32 shape; block 0 takes the
+// ragged end.
+template <class Op, int NF, int VB, int VSM>
+__global__ __launch_bounds__(kBlock) void k_tiles_split(const Slots<128> s, int n, void* __restrict__ out,
+                                                        size_t nvec, size_t nelem, size_t big_tiles) {
+  constexpr size_t kBig = (size_t)kBlock * VB, kSm = (size_t)kBlock * VSM;
+  const OutRef o = make_out<16>(out, nvec);
+  const size_t base = big_tiles * kBig;
+  const size_t small_full = (nvec - base) / kSm;
+  if (blockIdx.x == 0) {
+    if (base + small_full * kSm < nvec)
+      reduce_tile<Op, Slots<128>, NF, 8, VSM, 1, true, 16>(s, n, nullptr, o, base + small_full * kSm + threadIdx.x,
+                                                         nvec);
+    const size_t j = nvec * Op::E + threadIdx.x;
+    if (j < nelem) fold_scalar<Op, Slots<128>>(s, n, nullptr, out, j);
+    return;
+  }
+  const size_t b = blockIdx.x - 1;
+  if (b < big_tiles) {
+    const size_t lo = (threadIdx.x >> 6) * 64 * VB + (threadIdx.x & 63);
+    reduce_tile<Op, Slots<128>, NF, 8, VB, 1, false, 16, 64>(s, n, nullptr, o, b * kBig + lo, nvec);
+  } else {
+    const size_t lo = (threadIdx.x >> 6) * 64 * VSM + (threadIdx.x & 63);
+    reduce_tile<Op, Slots<128>, NF, 8, VSM, 1, false, 16, 64>(s, n, nullptr, o, base + (b - big_tiles) * kSm + lo,
+                                                            nvec);
+  }
+}
+
+template <class Op, int NF, int VB, int VSM>
+void launch_split(const Slots<128>& s, int n, void* out, size_t nvec, size_t nelem, hipStream_t st, int pct) {
+  const size_t kBig = (size_t)kBlock * VB, kSm = (size_t)kBlock * VSM;
+  const size_t big = (size_t)((double)nvec * pct / 100.0) / kBig;
+  const size_t small_full = (nvec - big * kBig) / kSm;
+  hipLaunchKernelGGL((k_tiles_split<Op, NF, VB, VSM>), dim3((unsigned)(1 + big + small_full)), dim3(kBlock), 0,
+                     st, s, n, out, nvec, nelem, big);
+}
+
 template <class Op, int NF>
 void add_nf(std::vector<Variant>& vs, int n) {
   if (n != NF) return;
@@ -235,6 +275,11 @@ void add_nf(std::vector<Variant>& vs, int n) {
   vs.push_back({p + "_V1_sc1_wave", launch_ts<Op, NF, 8, 1, 1, 16, true>, 0});
   vs.push_back({p + "_xcd_V4", launch_x<Op, NF, 4>, 0});
   vs.push_back({p + "_xcd_V2", launch_x<Op, NF, 2>, 0});
+  vs.push_back({p + "_split80_V1", launch_split<Op, NF, 4, 1>, 80});
+  vs.push_back({p + "_split90_V1", launch_split<Op, NF, 4, 1>, 90});
+  vs.push_back({p + "_split95_V1", launch_split<Op, NF, 4, 1>, 95});
+  vs.push_back({p + "_split90_V2", launch_split<Op, NF, 4, 2>, 90});
+  vs.push_back({p + "_split97_V1", launch_split<Op, NF, 4, 1>, 97});
 }
 
 template <class Op>
