@@ -152,12 +152,27 @@ __device__ __forceinline__ u32x4 ld_slot_scalar(const void* base, size_t v, size
   return r;
 }
 
-// Cascade fold of m rows for the VPT slots v0 + k*kBlock of one lane.
+// Launch shape of the cascade tiles: VPT 16-byte slots per lane, lane map
+// (WAVE: lane l of wave w owns slots w*64*VPT + l + k*64; else l' + k*256),
+// RF rows loaded per group before they are folded (RF divides 16).
+template <int VPT_, bool WAVE_, int RF_>
+struct CmShape {
+  static constexpr int VPT = VPT_;
+  static constexpr bool WAVE = WAVE_;
+  static constexpr int RF = RF_;
+  static constexpr int VS = WAVE_ ? 64 : kBlock;  // slot stride of one lane
+  __device__ static size_t lane_off() {
+    return WAVE_ ? (threadIdx.x >> 6) * 64 * VPT_ + (threadIdx.x & 63) : threadIdx.x;
+  }
+};
+
+// Cascade fold of m rows for the VPT slots v0 + k*VS of one lane.
 // LV: accumulator levels in use (2 while m < 256, else 4).
 // VEC: 16-B aligned task (vector loads, buffer stores); else scalar access.
-template <class Op, class A, int VPT, int LV, bool VEC, bool CHECK>
+template <class Op, class A, class SH, int LV, bool VEC, bool CHECK>
 __device__ __forceinline__ void cm_tile(const A& a, int m, const OutRef& o, size_t v0, size_t nvec,
                                         size_t ncol, float div) {
+  constexpr int VPT = SH::VPT, RF = SH::RF;
   float acc[LV][VPT][Op::E];
 #pragma unroll
   for (int l = 0; l < LV; ++l)
@@ -168,16 +183,16 @@ __device__ __forceinline__ void cm_tile(const A& a, int m, const OutRef& o, size
   for (int i0 = 0; i0 < m; i0 += 16) {
     const int cnt = m - i0 < 16 ? m - i0 : 16;
 #pragma unroll
-    for (int h = 0; h < 16; h += 8) {
+    for (int h = 0; h < 16; h += RF) {
       if (h < cnt) {
-        u32x4 r[8][VPT];
+        u32x4 r[RF][VPT];
 #pragma unroll
-        for (int g = 0; g < 8; ++g) {
+        for (int g = 0; g < RF; ++g) {
           if (h + g < cnt) {
             const void* src = a.ptr(i0 + h + g);
 #pragma unroll
             for (int v = 0; v < VPT; ++v) {
-              const size_t idx = v0 + static_cast<size_t>(v) * kBlock;
+              const size_t idx = v0 + static_cast<size_t>(v) * SH::VS;
               if constexpr (VEC) {
                 if (!CHECK || idx < nvec) r[g][v] = ld16<1>(src, idx);
                 else r[g][v] = u32x4{0u, 0u, 0u, 0u};
@@ -188,7 +203,7 @@ __device__ __forceinline__ void cm_tile(const A& a, int m, const OutRef& o, size
           }
         }
 #pragma unroll
-        for (int g = 0; g < 8; ++g) {
+        for (int g = 0; g < RF; ++g) {
           if (h + g < cnt) {
 #pragma unroll
             for (int v = 0; v < VPT; ++v) {
@@ -224,7 +239,7 @@ __device__ __forceinline__ void cm_tile(const A& a, int m, const OutRef& o, size
       for (int e = 0; e < Op::E; ++e) acc[0][v][e] = acc[0][v][e] + acc[l][v][e];
 #pragma unroll
   for (int v = 0; v < VPT; ++v) {
-    const size_t idx = v0 + static_cast<size_t>(v) * kBlock;
+    const size_t idx = v0 + static_cast<size_t>(v) * SH::VS;
     if (CHECK && idx >= nvec) continue;
     if constexpr (VEC) {
       store_vec<Op::kBytes == 4 ? 16 : kStNT>(o, idx, pack<Op>(acc[0][v], div));
@@ -294,48 +309,49 @@ __device__ __forceinline__ void cm_scalar_cols(const A& a, int m, void* out, siz
 
 // One task's share of the grid: local block 0 does the ragged end, local
 // block b >= 1 the full tile b - 1 of the cascade columns.
-template <class Op, class A, int VPT, int LV>
+template <class Op, class A, class SH, int LV>
 __device__ __forceinline__ void cm_task(const A& a, int m, void* out, size_t n, size_t ilp_begin,
                                         uint8_t flags, uint32_t local) {
   const float div = static_cast<float>(m);
   const size_t nvec = ilp_begin / Op::E;  // whole vectors of cascade columns
-  constexpr size_t kTile = static_cast<size_t>(kBlock) * VPT;
+  constexpr size_t kTile = static_cast<size_t>(kBlock) * SH::VPT;
   const size_t full = nvec / kTile;
   const bool vec = (flags & kCmVec) != 0;
   const OutRef o = make_out<Op::kBytes == 4 ? 16 : kStNT>(out, vec ? nvec : 0);
   if (local == 0) {
-    if (full * kTile < nvec) {
-      if (vec) cm_tile<Op, A, VPT, LV, true, true>(a, m, o, full * kTile + threadIdx.x, nvec, ilp_begin, div);
-      else cm_tile<Op, A, VPT, LV, false, true>(a, m, o, full * kTile + threadIdx.x, nvec, ilp_begin, div);
+    if (full * kTile < nvec) {  // the partial tile, block map (bounds-checked)
+      using PT = CmShape<SH::VPT, false, SH::RF>;
+      if (vec) cm_tile<Op, A, PT, LV, true, true>(a, m, o, full * kTile + threadIdx.x, nvec, ilp_begin, div);
+      else cm_tile<Op, A, PT, LV, false, true>(a, m, o, full * kTile + threadIdx.x, nvec, ilp_begin, div);
     }
     const size_t c0 = nvec * Op::E;
     if (c0 < n) cm_scalar_cols<Op, A>(a, m, out, c0, n, ilp_begin, (flags & kCmInner) != 0, div);
     return;
   }
-  const size_t v0 = static_cast<size_t>(local - 1) * kTile + threadIdx.x;
-  if (vec) cm_tile<Op, A, VPT, LV, true, false>(a, m, o, v0, nvec, ilp_begin, div);
-  else cm_tile<Op, A, VPT, LV, false, false>(a, m, o, v0, nvec, ilp_begin, div);
+  const size_t v0 = static_cast<size_t>(local - 1) * kTile + SH::lane_off();
+  if (vec) cm_tile<Op, A, SH, LV, true, false>(a, m, o, v0, nvec, ilp_begin, div);
+  else cm_tile<Op, A, SH, LV, false, false>(a, m, o, v0, nvec, ilp_begin, div);
 }
 
 // Kernel-argument batch: up to kCmMaxTasks tasks, kCmMaxPtrs inputs (so
 // m < 256 and two accumulator levels suffice).
-template <class Op, int VPT>
+template <class Op, class SH>
 __global__ __launch_bounds__(kBlock) void k_chunk_mean_batch(const ChunkMeanSlots s) {
   const uint32_t bid = blockIdx.x;
   int t = 0;
   while (t + 1 < s.ntasks && bid >= s.block_start[t + 1]) ++t;  // wave-uniform scan
   const PtrArgs a{s.p + s.ptr_off[t]};
-  cm_task<Op, PtrArgs, VPT, 2>(a, s.m[t], s.out[t], s.nelem[t], s.ilp_begin[t], s.flags[t],
+  cm_task<Op, PtrArgs, SH, 2>(a, s.m[t], s.out[t], s.nelem[t], s.ilp_begin[t], s.flags[t],
                                bid - s.block_start[t]);
 }
 
 // One task whose input pointers live in device memory (any m).
-template <class Op, int VPT>
+template <class Op, class SH>
 __global__ __launch_bounds__(kBlock) void k_chunk_mean_table(const void* const* __restrict__ ptrs, int m,
                                                              void* out, size_t n, size_t ilp_begin,
                                                              uint8_t flags) {
   const PtrArgs a{ptrs};
-  cm_task<Op, PtrArgs, VPT, 4>(a, m, out, n, ilp_begin, flags, blockIdx.x);
+  cm_task<Op, PtrArgs, SH, 4>(a, m, out, n, ilp_begin, flags, blockIdx.x);
 }
 
 }  // namespace dlsim

@@ -480,12 +480,16 @@ size_t chunk_mean_ilp_begin(int m, size_t n, int threads) {
   return b + (s1 >= 8 ? s1 / 32 * 32 : s1 / 4 * 4);
 }
 
-constexpr int kCmVpt = 4;
+// Chunk mean tiles: VPT 4, wave map, 8 rows per load group. Block and wave
+// maps, VPT 2/4 and 8/16 rows in flight measured within +-3% of each other
+// (profiles/r01_tune_chunk_mean_shapes.log); the wave map matches the fp32
+// reduce's shape.
+using CmDefault = dlsim::CmShape<4, true, 8>;
 
 template <class Op>
 int run_chunk_mean(int b, const int* fan_in, const void* const* in, void* const* outs, const size_t* nelem,
                    int threads, hipStream_t st) {
-  constexpr size_t tile = static_cast<size_t>(dlsim::kBlock) * kCmVpt;
+  constexpr size_t tile = static_cast<size_t>(dlsim::kBlock) * CmDefault::VPT;
   std::vector<size_t> off(static_cast<size_t>(b) + 1, 0);
   for (int t = 0; t < b; ++t) off[t + 1] = off[t] + static_cast<size_t>(fan_in[t]);
   auto task_flags = [&](int t) {
@@ -504,7 +508,7 @@ int run_chunk_mean(int b, const int* fan_in, const void* const* in, void* const*
     if (nt == 0) return DLSIM_OK;
     s.ntasks = nt;
     s.block_start[nt] = static_cast<uint32_t>(blocks);
-    hipLaunchKernelGGL((dlsim::k_chunk_mean_batch<Op, kCmVpt>), dim3(static_cast<unsigned>(blocks)),
+    hipLaunchKernelGGL((dlsim::k_chunk_mean_batch<Op, CmDefault>), dim3(static_cast<unsigned>(blocks)),
                        dim3(dlsim::kBlock), 0, st, s);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "chunk mean batch launch");
@@ -529,7 +533,7 @@ int run_chunk_mean(int b, const int* fan_in, const void* const* in, void* const*
       // pageable source: the copy is staged before the call returns
       e = hipMemcpyAsync(d, in + off[t], bytes, hipMemcpyHostToDevice, st);
       if (e == hipSuccess) {
-        hipLaunchKernelGGL((dlsim::k_chunk_mean_table<Op, kCmVpt>), dim3(static_cast<unsigned>(tb)),
+        hipLaunchKernelGGL((dlsim::k_chunk_mean_table<Op, CmDefault>), dim3(static_cast<unsigned>(tb)),
                            dim3(dlsim::kBlock), 0, st, static_cast<const void* const*>(d), m, outs[t], n, ib,
                            flags);
         e = hipGetLastError();
