@@ -91,6 +91,9 @@ def parse():
     ap.add_argument("--mode", default="exact", choices=["exact", "fast"])
     ap.add_argument("--strong", action="store_true",
                     help="strong scaling: split the config's params over ranks instead of per rank")
+    ap.add_argument("--slice-of", type=int, default=1,
+                    help="1 GPU only: run rank 0's slice of a strong split over this many ranks "
+                         "(the per-rank work of --strong at that world size, without the other ranks)")
     ap.add_argument("--batch", type=int, default=1,
                     help="B independent aggregates of the config per step, in batched launches "
                          "(dlsim_wreduce_batched; a simulated round's per-peer tasks)")
@@ -224,6 +227,9 @@ def main():
     if args.strong and world > 1:
         b, e = _native.shard_range(p_cfg, world, rank, 64)
         p = e - b
+    elif args.slice_of > 1 and world == 1:
+        b, e = _native.shard_range(p_cfg, args.slice_of, 0, 64)
+        p = e - b
     else:
         p = p_cfg
     tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
@@ -350,7 +356,8 @@ def main():
     if rank == 0:
         achieved = bytes_per_launch / (kern_avg_ms * 1e-3) / 1e9
         # PMC bytes were profiled for the plain single-task, per-rank-shard run
-        traffic = pmc_traffic(args.config, args.mode) if (B == 1 and not args.strong) else None
+        traffic = pmc_traffic(args.config, args.mode) if (B == 1 and not args.strong and args.slice_of <= 1) \
+            else None
         result = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -366,7 +373,9 @@ def main():
             "data": "synthetic: torch.randn*0.05 on device, 3 rotating input sets; "
                     f"{wkind} weights",
             "config": {"workload": args.config + ": " + desc + (f" x {B} tasks per launch" if B > 1 else "")
-                       + (f" (strong scaling: {p_cfg} params split over {world} ranks)" if args.strong and world > 1 else ""),
+                       + (f" (strong scaling: {p_cfg} params split over {world} ranks)" if args.strong and world > 1 else "")
+                       + (f" (rank 0's slice of a {args.slice_of}-rank strong split, alone on 1 GPU)"
+                          if args.slice_of > 1 and world == 1 else ""),
                        "backend": args.backend if world > 1 else None,
                        "n_models": n, "params_per_rank": p, "tasks_per_step": B,
                        "mode": args.mode, "parallelism": f"param-shard x{world}",
