@@ -367,14 +367,19 @@ def wreduce_tensors(inputs_by_model, weights_f32, outs, mode: int = DLSIM_EXACT,
         raise IndexError("list index out of range")
     t = len(outs)
     dt = dtype_code(outs[0].dtype) if t else DLSIM_F32
+    # get_device(): the CUDA ordinal as an int (-1 on the host), cheaper than
+    # building torch.device objects per tensor
+    odev = outs[0].get_device() if t else -1
+    spec = [(o.dtype, o.numel()) for o in outs]
+    if t and (odev < 0 or any(o.get_device() != odev for o in outs)):
+        raise ValueError("outputs must be CUDA tensors on one device")
     flat = []
     for row in inputs_by_model:
         if len(row) != t:
             raise ValueError("every model must have the same number of tensors")
         for k, x in enumerate(row):
-            if not x.is_cuda or not x.is_contiguous() or x.dtype != outs[k].dtype \
-                    or x.numel() != outs[k].numel() or x.device != outs[k].device \
-                    or outs[k].device != outs[0].device:
+            d, ne = spec[k]
+            if x.get_device() != odev or x.dtype is not d or x.numel() != ne or not x.is_contiguous():
                 raise ValueError(f"tensor {k}: device/contiguity/dtype/size mismatch")
             flat.append(x.data_ptr())
     ptrs = (ctypes.c_void_p * len(flat))(*flat)

@@ -36,11 +36,33 @@ from torch import nn
 from . import _native
 
 
+def module_params(module: nn.Module) -> List[nn.Parameter]:
+    """list(module.parameters()) without torch's generator stack: the modules
+    in named_modules() pre-order (each once), then each module's _parameters
+    in order, skipping None and parameters already seen (by identity) — the
+    same list, ~3x faster on the per-task path."""
+    out: List[nn.Parameter] = []
+    seen_p, seen_m = set(), set()
+    stack = [module]
+    while stack:
+        m = stack.pop()
+        if id(m) in seen_m:
+            continue
+        seen_m.add(id(m))
+        for p in m._parameters.values():
+            if p is not None and id(p) not in seen_p:
+                seen_p.add(id(p))
+                out.append(p)
+        kids = [c for c in m._modules.values() if c is not None]
+        stack.extend(reversed(kids))
+    return out
+
+
 class ParamLayout:
     """parameters() of a module grouped by dtype, with flat offsets."""
 
     def __init__(self, module: nn.Module):
-        self.params: List[nn.Parameter] = list(module.parameters())
+        self.params: List[nn.Parameter] = module_params(module)
         self.shapes = [tuple(p.shape) for p in self.params]
         self.groups: "OrderedDict[torch.dtype, List[int]]" = OrderedDict()
         for k, p in enumerate(self.params):
@@ -72,15 +94,14 @@ class ParamLayout:
         return other
 
     def check_compatible(self, module: nn.Module) -> List[nn.Parameter]:
-        ps = list(module.parameters())
+        ps = module_params(module)
         # The reference zips parameters() (fedavg.py:24) and silently truncates
         # on a mismatch; equal shapes are what it assumes, so insist on them.
-        if [(p.shape, p.dtype) for p in ps] != self._signature:
-            if len(ps) != len(self.params):
-                raise ValueError("models have different numbers of parameters")
-            for k, (a, b) in enumerate(zip(ps, self.params)):
-                if a.shape != b.shape or a.dtype != b.dtype:
-                    raise ValueError(f"parameter {k}: shape/dtype differs from models[0]")
+        if len(ps) != len(self.params):
+            raise ValueError("models have different numbers of parameters")
+        for k, (a, (shape, dt)) in enumerate(zip(ps, self._signature)):
+            if a.dtype is not dt or a.shape != shape:
+                raise ValueError(f"parameter {k}: shape/dtype differs from models[0]")
         return ps
 
     def arena_view(self, params: Sequence[torch.Tensor], dt: torch.dtype) -> Optional[torch.Tensor]:
@@ -331,7 +352,10 @@ def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, m
                     _native.wreduce(views, weights_f32, out, mode)
                     st.mark("kernel")
                     continue
-                rows = [[ps[k].detach().contiguous() for k in idx] for ps in all_params]
+                # the ABI reads data pointers only: no detach() objects for
+                # contiguous parameters
+                rows = [[ps[k] if ps[k].is_contiguous() else ps[k].detach().contiguous() for k in idx]
+                        for ps in all_params]
                 outs_k = [out[layout.offsets[k]:layout.offsets[k] + layout.params[k].numel()]
                           for k in idx]
                 _native.wreduce_tensors(rows, weights_f32, outs_k, mode)
@@ -455,7 +479,7 @@ def registered_arenas(module: nn.Module, params: Optional[List[nn.Parameter]] = 
         return None
     if e is None:
         return None
-    ps = list(module.parameters()) if params is None else params
+    ps = module_params(module) if params is None else params
     if len(ps) != len(e.ptrs):
         return None
     for q, (ptr, shape) in zip(ps, e.ptrs):
@@ -526,7 +550,7 @@ def aggregate_modules(models: List[nn.Module], weights: Optional[Sequence[float]
         assert len(weights) == len(models)
     model0 = models[0]  # IndexError for an empty list, as the reference
     w32 = _native.fp32_weights(weights)
-    host_out = to_host if to_host is not None else not any(p.is_cuda for p in model0.parameters())
+    host_out = to_host if to_host is not None else not any(p.is_cuda for p in module_params(model0))
     layout, arenas, dev, on_host = reduce_modules_to_arenas(models, w32, mode, device, timing, host_out)
     stream = torch.cuda.current_stream(dev)
     st = _Stages(timing, stream)

@@ -28,10 +28,19 @@ import torch
 from torch import nn
 
 from . import _native
-from .arena import _target_device, input_arenas
+from .arena import ParamLayout, _target_device, module_params, registered_arenas
 from .batch import _device_views, _resolve, aggregate_arena_tasks
 
 Task = Tuple[str, str, dict]  # (task_name, func_name, data with placeholders)
+
+
+def _same_signature(ps, sig) -> bool:
+    if len(ps) != len(sig):
+        return False
+    for p, (shape, dt) in zip(ps, sig):
+        if p.dtype is not dt or p.shape != shape:
+            return False
+    return True
 
 
 def _is_ref(v) -> bool:
@@ -65,6 +74,7 @@ class RoundExecutor:
         self.mode = mode
         self.results: Dict[str, list] = {}
         self.waves: List[List[str]] = []
+        self._layouts: Dict[type, object] = {}  # model class -> a ParamLayout of it
 
     def _resolve(self, v):
         if _is_ref(v):
@@ -82,7 +92,23 @@ class RoundExecutor:
         hit = cache.get(id(m))
         if hit is not None and hit[0] is m:
             return hit[1], hit[2]
-        layout, params, views = input_arenas([m])
+        reg = registered_arenas(m)
+        if reg is not None:  # an aggregate output: its arenas as they are
+            layout, ar = reg
+            views = {dt: [ar[dt]] for dt in layout.groups}
+        else:
+            # a model of a class seen before reuses that layout when the
+            # parameter signature matches (no per-model ParamLayout build)
+            known = self._layouts.get(type(m))
+            ps = module_params(m)
+            if known is not None and _same_signature(ps, known._signature):
+                layout = known.rebind(ps)
+            else:
+                layout = ParamLayout(m)
+                self._layouts[type(m)] = layout
+            views = {dt: None if (v := layout.arena_view(layout.params, dt)) is None else [v]
+                     for dt in layout.groups}
+        params = [layout.params]
         dev = _device_views(views)
         if dev is not None and (self.device is None or dev == torch.device(self.device)):
             arenas = {dt: vs[0] for dt, vs in views.items()}

@@ -116,6 +116,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--cpu-rounds", type=int, default=2)
     ap.add_argument("--profile", default=None, help="cProfile the batched run into this file")
+    ap.add_argument("--profile-seq", default=None, help="cProfile the sequential run into this file")
     a = ap.parse_args()
     from dasklearn_amd.functions import aggregate
     from dasklearn_amd.rounds import RoundExecutor
@@ -144,11 +145,21 @@ def main():
         ex.run(tasks, seed={"init": [init_d]})
         prof.disable()
         with open(a.profile, "w") as f:
-            pstats.Stats(prof, stream=f).sort_stats("cumulative").print_stats(40)
+            pstats.Stats(prof, stream=f).sort_stats("tottime").print_stats(45)
     else:
         ex.run(tasks, seed={"init": [init_d]})
     bt, bn = ex.stats["aggregate"], ex.stats["aggregate_tasks"]
-    st, sn = sequential(tasks, aggregate, init_d, sync)
+    if a.profile_seq:
+        import cProfile
+        import pstats
+        prof = cProfile.Profile()
+        prof.enable()
+        st, sn = sequential(tasks, aggregate, init_d, sync)
+        prof.disable()
+        with open(a.profile_seq, "w") as f:
+            pstats.Stats(prof, stream=f).sort_stats("tottime").print_stats(45)
+    else:
+        st, sn = sequential(tasks, aggregate, init_d, sync)
 
     def cpu_agg(settings, d):
         return [fedavg_torch.aggregate_modules(d["models"], d.get("weights"))]

@@ -257,3 +257,27 @@ def test_host_pipeline_chunk_plan_covers_the_arena(monkeypatch, chunk_bytes):
         assert per.get(j, 0) == a
         per[j] = b
     assert [per[j] for j in range(len(lay.split_sizes[torch.float32]))] == lay.split_sizes[torch.float32]
+
+
+def test_module_params_matches_parameters():
+    """arena.module_params restates list(module.parameters()): pre-order
+    modules, each once; parameters in registration order, each once; None
+    slots skipped."""
+    from dasklearn_amd.arena import module_params
+
+    class Odd(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = nn.Linear(3, 4)
+            self.shared = nn.Linear(4, 4)
+            self.seq = nn.Sequential(nn.Conv2d(2, 3, 3), nn.ReLU(), self.shared, nn.BatchNorm1d(4))
+            self.register_parameter("none_slot", None)
+            self.tied = nn.Linear(3, 4)
+            self.tied.weight = self.a.weight  # shared parameter
+            self.w = nn.Parameter(torch.zeros(2))
+            self.empty = nn.Module()
+            self.shared_again = self.seq  # shared submodule
+
+    for m in (Odd(), nn.Sequential(nn.Linear(2, 2), nn.Linear(2, 2)), nn.Linear(1, 1), nn.Module()):
+        got, ref = module_params(m), list(m.parameters())
+        assert len(got) == len(ref) and all(a is b for a, b in zip(got, ref))
