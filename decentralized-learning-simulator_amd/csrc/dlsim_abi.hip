@@ -1,6 +1,7 @@
 // dlsim_abi.hip — the C ABI of include/dlsim.h over the gfx950 kernels of
 // wreduce_kernels.hpp. Host-side dispatch only: argument checks, choice of
 // vector vs scalar kernel, kernarg packing, multi-pass for n > 128.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -562,6 +563,29 @@ int run_chunk_mean(int b, const int* fan_in, const void* const* in, void* const*
   return flush();
 }
 
+// ---- RCCL, bound at run time --------------------------------------------------
+// The sharded entry point drives collectives on a caller's RCCL communicator.
+// The library does not link RCCL: dlsim_rccl_bind() dlopens the copy the
+// caller already uses (for a PyTorch process, the librccl.so next to
+// libtorch_hip.so, whose communicator ProcessGroupNCCL._comm_ptr() returns),
+// so one RCCL instance owns the communicator and its calls.
+typedef int rccl_result_t;  // ncclResult_t
+struct Rccl {
+  void* lib = nullptr;
+  rccl_result_t (*bcast)(const void*, void*, size_t, int, int, void*, hipStream_t) = nullptr;
+  rccl_result_t (*group_start)() = nullptr;
+  rccl_result_t (*group_end)() = nullptr;
+  rccl_result_t (*count)(void*, int*) = nullptr;
+  rccl_result_t (*user_rank)(void*, int*) = nullptr;
+  const char* (*err)(rccl_result_t) = nullptr;
+};
+Rccl g_rccl;
+constexpr int kRcclFloat32 = 7, kRcclBfloat16 = 9;  // ncclDataType_t (rccl.h)
+
+int rccl_fail(rccl_result_t r, const char* what) {
+  return fail(DLSIM_E_RCCL, "%s: %s (ncclResult %d)", what, g_rccl.err ? g_rccl.err(r) : "?", r);
+}
+
 }  // namespace
 
 extern "C" {
@@ -731,6 +755,70 @@ int dlsim_chunk_mean_batched(int b, const int* fan_in, const void* const* d_inpu
   return dtype == DLSIM_F32
              ? run_chunk_mean<dlsim::F32Mean>(b, fan_in, d_inputs, d_outs, n_elems, cpu_threads, st)
              : run_chunk_mean<dlsim::BF16Mean>(b, fan_in, d_inputs, d_outs, n_elems, cpu_threads, st);
+}
+
+int dlsim_rccl_bind(const char* librccl_path) {
+  g_err.clear();
+  if (!librccl_path || !*librccl_path) return fail(DLSIM_E_ARG, "null/empty librccl path");
+  void* h = dlopen(librccl_path, RTLD_NOW | RTLD_LOCAL);
+  if (!h) return fail(DLSIM_E_RCCL, "dlopen(%s): %s", librccl_path, dlerror());
+  Rccl r;
+  r.lib = h;
+  r.bcast = reinterpret_cast<decltype(r.bcast)>(dlsym(h, "ncclBroadcast"));
+  r.group_start = reinterpret_cast<decltype(r.group_start)>(dlsym(h, "ncclGroupStart"));
+  r.group_end = reinterpret_cast<decltype(r.group_end)>(dlsym(h, "ncclGroupEnd"));
+  r.count = reinterpret_cast<decltype(r.count)>(dlsym(h, "ncclCommCount"));
+  r.user_rank = reinterpret_cast<decltype(r.user_rank)>(dlsym(h, "ncclCommUserRank"));
+  r.err = reinterpret_cast<decltype(r.err)>(dlsym(h, "ncclGetErrorString"));
+  if (!r.bcast || !r.group_start || !r.group_end || !r.count || !r.user_rank || !r.err)
+    return fail(DLSIM_E_RCCL, "%s lacks an RCCL symbol", librccl_path);
+  g_rccl = r;
+  return DLSIM_OK;
+}
+
+int dlsim_wreduce_sharded(const void* const* d_slices, int n, const float* h_weights, void* d_out,
+                          size_t n_elems, int dtype, int mode, void* rccl_comm, int gather, void* stream) {
+  g_err.clear();
+  if (!g_rccl.lib) return fail(DLSIM_E_RCCL, "RCCL not bound (call dlsim_rccl_bind first)");
+  if (!rccl_comm) return fail(DLSIM_E_ARG, "null RCCL communicator");
+  int world = 0, rank = 0;
+  rccl_result_t rr = g_rccl.count(rccl_comm, &world);
+  if (rr != 0) return rccl_fail(rr, "ncclCommCount");
+  rr = g_rccl.user_rank(rccl_comm, &rank);
+  if (rr != 0) return rccl_fail(rr, "ncclCommUserRank");
+  if (n_elems > 0 && !d_out) return fail(DLSIM_E_ARG, "null output pointer");
+  size_t b = 0, e = 0;
+  int rc = dlsim_shard_range(n_elems, world, rank, 64, &b, &e);
+  if (rc != DLSIM_OK) return rc;
+  const size_t esz = elem_bytes(dtype);
+  char* out = static_cast<char*>(d_out);
+  // this rank's slice of every model -> this rank's slice of the output
+  if (e > b) {
+    rc = dlsim_wreduce(d_slices, n, h_weights, out + b * esz, e - b, dtype, mode, stream);
+    if (rc != DLSIM_OK) return rc;
+  } else {
+    rc = check_args(d_slices, n, h_weights, nullptr, 0, dtype, mode);
+    if (rc != DLSIM_OK) return rc;
+  }
+  if (!gather || world == 1 || n_elems == 0) return DLSIM_OK;
+  // variable-size all-gather: every rank broadcasts its slice in place
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int dt = dtype == DLSIM_BF16 ? kRcclBfloat16 : kRcclFloat32;
+  rr = g_rccl.group_start();
+  if (rr != 0) return rccl_fail(rr, "ncclGroupStart");
+  for (int r = 0; r < world; ++r) {
+    size_t rb = 0, re = 0;
+    dlsim_shard_range(n_elems, world, r, 64, &rb, &re);
+    if (re == rb) continue;
+    rr = g_rccl.bcast(out + rb * esz, out + rb * esz, re - rb, dt, r, rccl_comm, st);
+    if (rr != 0) {
+      g_rccl.group_end();
+      return rccl_fail(rr, "ncclBroadcast");
+    }
+  }
+  rr = g_rccl.group_end();
+  if (rr != 0) return rccl_fail(rr, "ncclGroupEnd");
+  return DLSIM_OK;
 }
 
 int dlsim_shard_range(size_t n_elems, int world, int rank, size_t align_elems, size_t* begin,

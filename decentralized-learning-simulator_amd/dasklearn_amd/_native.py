@@ -34,6 +34,8 @@ EXPORTS = (
     "dlsim_mean_batched",
     "dlsim_chunk_mean_batched",
     "dlsim_chunk_mean_ilp_begin",
+    "dlsim_rccl_bind",
+    "dlsim_wreduce_sharded",
     "dlsim_shard_range",
     "dlsim_probe_copy",
     "dlsim_last_error",
@@ -96,6 +98,11 @@ def load() -> ctypes.CDLL:
         lib.dlsim_chunk_mean_batched.restype = i
         lib.dlsim_chunk_mean_ilp_begin.argtypes = [i, sz, i]
         lib.dlsim_chunk_mean_ilp_begin.restype = sz
+        lib.dlsim_rccl_bind.argtypes = [ctypes.c_char_p]
+        lib.dlsim_rccl_bind.restype = i
+        lib.dlsim_wreduce_sharded.argtypes = [ctypes.POINTER(vp), i, ctypes.POINTER(ctypes.c_float), vp, sz, i, i,
+                                              vp, i, vp]
+        lib.dlsim_wreduce_sharded.restype = i
         lib.dlsim_shard_range.argtypes = [sz, i, i, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)]
         lib.dlsim_shard_range.restype = i
         lib.dlsim_probe_copy.argtypes = [vp, vp, sz, vp]
@@ -352,6 +359,50 @@ def chunk_mean_batched(tasks, threads=None, stream=None):
                                         (ctypes.c_void_p * b)(*outs), (ctypes.c_size_t * b)(*numels), dt,
                                         int(threads), _stream_handle(out0.device, stream)))
     return [t[1] for t in tasks]
+
+
+_RCCL_BOUND = None
+
+
+def rccl_bind(path: Optional[str] = None) -> str:
+    """Bind the RCCL that owns the caller's communicators (default: the
+    librccl.so PyTorch loaded, next to libtorch_hip.so)."""
+    global _RCCL_BOUND
+    if path is None:
+        import torch
+        path = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+        if not os.path.exists(path):
+            path = "librccl.so.1"
+    if _RCCL_BOUND != path:
+        _check("dlsim_rccl_bind", load().dlsim_rccl_bind(path.encode()))
+        _RCCL_BOUND = path
+    return path
+
+
+def wreduce_sharded(slices, weights_f32, out, comm_ptr: int, gather: bool = True,
+                    mode: int = DLSIM_EXACT, stream=None):
+    """dlsim_wreduce_sharded: `slices[i]` is this rank's slice of model i,
+    `out` the full-size output; `comm_ptr` an RCCL communicator (e.g.
+    ProcessGroupNCCL._comm_ptr())."""
+    lib = load()
+    rccl_bind()
+    n = len(slices)
+    if n < 1:
+        raise IndexError("list index out of range")
+    for x in slices:
+        if not x.is_cuda or x.dtype != out.dtype or not x.is_contiguous() or x.device != out.device:
+            raise ValueError("slices must be contiguous device tensors of the output's dtype and device")
+    if not out.is_cuda or not out.is_contiguous():
+        raise ValueError("out must be a contiguous device tensor")
+    w = np.ascontiguousarray(weights_f32, dtype=np.float32)
+    if w.size != n:
+        raise AssertionError("weights/models length mismatch")
+    ptrs = (ctypes.c_void_p * n)(*[x.data_ptr() for x in slices])
+    _check("dlsim_wreduce_sharded",
+           lib.dlsim_wreduce_sharded(ptrs, n, w.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), out.data_ptr(),
+                                     out.numel(), dtype_code(out.dtype), mode, ctypes.c_void_p(comm_ptr),
+                                     1 if gather else 0, _stream_handle(out.device, stream)))
+    return out
 
 
 def chunk_mean_ilp_begin(m: int, n: int, threads: int) -> int:

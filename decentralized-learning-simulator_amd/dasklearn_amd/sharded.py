@@ -12,7 +12,9 @@ Three entry points:
 * `aggregate_param_sharded` — rank r already holds slice r of every model
   (e.g. a device-resident arena partitioned at load time): one local exact
   reduce, no data-path collective; optionally an all-gather materialises the
-  full output. Bit-identical to the single-GPU (and reference) result.
+  full output. Bit-identical to the single-GPU (and reference) result. On an
+  "nccl" group this is the C ABI's `dlsim_wreduce_sharded` on the group's own
+  RCCL communicator (local reduce + grouped in-place broadcasts).
 * `aggregate_model_sharded(exact=True)` — whole models live on different
   ranks: an all-to-all moves slice j of every model to rank j (in global
   model order), then the exact local reduce, then an all-gather.
@@ -62,6 +64,20 @@ class ShardedAggregator:
     def all_bounds(self, n_elems: int) -> List[Tuple[int, int]]:
         return [self.bounds(n_elems, r) for r in range(self.world)]
 
+    def _rccl_comm(self, device) -> Optional[int]:
+        """The RCCL communicator behind this group (ProcessGroupNCCL._comm_ptr)
+        when the HIP kernel is the local reduce and the group runs on "nccl";
+        else None (gloo rehearsals, injected local reduces)."""
+        if self.local_reduce is not _hip_reduce or not device.type == "cuda" \
+                or dist.get_backend(self.group) != "nccl":
+            return None
+        try:
+            pg = self.group if self.group is not None else dist.distributed_c10d._get_default_group()
+            ptr = pg._get_backend(device)._comm_ptr()
+        except Exception:
+            return None
+        return int(ptr) or None
+
     # ---- collectives ------------------------------------------------------------
     def all_gather(self, shard: torch.Tensor, n_elems: int) -> torch.Tensor:
         """Concatenate every rank's slice into the full vector (ragged last
@@ -91,6 +107,13 @@ class ShardedAggregator:
         for x in shard_inputs:
             if x.numel() != e - b:
                 raise ValueError(f"rank {self.rank}: shard has {x.numel()} elements, expected {e - b}")
+        comm = self._rccl_comm(shard_inputs[0].device)
+        if comm is not None:
+            # the C ABI end to end: local reduce into the full buffer, then the
+            # grouped in-place broadcasts on the caller's RCCL communicator
+            full = torch.empty(n_elems, dtype=shard_inputs[0].dtype, device=shard_inputs[0].device)
+            _native.wreduce_sharded(list(shard_inputs), w32, full, comm, gather, mode)
+            return full if gather else full[b:e]
         out = torch.empty(e - b, dtype=shard_inputs[0].dtype, device=shard_inputs[0].device)
         if e > b:
             self.local_reduce(list(shard_inputs), w32, out, mode)

@@ -56,6 +56,7 @@ enum dlsim_mode {
 #define DLSIM_E_ARG (-1)      /* null pointer, n < 1, overlapping out/in, ... */
 #define DLSIM_E_DTYPE (-2)    /* dtype not in enum dlsim_dtype                */
 #define DLSIM_E_MODE (-3)     /* mode not in enum dlsim_mode                  */
+#define DLSIM_E_RCCL (-4)     /* RCCL not bound, or an RCCL call failed       */
 #define DLSIM_E_HIP (-100)    /* a HIP call failed: code = -100 - hipError_t  */
 
 /* Maximum inputs fused into one kernel launch; larger n is processed in
@@ -196,6 +197,31 @@ int dlsim_chunk_mean_batched(int b, const int* fan_in, const void* const* d_inpu
  * threads (host logic, no GPU; exposed for tests).
  */
 size_t dlsim_chunk_mean_ilp_begin(int m, size_t n_elems, int cpu_threads);
+
+/*
+ * dlsim_rccl_bind — dlopen the RCCL library whose communicators will be
+ * passed to dlsim_wreduce_sharded (the library does not link RCCL, so a
+ * process keeps one RCCL instance: from PyTorch, torch/lib/librccl.so, whose
+ * communicator ProcessGroupNCCL._comm_ptr() returns). Idempotent.
+ */
+int dlsim_rccl_bind(const char* librccl_path);
+
+/*
+ * dlsim_wreduce_sharded — the parameter-sharded aggregate across the ranks of
+ * an RCCL communicator (one process per GPU, xGMI). SURVEY.md §8b's
+ * `dlsim_wreduce_sharded(..., rcclComm)`; no reference counterpart (the
+ * reference is single-process CPU, fedavg.py:12-26).
+ *   rank r of W (from the communicator) owns elements [b_r, e_r) =
+ *   dlsim_shard_range(n_elems, W, r, 64); d_slices[i] points at that slice of
+ *   model i (e_r - b_r elements); d_out is a full n_elems buffer, and the
+ *   exact reduce of the slices lands at d_out + b_r. gather != 0: every
+ *   rank's slice is then broadcast in place (a variable-size all-gather,
+ *   grouped ncclBroadcast on `stream`), so every rank ends with the whole
+ *   output. Each element's N terms stay on one GPU in input order: results
+ *   are bit-identical to dlsim_wreduce on one GPU.
+ */
+int dlsim_wreduce_sharded(const void* const* d_slices, int n, const float* h_weights, void* d_out,
+                          size_t n_elems, int dtype, int mode, void* rccl_comm, int gather, void* stream);
 
 /*
  * dlsim_shard_range — parameter-axis partition used by the sharded path.

@@ -80,3 +80,28 @@ def test_sharded_entry_points_rccl(rccl_world1, n, p, dtype):
     assert torch.all((fast - expect.float()).abs() <= (n + 2) * ulp * scale + 1e-30)
     # uniform weights (fedavg.py:14-15)
     assert _same(agg.aggregate_param_sharded(xs, None, p), _expect(xs, orc.reference_weights(n, None), dtype))
+
+
+@pytest.mark.parametrize("n,p,dtype", [(4, 70_001, torch.float32), (3, 50_001, torch.bfloat16)])
+def test_c_abi_sharded_entry_on_torch_rccl_comm(rccl_world1, n, p, dtype):
+    """dlsim_wreduce_sharded driven directly on the process group's own RCCL
+    communicator (ProcessGroupNCCL._comm_ptr, RCCL bound from torch/lib):
+    gather and no-gather, bit-identical to the oracle."""
+    from dasklearn_amd import _native
+    from dasklearn_amd.sharded import ShardedAggregator
+    from oracle import oracle as orc
+
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(5 + n)
+    xs = [(torch.randn(p, generator=g, device=dev) * 0.05).to(dtype) for _ in range(n)]
+    w32 = orc.reference_weights(n, None)
+    expect = _expect(xs, w32, dtype)
+    agg = ShardedAggregator()
+    comm = agg._rccl_comm(dev)
+    assert comm is not None  # the ABI path is the one aggregate_param_sharded takes here
+    for gather in (True, False):
+        out = torch.full((p,), float("nan"), dtype=dtype, device=dev)
+        _native.wreduce_sharded(xs, w32, out, comm, gather=gather)
+        assert _same(out, expect)
+    # a null communicator is an argument error, not a crash
+    assert _native.load().dlsim_wreduce_sharded(None, 0, None, None, 0, 0, 0, None, 0, None) == -1
