@@ -776,8 +776,9 @@ int dlsim_rccl_bind(const char* librccl_path) {
   return DLSIM_OK;
 }
 
-int dlsim_wreduce_sharded(const void* const* d_slices, int n, const float* h_weights, void* d_out,
-                          size_t n_elems, int dtype, int mode, void* rccl_comm, int gather, void* stream) {
+int dlsim_wreduce_sharded(const void* const* d_slices, size_t slice_elems, int n, const float* h_weights,
+                          void* d_out, size_t n_elems, int dtype, int mode, void* rccl_comm, int gather,
+                          void* stream) {
   g_err.clear();
   if (!g_rccl.lib) return fail(DLSIM_E_RCCL, "RCCL not bound (call dlsim_rccl_bind first)");
   if (!rccl_comm) return fail(DLSIM_E_ARG, "null RCCL communicator");
@@ -790,6 +791,9 @@ int dlsim_wreduce_sharded(const void* const* d_slices, int n, const float* h_wei
   size_t b = 0, e = 0;
   int rc = dlsim_shard_range(n_elems, world, rank, 64, &b, &e);
   if (rc != DLSIM_OK) return rc;
+  if (slice_elems != e - b)
+    return fail(DLSIM_E_ARG, "rank %d of %d: slices have %zu elements, its shard [%zu, %zu) has %zu", rank, world,
+                slice_elems, b, e, e - b);
   const size_t esz = elem_bytes(dtype);
   char* out = static_cast<char*>(d_out);
   // this rank's slice of every model -> this rank's slice of the output

@@ -100,8 +100,8 @@ def load() -> ctypes.CDLL:
         lib.dlsim_chunk_mean_ilp_begin.restype = sz
         lib.dlsim_rccl_bind.argtypes = [ctypes.c_char_p]
         lib.dlsim_rccl_bind.restype = i
-        lib.dlsim_wreduce_sharded.argtypes = [ctypes.POINTER(vp), i, ctypes.POINTER(ctypes.c_float), vp, sz, i, i,
-                                              vp, i, vp]
+        lib.dlsim_wreduce_sharded.argtypes = [ctypes.POINTER(vp), sz, i, ctypes.POINTER(ctypes.c_float), vp, sz, i,
+                                              i, vp, i, vp]
         lib.dlsim_wreduce_sharded.restype = i
         lib.dlsim_shard_range.argtypes = [sz, i, i, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)]
         lib.dlsim_shard_range.restype = i
@@ -390,8 +390,10 @@ def wreduce_sharded(slices, weights_f32, out, comm_ptr: int, gather: bool = True
     if n < 1:
         raise IndexError("list index out of range")
     for x in slices:
-        if not x.is_cuda or x.dtype != out.dtype or not x.is_contiguous() or x.device != out.device:
-            raise ValueError("slices must be contiguous device tensors of the output's dtype and device")
+        if not x.is_cuda or x.dtype != out.dtype or not x.is_contiguous() or x.device != out.device \
+                or x.numel() != slices[0].numel():
+            raise ValueError("slices must be equal-length contiguous device tensors of the output's dtype "
+                             "and device")
     if not out.is_cuda or not out.is_contiguous():
         raise ValueError("out must be a contiguous device tensor")
     w = np.ascontiguousarray(weights_f32, dtype=np.float32)
@@ -399,7 +401,8 @@ def wreduce_sharded(slices, weights_f32, out, comm_ptr: int, gather: bool = True
         raise AssertionError("weights/models length mismatch")
     ptrs = (ctypes.c_void_p * n)(*[x.data_ptr() for x in slices])
     _check("dlsim_wreduce_sharded",
-           lib.dlsim_wreduce_sharded(ptrs, n, w.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), out.data_ptr(),
+           lib.dlsim_wreduce_sharded(ptrs, slices[0].numel(), n, w.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                                     out.data_ptr(),
                                      out.numel(), dtype_code(out.dtype), mode, ctypes.c_void_p(comm_ptr),
                                      1 if gather else 0, _stream_handle(out.device, stream)))
     return out

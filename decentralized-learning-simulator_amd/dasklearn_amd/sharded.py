@@ -68,7 +68,7 @@ class ShardedAggregator:
         """The RCCL communicator behind this group (ProcessGroupNCCL._comm_ptr)
         when the HIP kernel is the local reduce and the group runs on "nccl";
         else None (gloo rehearsals, injected local reduces)."""
-        if self.local_reduce is not _hip_reduce or not device.type == "cuda" \
+        if self.local_reduce is not _hip_reduce or not device.type == "cuda" or self.align != 64 \
                 or dist.get_backend(self.group) != "nccl":
             return None
         try:

@@ -213,15 +213,17 @@ int dlsim_rccl_bind(const char* librccl_path);
  * reference is single-process CPU, fedavg.py:12-26).
  *   rank r of W (from the communicator) owns elements [b_r, e_r) =
  *   dlsim_shard_range(n_elems, W, r, 64); d_slices[i] points at that slice of
- *   model i (e_r - b_r elements); d_out is a full n_elems buffer, and the
+ *   model i (slice_elems elements, which must equal e_r - b_r, else
+ *   DLSIM_E_ARG); d_out is a full n_elems buffer, and the
  *   exact reduce of the slices lands at d_out + b_r. gather != 0: every
  *   rank's slice is then broadcast in place (a variable-size all-gather,
  *   grouped ncclBroadcast on `stream`), so every rank ends with the whole
  *   output. Each element's N terms stay on one GPU in input order: results
  *   are bit-identical to dlsim_wreduce on one GPU.
  */
-int dlsim_wreduce_sharded(const void* const* d_slices, int n, const float* h_weights, void* d_out,
-                          size_t n_elems, int dtype, int mode, void* rccl_comm, int gather, void* stream);
+int dlsim_wreduce_sharded(const void* const* d_slices, size_t slice_elems, int n, const float* h_weights,
+                          void* d_out, size_t n_elems, int dtype, int mode, void* rccl_comm, int gather,
+                          void* stream);
 
 /*
  * dlsim_shard_range — parameter-axis partition used by the sharded path.

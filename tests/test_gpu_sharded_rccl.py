@@ -103,5 +103,8 @@ def test_c_abi_sharded_entry_on_torch_rccl_comm(rccl_world1, n, p, dtype):
         out = torch.full((p,), float("nan"), dtype=dtype, device=dev)
         _native.wreduce_sharded(xs, w32, out, comm, gather=gather)
         assert _same(out, expect)
-    # a null communicator is an argument error, not a crash
-    assert _native.load().dlsim_wreduce_sharded(None, 0, None, None, 0, 0, 0, None, 0, None) == -1
+    # a null communicator and a slice length that is not this rank's shard are
+    # argument errors, not launches
+    assert _native.load().dlsim_wreduce_sharded(None, 0, 0, None, None, 0, 0, 0, None, 0, None) == -1
+    with pytest.raises(_native.DlsimError, match="shard"):
+        _native.wreduce_sharded([x[:p - 1] for x in xs], w32, torch.empty(p, dtype=dtype, device=dev), comm)
