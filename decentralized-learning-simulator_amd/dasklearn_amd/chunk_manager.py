@@ -121,13 +121,24 @@ class ChunkManager:
                     if k:
                         tasks.append(([d_in[x:x + k] for x in offs], d_out[o:o + k]))
                 _native.chunk_mean_batched(tasks)
-                host = torch.empty(max(n_out, 1), dtype=dt, pin_memory=True)
-                host.copy_(d_out, non_blocking=True)
+                # the host result is always back to back (reconstruct_model
+                # then uses it without a cat): one D2H when the device
+                # layout is tight too, else one per chunk index
+                host_off = [0]
+                for k in sizes:
+                    host_off.append(host_off[-1] + k)
+                host = torch.empty(max(host_off[-1], 1), dtype=dt, pin_memory=True)
+                if tight:
+                    host.copy_(d_out, non_blocking=True)
+                else:
+                    for k, o, h in zip(sizes, out_off, host_off):
+                        if k:
+                            host[h:h + k].copy_(d_out[o:o + k], non_blocking=True)
                 torch.cuda.current_stream(dev).synchronize()
-                for ci, o in zip(idxs, out_off):
+                for ci, o, h in zip(idxs, out_off, host_off):
                     first = chunks[ci][0]
-                    src = host if not first.is_cuda else d_out
-                    results[ci] = src[o:o + first.numel()].view(first.shape)
+                    src = host[h:h + first.numel()] if not first.is_cuda else d_out[o:o + first.numel()]
+                    results[ci] = src.view(first.shape)
         return results
 
     @staticmethod
@@ -140,12 +151,24 @@ class ChunkManager:
         flat_params = _span(chunks)
         if flat_params is None:
             flat_params = torch.cat(chunks)
+        # chunk_manager.py:45-52: copy consecutive slices of the flat means
+        # into every state_dict tensor (parameters and buffers, with the
+        # dtype conversion of copy_). The copies go out as one
+        # torch._foreach_copy_ (a few multi-tensor launches for a device
+        # model instead of one per tensor).
+        dsts, srcs = [], []
         pointer = 0
+        for param in model.state_dict().values():
+            numel = param.data.numel()
+            dsts.append(param.data)
+            srcs.append(flat_params[pointer:pointer + numel].view(param.data.shape))
+            pointer += numel
         with torch.no_grad():
-            for param in model.state_dict().values():
-                numel = param.data.numel()
-                param.data.copy_(flat_params[pointer:pointer + numel].view(param.data.shape))
-                pointer += numel
+            if dsts and all(d.device == flat_params.device for d in dsts):
+                torch._foreach_copy_(dsts, srcs)
+            else:
+                for d, src in zip(dsts, srcs):
+                    d.copy_(src)
         return model
 
 

@@ -132,6 +132,60 @@ def main():
         del dflats, dev_chunks, dev_by_index, outs, tasks
 
 
+class ResNet18(nn.Module):
+    """torchvision resnet18(num_classes=10)'s module structure (the reference's
+    create_model("cifar10", "resnet18")): 62 parameters, 60 BatchNorm buffers
+    (num_batches_tracked int64), 122 state_dict entries, 11,181,642 params."""
+
+    def __init__(self):
+        super().__init__()
+        self.conv1 = nn.Conv2d(3, 64, 7, 2, 3, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        blocks, cin = [], 64
+        for cout, stride in ((64, 1), (128, 2), (256, 2), (512, 2)):
+            for b in range(2):
+                s = stride if b == 0 else 1
+                blk = nn.Module()
+                blk.conv1 = nn.Conv2d(cin, cout, 3, s, 1, bias=False)
+                blk.bn1 = nn.BatchNorm2d(cout)
+                blk.conv2 = nn.Conv2d(cout, cout, 3, 1, 1, bias=False)
+                blk.bn2 = nn.BatchNorm2d(cout)
+                if b == 0 and (s != 1 or cin != cout):
+                    blk.downsample = nn.Sequential(nn.Conv2d(cin, cout, 1, s, bias=False), nn.BatchNorm2d(cout))
+                blocks.append(blk)
+                cin = cout
+        self.blocks = nn.ModuleList(blocks)
+        self.fc = nn.Linear(512, 10)
+
+
+def resnet_case(dev, m=4, k=10):
+    """Conflux's reconstruct on a real state_dict: m peers' ResNet-18 models
+    chunked into k pieces, rebuilt into a fresh model (host and device)."""
+    torch.manual_seed(0)
+    models = [ResNet18() for _ in range(m)]
+    for mdl in models:
+        with torch.no_grad():
+            for t in mdl.state_dict().values():
+                if t.is_floating_point():
+                    t.copy_(torch.randn(t.shape) * 0.05)
+    host_chunks = [ChunkManager.chunk_model(mdl, k) for mdl in models]
+    by_index = [[host_chunks[i][c] for i in range(m)] for c in range(k)]
+    dev_by_index = [[c.to(dev) for c in cs] for cs in by_index]
+    res = {"case": "resnet18_state_dict", "k": k, "m": m, "entries": len(models[0].state_dict())}
+    tgt_d = ResNet18().to(dev)
+    res["device_ms"] = round(med(lambda: ChunkManager.reconstruct_model([list(c) for c in dev_by_index],
+                                                                       tgt_d)) * 1e3, 3)
+    tgt_h = ResNet18()
+    res["host_ms"] = round(med(lambda: ChunkManager.reconstruct_model([list(c) for c in by_index], tgt_h)) * 1e3, 3)
+    nt = torch.get_num_threads()
+    torch.set_num_threads(4)
+    tgt_c = ResNet18()
+    res["cpu_ref_4t_ms"] = round(med(lambda: cpu_reconstruct([list(c) for c in by_index], tgt_c), reps=5,
+                                     sync=False) * 1e3, 3)
+    torch.set_num_threads(nt)
+    return res
+
+
 def _wrap(flat):
     m = Flat()
     m.w = nn.Parameter(flat, requires_grad=False)
@@ -140,3 +194,4 @@ def _wrap(flat):
 
 if __name__ == "__main__":
     main()
+    print(json.dumps(resnet_case(torch.device("cuda", 0))), flush=True)
