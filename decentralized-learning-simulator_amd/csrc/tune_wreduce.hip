@@ -215,6 +215,33 @@ void launch_x(const Slots<128>& s, int n, void* out, size_t nvec, size_t, hipStr
                      nvec, per);
 }
 
+// Memory-ceiling probe: the shipped fp32 access pattern (wave map, nt
+// loads, sc1 stores, same tiles) with the arithmetic replaced by a bitwise
+// XOR of the inputs. Its time is what the HBM allows for exactly this
+// read/write mix; the exact reduce is compared against it.
+struct XorProbe {
+  static constexpr int E = 4;
+  static constexpr int kBytes = 4;
+  __device__ static float init(float) { return 0.0f; }
+  __device__ static float step(float acc, float, float x) {
+    return __uint_as_float(__float_as_uint(acc) ^ __float_as_uint(x));
+  }
+  __device__ static void step2(float& a0, float& a1, float w, float x0, float x1) {
+    a0 = step(a0, w, x0);
+    a1 = step(a1, w, x1);
+  }
+  __device__ static float finish(float a, float) { return a; }
+};
+
+template <class Op, int NF>
+void launch_probe(const Slots<128>& s, int n, void* out, size_t nvec, size_t nelem, hipStream_t st, int) {
+  if constexpr (Op::kBytes == 4) {
+    const size_t full = nvec / ((size_t)kBlock * 4);
+    hipLaunchKernelGGL((k_wreduce_tiles<XorProbe, 128, NF, 8, 4, 1, 16, true>), dim3((unsigned)(full + 1)),
+                       dim3(kBlock), 0, st, s, n, nullptr, out, nvec, nelem);
+  }
+}
+
 // Two tile sizes in one grid: the first ~gm percent of the vectors in big
 // tiles (VB vectors per lane), the rest in small tiles (VSM) dispatched last,
 // so the blocks still running at the end of the launch are short (a finer
@@ -275,6 +302,7 @@ void add_nf(std::vector<Variant>& vs, int n) {
   vs.push_back({p + "_V1_sc1_wave", launch_ts<Op, NF, 8, 1, 1, 16, true>, 0});
   vs.push_back({p + "_xcd_V4", launch_x<Op, NF, 4>, 0});
   vs.push_back({p + "_xcd_V2", launch_x<Op, NF, 2>, 0});
+  vs.push_back({p + "_xorprobe", launch_probe<Op, NF>, 0});
   vs.push_back({p + "_split80_V1", launch_split<Op, NF, 4, 1>, 80});
   vs.push_back({p + "_split90_V1", launch_split<Op, NF, 4, 1>, 90});
   vs.push_back({p + "_split95_V1", launch_split<Op, NF, 4, 1>, 95});
@@ -288,6 +316,8 @@ std::vector<Variant> variants(int n) {
       {"T_G8_V2", launch_t<Op, 0, 8, 2, true>, 0},
       {"T_G8_V4", launch_t<Op, 0, 8, 4, true>, 0},
       {"T_G8_V4_sc1", launch_ts<Op, 0, 8, 4, 1, 16>, 0},
+      {"T_G8_V4_sc1_wave", launch_ts<Op, 0, 8, 4, 1, 16, true>, 0},
+      {"T_xorprobe", launch_probe<Op, 0>, 0},
   };
   add_nf<Op, 2>(vs, n);
   add_nf<Op, 8>(vs, n);
