@@ -242,6 +242,34 @@ void launch_probe(const Slots<128>& s, int n, void* out, size_t nvec, size_t nel
   }
 }
 
+// Contiguous persistent: gm*256 blocks, block b sweeps tiles
+// [b*T/B, (b+1)*T/B) in order (wave map), so each wave streams long
+// contiguous runs of every input instead of one 4 KiB piece per block.
+template <class Op, int NF>
+__global__ __launch_bounds__(kBlock) void k_tiles_contig(const Slots<128> s, int n, void* __restrict__ out,
+                                                         size_t nvec, size_t nelem) {
+  constexpr size_t kTile = (size_t)kBlock * 4;
+  const size_t full = nvec / kTile;
+  const OutRef o = make_out<16>(out, nvec);
+  const size_t B = gridDim.x;
+  if (blockIdx.x == 0) {
+    if (full * kTile < nvec)
+      reduce_tile<Op, Slots<128>, NF, 8, 4, 1, true, 16>(s, n, nullptr, o, full * kTile + threadIdx.x, nvec);
+    const size_t j = nvec * Op::E + threadIdx.x;
+    if (j < nelem) fold_scalar<Op, Slots<128>>(s, n, nullptr, out, j);
+  }
+  const size_t t0 = full * blockIdx.x / B, t1 = full * (blockIdx.x + 1) / B;
+  const size_t lo = (threadIdx.x >> 6) * 64 * 4 + (threadIdx.x & 63);
+  for (size_t t = t0; t < t1; ++t)
+    reduce_tile<Op, Slots<128>, NF, 8, 4, 1, false, 16, 64>(s, n, nullptr, o, t * kTile + lo, nvec);
+}
+
+template <class Op, int NF>
+void launch_contig(const Slots<128>& s, int n, void* out, size_t nvec, size_t nelem, hipStream_t st, int gm) {
+  hipLaunchKernelGGL((k_tiles_contig<Op, NF>), dim3((unsigned)(gm * 256)), dim3(kBlock), 0, st, s, n, out, nvec,
+                     nelem);
+}
+
 // Two tile sizes in one grid: the first ~gm percent of the vectors in big
 // tiles (VB vectors per lane), the rest in small tiles (VSM) dispatched last,
 // so the blocks still running at the end of the launch are short (a finer
@@ -303,6 +331,9 @@ void add_nf(std::vector<Variant>& vs, int n) {
   vs.push_back({p + "_xcd_V4", launch_x<Op, NF, 4>, 0});
   vs.push_back({p + "_xcd_V2", launch_x<Op, NF, 2>, 0});
   vs.push_back({p + "_xorprobe", launch_probe<Op, NF>, 0});
+  vs.push_back({p + "_contig2", launch_contig<Op, NF>, 2});
+  vs.push_back({p + "_contig3", launch_contig<Op, NF>, 3});
+  vs.push_back({p + "_contig6", launch_contig<Op, NF>, 6});
   vs.push_back({p + "_split80_V1", launch_split<Op, NF, 4, 1>, 80});
   vs.push_back({p + "_split90_V1", launch_split<Op, NF, 4, 1>, 90});
   vs.push_back({p + "_split95_V1", launch_split<Op, NF, 4, 1>, 95});
