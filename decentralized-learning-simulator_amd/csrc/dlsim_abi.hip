@@ -421,11 +421,30 @@ int table_launch(const void* h_table, const void* d_table, hipStream_t st) {
   return DLSIM_OK;
 }
 
-size_t elem_bytes(int dtype) { return dtype == DLSIM_BF16 ? 2 : 4; }
+size_t elem_bytes(int dtype) { return dtype == DLSIM_F32 ? 4 : 2; }
+
+bool known_dtype(int dtype) { return dtype == DLSIM_F32 || dtype == DLSIM_BF16 || dtype == DLSIM_F16; }
+
+// f(Op{}) with the element policy of (dtype, mode). Callers check both first.
+template <class F>
+int with_policy(int dtype, int mode, F&& f) {
+  const bool fast = mode == DLSIM_FAST;
+  if (dtype == DLSIM_F32) return fast ? f(dlsim::F32Fast{}) : f(dlsim::F32Exact{});
+  if (dtype == DLSIM_BF16) return fast ? f(dlsim::BF16Fast{}) : f(dlsim::BF16Exact{});
+  return fast ? f(dlsim::F16Fast{}) : f(dlsim::F16Exact{});
+}
+
+// f(Op{}) with the mean policy (element format) of dtype.
+template <class F>
+int with_mean_policy(int dtype, F&& f) {
+  if (dtype == DLSIM_F32) return f(dlsim::F32Mean{});
+  if (dtype == DLSIM_BF16) return f(dlsim::BF16Mean{});
+  return f(dlsim::F16Mean{});
+}
 
 int check_args(const void* const* in, int n, const float* w, const void* out, size_t nelem,
                int dtype, int mode, bool need_w = true) {
-  if (dtype != DLSIM_F32 && dtype != DLSIM_BF16) return fail(DLSIM_E_DTYPE, "unsupported dtype %d", dtype);
+  if (!known_dtype(dtype)) return fail(DLSIM_E_DTYPE, "unsupported dtype %d", dtype);
   if (mode != DLSIM_EXACT && mode != DLSIM_FAST) return fail(DLSIM_E_MODE, "unsupported mode %d", mode);
   if (n < 1) return fail(DLSIM_E_ARG, "n must be >= 1 (got %d)", n);
   if (!in || (need_w && !w)) return fail(DLSIM_E_ARG, "null inputs or weights array");
@@ -446,11 +465,7 @@ int check_args(const void* const* in, int n, const float* w, const void* out, si
 
 int dispatch(const void* const* in, int n, const float* w, void* out, size_t nelem, int dtype,
              int mode, hipStream_t st) {
-  if (dtype == DLSIM_F32)
-    return mode == DLSIM_EXACT ? run<dlsim::F32Exact>(in, n, w, out, nelem, st)
-                               : run<dlsim::F32Fast>(in, n, w, out, nelem, st);
-  return mode == DLSIM_EXACT ? run<dlsim::BF16Exact>(in, n, w, out, nelem, st)
-                             : run<dlsim::BF16Fast>(in, n, w, out, nelem, st);
+  return with_policy(dtype, mode, [&](auto op) { return run<decltype(op)>(in, n, w, out, nelem, st); });
 }
 
 // ---- chunk mean in PyTorch's CPU order (chunk_mean_kernels.hpp) --------------
@@ -580,7 +595,7 @@ struct Rccl {
   const char* (*err)(rccl_result_t) = nullptr;
 };
 Rccl g_rccl;
-constexpr int kRcclFloat32 = 7, kRcclBfloat16 = 9;  // ncclDataType_t (rccl.h)
+constexpr int kRcclFloat16 = 6, kRcclFloat32 = 7, kRcclBfloat16 = 9;  // ncclDataType_t (rccl.h)
 
 int rccl_fail(rccl_result_t r, const char* what) {
   return fail(DLSIM_E_RCCL, "%s: %s (ncclResult %d)", what, g_rccl.err ? g_rccl.err(r) : "?", r);
@@ -622,13 +637,9 @@ int dlsim_wreduce_tensors(const void* const* d_inputs, int n, int t, const size_
   }
   if (t == 0) return DLSIM_OK;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (dtype == DLSIM_F32)
-    return mode == DLSIM_EXACT
-               ? run_batched<dlsim::F32Exact>(t, fan.data(), ins.data(), ws.data(), d_outs, numels, st)
-               : run_batched<dlsim::F32Fast>(t, fan.data(), ins.data(), ws.data(), d_outs, numels, st);
-  return mode == DLSIM_EXACT
-             ? run_batched<dlsim::BF16Exact>(t, fan.data(), ins.data(), ws.data(), d_outs, numels, st)
-             : run_batched<dlsim::BF16Fast>(t, fan.data(), ins.data(), ws.data(), d_outs, numels, st);
+  return with_policy(dtype, mode, [&](auto op) {
+    return run_batched<decltype(op)>(t, fan.data(), ins.data(), ws.data(), d_outs, numels, st);
+  });
 }
 
 int dlsim_wreduce_batched(int b, const int* fan_in, const void* const* d_inputs,
@@ -645,24 +656,21 @@ int dlsim_wreduce_batched(int b, const int* fan_in, const void* const* d_inputs,
     off += static_cast<size_t>(fan_in[t]);
   }
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (dtype == DLSIM_F32)
-    return mode == DLSIM_EXACT
-               ? run_batched<dlsim::F32Exact>(b, fan_in, d_inputs, h_weights, d_outs, n_elems, st)
-               : run_batched<dlsim::F32Fast>(b, fan_in, d_inputs, h_weights, d_outs, n_elems, st);
-  return mode == DLSIM_EXACT
-             ? run_batched<dlsim::BF16Exact>(b, fan_in, d_inputs, h_weights, d_outs, n_elems, st)
-             : run_batched<dlsim::BF16Fast>(b, fan_in, d_inputs, h_weights, d_outs, n_elems, st);
+  return with_policy(dtype, mode, [&](auto op) {
+    return run_batched<decltype(op)>(b, fan_in, d_inputs, h_weights, d_outs, n_elems, st);
+  });
 }
 
 int dlsim_batch_table_bytes(int b, const int* fan_in, const size_t* n_elems, int dtype, size_t* bytes) {
   g_err.clear();
   if (b < 0 || (b > 0 && (!fan_in || !n_elems)) || !bytes) return fail(DLSIM_E_ARG, "bad arguments");
-  if (dtype != DLSIM_F32 && dtype != DLSIM_BF16) return fail(DLSIM_E_DTYPE, "unsupported dtype %d", dtype);
+  if (!known_dtype(dtype)) return fail(DLSIM_E_DTYPE, "unsupported dtype %d", dtype);
   for (int t = 0; t < b; ++t)
     if (fan_in[t] < 1) return fail(DLSIM_E_ARG, "task %d: fan-in must be >= 1", t);
   TableLayout L;
-  const bool ok = dtype == DLSIM_F32 ? table_layout<dlsim::F32Exact>(b, fan_in, n_elems, &L)
-                                     : table_layout<dlsim::BF16Exact>(b, fan_in, n_elems, &L);
+  const bool ok = with_policy(dtype, DLSIM_EXACT, [&](auto op) {
+    return table_layout<decltype(op)>(b, fan_in, n_elems, &L) ? 1 : 0;
+  }) != 0;
   if (!ok) return fail(DLSIM_E_ARG, "batch too large");
   *bytes = L.bytes;
   return DLSIM_OK;
@@ -681,22 +689,18 @@ int dlsim_batch_table_fill(int b, const int* fan_in, const void* const* d_inputs
     if (rc != DLSIM_OK) return fail(rc, "task %d: %s", t, g_err.c_str());
     off += static_cast<size_t>(fan_in[t]);
   }
-  return dtype == DLSIM_F32
-             ? table_fill<dlsim::F32Exact>(b, fan_in, d_inputs, h_weights, d_outs, n_elems, h_table, table_bytes)
-             : table_fill<dlsim::BF16Exact>(b, fan_in, d_inputs, h_weights, d_outs, n_elems, h_table, table_bytes);
+  return with_policy(dtype, DLSIM_EXACT, [&](auto op) {
+    return table_fill<decltype(op)>(b, fan_in, d_inputs, h_weights, d_outs, n_elems, h_table, table_bytes);
+  });
 }
 
 int dlsim_batch_table_launch(const void* h_table, const void* d_table, int dtype, int mode, void* stream) {
   g_err.clear();
   if (!h_table || !d_table) return fail(DLSIM_E_ARG, "null table");
-  if (dtype != DLSIM_F32 && dtype != DLSIM_BF16) return fail(DLSIM_E_DTYPE, "unsupported dtype %d", dtype);
+  if (!known_dtype(dtype)) return fail(DLSIM_E_DTYPE, "unsupported dtype %d", dtype);
   if (mode != DLSIM_EXACT && mode != DLSIM_FAST) return fail(DLSIM_E_MODE, "unsupported mode %d", mode);
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (dtype == DLSIM_F32)
-    return mode == DLSIM_EXACT ? table_launch<dlsim::F32Exact>(h_table, d_table, st)
-                               : table_launch<dlsim::F32Fast>(h_table, d_table, st);
-  return mode == DLSIM_EXACT ? table_launch<dlsim::BF16Exact>(h_table, d_table, st)
-                             : table_launch<dlsim::BF16Fast>(h_table, d_table, st);
+  return with_policy(dtype, mode, [&](auto op) { return table_launch<decltype(op)>(h_table, d_table, st); });
 }
 
 int dlsim_mean(const void* const* d_inputs, int n, void* d_out, size_t n_elems, int dtype,
@@ -706,8 +710,9 @@ int dlsim_mean(const void* const* d_inputs, int n, void* d_out, size_t n_elems, 
   if (rc != DLSIM_OK) return rc;
   hipStream_t st = static_cast<hipStream_t>(stream);
   const float div = static_cast<float>(n);
-  return dtype == DLSIM_F32 ? run<dlsim::F32Mean>(d_inputs, n, nullptr, d_out, n_elems, st, div)
-                            : run<dlsim::BF16Mean>(d_inputs, n, nullptr, d_out, n_elems, st, div);
+  return with_mean_policy(dtype, [&](auto op) {
+    return run<decltype(op)>(d_inputs, n, nullptr, d_out, n_elems, st, div);
+  });
 }
 
 int dlsim_mean_batched(int b, const int* fan_in, const void* const* d_inputs, void* const* d_outs,
@@ -726,9 +731,9 @@ int dlsim_mean_batched(int b, const int* fan_in, const void* const* d_inputs, vo
   }
   const std::vector<float> ones(off, 1.0f);  // unused by the mean policies
   hipStream_t st = static_cast<hipStream_t>(stream);
-  return dtype == DLSIM_F32
-             ? run_batched<dlsim::F32Mean>(b, fan_in, d_inputs, ones.data(), d_outs, n_elems, st, divs.data())
-             : run_batched<dlsim::BF16Mean>(b, fan_in, d_inputs, ones.data(), d_outs, n_elems, st, divs.data());
+  return with_mean_policy(dtype, [&](auto op) {
+    return run_batched<decltype(op)>(b, fan_in, d_inputs, ones.data(), d_outs, n_elems, st, divs.data());
+  });
 }
 
 size_t dlsim_chunk_mean_ilp_begin(int m, size_t n_elems, int cpu_threads) {
@@ -752,9 +757,9 @@ int dlsim_chunk_mean_batched(int b, const int* fan_in, const void* const* d_inpu
     off += static_cast<size_t>(fan_in[t]);
   }
   hipStream_t st = static_cast<hipStream_t>(stream);
-  return dtype == DLSIM_F32
-             ? run_chunk_mean<dlsim::F32Mean>(b, fan_in, d_inputs, d_outs, n_elems, cpu_threads, st)
-             : run_chunk_mean<dlsim::BF16Mean>(b, fan_in, d_inputs, d_outs, n_elems, cpu_threads, st);
+  return with_mean_policy(dtype, [&](auto op) {
+    return run_chunk_mean<decltype(op)>(b, fan_in, d_inputs, d_outs, n_elems, cpu_threads, st);
+  });
 }
 
 int dlsim_rccl_bind(const char* librccl_path) {
@@ -807,7 +812,7 @@ int dlsim_wreduce_sharded(const void* const* d_slices, size_t slice_elems, int n
   if (!gather || world == 1 || n_elems == 0) return DLSIM_OK;
   // variable-size all-gather: every rank broadcasts its slice in place
   hipStream_t st = static_cast<hipStream_t>(stream);
-  const int dt = dtype == DLSIM_BF16 ? kRcclBfloat16 : kRcclFloat32;
+  const int dt = dtype == DLSIM_BF16 ? kRcclBfloat16 : dtype == DLSIM_F16 ? kRcclFloat16 : kRcclFloat32;
   rr = g_rccl.group_start();
   if (rr != 0) return rccl_fail(rr, "ncclGroupStart");
   for (int r = 0; r < world; ++r) {

@@ -22,6 +22,7 @@ namespace dlsim {
 struct BF16ExactOld {  // integer RNE with an explicit NaN branch (round-1 shape)
   static constexpr int E = 8;
   static constexpr int kBytes = 2;
+  static constexpr int kFmt = kFmtBF16;
   __device__ static float init(float x) { return bf16_round(x * 0.0f); }
   __device__ static float step(float acc, float w, float x) {
     return bf16_round(acc + bf16_round(w * x));
@@ -39,6 +40,7 @@ __device__ __forceinline__ float bf16_round_nonan(float f) {  // valid when NaNs
 struct BF16ExactInt {
   static constexpr int E = 8;
   static constexpr int kBytes = 2;
+  static constexpr int kFmt = kFmtBF16;
   __device__ static float init(float x) { return x * 0.0f; }
   __device__ static float step(float acc, float w, float x) {
     return bf16_round_nonan(acc + bf16_round_nonan(w * x));
@@ -222,6 +224,7 @@ void launch_x(const Slots<128>& s, int n, void* out, size_t nvec, size_t, hipStr
 struct XorProbe {
   static constexpr int E = 4;
   static constexpr int kBytes = 4;
+  static constexpr int kFmt = kFmtF32;
   __device__ static float init(float) { return 0.0f; }
   __device__ static float step(float acc, float, float x) {
     return __uint_as_float(__float_as_uint(acc) ^ __float_as_uint(x));

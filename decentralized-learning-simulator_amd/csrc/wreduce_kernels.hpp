@@ -59,6 +59,23 @@ __device__ __forceinline__ void bf16_round2(float& a0, float& a1) {
   a1 = __uint_as_float(u & 0xffff0000u);
 }
 
+// ---- fp16 helpers -------------------------------------------------------------
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+
+// fp32 -> fp16 -> fp32, nearest-even (hardware conversion; NaN stays NaN,
+// overflow to inf, fp16 subnormals kept).
+__device__ __forceinline__ float f16_round(float f) { return static_cast<float>(static_cast<_Float16>(f)); }
+
+__device__ __forceinline__ void f16_round2(float& a0, float& a1) {
+  const f32x2 v = {a0, a1};
+  const f32x2 r = __builtin_convertvector(__builtin_convertvector(v, f16x2), f32x2);
+  a0 = r[0];
+  a1 = r[1];
+}
+
+// Element formats: what a 16-bit element means (kBytes == 2 policies).
+constexpr int kFmtF32 = 0, kFmtBF16 = 1, kFmtF16 = 2;
+
 // ---- element policies -------------------------------------------------------
 // E  = elements per 16-byte vector
 // init(x0): value of acc after p.mul_(0)
@@ -68,6 +85,7 @@ __device__ __forceinline__ void bf16_round2(float& a0, float& a1) {
 struct F32Exact {
   static constexpr int E = 4;
   static constexpr int kBytes = 4;
+  static constexpr int kFmt = kFmtF32;
   __device__ static float init(float x) { return x * 0.0f; }
   __device__ static float step(float acc, float w, float x) {
     const float p = w * x;  // rounded: contraction is off
@@ -83,6 +101,7 @@ struct F32Exact {
 struct F32Fast {
   static constexpr int E = 4;
   static constexpr int kBytes = 4;
+  static constexpr int kFmt = kFmtF32;
   __device__ static float init(float x) { return x * 0.0f; }
   __device__ static float step(float acc, float w, float x) { return __builtin_fmaf(w, x, acc); }
   __device__ static void step2(float& a0, float& a1, float w, float x0, float x1) {
@@ -97,6 +116,7 @@ struct F32Fast {
 struct BF16Exact {
   static constexpr int E = 8;
   static constexpr int kBytes = 2;
+  static constexpr int kFmt = kFmtBF16;
   __device__ static float init(float x) { return x * 0.0f; }
   __device__ static float step(float acc, float w, float x) {
     const float p = bf16_round(w * x);
@@ -115,6 +135,7 @@ struct BF16Exact {
 struct BF16Fast {
   static constexpr int E = 8;
   static constexpr int kBytes = 2;
+  static constexpr int kFmt = kFmtBF16;
   __device__ static float init(float x) { return x * 0.0f; }
   __device__ static float step(float acc, float w, float x) { return __builtin_fmaf(w, x, acc); }
   __device__ static void step2(float& a0, float& a1, float w, float x0, float x1) {
@@ -122,6 +143,40 @@ struct BF16Fast {
     a1 = step(a1, w, x1);
   }
   __device__ static float finish(float a, float) { return bf16_round(a); }
+};
+
+// fp16 exact: as bf16 (PyTorch's CPU opmath for Half is fp32 too): the
+// product and the sum each rounded to fp16, nearest-even.
+struct F16Exact {
+  static constexpr int E = 8;
+  static constexpr int kBytes = 2;
+  static constexpr int kFmt = kFmtF16;
+  __device__ static float init(float x) { return x * 0.0f; }
+  __device__ static float step(float acc, float w, float x) {
+    const float p = f16_round(w * x);
+    return f16_round(acc + p);
+  }
+  __device__ static void step2(float& a0, float& a1, float w, float x0, float x1) {
+    float p0 = w * x0, p1 = w * x1;
+    f16_round2(p0, p1);
+    a0 = a0 + p0;
+    a1 = a1 + p1;
+    f16_round2(a0, a1);
+  }
+  __device__ static float finish(float a, float) { return a; }
+};
+
+struct F16Fast {
+  static constexpr int E = 8;
+  static constexpr int kBytes = 2;
+  static constexpr int kFmt = kFmtF16;
+  __device__ static float init(float x) { return x * 0.0f; }
+  __device__ static float step(float acc, float w, float x) { return __builtin_fmaf(w, x, acc); }
+  __device__ static void step2(float& a0, float& a1, float w, float x0, float x1) {
+    a0 = step(a0, w, x0);
+    a1 = step(a1, w, x1);
+  }
+  __device__ static float finish(float a, float) { return f16_round(a); }
 };
 
 // Mean of the inputs in input order (dlsim_mean): acc starts at +0 (the
@@ -134,6 +189,7 @@ struct BF16Fast {
 struct F32Mean {
   static constexpr int E = 4;
   static constexpr int kBytes = 4;
+  static constexpr int kFmt = kFmtF32;
   __device__ static float init(float) { return 0.0f; }
   __device__ static float step(float acc, float, float x) { return acc + x; }
   __device__ static void step2(float& a0, float& a1, float, float x0, float x1) {
@@ -146,6 +202,7 @@ struct F32Mean {
 struct BF16Mean {
   static constexpr int E = 8;
   static constexpr int kBytes = 2;
+  static constexpr int kFmt = kFmtBF16;
   __device__ static float init(float) { return 0.0f; }
   __device__ static float step(float acc, float, float x) { return acc + x; }
   __device__ static void step2(float& a0, float& a1, float, float x0, float x1) {
@@ -155,12 +212,32 @@ struct BF16Mean {
   __device__ static float finish(float a, float div) { return bf16_round(a / div); }
 };
 
+struct F16Mean {
+  static constexpr int E = 8;
+  static constexpr int kBytes = 2;
+  static constexpr int kFmt = kFmtF16;
+  __device__ static float init(float) { return 0.0f; }
+  __device__ static float step(float acc, float, float x) { return acc + x; }
+  __device__ static void step2(float& a0, float& a1, float, float x0, float x1) {
+    a0 = a0 + x0;
+    a1 = a1 + x1;
+  }
+  __device__ static float finish(float a, float div) { return f16_round(a / div); }
+};
+
 // ---- 16-byte vector <-> E floats --------------------------------------------
 template <class Op>
 __device__ __forceinline__ void unpack(const u32x4& r, float (&x)[Op::E]) {
   if constexpr (Op::kBytes == 4) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) x[e] = __uint_as_float(r[e]);
+  } else if constexpr (Op::kFmt == kFmtF16) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const uint32_t u = r[e];
+      x[2 * e] = static_cast<float>(__builtin_bit_cast(_Float16, static_cast<uint16_t>(u & 0xffffu)));
+      x[2 * e + 1] = static_cast<float>(__builtin_bit_cast(_Float16, static_cast<uint16_t>(u >> 16)));
+    }
   } else {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -176,6 +253,14 @@ __device__ __forceinline__ u32x4 pack(const float (&a)[Op::E], float div) {
   if constexpr (Op::kBytes == 4) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) r[e] = __float_as_uint(Op::finish(a[e], div));
+  } else if constexpr (Op::kFmt == kFmtF16) {
+    // finish() already rounded to fp16, so the conversion is exact
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const uint32_t lo = __builtin_bit_cast(uint16_t, static_cast<_Float16>(Op::finish(a[2 * e], div)));
+      const uint32_t hi = __builtin_bit_cast(uint16_t, static_cast<_Float16>(Op::finish(a[2 * e + 1], div)));
+      r[e] = lo | (hi << 16);
+    }
   } else {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -192,6 +277,8 @@ template <class Op>
 __device__ __forceinline__ float load_elem(const void* p, size_t j) {
   if constexpr (Op::kBytes == 4) {
     return static_cast<const float*>(p)[j];
+  } else if constexpr (Op::kFmt == kFmtF16) {
+    return static_cast<float>(static_cast<const _Float16*>(p)[j]);
   } else {
     return __uint_as_float(static_cast<uint32_t>(static_cast<const uint16_t*>(p)[j]) << 16);
   }
@@ -201,6 +288,8 @@ template <class Op>
 __device__ __forceinline__ void store_elem(void* p, size_t j, float a, float div) {
   if constexpr (Op::kBytes == 4) {
     static_cast<float*>(p)[j] = Op::finish(a, div);
+  } else if constexpr (Op::kFmt == kFmtF16) {
+    static_cast<_Float16*>(p)[j] = static_cast<_Float16>(Op::finish(a, div));
   } else {
     static_cast<uint16_t*>(p)[j] = static_cast<uint16_t>(__float_as_uint(Op::finish(a, div)) >> 16);
   }

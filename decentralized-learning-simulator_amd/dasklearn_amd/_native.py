@@ -17,6 +17,7 @@ LIB_PATH = os.path.join(LIB_DIR, "libdlsim_hip.so")
 
 DLSIM_F32 = 0
 DLSIM_BF16 = 1
+DLSIM_F16 = 2
 DLSIM_EXACT = 0
 DLSIM_FAST = 1
 MAX_FUSED_INPUTS = 128
@@ -145,7 +146,9 @@ def dtype_code(torch_dtype) -> int:
         return DLSIM_F32
     if torch_dtype == torch.bfloat16:
         return DLSIM_BF16
-    raise TypeError(f"aggregation supports float32 and bfloat16 parameters, got {torch_dtype}")
+    if torch_dtype == torch.float16:
+        return DLSIM_F16
+    raise TypeError(f"aggregation supports float32, bfloat16 and float16 parameters, got {torch_dtype}")
 
 
 def _stream_handle(device, stream) -> Optional[int]:

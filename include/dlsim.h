@@ -36,17 +36,19 @@ extern "C" {
 /* ---- element types and summation modes ---------------------------------- */
 enum dlsim_dtype {
   DLSIM_F32 = 0,  /* IEEE binary32                                      */
-  DLSIM_BF16 = 1  /* bfloat16 (upper 16 bits of binary32), RNE rounding  */
+  DLSIM_BF16 = 1, /* bfloat16 (upper 16 bits of binary32), RNE rounding  */
+  DLSIM_F16 = 2   /* IEEE binary16, RNE rounding                        */
 };
 
 enum dlsim_mode {
   /* Bit-identical to FedAvg.aggregate (fedavg.py:20-25) on the same inputs:
    *   acc = x0 * 0;  for i in 0..n-1: acc = acc + fl32(w_i) * x_i
    * in that order, multiply and add rounded separately (no FMA); for bf16
-   * the product and every partial sum are rounded to bf16 (PyTorch's CPU
-   * opmath semantics). NaN payloads are not part of the contract. */
+   * and f16 the product and every partial sum are rounded to the element
+   * type (PyTorch's CPU opmath semantics). NaN payloads are not part of the
+   * contract. */
   DLSIM_EXACT = 0,
-  /* Fused multiply-add, fp32 accumulation (bf16: one final rounding).
+  /* Fused multiply-add, fp32 accumulation (bf16/f16: one final rounding).
    * Within n * 2^-23 relative (fp32) of EXACT; not bit-identical. */
   DLSIM_FAST = 1
 };

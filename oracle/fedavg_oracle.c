@@ -42,7 +42,44 @@ uint16_t oracle_f32_to_bf16(float f) {
 
 float oracle_bf16_to_f32(uint16_t h) { return u2f((uint32_t)h << 16); }
 
-static float bf16r(float f) { return oracle_bf16_to_f32(oracle_f32_to_bf16(f)); }
+
+/* fp32 -> IEEE binary16 bits, round-to-nearest-even, subnormals kept,
+ * overflow to inf; NaN stays NaN (quiet). */
+uint16_t oracle_f32_to_f16(float f) {
+  const uint32_t x = f2u(f);
+  const uint16_t sign = (uint16_t)((x >> 16) & 0x8000u);
+  const uint32_t ax = x & 0x7fffffffu;
+  if (ax > 0x7f800000u) return (uint16_t)(sign | 0x7e00u | ((ax >> 13) & 0x3ffu));
+  if (ax >= 0x477ff000u) return (uint16_t)(sign | 0x7c00u); /* >= 65520: inf (ties to even) */
+  if (ax < 0x38800000u) {                                    /* below 2^-14: subnormal or zero */
+    if (ax < 0x33000000u) return sign;                       /* <= 2^-25 rounds to zero */
+    const uint32_t e = ax >> 23, m = (ax & 0x7fffffu) | 0x800000u;
+    const uint32_t shift = 126u - e; /* value / 2^-24 = m >> shift */
+    uint32_t q = m >> shift;
+    const uint32_t rem = m & ((1u << shift) - 1u), half = 1u << (shift - 1u);
+    if (rem > half || (rem == half && (q & 1u))) ++q;
+    return (uint16_t)(sign | q);
+  }
+  uint32_t r = ax - (112u << 23);
+  r += 0xfffu + ((r >> 13) & 1u);
+  return (uint16_t)(sign | (r >> 13));
+}
+
+float oracle_f16_to_f32(uint16_t h) {
+  const uint32_t sign = (uint32_t)(h & 0x8000u) << 16;
+  const uint32_t e = (h >> 10) & 0x1fu, m = h & 0x3ffu;
+  if (e == 0) {
+    const float v = ldexpf((float)m, -24);
+    return sign ? -v : v;
+  }
+  if (e == 31) return u2f(sign | 0x7f800000u | (m << 13));
+  return u2f(sign | ((e + 112u) << 23) | (m << 13));
+}
+
+/* 16-bit element formats: bf16 and IEEE f16 share every routine below
+ * through these conversions. */
+typedef float (*h2f_fn)(uint16_t);
+typedef uint16_t (*f2h_fn)(float);
 
 /* out[j] = fold over i of fl(w[i] * in[i][j]), starting from in[0][j] * 0. */
 int oracle_wreduce_f32(const float* const* in, int n, const float* w, float* out, size_t p) {
@@ -75,18 +112,28 @@ int oracle_wreduce_f32_rows(const float* x, int n, const float* w, float* out, s
   return 0;
 }
 
-int oracle_wreduce_bf16(const uint16_t* const* in, int n, const float* w, uint16_t* out,
-                        size_t p) {
+static int wreduce_h16(const uint16_t* const* in, int n, const float* w, uint16_t* out, size_t p,
+                       h2f_fn h2f, f2h_fn f2h) {
   if (n < 1 || !in || !w || !out) return -1;
   for (size_t j = 0; j < p; ++j) {
-    float acc = bf16r(oracle_bf16_to_f32(in[0][j]) * 0.0f);
+    float acc = h2f(f2h(h2f(in[0][j]) * 0.0f));
     for (int i = 0; i < n; ++i) {
-      float prod = bf16r(w[i] * oracle_bf16_to_f32(in[i][j]));
-      acc = bf16r(acc + prod);
+      float prod = h2f(f2h(w[i] * h2f(in[i][j])));
+      acc = h2f(f2h(acc + prod));
     }
-    out[j] = oracle_f32_to_bf16(acc);
+    out[j] = f2h(acc);
   }
   return 0;
+}
+
+int oracle_wreduce_bf16(const uint16_t* const* in, int n, const float* w, uint16_t* out, size_t p) {
+  return wreduce_h16(in, n, w, out, p, oracle_bf16_to_f32, oracle_f32_to_bf16);
+}
+
+/* fp16 (torch.float16 models): the same opmath as bf16 — fp32 products and
+ * sums, each rounded to binary16 (checked against torch's CPU Half ops). */
+int oracle_wreduce_f16(const uint16_t* const* in, int n, const float* w, uint16_t* out, size_t p) {
+  return wreduce_h16(in, n, w, out, p, oracle_f16_to_f32, oracle_f32_to_f16);
 }
 
 /* FAST-mode reference: fp32 fma chain (bf16: fp32 accumulation, one final
@@ -102,15 +149,23 @@ int oracle_wreduce_fast_f32(const float* const* in, int n, const float* w, float
   return 0;
 }
 
-int oracle_wreduce_fast_bf16(const uint16_t* const* in, int n, const float* w, uint16_t* out,
-                             size_t p) {
+static int wreduce_fast_h16(const uint16_t* const* in, int n, const float* w, uint16_t* out, size_t p,
+                            h2f_fn h2f, f2h_fn f2h) {
   if (n < 1 || !in || !w || !out) return -1;
   for (size_t j = 0; j < p; ++j) {
-    float acc = oracle_bf16_to_f32(in[0][j]) * 0.0f;
-    for (int i = 0; i < n; ++i) acc = fmaf(w[i], oracle_bf16_to_f32(in[i][j]), acc);
-    out[j] = oracle_f32_to_bf16(acc);
+    float acc = h2f(in[0][j]) * 0.0f;
+    for (int i = 0; i < n; ++i) acc = fmaf(w[i], h2f(in[i][j]), acc);
+    out[j] = f2h(acc);
   }
   return 0;
+}
+
+int oracle_wreduce_fast_bf16(const uint16_t* const* in, int n, const float* w, uint16_t* out, size_t p) {
+  return wreduce_fast_h16(in, n, w, out, p, oracle_bf16_to_f32, oracle_f32_to_bf16);
+}
+
+int oracle_wreduce_fast_f16(const uint16_t* const* in, int n, const float* w, uint16_t* out, size_t p) {
+  return wreduce_fast_h16(in, n, w, out, p, oracle_f16_to_f32, oracle_f32_to_f16);
 }
 
 /* Mean of n rows, as PyTorch's CPU `torch.mean(torch.stack(xs), 0)` computes
@@ -129,14 +184,22 @@ int oracle_mean_f32(const float* const* in, int n, float* out, size_t p) {
   return 0;
 }
 
-int oracle_mean_bf16(const uint16_t* const* in, int n, uint16_t* out, size_t p) {
+static int mean_h16(const uint16_t* const* in, int n, uint16_t* out, size_t p, h2f_fn h2f, f2h_fn f2h) {
   if (n < 1 || !in || !out) return -1;
   for (size_t j = 0; j < p; ++j) {
     float acc = 0.0f;
-    for (int i = 0; i < n; ++i) acc = acc + oracle_bf16_to_f32(in[i][j]);
-    out[j] = oracle_f32_to_bf16(acc / (float)n);
+    for (int i = 0; i < n; ++i) acc = acc + h2f(in[i][j]);
+    out[j] = f2h(acc / (float)n);
   }
   return 0;
+}
+
+int oracle_mean_bf16(const uint16_t* const* in, int n, uint16_t* out, size_t p) {
+  return mean_h16(in, n, out, p, oracle_bf16_to_f32, oracle_f32_to_bf16);
+}
+
+int oracle_mean_f16(const uint16_t* const* in, int n, uint16_t* out, size_t p) {
+  return mean_h16(in, n, out, p, oracle_f16_to_f32, oracle_f32_to_f16);
 }
 
 /* ---- torch.mean(torch.stack(rows), 0) in PyTorch's own CPU order ----------
@@ -257,7 +320,8 @@ int oracle_chunk_mean_f32(const float* const* in, int m, float* out, size_t n, i
   return 0;
 }
 
-int oracle_chunk_mean_bf16(const uint16_t* const* in, int m, uint16_t* out, size_t n, int threads) {
+static int chunk_mean_h16(const uint16_t* const* in, int m, uint16_t* out, size_t n, int threads, h2f_fn h2f,
+                          f2h_fn f2h) {
   if (m < 1 || !in || !out) return -1;
   float* tmp = (float*)malloc(sizeof(float) * (n ? n : 1));
   float** rows = (float**)malloc(sizeof(float*) * (size_t)m);
@@ -267,14 +331,22 @@ int oracle_chunk_mean_bf16(const uint16_t* const* in, int m, uint16_t* out, size
   for (int i = 0; i < m && rc == 0; ++i) {
     rows[i] = (float*)malloc(sizeof(float) * (n ? n : 1));
     if (!rows[i]) { rc = -2; for (int k = 0; k < i; ++k) free(rows[k]); break; }
-    for (size_t j = 0; j < n; ++j) rows[i][j] = oracle_bf16_to_f32(in[i][j]);
+    for (size_t j = 0; j < n; ++j) rows[i][j] = h2f(in[i][j]);
   }
   if (rc == 0) {
     rc = oracle_chunk_mean_f32((const float* const*)rows, m, tmp, n, threads);
-    for (size_t j = 0; j < n && rc == 0; ++j) out[j] = oracle_f32_to_bf16(tmp[j]);
+    for (size_t j = 0; j < n && rc == 0; ++j) out[j] = f2h(tmp[j]);
     for (int i = 0; i < m; ++i) free(rows[i]);
   }
   free(tmp);
   free(rows);
   return rc;
+}
+
+int oracle_chunk_mean_bf16(const uint16_t* const* in, int m, uint16_t* out, size_t n, int threads) {
+  return chunk_mean_h16(in, m, out, n, threads, oracle_bf16_to_f32, oracle_f32_to_bf16);
+}
+
+int oracle_chunk_mean_f16(const uint16_t* const* in, int m, uint16_t* out, size_t n, int threads) {
+  return chunk_mean_h16(in, m, out, n, threads, oracle_f16_to_f32, oracle_f32_to_f16);
 }

@@ -43,15 +43,15 @@ def _load():
     lib = ctypes.CDLL(_LIB_PATH)
     pp = ctypes.POINTER(ctypes.c_void_p)
     for name in ("oracle_wreduce_f32", "oracle_wreduce_bf16", "oracle_wreduce_fast_f32",
-                 "oracle_wreduce_fast_bf16"):
+                 "oracle_wreduce_fast_bf16", "oracle_wreduce_f16", "oracle_wreduce_fast_f16"):
         fn = getattr(lib, name)
         fn.argtypes = [pp, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
         fn.restype = ctypes.c_int
-    for name in ("oracle_mean_f32", "oracle_mean_bf16"):
+    for name in ("oracle_mean_f32", "oracle_mean_bf16", "oracle_mean_f16"):
         fn = getattr(lib, name)
         fn.argtypes = [pp, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t]
         fn.restype = ctypes.c_int
-    for name in ("oracle_chunk_mean_f32", "oracle_chunk_mean_bf16"):
+    for name in ("oracle_chunk_mean_f32", "oracle_chunk_mean_bf16", "oracle_chunk_mean_f16"):
         fn = getattr(lib, name)
         fn.argtypes = [pp, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
         fn.restype = ctypes.c_int
@@ -86,9 +86,9 @@ def _as_rows(xs, np_dtype):
 def wreduce(xs, weights, dtype: str = "f32", mode: str = "exact") -> np.ndarray:
     """N-way weighted reduce of flat arrays, reference rounding order.
 
-    xs: sequence of N arrays — float32 for "f32", uint16 bf16 bit patterns for
-    "bf16". weights: fp32 array-like of length N (already resolved).
-    Returns float32 (f32) or uint16 (bf16 bits).
+    xs: sequence of N arrays — float32 for "f32", uint16 bit patterns for
+    "bf16" and "f16". weights: fp32 array-like of length N (already resolved).
+    Returns float32 (f32) or uint16 bit patterns (bf16, f16).
     """
     lib = _load()
     n = len(xs)
@@ -101,10 +101,10 @@ def wreduce(xs, weights, dtype: str = "f32", mode: str = "exact") -> np.ndarray:
         rows, p = _as_rows(xs, np.float32)
         out = np.empty(p, dtype=np.float32)
         fn = lib.oracle_wreduce_f32 if mode == "exact" else lib.oracle_wreduce_fast_f32
-    elif dtype == "bf16":
+    elif dtype in ("bf16", "f16"):
         rows, p = _as_rows(xs, np.uint16)
         out = np.empty(p, dtype=np.uint16)
-        fn = lib.oracle_wreduce_bf16 if mode == "exact" else lib.oracle_wreduce_fast_bf16
+        fn = getattr(lib, f"oracle_wreduce_{dtype}" if mode == "exact" else f"oracle_wreduce_fast_{dtype}")
     else:
         raise ValueError(f"unsupported dtype {dtype}")
     ptrs = (ctypes.c_void_p * n)(*[r.ctypes.data for r in rows])
@@ -127,10 +127,12 @@ def mean(xs, dtype: str = "f32") -> np.ndarray:
         rows, p = _as_rows(xs, np.float32)
         out = np.empty(p, dtype=np.float32)
         fn = lib.oracle_mean_f32
-    else:
+    elif dtype in ("bf16", "f16"):
         rows, p = _as_rows(xs, np.uint16)
         out = np.empty(p, dtype=np.uint16)
-        fn = lib.oracle_mean_bf16
+        fn = getattr(lib, f"oracle_mean_{dtype}")
+    else:
+        raise ValueError(f"unsupported dtype {dtype}")
     ptrs = (ctypes.c_void_p * n)(*[r.ctypes.data for r in rows])
     if fn(ctypes.cast(ptrs, ctypes.POINTER(ctypes.c_void_p)), n, out.ctypes.data, p) != 0:
         raise RuntimeError("oracle mean failed")
@@ -150,10 +152,12 @@ def chunk_mean(xs, dtype: str = "f32", threads: int = 4) -> np.ndarray:
         rows, p = _as_rows(xs, np.float32)
         out = np.empty(p, dtype=np.float32)
         fn = lib.oracle_chunk_mean_f32
-    else:
+    elif dtype in ("bf16", "f16"):
         rows, p = _as_rows(xs, np.uint16)
         out = np.empty(p, dtype=np.uint16)
-        fn = lib.oracle_chunk_mean_bf16
+        fn = getattr(lib, f"oracle_chunk_mean_{dtype}")
+    else:
+        raise ValueError(f"unsupported dtype {dtype}")
     ptrs = (ctypes.c_void_p * n)(*[r.ctypes.data for r in rows])
     if fn(ctypes.cast(ptrs, ctypes.POINTER(ctypes.c_void_p)), n, out.ctypes.data, p, threads) != 0:
         raise RuntimeError("oracle chunk mean failed")
@@ -186,6 +190,16 @@ def f32_to_bf16_bits(x: np.ndarray) -> np.ndarray:
     r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
     r[nan] = 0x7FC0
     return r
+
+
+def f32_to_f16_bits(x: np.ndarray) -> np.ndarray:
+    """RNE fp32 -> IEEE binary16 bit patterns (numpy's conversion)."""
+    with np.errstate(over="ignore"):  # overflow to inf is the rounding rule
+        return np.asarray(x, dtype=np.float32).astype(np.float16).view(np.uint16)
+
+
+def f16_bits_to_f32(h: np.ndarray) -> np.ndarray:
+    return np.asarray(h, dtype=np.uint16).view(np.float16).astype(np.float32)
 
 
 def bf16_bits_to_f32(h: np.ndarray) -> np.ndarray:

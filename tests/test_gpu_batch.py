@@ -25,9 +25,10 @@ def dev():
 
 def make_task(rng, n, p, dtype, misalign=False):
     x = rng.standard_normal((n, p + 1)).astype(np.float32) * np.float32(0.05)
-    rows = orc.f32_to_bf16_bits(x) if dtype == "bf16" else x
-    if dtype == "bf16":
-        t = [torch.from_numpy(r.view(np.int16).copy()).view(torch.bfloat16).to(dev()) for r in rows]
+    rows = orc.f32_to_bf16_bits(x) if dtype == "bf16" else orc.f32_to_f16_bits(x) if dtype == "f16" else x
+    if dtype in ("bf16", "f16"):
+        tdt = torch.bfloat16 if dtype == "bf16" else torch.float16
+        t = [torch.from_numpy(r.view(np.int16).copy()).view(tdt).to(dev()) for r in rows]
     else:
         t = [torch.from_numpy(r.copy()).to(dev()) for r in rows]
     s = 1 if misalign else 0
@@ -42,19 +43,19 @@ def check(tasks, dtype, mode=_native.DLSIM_EXACT):
     _native.wreduce_batched([(t[0], t[2], t[3]) for t in tasks], mode)
     for ins, host, w, out in tasks:
         got = out.cpu()
-        got = got.view(torch.int16).numpy().view(np.uint16) if dtype == "bf16" else got.numpy()
+        got = got.view(torch.int16).numpy().view(np.uint16) if dtype != "f32" else got.numpy()
         exp = orc.wreduce(host, w, dtype, "exact" if mode == 0 else "fast")
         assert orc.same_bits(got, exp)
 
 
-@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16"])
 def test_uniform_fan_in_batch(dtype):
     rng = np.random.default_rng(1)
     tasks = [make_task(rng, 4, 85_354 + k, dtype) for k in range(10)]
     check(tasks, dtype)
 
 
-@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16"])
 def test_mixed_fan_in_and_sizes(dtype):
     rng = np.random.default_rng(2)
     tasks = [make_task(rng, n, p, dtype) for n, p in [(2, 1), (3, 17), (9, 4096), (16, 100_003),
@@ -96,7 +97,7 @@ def _cpu(m):
     return copy.deepcopy(m).cpu()
 
 
-@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16"])
 def test_table_plan_whole_round(dtype):
     """100 peers x fan-in 8 (one D-PSGD round of GNLeNet-sized tasks) in one
     table launch, launched twice (the table is reusable)."""
@@ -109,7 +110,7 @@ def test_table_plan_whole_round(dtype):
         plan.launch()
         for ins, host, w, out in tasks:
             got = out.cpu()
-            got = got.view(torch.int16).numpy().view(np.uint16) if dtype == "bf16" else got.numpy()
+            got = got.view(torch.int16).numpy().view(np.uint16) if dtype != "f32" else got.numpy()
             assert orc.same_bits(got, orc.wreduce(host, w, dtype))
 
 

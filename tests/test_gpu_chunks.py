@@ -148,10 +148,11 @@ def _rows_t(rng, m, n, dtype, offset=0):
     """m rows of n elements as device tensors, `offset` elements into their
     buffers (offset 1: not 16-byte aligned)."""
     x = (rng.standard_normal((m, n)) * np.exp(rng.standard_normal((m, n)) * 2)).astype(np.float32)
-    rows = orc.f32_to_bf16_bits(x) if dtype == "bf16" else x
+    rows = orc.f32_to_bf16_bits(x) if dtype == "bf16" else orc.f32_to_f16_bits(x) if dtype == "f16" else x
+    tdt = torch.bfloat16 if dtype == "bf16" else torch.float16
     ts = []
     for r in rows:
-        h = torch.from_numpy(r.view(np.int16).copy()).view(torch.bfloat16) if dtype == "bf16" \
+        h = torch.from_numpy(r.view(np.int16).copy()).view(tdt) if dtype != "f32" \
             else torch.from_numpy(r.copy())
         buf = torch.empty(n + offset, dtype=h.dtype, device=dev())
         buf[offset:].copy_(h)
@@ -161,10 +162,10 @@ def _rows_t(rng, m, n, dtype, offset=0):
 
 def _bits(t):
     t = t.cpu()
-    return t.view(torch.int16).numpy().view(np.uint16) if t.dtype == torch.bfloat16 else t.numpy()
+    return t.view(torch.int16).numpy().view(np.uint16) if t.dtype != torch.float32 else t.numpy()
 
 
-@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16"])
 @pytest.mark.parametrize("threads", [1, 4, 8])
 def test_chunk_mean_matches_torch_order(dtype, threads):
     """Every (m, n) class of PyTorch's CPU sum order — cascade blocks, the
@@ -172,7 +173,7 @@ def test_chunk_mean_matches_torch_order(dtype, threads):
     reduction, the level-1 flush at 16 rows — in batches that cross the
     32-task / 192-input launch limits: each task bit-identical to the
     order-exact oracle (pinned against torch.mean on the CPU)."""
-    rng = np.random.default_rng(threads * 10 + (dtype == "bf16"))
+    rng = np.random.default_rng(threads * 10 + ["f32", "bf16", "f16"].index(dtype))
     tasks, exp = [], []
     for m in (1, 2, 3, 4, 5, 8, 9, 16, 17, 18, 33, 100):
         for n in (1, 2, 3, 5, 7, 8, 9, 31, 33, 65, 1000, 4099, 40001):
@@ -184,7 +185,7 @@ def test_chunk_mean_matches_torch_order(dtype, threads):
         assert orc.same_bits(_bits(out), e), (len(ts), out.numel())
 
 
-@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16"])
 def test_chunk_mean_unaligned_and_aliased(dtype):
     """Rows one element into their buffers (scalar path), and the output
     aliasing input 0."""

@@ -32,7 +32,7 @@ class Ragged(nn.Module):
 
 def modules_from_golden(g):
     meta = g["meta"]
-    dt = torch.bfloat16 if meta["dtype"] == "bf16" else torch.float32
+    dt = {"bf16": torch.bfloat16, "f16": torch.float16}.get(meta["dtype"], torch.float32)
     models = []
     for row in g["inputs"]:
         m = Ragged(meta["shapes"], dt)
@@ -41,8 +41,8 @@ def modules_from_golden(g):
             for p in m.parameters():
                 k = p.numel()
                 src = row[off:off + k]
-                if meta["dtype"] == "bf16":
-                    t = torch.from_numpy(src.view(np.int16).copy()).view(torch.bfloat16)
+                if meta["dtype"] in ("bf16", "f16"):
+                    t = torch.from_numpy(src.view(np.int16).copy()).view(dt)
                 else:
                     t = torch.from_numpy(src.copy())
                 p.copy_(t.view_as(p))
@@ -53,7 +53,7 @@ def modules_from_golden(g):
 
 def flat_of(model):
     t = torch.cat([p.detach().reshape(-1).cpu() for p in model.parameters()])
-    if t.dtype == torch.bfloat16:
+    if t.dtype in (torch.bfloat16, torch.float16):
         return t.view(torch.int16).numpy().view(np.uint16)
     return t.numpy()
 
@@ -228,7 +228,7 @@ def test_wire_decode_to_device_feeds_aggregate_without_packing():
 # ---- chunked host pipeline (arena._host_pipeline) ------------------------------------
 
 class Mixed(nn.Module):
-    """fp32 and bf16 parameter groups, interleaved (two arenas)."""
+    """fp32, bf16 and fp16 parameter groups, interleaved (three arenas)."""
 
     def __init__(self, seed):
         super().__init__()
@@ -238,17 +238,18 @@ class Mixed(nn.Module):
         self.c = nn.Parameter(torch.randn(4097, generator=g) * 0.05)
         self.d = nn.Parameter((torch.randn(64, 65, generator=g) * 0.05).to(torch.bfloat16))
         self.e = nn.Parameter(torch.randn(3, generator=g))
+        self.f = nn.Parameter((torch.randn(777, generator=g) * 0.05).to(torch.float16))
 
 
 def _expected_by_dtype(models, weights):
     w = orc.reference_weights(len(models), weights)
     out = {}
-    for dt, code in ((torch.float32, "f32"), (torch.bfloat16, "bf16")):
+    for dt, code in ((torch.float32, "f32"), (torch.bfloat16, "bf16"), (torch.float16, "f16")):
         rows = []
         for m in models:
             ps = [p.detach().reshape(-1) for p in m.parameters() if p.dtype == dt]
             t = torch.cat(ps)
-            rows.append(t.view(torch.int16).numpy().view(np.uint16) if dt == torch.bfloat16 else t.numpy())
+            rows.append(t.view(torch.int16).numpy().view(np.uint16) if dt != torch.float32 else t.numpy())
         out[dt] = orc.wreduce(rows, w, code)
     return out
 
@@ -267,9 +268,9 @@ def test_host_pipeline_chunks_are_exact(monkeypatch, chunk_bytes, to_host):
     out = FedAvg.aggregate(models, weights, to_host=to_host)
     assert all(p.is_cuda == (to_host is False) for p in out.parameters())
     exp = _expected_by_dtype(models, weights)
-    for dt in (torch.float32, torch.bfloat16):
+    for dt in (torch.float32, torch.bfloat16, torch.float16):
         t = torch.cat([p.detach().reshape(-1).cpu() for p in out.parameters() if p.dtype == dt])
-        got = t.view(torch.int16).numpy().view(np.uint16) if dt == torch.bfloat16 else t.numpy()
+        got = t.view(torch.int16).numpy().view(np.uint16) if dt != torch.float32 else t.numpy()
         assert orc.same_bits(got, exp[dt]), (dt, chunk_bytes)
 
 

@@ -27,16 +27,19 @@ def dev():
     return torch.device("cuda", 0)
 
 
+HALF = {"bf16": torch.bfloat16, "f16": torch.float16}
+
+
 def to_dev(rows, dtype):
-    if dtype == "bf16":
-        return [torch.from_numpy(np.ascontiguousarray(r).view(np.int16).copy()).view(torch.bfloat16).to(dev())
+    if dtype in HALF:
+        return [torch.from_numpy(np.ascontiguousarray(r).view(np.int16).copy()).view(HALF[dtype]).to(dev())
                 for r in rows]
     return [torch.from_numpy(np.ascontiguousarray(r, dtype=np.float32)).to(dev()) for r in rows]
 
 
 def from_dev(t):
     t = t.cpu()
-    if t.dtype == torch.bfloat16:
+    if t.dtype in (torch.bfloat16, torch.float16):
         return t.view(torch.int16).numpy().view(np.uint16)
     return t.numpy()
 
@@ -70,10 +73,12 @@ def make_rows(n, p, seed, dtype):
     x = (rng.standard_normal((n, p)).astype(np.float32) * np.float32(0.05))
     if dtype == "bf16":
         return orc.f32_to_bf16_bits(x)
+    if dtype == "f16":
+        return orc.f32_to_f16_bits(x)
     return x
 
 
-@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16"])
 @pytest.mark.parametrize("n", NS)
 def test_exact_vs_oracle_across_n(n, dtype):
     p = 4097 + n  # ragged tail of every width
@@ -83,7 +88,7 @@ def test_exact_vs_oracle_across_n(n, dtype):
     assert orc.same_bits(got, orc.wreduce(list(rows), w, dtype))
 
 
-@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16"])
 @pytest.mark.parametrize("p", SIZES)
 def test_exact_vs_oracle_across_sizes(p, dtype):
     n = 8
@@ -93,7 +98,7 @@ def test_exact_vs_oracle_across_sizes(p, dtype):
     assert orc.same_bits(got, orc.wreduce(list(rows), w, dtype))
 
 
-@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16"])
 def test_misaligned_inputs_take_scalar_path(dtype):
     """Views offset by one element are not 16-byte aligned: scalar kernel."""
     n, p = 5, 10_001
@@ -105,7 +110,7 @@ def test_misaligned_inputs_take_scalar_path(dtype):
     assert orc.same_bits(from_dev(out), orc.wreduce([r[1:] for r in rows], w, dtype))
 
 
-@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16"])
 def test_output_may_alias_first_input(dtype):
     n, p = 4, 50_003
     rows = make_rows(n, p, 5, dtype)
@@ -128,14 +133,14 @@ def test_empty_tensor_is_noop():
 
 
 def test_unsupported_dtype_raises():
-    x = torch.zeros(16, dtype=torch.float16, device=dev())
+    x = torch.zeros(16, dtype=torch.float64, device=dev())
     with pytest.raises(TypeError):
         _native.wreduce([x], orc.reference_weights(1, None), x)
 
 
 # ---- tensor-list entry ----------------------------------------------------------
 
-@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16"])
 @pytest.mark.parametrize("n", [3, 130])
 def test_tensor_list_entry_matches_flat(n, dtype):
     sizes = [1027, 64, 3, 517, 1, 4096]
@@ -185,6 +190,21 @@ def test_fast_mode_bf16_within_tolerance(n):
     # (2^-8 relative) of the magnitude sum
     scale = np.abs(w[:, None] * orc.bf16_bits_to_f32(rows)).sum(axis=0)
     assert np.all(np.abs(g - exact) <= (n + 1) * 2.0 ** -8 * scale + 1e-30)
+
+
+@pytest.mark.parametrize("n", [2, 17])
+def test_fast_mode_f16_within_tolerance(n):
+    p = 100_003
+    rows = make_rows(n, p, 5321 + n, "f16")
+    w = orc.reference_weights(n, None)
+    got = hip_reduce(list(rows), w, "f16", _native.DLSIM_FAST)
+    assert orc.same_bits(got, orc.wreduce(list(rows), w, "f16", mode="fast"))
+    exact = orc.f16_bits_to_f32(orc.wreduce(list(rows), w, "f16"))
+    g = orc.f16_bits_to_f32(got)
+    # one final f16 rounding vs n per-step roundings: within (n+1) f16 ulps
+    # (2^-11 relative) of the magnitude sum, plus the subnormal spacing
+    scale = np.abs(w[:, None] * orc.f16_bits_to_f32(rows)).sum(axis=0)
+    assert np.all(np.abs(g - exact) <= (n + 1) * 2.0 ** -11 * scale + (n + 1) * 2.0 ** -24)
 
 
 # ---- full-size configurations (BASELINE.json) --------------------------------------

@@ -39,15 +39,16 @@ def rccl_world1():
 
 def _expect(xs, w32, dtype):
     from oracle import oracle as orc
-    if dtype == torch.bfloat16:
+    if dtype in (torch.bfloat16, torch.float16):
+        code = "bf16" if dtype == torch.bfloat16 else "f16"
         rows = [x.cpu().view(torch.int16).numpy().view(np.uint16) for x in xs]
-        return torch.from_numpy(orc.wreduce(rows, w32, "bf16").view(np.int16).copy()).view(torch.bfloat16)
+        return torch.from_numpy(orc.wreduce(rows, w32, code).view(np.int16).copy()).view(dtype)
     return torch.from_numpy(orc.wreduce([x.cpu().numpy() for x in xs], w32, "f32"))
 
 
 def _same(a, b):
     a, b = a.cpu(), b.cpu()
-    if a.dtype == torch.bfloat16:
+    if a.dtype in (torch.bfloat16, torch.float16):
         return torch.equal(a.view(torch.int16), b.view(torch.int16))
     return torch.equal(a.view(torch.int32), b.view(torch.int32))
 
@@ -82,7 +83,8 @@ def test_sharded_entry_points_rccl(rccl_world1, n, p, dtype):
     assert _same(agg.aggregate_param_sharded(xs, None, p), _expect(xs, orc.reference_weights(n, None), dtype))
 
 
-@pytest.mark.parametrize("n,p,dtype", [(4, 70_001, torch.float32), (3, 50_001, torch.bfloat16)])
+@pytest.mark.parametrize("n,p,dtype", [(4, 70_001, torch.float32), (3, 50_001, torch.bfloat16),
+                                       (5, 30_003, torch.float16)])
 def test_c_abi_sharded_entry_on_torch_rccl_comm(rccl_world1, n, p, dtype):
     """dlsim_wreduce_sharded driven directly on the process group's own RCCL
     communicator (ProcessGroupNCCL._comm_ptr, RCCL bound from torch/lib):

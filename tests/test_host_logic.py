@@ -47,7 +47,9 @@ def test_no_cpu_fallback_without_gpu():
 
 
 def test_unsupported_param_dtype_raises():
-    m = nn.Linear(3, 3).to(torch.float16)
+    """float32, bfloat16 and float16 parameters run on the GPU; others raise."""
+    arena.ParamLayout(nn.Linear(3, 3).to(torch.float16))
+    m = nn.Linear(3, 3).to(torch.float64)
     with pytest.raises(TypeError):
         arena.ParamLayout(m)
 
