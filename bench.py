@@ -79,7 +79,13 @@ CONFIGS = {
              "gossip 2-way bf16 merge, 125,000,000 params/rank, age weights [3/8, 5/8]"),
     "cfg5": (100, RESNET18_P, "f32", "dirichlet",
              "FedAvg 100-client weighted fp32 reduce, 11,181,642 params/rank"),
+    # not a BASELINE.json config: fp16 models through the same path
+    "cfg4_f16": (2, 125_000_000, "f16", "age",
+                 "gossip 2-way fp16 merge, 125,000,000 params/rank, age weights [3/8, 5/8]"),
 }
+
+TORCH_DTYPE = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16}
+ELEM_BYTES = {"f32": 4, "bf16": 2, "f16": 2}
 
 
 def parse():
@@ -150,7 +156,7 @@ def cpu_baseline(config, n, p, dtype, weights, budget_s):
     "all_cores" (SURVEY.md §8d asks for both)."""
     from torch import nn
     from oracle import fedavg_torch
-    tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
+    tdt = TORCH_DTYPE[dtype]
     shapes = LAYOUTS[config]() if config in LAYOUTS else [(p,)]
     assert sum(int(torch.Size(sh).numel()) for sh in shapes) == p
 
@@ -162,7 +168,7 @@ def cpu_baseline(config, n, p, dtype, weights, budget_s):
                 [nn.Parameter((torch.randn(sh, generator=g) * 0.05).to(tdt)) for sh in shapes])
 
     models = [Shaped(1234 + i) for i in range(n)]
-    bytes_ = (n + 1) * p * (2 if dtype == "bf16" else 4)
+    bytes_ = (n + 1) * p * ELEM_BYTES[dtype]
 
     def timed(threads, budget):
         prev = torch.get_num_threads()
@@ -232,8 +238,8 @@ def main():
         p = e - b
     else:
         p = p_cfg
-    tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
-    esz = 2 if dtype == "bf16" else 4
+    tdt = TORCH_DTYPE[dtype]
+    esz = ELEM_BYTES[dtype]
     mode = _native.DLSIM_EXACT if args.mode == "exact" else _native.DLSIM_FAST
     weights = weights_for(wkind, n)
     w32 = _native.fp32_weights(weights)

@@ -12,7 +12,7 @@ mkdir -p $O
 step() { echo "[$(date +%T)] $*"; }
 BYTES=$(python3 -c "
 import sys; sys.path.insert(0, '.')
-import bench; n, p, dt, _, _ = bench.CONFIGS['$C']; print((n + 1) * p * (2 if dt == 'bf16' else 4))")
+import bench; n, p, dt, _, _ = bench.CONFIGS['$C']; print((n + 1) * p * bench.ELEM_BYTES[dt])")
 step bench;  timeout -k 10 300 python3 bench.py --config $C "$@" > $O/bench_$C.json 2> $O/bench.err || exit $?
 cat $O/bench_$C.json
 step trace;  timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/trace_$C -- python3 bench.py --config $C --no-cpu-baseline --steps 200 --warmup 20 "$@" > $O/trace.log 2>&1 || exit $?
