@@ -24,15 +24,18 @@ def _torch_mean(x: np.ndarray, threads: int, dtype: str) -> np.ndarray:
     prev = torch.get_num_threads()
     torch.set_num_threads(threads)
     try:
-        t = torch.from_numpy(x.view(np.int16)).view(torch.bfloat16) if dtype == "bf16" else torch.from_numpy(x)
+        half = {"bf16": torch.bfloat16, "f16": torch.float16}.get(dtype)
+        t = torch.from_numpy(x.view(np.int16)).view(half) if half else torch.from_numpy(x)
         r = torch.mean(torch.stack(list(t)), dim=0)
-        return r.view(torch.int16).numpy().view(np.uint16) if dtype == "bf16" else r.numpy()
+        return r.view(torch.int16).numpy().view(np.uint16) if half else r.numpy()
     finally:
         torch.set_num_threads(prev)
 
 
 def _rows(rng, m, n, dtype):
     x = (rng.standard_normal((m, n)) * np.exp(rng.standard_normal((m, n)) * 2)).astype(np.float32)
+    if dtype == "f16":
+        return orc.f32_to_f16_bits(np.clip(x, -6e4, 6e4))
     return orc.f32_to_bf16_bits(x) if dtype == "bf16" else x
 
 
@@ -67,13 +70,15 @@ def test_multilevel_cascade_matches_torch(m):
         assert orc.same_bits(orc.chunk_mean(list(x), "f32", 4), _torch_mean(x, 4, "f32")), n
 
 
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
 @pytest.mark.parametrize("m", [2, 3, 5, 17, 20])
-def test_bf16_matches_torch(m):
-    """bf16 chunks: summed in fp32 in the same order, divided, rounded once."""
+def test_half_types_match_torch(m, dtype):
+    """bf16 and fp16 chunks: summed in fp32 in the same order, divided,
+    rounded once."""
     rng = np.random.default_rng(100 + m)
     for n in (1, 7, 1000, 9001):
-        x = _rows(rng, m, n, "bf16")
-        assert orc.same_bits(orc.chunk_mean(list(x), "bf16", 4), _torch_mean(x, 4, "bf16")), n
+        x = _rows(rng, m, n, dtype)
+        assert orc.same_bits(orc.chunk_mean(list(x), dtype, 4), _torch_mean(x, 4, dtype)), n
 
 
 def test_ilp_begin_rule():
