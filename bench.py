@@ -219,9 +219,16 @@ def main():
     local_dev = local % max(1, ndev)  # gloo rehearsal may share a GPU
     torch.cuda.set_device(local_dev)
     dev = torch.device("cuda", local_dev)
+    backend_note = None
     if world > 1:
         if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            try:
+                dist.init_process_group("nccl", device_id=dev)
+            except Exception as e:  # the data path has no collective: keep measuring
+                backend_note = f"gloo control plane (RCCL init failed: {type(e).__name__}: {e})"[:300]
+                print(f"bench.py: {backend_note}", file=sys.stderr)
+                args.backend = "gloo"
+                dist.init_process_group("gloo")
         else:
             dist.init_process_group("gloo")
     # small control-plane tensors live where the backend can reduce them
@@ -382,7 +389,7 @@ def main():
                        + (f" (strong scaling: {p_cfg} params split over {world} ranks)" if args.strong and world > 1 else "")
                        + (f" (rank 0's slice of a {args.slice_of}-rank strong split, alone on 1 GPU)"
                           if args.slice_of > 1 and world == 1 else ""),
-                       "backend": args.backend if world > 1 else None,
+                       "backend": (backend_note or args.backend) if world > 1 else None,
                        "n_models": n, "params_per_rank": p, "tasks_per_step": B,
                        "mode": args.mode, "parallelism": f"param-shard x{world}",
                        "bytes_per_step_per_rank": bytes_per_launch},
