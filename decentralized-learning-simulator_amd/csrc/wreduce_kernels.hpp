@@ -62,6 +62,16 @@ __device__ __forceinline__ void bf16_round2(float& a0, float& a1) {
 // ---- fp16 helpers -------------------------------------------------------------
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 
+// An fp32 value pinned in a VGPR. Without it the backend selects
+// v_fma_mix{lo}_f16 for fptrunc(w * x) and fptrunc(a + b): one rounding of the
+// exact result straight to fp16 (and an fma with a +0 addend, which turns a
+// -0 product into +0) instead of the reference's fp32 rounding followed by
+// the fp16 one. Found by scripts/fuzz_parity.py.
+__device__ __forceinline__ float pin_f32(float v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
 // fp32 -> fp16 -> fp32, nearest-even (hardware conversion; NaN stays NaN,
 // overflow to inf, fp16 subnormals kept).
 __device__ __forceinline__ float f16_round(float f) { return static_cast<float>(static_cast<_Float16>(f)); }
@@ -153,14 +163,14 @@ struct F16Exact {
   static constexpr int kFmt = kFmtF16;
   __device__ static float init(float x) { return x * 0.0f; }
   __device__ static float step(float acc, float w, float x) {
-    const float p = f16_round(w * x);
-    return f16_round(acc + p);
+    const float p = f16_round(pin_f32(w * x));
+    return f16_round(pin_f32(acc + p));
   }
   __device__ static void step2(float& a0, float& a1, float w, float x0, float x1) {
-    float p0 = w * x0, p1 = w * x1;
+    float p0 = pin_f32(w * x0), p1 = pin_f32(w * x1);
     f16_round2(p0, p1);
-    a0 = a0 + p0;
-    a1 = a1 + p1;
+    a0 = pin_f32(a0 + p0);
+    a1 = pin_f32(a1 + p1);
     f16_round2(a0, a1);
   }
   __device__ static float finish(float a, float) { return a; }
@@ -222,7 +232,7 @@ struct F16Mean {
     a0 = a0 + x0;
     a1 = a1 + x1;
   }
-  __device__ static float finish(float a, float div) { return f16_round(a / div); }
+  __device__ static float finish(float a, float div) { return f16_round(pin_f32(a / div)); }
 };
 
 // ---- 16-byte vector <-> E floats --------------------------------------------

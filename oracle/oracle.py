@@ -75,7 +75,9 @@ def reference_weights(n: int, weights: Optional[Sequence[float]]) -> np.ndarray:
 
 
 def _as_rows(xs, np_dtype):
-    rows = [np.ascontiguousarray(x, dtype=np_dtype).reshape(-1) for x in xs]
+    # 16-bit rows: float16 arrays are taken by their bits, not converted
+    rows = [np.ascontiguousarray(np.asarray(x).view(np.uint16) if np.asarray(x).dtype == np.float16
+                                 else x, dtype=np_dtype).reshape(-1) for x in xs]
     p = rows[0].size
     for r in rows:
         if r.size != p:
@@ -112,7 +114,7 @@ def wreduce(xs, weights, dtype: str = "f32", mode: str = "exact") -> np.ndarray:
             out.ctypes.data, p)
     if rc != 0:
         raise RuntimeError(f"oracle failed rc={rc}")
-    return out
+    return out.view(np.float16) if dtype == "f16" else out
 
 
 def mean(xs, dtype: str = "f32") -> np.ndarray:
@@ -136,7 +138,7 @@ def mean(xs, dtype: str = "f32") -> np.ndarray:
     ptrs = (ctypes.c_void_p * n)(*[r.ctypes.data for r in rows])
     if fn(ctypes.cast(ptrs, ctypes.POINTER(ctypes.c_void_p)), n, out.ctypes.data, p) != 0:
         raise RuntimeError("oracle mean failed")
-    return out
+    return out.view(np.float16) if dtype == "f16" else out
 
 
 def chunk_mean(xs, dtype: str = "f32", threads: int = 4) -> np.ndarray:
@@ -161,7 +163,7 @@ def chunk_mean(xs, dtype: str = "f32", threads: int = 4) -> np.ndarray:
     ptrs = (ctypes.c_void_p * n)(*[r.ctypes.data for r in rows])
     if fn(ctypes.cast(ptrs, ctypes.POINTER(ctypes.c_void_p)), n, out.ctypes.data, p, threads) != 0:
         raise RuntimeError("oracle chunk mean failed")
-    return out
+    return out.view(np.float16) if dtype == "f16" else out
 
 
 def chunk_mean_ilp_begin(m: int, n: int, threads: int) -> int:
@@ -193,13 +195,15 @@ def f32_to_bf16_bits(x: np.ndarray) -> np.ndarray:
 
 
 def f32_to_f16_bits(x: np.ndarray) -> np.ndarray:
-    """RNE fp32 -> IEEE binary16 bit patterns (numpy's conversion)."""
+    """RNE fp32 -> IEEE binary16 (numpy's conversion), as np.float16 arrays
+    (same_bits compares them as binary16)."""
     with np.errstate(over="ignore"):  # overflow to inf is the rounding rule
-        return np.asarray(x, dtype=np.float32).astype(np.float16).view(np.uint16)
+        return np.asarray(x, dtype=np.float32).astype(np.float16)
 
 
 def f16_bits_to_f32(h: np.ndarray) -> np.ndarray:
-    return np.asarray(h, dtype=np.uint16).view(np.float16).astype(np.float32)
+    h = np.asarray(h)
+    return (h if h.dtype == np.float16 else h.astype(np.uint16).view(np.float16)).astype(np.float32)
 
 
 def bf16_bits_to_f32(h: np.ndarray) -> np.ndarray:
@@ -208,12 +212,19 @@ def bf16_bits_to_f32(h: np.ndarray) -> np.ndarray:
 
 def same_bits(a: np.ndarray, b: np.ndarray) -> bool:
     """Bit equality with every NaN treated as equal to every NaN (NaN payloads
-    differ between the reference's scalar/vector CPU paths and the GPU)."""
+    differ between the reference's scalar/vector CPU paths and the GPU).
+    16-bit formats: np.float16 arrays are IEEE binary16 (if either side is
+    float16, a uint16 other side holds binary16 bits); other uint16 arrays
+    are bf16 bit patterns."""
     a = np.asarray(a)
     b = np.asarray(b)
     if a.shape != b.shape:
         return False
-    if a.dtype == np.uint16:
+    if np.float16 in (a.dtype, b.dtype):
+        ia = a.view(np.uint16) if a.dtype == np.float16 else a.astype(np.uint16)
+        ib = b.view(np.uint16) if b.dtype == np.float16 else b.astype(np.uint16)
+        fa, fb = ia.view(np.float16), ib.view(np.float16)
+    elif a.dtype == np.uint16:
         fa, fb = bf16_bits_to_f32(a), bf16_bits_to_f32(b)
         ia, ib = a, b
     else:

@@ -1,0 +1,193 @@
+"""Randomised parity soak (GPU): every entry point against the oracle on random
+shapes, dtypes, alignments, weights and special values, for a time budget.
+
+  reduce      dlsim_wreduce (flat; exact bit-for-bit, FAST against its own oracle)
+  tensors     dlsim_wreduce_tensors (one model split into random tensors)
+  batched     dlsim_wreduce_batched (random tasks, mixed fan-in and sizes)
+  chunk_mean  dlsim_chunk_mean_batched (random m, n, threads) vs PyTorch's CPU order
+
+Prints one JSON line with the case counts and the first failures (if any).
+
+    python scripts/fuzz_parity.py [--seconds 120] [--seed 0]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "decentralized-learning-simulator_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from dasklearn_amd import _native  # noqa: E402
+from oracle import oracle as orc  # noqa: E402
+
+DT = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16}
+
+
+def rand_values(rng, n, p, dtype):
+    scale = np.exp(rng.uniform(-6, 6)) if dtype == "f32" else np.exp(rng.uniform(-4, 4))
+    x = (rng.standard_normal((n, p)) * scale).astype(np.float32)
+    if rng.random() < 0.3 and p > 0:  # sprinkle special values
+        k = max(1, p // 50)
+        specials = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1e-40, -1e-40, 3e38, 6e4, 1e-7],
+                            dtype=np.float32)
+        idx = rng.integers(0, p, size=k)
+        rows = rng.integers(0, n, size=k)
+        x[rows, idx] = rng.choice(specials, size=k)
+    if dtype == "bf16":
+        return orc.f32_to_bf16_bits(x)
+    if dtype == "f16":
+        return orc.f32_to_f16_bits(x)
+    return x
+
+
+def to_dev(rows, dtype, offset):
+    out = []
+    for r in rows:
+        h = torch.from_numpy(np.ascontiguousarray(r).view(np.int16).copy()).view(DT[dtype]) if dtype != "f32" \
+            else torch.from_numpy(np.ascontiguousarray(r).copy())
+        buf = torch.empty(h.numel() + offset, dtype=h.dtype, device="cuda")
+        buf[offset:].copy_(h)
+        out.append(buf[offset:])
+    return out
+
+
+def bits(t):
+    t = t.cpu()
+    return t.view(torch.int16).numpy().view(np.uint16) if t.dtype == torch.bfloat16 else t.numpy()
+
+
+def first_diff(got, exp, rows, w):
+    """Details of the first element where got and exp differ (for a report)."""
+    g = np.asarray(got)
+    e = np.asarray(exp)
+    gi = g.view(np.uint16) if g.dtype == np.float16 else g.view(np.uint32) if g.dtype == np.float32 else g
+    ei = e.view(np.uint16) if e.dtype == np.float16 else e.view(np.uint32) if e.dtype == np.float32 else e
+    d = np.nonzero(gi != ei)[0]
+    if len(d) == 0:
+        return None
+    j = int(d[0])
+    col = [np.asarray(r).view(np.uint16)[j] if np.asarray(r).dtype != np.float32 else np.asarray(r).view(np.uint32)[j]
+           for r in rows]
+    return dict(idx=j, ndiff=int(len(d)), got=hex(int(gi[j])), exp=hex(int(ei[j])),
+                inputs=[hex(int(c)) for c in col[:8]], weights=[float(x) for x in np.asarray(w)[:8]])
+
+
+def rand_weights(rng, n):
+    kind = rng.integers(0, 4)
+    if kind == 0:
+        return orc.reference_weights(n, None)
+    if kind == 1:
+        return orc.reference_weights(n, list(rng.dirichlet(np.ones(n))))
+    if kind == 2:
+        return orc.reference_weights(n, list(rng.standard_normal(n)))  # negative weights
+    return orc.reference_weights(n, list(rng.choice([0.0, 1.0, 1e-39, -2.5, 0.5], size=n)))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seconds", type=float, default=120.0)
+    ap.add_argument("--seed", type=int, default=0)
+    a = ap.parse_args()
+    rng = np.random.default_rng(a.seed)
+    counts = {"reduce": 0, "reduce_fast": 0, "tensors": 0, "batched": 0, "chunk_mean": 0}
+    fails = []
+    t_end = time.time() + a.seconds
+    t_note = time.time() + 20
+    while time.time() < t_end and len(fails) < 10:
+        if time.time() > t_note:  # progress (long runs must keep writing)
+            print(json.dumps({"progress": counts, "failures": len(fails)}), file=sys.stderr, flush=True)
+            t_note = time.time() + 20
+        dtype = rng.choice(["f32", "bf16", "f16"])
+        which = rng.choice(["reduce", "tensors", "batched", "chunk_mean"], p=[0.35, 0.15, 0.2, 0.3])
+        try:
+            if which == "reduce":
+                n = int(rng.choice([1, 2, 3, 5, 8, 9, 14, 15, 16, 17, 33, 128, 129, 200]))
+                p = int(rng.choice([1, 2, 7, 8, 9, 63, 1000, 4099, 65537, 300_001]))
+                rows = rand_values(rng, n, p, dtype)
+                off = int(rng.choice([0, 0, 0, 1]))
+                xs = to_dev(rows, dtype, off)
+                w = rand_weights(rng, n)
+                # FAST folds n > 128 in passes that round the partial sum to the
+                # element type between passes (tolerance-only there)
+                fast = n <= 128 and rng.random() < 0.2
+                out = to_dev([np.zeros(p, dtype=np.float32 if dtype == "f32" else np.uint16)], dtype,
+                             int(rng.choice([0, 0, 1])))[0]
+                _native.wreduce(xs, w, out, _native.DLSIM_FAST if fast else _native.DLSIM_EXACT)
+                exp = orc.wreduce(list(rows), w, dtype, "fast" if fast else "exact")
+                ok = orc.same_bits(bits(out), exp)
+                counts["reduce_fast" if fast else "reduce"] += 1
+                case = dict(kind="reduce", dtype=dtype, n=n, p=p, off=off, fast=bool(fast))
+                if not ok:
+                    case["diff"] = first_diff(bits(out), exp, rows, w)
+            elif which == "tensors":
+                n = int(rng.choice([1, 2, 4, 8, 17, 130]))
+                sizes = [int(s) for s in rng.integers(1, 5000, size=int(rng.integers(1, 12)))]
+                p = sum(sizes)
+                rows = rand_values(rng, n, p, dtype)
+                flat = to_dev(rows, dtype, 0)
+                by_model = [[t[o:o + s].clone() for o, s in zip(np.cumsum([0] + sizes[:-1]), sizes)]
+                            for t in flat]
+                outs = [torch.empty(s, dtype=DT[dtype], device="cuda") for s in sizes]
+                w = rand_weights(rng, n)
+                _native.wreduce_tensors(by_model, w, outs)
+                got = np.concatenate([bits(o) for o in outs])
+                ok = orc.same_bits(got, orc.wreduce(list(rows), w, dtype))
+                counts["tensors"] += 1
+                case = dict(kind="tensors", dtype=dtype, n=n, sizes=len(sizes))
+            elif which == "batched":
+                tasks, exps = [], []
+                for _ in range(int(rng.integers(1, 60))):
+                    n = int(rng.choice([1, 2, 3, 7, 8, 16, 17, 40]))
+                    p = int(rng.choice([1, 5, 100, 4097, 85_354]))
+                    rows = rand_values(rng, n, p, dtype)
+                    xs = to_dev(rows, dtype, int(rng.choice([0, 0, 0, 1])))
+                    w = rand_weights(rng, n)
+                    out = torch.empty(p, dtype=DT[dtype], device="cuda")
+                    tasks.append((xs, w, out))
+                    exps.append((orc.wreduce(list(rows), w, dtype), rows, n, p))
+                _native.wreduce_batched(tasks)
+                oks = [orc.same_bits(bits(t[2]), e[0]) for t, e in zip(tasks, exps)]
+                ok = all(oks)
+                counts["batched"] += 1
+                case = dict(kind="batched", dtype=dtype, tasks=len(tasks))
+                if not ok:
+                    i = oks.index(False)
+                    e, rows, n, p = exps[i]
+                    case.update(task=i, n=n, p=p, diff=first_diff(bits(tasks[i][2]), e, rows, tasks[i][1]))
+            else:
+                threads = int(rng.choice([1, 2, 4, 8, 16]))
+                tasks, exps = [], []
+                for _ in range(int(rng.integers(1, 24))):
+                    m = int(rng.choice([1, 2, 3, 4, 5, 8, 9, 15, 16, 17, 31, 33, 64, 100, 250]))
+                    n = int(rng.choice([1, 2, 3, 4, 7, 8, 9, 31, 32, 33, 95, 1000, 8193, 100_003]))
+                    if m * n > 1_000_000:  # keeps one case's oracle work to well under a second
+                        n = int(rng.choice([1, 7, 33, 1000]))
+                    rows = rand_values(rng, m, n, dtype)
+                    xs = to_dev(rows, dtype, int(rng.choice([0, 0, 0, 1])))
+                    out = torch.empty(n, dtype=DT[dtype], device="cuda")
+                    tasks.append((xs, out))
+                    exps.append(orc.chunk_mean(list(rows), dtype, threads))
+                _native.chunk_mean_batched(tasks, threads=threads)
+                ok = all(orc.same_bits(bits(t[1]), e) for t, e in zip(tasks, exps))
+                counts["chunk_mean"] += 1
+                case = dict(kind="chunk_mean", dtype=dtype, tasks=len(tasks), threads=threads)
+        except Exception as e:  # an unexpected exception is a failure too
+            ok, case = False, dict(kind=str(which), dtype=str(dtype), error=f"{type(e).__name__}: {e}"[:300])
+        if not ok:
+            fails.append(case)
+    torch.cuda.synchronize()
+    print(json.dumps({"seconds": a.seconds, "seed": a.seed, "cases": counts, "failures": fails}), flush=True)
+    sys.exit(1 if fails else 0)
+
+
+if __name__ == "__main__":
+    main()

@@ -27,7 +27,7 @@ def _torch_mean(x: np.ndarray, threads: int, dtype: str) -> np.ndarray:
         half = {"bf16": torch.bfloat16, "f16": torch.float16}.get(dtype)
         t = torch.from_numpy(x.view(np.int16)).view(half) if half else torch.from_numpy(x)
         r = torch.mean(torch.stack(list(t)), dim=0)
-        return r.view(torch.int16).numpy().view(np.uint16) if half else r.numpy()
+        return r.view(torch.int16).numpy().view(np.uint16) if half == torch.bfloat16 else r.numpy()
     finally:
         torch.set_num_threads(prev)
 

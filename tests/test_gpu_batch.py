@@ -43,7 +43,7 @@ def check(tasks, dtype, mode=_native.DLSIM_EXACT):
     _native.wreduce_batched([(t[0], t[2], t[3]) for t in tasks], mode)
     for ins, host, w, out in tasks:
         got = out.cpu()
-        got = got.view(torch.int16).numpy().view(np.uint16) if dtype != "f32" else got.numpy()
+        got = got.view(torch.int16).numpy().view(np.uint16) if dtype == "bf16" else got.numpy()
         exp = orc.wreduce(host, w, dtype, "exact" if mode == 0 else "fast")
         assert orc.same_bits(got, exp)
 
@@ -110,7 +110,7 @@ def test_table_plan_whole_round(dtype):
         plan.launch()
         for ins, host, w, out in tasks:
             got = out.cpu()
-            got = got.view(torch.int16).numpy().view(np.uint16) if dtype != "f32" else got.numpy()
+            got = got.view(torch.int16).numpy().view(np.uint16) if dtype == "bf16" else got.numpy()
             assert orc.same_bits(got, orc.wreduce(host, w, dtype))
 
 

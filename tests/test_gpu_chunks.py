@@ -162,7 +162,7 @@ def _rows_t(rng, m, n, dtype, offset=0):
 
 def _bits(t):
     t = t.cpu()
-    return t.view(torch.int16).numpy().view(np.uint16) if t.dtype != torch.float32 else t.numpy()
+    return t.view(torch.int16).numpy().view(np.uint16) if t.dtype == torch.bfloat16 else t.numpy()
 
 
 @pytest.mark.parametrize("dtype", ["f32", "bf16", "f16"])

@@ -53,7 +53,7 @@ def modules_from_golden(g):
 
 def flat_of(model):
     t = torch.cat([p.detach().reshape(-1).cpu() for p in model.parameters()])
-    if t.dtype in (torch.bfloat16, torch.float16):
+    if t.dtype == torch.bfloat16:
         return t.view(torch.int16).numpy().view(np.uint16)
     return t.numpy()
 
@@ -270,7 +270,7 @@ def test_host_pipeline_chunks_are_exact(monkeypatch, chunk_bytes, to_host):
     exp = _expected_by_dtype(models, weights)
     for dt in (torch.float32, torch.bfloat16, torch.float16):
         t = torch.cat([p.detach().reshape(-1).cpu() for p in out.parameters() if p.dtype == dt])
-        got = t.view(torch.int16).numpy().view(np.uint16) if dt != torch.float32 else t.numpy()
+        got = t.view(torch.int16).numpy().view(np.uint16) if dt == torch.bfloat16 else t.numpy()
         assert orc.same_bits(got, exp[dt]), (dt, chunk_bytes)
 
 

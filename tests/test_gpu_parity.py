@@ -39,9 +39,9 @@ def to_dev(rows, dtype):
 
 def from_dev(t):
     t = t.cpu()
-    if t.dtype in (torch.bfloat16, torch.float16):
+    if t.dtype == torch.bfloat16:
         return t.view(torch.int16).numpy().view(np.uint16)
-    return t.numpy()
+    return t.numpy()  # float32, or float16 (compared as binary16)
 
 
 def hip_reduce(rows, w, dtype, mode=_native.DLSIM_EXACT):
@@ -295,3 +295,59 @@ def test_output_longer_than_one_launch_window():
     assert orc.same_bits(from_dev(out[idx]), orc.wreduce(rows, w, "f32"))
     del a, b, out
     torch.cuda.empty_cache()
+
+
+def _double_rounding_pairs(count=64):
+    """fp32 weights w and fp16 values x where rounding w*x to fp32 first and
+    then to fp16 (the reference) differs from one rounding of the exact
+    product straight to fp16 (what a fused v_fma_mix_f16 computes)."""
+    rng = np.random.default_rng(123)
+    ws, xs = [], []
+    while len(ws) < count:
+        w = rng.standard_normal(20000).astype(np.float32)
+        x = rng.standard_normal(20000).astype(np.float16)
+        exact = w.astype(np.float64) * x.astype(np.float64)
+        with np.errstate(over="ignore"):
+            twice = (w * x.astype(np.float32)).astype(np.float16)
+            once = exact.astype(np.float16)
+        k = np.nonzero(twice.view(np.uint16) != once.view(np.uint16))[0]
+        ws += list(w[k])
+        xs += list(x[k])
+    return np.array(ws[:count], np.float32), np.array(xs[:count], np.float16)
+
+
+@pytest.mark.parametrize("p", [64, 4099])  # vector tiles, and the scalar tail
+def test_f16_products_round_to_fp32_first(p):
+    """Regression (found by scripts/fuzz_parity.py): hipcc fused
+    fptrunc(w * x) into v_fma_mix{lo}_f16, one rounding straight to fp16
+    plus a +0 addend. The reference rounds w * x to fp32, then to fp16, and a
+    -0 product stays -0."""
+    ws, xs = _double_rounding_pairs()
+    for i in range(0, len(ws), 16):
+        w = ws[i:i + 16]
+        n = len(w)
+        rows = np.tile(xs[i:i + n, None], (1, p)).astype(np.float16)
+        rows[:, ::7] = np.float16(-0.0)  # -0 products
+        got = hip_reduce(list(rows), w, "f16")
+        assert orc.same_bits(got, orc.wreduce(list(rows), w, "f16"))
+        # n = 1 per row, through the batched kernel too
+        tasks, exps = [], []
+        for k in range(n):
+            x = to_dev([rows[k]], "f16")
+            out = torch.empty(p, dtype=torch.float16, device=dev())
+            tasks.append((x, w[k:k + 1], out))
+            exps.append(orc.wreduce([rows[k]], w[k:k + 1], "f16"))
+        _native.wreduce_batched(tasks)
+        for (_, _, out), e in zip(tasks, exps):
+            assert orc.same_bits(from_dev(out), e)
+
+
+def test_randomised_parity_soak():
+    """scripts/fuzz_parity.py for a short budget: random shapes, dtypes,
+    alignments, weights and special values through every entry point."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "scripts", "fuzz_parity.py"), "--seconds", "20",
+                        "--seed", "7"], capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
