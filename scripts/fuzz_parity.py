@@ -5,6 +5,10 @@ shapes, dtypes, alignments, weights and special values, for a time budget.
   tensors     dlsim_wreduce_tensors (one model split into random tensors)
   batched     dlsim_wreduce_batched (random tasks, mixed fan-in and sizes)
   chunk_mean  dlsim_chunk_mean_batched (random m, n, threads) vs PyTorch's CPU order
+  modules     FedAvg.aggregate on random module trees (mixed fp32/bf16/fp16
+              parameters, buffers, host or device) vs the oracle per dtype group
+  reconstruct ChunkManager.reconstruct_model on random models and chunkings vs
+              the reference's own arithmetic (torch.mean of torch.stack on the CPU)
 
 Prints one JSON line with the case counts and the first failures (if any).
 
@@ -92,13 +96,39 @@ def rand_weights(rng, n):
     return orc.reference_weights(n, list(rng.choice([0.0, 1.0, 1e-39, -2.5, 0.5], size=n)))
 
 
+def rand_module(rng, seed):
+    """A random nn.Module tree: nested submodules, parameters of random shapes
+    and dtypes, a BatchNorm (buffers incl. an int64 counter), a frozen
+    parameter."""
+    from torch import nn
+    g = torch.Generator().manual_seed(int(seed))
+    n_leaf = int(rng.integers(1, 6))
+    dts = [DT[str(d)] for d in rng.choice(["f32", "f32", "bf16", "f16"], size=n_leaf)]
+    shapes = [tuple(int(v) for v in rng.integers(1, 40, size=int(rng.integers(1, 4)))) for _ in range(n_leaf)]
+
+    class Leaf(nn.Module):
+        def __init__(self, shape, dt):
+            super().__init__()
+            self.w = nn.Parameter((torch.randn(shape, generator=g) * 0.1).to(dt))
+
+    class Tree(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.leaves = nn.ModuleList([Leaf(sh, dt) for sh, dt in zip(shapes, dts)])
+            self.bn = nn.BatchNorm1d(7)
+            self.frozen = nn.Parameter(torch.randn(5, generator=g), requires_grad=False)
+
+    return Tree()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=120.0)
     ap.add_argument("--seed", type=int, default=0)
     a = ap.parse_args()
     rng = np.random.default_rng(a.seed)
-    counts = {"reduce": 0, "reduce_fast": 0, "tensors": 0, "batched": 0, "chunk_mean": 0}
+    counts = {"reduce": 0, "reduce_fast": 0, "tensors": 0, "batched": 0, "chunk_mean": 0, "modules": 0,
+              "reconstruct": 0}
     fails = []
     t_end = time.time() + a.seconds
     t_note = time.time() + 20
@@ -107,7 +137,8 @@ def main():
             print(json.dumps({"progress": counts, "failures": len(fails)}), file=sys.stderr, flush=True)
             t_note = time.time() + 20
         dtype = rng.choice(["f32", "bf16", "f16"])
-        which = rng.choice(["reduce", "tensors", "batched", "chunk_mean"], p=[0.35, 0.15, 0.2, 0.3])
+        which = rng.choice(["reduce", "tensors", "batched", "chunk_mean", "modules", "reconstruct"],
+                           p=[0.3, 0.1, 0.15, 0.25, 0.1, 0.1])
         try:
             if which == "reduce":
                 n = int(rng.choice([1, 2, 3, 5, 8, 9, 14, 15, 16, 17, 33, 128, 129, 200]))
@@ -163,6 +194,65 @@ def main():
                     i = oks.index(False)
                     e, rows, n, p = exps[i]
                     case.update(task=i, n=n, p=p, diff=first_diff(bits(tasks[i][2]), e, rows, tasks[i][1]))
+            elif which == "modules":
+                from dasklearn_amd.gradient_aggregation.fedavg import FedAvg
+                n = int(rng.choice([1, 2, 3, 8, 17]))
+                base = int(rng.integers(0, 1 << 30))
+                models = [rand_module(np.random.default_rng(base), base + i) for i in range(n)]
+                on_dev = bool(rng.random() < 0.5)
+                if on_dev:
+                    models = [m.to("cuda") for m in models]
+                weights = None if rng.random() < 0.4 else [float(v) for v in rand_weights(rng, n)]
+                out = FedAvg.aggregate(models, weights)
+                w = orc.reference_weights(n, weights)
+                ok = all(p.is_cuda == on_dev for p in out.parameters())
+                for dt, code in ((torch.float32, "f32"), (torch.bfloat16, "bf16"), (torch.float16, "f16")):
+                    rows = []
+                    for m in models:
+                        ps = [p.detach().reshape(-1).cpu() for p in m.parameters() if p.dtype == dt]
+                        if ps:
+                            t = torch.cat(ps)
+                            rows.append(t.view(torch.int16).numpy().view(np.uint16) if dt == torch.bfloat16
+                                        else t.numpy())
+                    if rows:
+                        got = torch.cat([p.detach().reshape(-1).cpu() for p in out.parameters() if p.dtype == dt])
+                        ok = ok and orc.same_bits(bits(got), orc.wreduce(rows, w, code))
+                ok = ok and all(torch.equal(a.cpu(), b.cpu()) for a, b in zip(out.buffers(), models[0].buffers()))
+                ok = ok and [p.requires_grad for p in out.parameters()] == [p.requires_grad for p in models[0].parameters()]
+                counts["modules"] += 1
+                case = dict(kind="modules", n=n, device=on_dev, weighted=weights is not None)
+            elif which == "reconstruct":
+                from torch import nn
+                from dasklearn_amd.chunk_manager import ChunkManager
+                k = int(rng.integers(1, 12))
+                n_peers = int(rng.integers(1, 12))
+                base = int(rng.integers(0, 1 << 30))
+                shape_rng = np.random.default_rng(base)
+                models = [rand_module(np.random.default_rng(base), base + i) for i in range(n_peers)]
+                models = [m.float() for m in models]  # chunk_model cats the state_dict (one dtype)
+                chunked = [ChunkManager.chunk_model(m, k) for m in models]
+                # each chunk index gets a random non-empty subset of the peers
+                by_index = []
+                for c in range(k):
+                    who = [i for i in range(n_peers) if shape_rng.random() < 0.6] or [0]
+                    by_index.append([chunked[i][c] for i in who])
+                threads = int(rng.choice([1, 4, 8]))
+                prev = torch.get_num_threads()
+                torch.set_num_threads(threads)
+                try:
+                    expect = torch.cat([torch.mean(torch.stack(cs), dim=0) for cs in by_index])
+                    on_dev = bool(rng.random() < 0.5)
+                    chunks = [[c.to("cuda") for c in cs] if on_dev else list(cs) for cs in by_index]
+                    target = rand_module(np.random.default_rng(base), base).float()
+                    if on_dev:
+                        target = target.to("cuda")
+                    ChunkManager.reconstruct_model(chunks, target)
+                finally:
+                    torch.set_num_threads(prev)
+                got = ChunkManager.get_flat_params(target).cpu()
+                ok = orc.same_bits(got.numpy(), expect.numpy())
+                counts["reconstruct"] += 1
+                case = dict(kind="reconstruct", k=k, peers=n_peers, threads=threads, device=on_dev)
             else:
                 threads = int(rng.choice([1, 2, 4, 8, 16]))
                 tasks, exps = [], []
