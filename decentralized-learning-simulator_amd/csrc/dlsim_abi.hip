@@ -9,12 +9,15 @@
 #include <cstdio>
 #include <cstdint>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "dlsim.h"
 #include "wreduce_kernels.hpp"
 #include "chunk_mean_kernels.hpp"
+#include "host_pack.hpp"
 
 namespace {
 
@@ -828,6 +831,120 @@ int dlsim_wreduce_sharded(const void* const* d_slices, size_t slice_elems, int n
   rr = g_rccl.group_end();
   if (rr != 0) return rccl_fail(rr, "ncclGroupEnd");
   return DLSIM_OK;
+}
+
+int dlsim_host_wreduce(int n, int t, const void* const* h_srcs, const size_t* numels,
+                       const float* h_weights, void* h_staging, void* d_rows, size_t row_stride,
+                       void* d_out, void* h_out, int dtype, int mode, size_t chunk_elems, int threads,
+                       void* stream, void* h2d_stream, void* d2h_stream) {
+  g_err.clear();
+  if (!known_dtype(dtype)) return fail(DLSIM_E_DTYPE, "unsupported dtype %d", dtype);
+  if (mode != DLSIM_EXACT && mode != DLSIM_FAST) return fail(DLSIM_E_MODE, "unsupported mode %d", mode);
+  if (n < 1 || t < 0) return fail(DLSIM_E_ARG, "need n >= 1 and t >= 0 (got %d, %d)", n, t);
+  if (!h_weights || (t > 0 && (!h_srcs || !numels))) return fail(DLSIM_E_ARG, "null array argument");
+  const size_t esz = elem_bytes(dtype);
+  size_t total = 0;
+  for (int k = 0; k < t; ++k) total += numels[k];
+  if (total == 0) return DLSIM_OK;
+  if (!h_staging || !d_rows || !d_out) return fail(DLSIM_E_ARG, "null staging, rows or output");
+  if (!aligned16(h_staging) || !aligned16(d_rows) || row_stride % 8 != 0)
+    return fail(DLSIM_E_ARG, "staging rows must be 16-B aligned with a stride that is a multiple of 8");
+  if (row_stride < total) return fail(DLSIM_E_ARG, "row_stride %zu < %zu elements", row_stride, total);
+  for (size_t j = 0; j < static_cast<size_t>(n) * t; ++j)
+    if (!h_srcs[j] && numels[j % t] > 0) return fail(DLSIM_E_ARG, "null source pointer at index %zu", j);
+  const size_t chunk = chunk_elems == 0 || chunk_elems >= total ? total : (chunk_elems + 1023) / 1024 * 1024;
+  const size_t n_chunks = (total + chunk - 1) / chunk;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  hipStream_t h2d = h2d_stream ? static_cast<hipStream_t>(h2d_stream) : st;
+  hipStream_t d2h = d2h_stream ? static_cast<hipStream_t>(d2h_stream) : st;
+  char* stage = static_cast<char*>(h_staging);
+  char* rows = static_cast<char*>(d_rows);
+  char* out = static_cast<char*>(d_out);
+  const size_t row_bytes = row_stride * esz;
+
+  // Units u = c * n + i (chunk c of model i), slices in that order.
+  dlsim::PackJob job;
+  {
+    std::vector<size_t> off(static_cast<size_t>(t) + 1, 0);
+    for (int k = 0; k < t; ++k) off[k + 1] = off[k] + numels[k];
+    for (size_t c = 0; c < n_chunks; ++c) {
+      const size_t c0 = c * chunk, c1 = std::min(total, c0 + chunk);
+      const int k0 = static_cast<int>(std::upper_bound(off.begin(), off.end(), c0) - off.begin()) - 1;
+      for (int i = 0; i < n; ++i) {
+        const uint32_t u = static_cast<uint32_t>(c * n + i);
+        for (int k = k0; k < t && off[k] < c1; ++k) {
+          const size_t a = std::max(c0, off[k]), b = std::min(c1, off[k + 1]);
+          if (a >= b) continue;
+          const char* src = static_cast<const char*>(h_srcs[static_cast<size_t>(i) * t + k]);
+          job.add(u, src + (a - off[k]) * esz, stage + i * row_bytes + a * esz, (b - a) * esz);
+        }
+      }
+    }
+    job.seal(n_chunks * n);
+  }
+
+  // Events: `stream` -> copy streams before the first copy (earlier work on
+  // the rows), copy streams -> `stream` at the end; per chunk, H2D -> reduce
+  // and reduce -> D2H. Destroying a recorded event is deferred by the
+  // runtime until it completes.
+  int rc = DLSIM_OK;
+  std::vector<hipEvent_t> evs;
+  auto event_on = [&](hipStream_t from, hipStream_t to, const char* what) {
+    if (rc != DLSIM_OK || from == to) return;
+    hipEvent_t ev;
+    hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (e != hipSuccess) { rc = hip_fail(e, what); return; }
+    evs.push_back(ev);
+    e = hipEventRecord(ev, from);
+    if (e == hipSuccess) e = hipStreamWaitEvent(to, ev, 0);
+    if (e != hipSuccess) rc = hip_fail(e, what);
+  };
+  event_on(st, h2d, "order H2D after stream");
+  if (h_out) event_on(st, d2h, "order D2H after stream");
+
+  std::vector<const void*> ins(static_cast<size_t>(n));
+  auto dispatch_unit = [&](size_t u) {
+    if (rc != DLSIM_OK) return;
+    const size_t c = u / n, i = u % n;
+    const size_t c0 = c * chunk, c1 = std::min(total, c0 + chunk);
+    const size_t o = i * row_bytes + c0 * esz;
+    hipError_t e = hipMemcpyAsync(rows + o, stage + o, (c1 - c0) * esz, hipMemcpyHostToDevice, h2d);
+    if (e != hipSuccess) { rc = hip_fail(e, "staging H2D"); return; }
+    if (i + 1 < static_cast<size_t>(n)) return;
+    event_on(h2d, st, "order reduce after H2D");
+    if (rc != DLSIM_OK) return;
+    for (int r = 0; r < n; ++r) ins[r] = rows + r * row_bytes + c0 * esz;
+    rc = dispatch(ins.data(), n, h_weights, out + c0 * esz, c1 - c0, dtype, mode, st);
+    if (rc != DLSIM_OK || !h_out) return;
+    event_on(st, d2h, "order D2H after reduce");
+    if (rc != DLSIM_OK) return;
+    e = hipMemcpyAsync(static_cast<char*>(h_out) + c0 * esz, out + c0 * esz, (c1 - c0) * esz,
+                       hipMemcpyDeviceToHost, d2h);
+    if (e != hipSuccess) rc = hip_fail(e, "result D2H");
+  };
+
+  // Below ~1 MiB of input the helpers' wake-up costs more than they save.
+  const size_t in_bytes = total * esz * n;
+  int helpers = in_bytes < (size_t{1} << 20) ? 0 : std::min(std::max(threads, 1), 64) - 1;
+  dlsim::PackPool& pool = dlsim::PackPool::get();
+  {
+    std::lock_guard<std::mutex> lk(pool.call_mutex());
+    if (helpers > 0) pool.start(&job, helpers);
+    // This thread packs too, and starts each unit's DMA (and each chunk's
+    // reduce) as soon as the unit is complete, in unit order.
+    for (size_t u = 0; u < job.units;) {
+      if (job.unit_done(u)) {
+        dispatch_unit(u++);
+      } else if (!job.run_one()) {
+        std::this_thread::yield();
+      }
+    }
+    if (helpers > 0) pool.join();
+  }
+  // (every H2D is already ordered before its chunk's reduce on `stream`)
+  if (h_out) event_on(d2h, st, "order stream after D2H");
+  for (hipEvent_t ev : evs) (void)hipEventDestroy(ev);
+  return rc;
 }
 
 int dlsim_shard_range(size_t n_elems, int world, int rank, size_t align_elems, size_t* begin,

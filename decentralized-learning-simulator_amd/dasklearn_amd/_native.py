@@ -37,6 +37,7 @@ EXPORTS = (
     "dlsim_chunk_mean_ilp_begin",
     "dlsim_rccl_bind",
     "dlsim_wreduce_sharded",
+    "dlsim_host_wreduce",
     "dlsim_shard_range",
     "dlsim_probe_copy",
     "dlsim_last_error",
@@ -104,6 +105,10 @@ def load() -> ctypes.CDLL:
         lib.dlsim_wreduce_sharded.argtypes = [ctypes.POINTER(vp), sz, i, ctypes.POINTER(ctypes.c_float), vp, sz, i,
                                               i, vp, i, vp]
         lib.dlsim_wreduce_sharded.restype = i
+        lib.dlsim_host_wreduce.argtypes = [i, i, ctypes.POINTER(vp), ctypes.POINTER(sz),
+                                           ctypes.POINTER(ctypes.c_float), vp, vp, sz, vp, vp, i, i, sz, i,
+                                           vp, vp, vp]
+        lib.dlsim_host_wreduce.restype = i
         lib.dlsim_shard_range.argtypes = [sz, i, i, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)]
         lib.dlsim_shard_range.restype = i
         lib.dlsim_probe_copy.argtypes = [vp, vp, sz, vp]
@@ -450,6 +455,56 @@ def wreduce_tensors(inputs_by_model, weights_f32, outs, mode: int = DLSIM_EXACT,
                                    optrs, dt, mode, _stream_handle(dev, stream) if t else None)
     _check("dlsim_wreduce_tensors", rc)
     return outs
+
+
+def host_wreduce(inputs_by_model, weights_f32, staging, rows, out, host_out=None, mode: int = DLSIM_EXACT,
+                 chunk_elems: int = 0, threads: Optional[int] = None, stream=None, h2d_stream=None,
+                 d2h_stream=None):
+    """dlsim_host_wreduce: inputs_by_model[i][k] is host tensor k of model i
+    (one dtype); `staging` (pinned) and `rows` (device) are [n, >= total]
+    row buffers with equal row strides; `out` the device result, `host_out`
+    an optional pinned host copy. Returns after packing; the copies and
+    reduces are queued (synchronise `stream` before reading host_out)."""
+    import torch
+    lib = load()
+    n = len(inputs_by_model)
+    if n < 1:
+        raise IndexError("list index out of range")
+    t = len(inputs_by_model[0])
+    dt = out.dtype
+    flat, keep = [], []
+    numels = [x.numel() for x in inputs_by_model[0]]
+    for row in inputs_by_model:
+        if len(row) != t:
+            raise ValueError("every model must have the same number of tensors")
+        for k, x in enumerate(row):
+            if x.dtype is not dt or x.get_device() != -1 or x.numel() != numels[k]:
+                raise ValueError(f"tensor {k}: host tensors of the output's dtype and size expected")
+            if not x.is_contiguous():
+                x = x.contiguous()
+                keep.append(x)
+            flat.append(x.data_ptr())
+    total = sum(numels)
+    if out.numel() != total or not out.is_cuda or not out.is_contiguous():
+        raise ValueError("out must be a contiguous device tensor of the models' size")
+    if staging.shape[0] < n or rows.shape[0] < n or staging.stride(0) != rows.stride(0) \
+            or staging.dtype != dt or rows.dtype != dt or rows.device != out.device:
+        raise ValueError("staging/rows: [n, >= total] buffers of the output's dtype, equal strides")
+    if host_out is not None and (host_out.numel() != total or host_out.dtype != dt or host_out.is_cuda):
+        raise ValueError("host_out must be a host tensor of the output's size and dtype")
+    w = np.ascontiguousarray(weights_f32, dtype=np.float32)
+    if w.size != n:
+        raise AssertionError("weights/models length mismatch")
+    st = _stream_handle(out.device, stream)
+    rc = lib.dlsim_host_wreduce(
+        n, t, (ctypes.c_void_p * len(flat))(*flat), (ctypes.c_size_t * t)(*numels),
+        w.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), staging.data_ptr(), rows.data_ptr(),
+        staging.stride(0), out.data_ptr(), None if host_out is None else host_out.data_ptr(),
+        dtype_code(dt), mode, chunk_elems, torch.get_num_threads() if threads is None else threads, st,
+        None if h2d_stream is None else h2d_stream.cuda_stream,
+        None if d2h_stream is None else d2h_stream.cuda_stream)
+    _check("dlsim_host_wreduce", rc)
+    return out
 
 
 def probe_copy(src, dst, stream=None) -> None:

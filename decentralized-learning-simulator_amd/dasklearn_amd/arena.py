@@ -240,81 +240,39 @@ def _side_streams(dev: torch.device):
 
 
 # Host pipeline chunking: about this many bytes of each model per chunk, at
-# most this many chunks, boundaries on multiples of this many elements (keeps
-# every chunk of a 256-B aligned staging row 16-B aligned for the vector kernel).
-PIPELINE_CHUNK_BYTES = 16 << 20
-PIPELINE_MAX_CHUNKS = 8
-_CHUNK_ALIGN = 1024
+# most this many chunks (dlsim_host_wreduce rounds the chunk to 1024 elements,
+# which keeps every chunk of a 256-B aligned staging row 16-B aligned).
+PIPELINE_CHUNK_BYTES = 8 << 20
+PIPELINE_MAX_CHUNKS = 32
 
 
-def _chunk_plan(layout: ParamLayout, dt: torch.dtype, esz: int):
-    """[(c0, c1, [(j, a, b)])]: element ranges of the dtype group's arena and,
-    per range, the pieces [a, b) of group tensor j that fill it in order."""
-    total = layout.totals[dt]
+def pipeline_chunk_elems(total: int, esz: int) -> int:
+    """Chunk length of the host pipeline for a total-element arena (0 = one chunk)."""
     k = max(1, min(PIPELINE_MAX_CHUNKS, round(total * esz / PIPELINE_CHUNK_BYTES)))
-    bounds = [0]
-    for c in range(1, k):
-        b = (total * c // k) // _CHUNK_ALIGN * _CHUNK_ALIGN
-        if b > bounds[-1]:
-            bounds.append(b)
-    bounds.append(total)
-    offs, sizes = layout._group_offsets[dt], layout.split_sizes[dt]
-    plan = []
-    for c0, c1 in zip(bounds, bounds[1:]):
-        pieces = []
-        for j, (off, sz) in enumerate(zip(offs, sizes)):
-            a, b = max(c0, off), min(c1, off + sz)
-            if a < b:
-                pieces.append((j, a - off, b - off))
-        plan.append((c0, c1, pieces))
-    return plan
+    return 0 if k == 1 else -(-total // k)
 
 
 def _host_pipeline(all_params, idx, layout, dt, dev, out, weights_f32, mode, stream, want_host):
-    """Host models -> device reduce (-> host result), pipelined over chunks of
-    the parameter axis: chunk c of every model is packed into pinned staging
-    (CPU) and copied H2D on the H2D stream while chunk c-1 is reduced on the
-    caller's stream and chunk c-2's result goes back on the D2H stream. Bytes
-    and results are those of the unchunked path (elements are independent);
-    what changes is that the kernel and the D2H hide under the H2D stream.
-    Returns the pinned host result (want_host, more than one chunk) or None
-    (the result is in `out` on the device, queued on `stream`)."""
+    """Host models -> device reduce (-> host result) in one dlsim_host_wreduce
+    call: the parameters are packed into pinned staging rows by the library's
+    thread pool (torch's intra-op thread count), chunk by chunk of the
+    parameter axis; each model's share of a chunk goes H2D on the H2D stream as
+    soon as it is packed, each chunk is reduced on the caller's stream once all
+    its shares are on the device, and its result comes back on the D2H
+    stream (PCIe is full duplex). Bytes and results are those of the
+    unchunked reduce (elements are independent). One-chunk models use the
+    caller's stream for everything (the side-stream events cost more than
+    they hide there). Returns the pinned host result (want_host; complete
+    once `stream` is) or None (the result is in `out`, queued on `stream`)."""
     n = len(all_params)
     total = layout.totals[dt]
     dev_rows, pinned = STAGING.acquire(dev, dt, n, total, stream)
-    plan = _chunk_plan(layout, dt, out.element_size())
-    if len(plan) == 1:
-        # one chunk: no side streams (their events cost more than they hide
-        # for small models) — pack model i while model i-1's H2D runs
-        for i, ps in enumerate(all_params):
-            torch.cat([ps[k].detach().reshape(-1) for k in idx], out=pinned[i])
-            dev_rows[i].copy_(pinned[i], non_blocking=True)
-        _native.wreduce([dev_rows[i] for i in range(n)], weights_f32, out, mode, stream)
-        STAGING.release(dev, dt, n, total, stream)
-        return None
-    h2d, d2h = _side_streams(dev)
-    h2d.wait_stream(stream)
+    chunk = pipeline_chunk_elems(total, out.element_size())
+    h2d, d2h = _side_streams(dev) if chunk else (None, None)
     host = torch.empty(total, dtype=dt, pin_memory=True) if want_host else None
-    sizes = layout.split_sizes[dt]
-    flats = [[ps[k].detach().reshape(-1) for k in idx] for ps in all_params]
-    for c0, c1, pieces in plan:
-        for i in range(n):
-            fl = flats[i]
-            src = [fl[j] if (a == 0 and b == sizes[j]) else fl[j][a:b] for j, a, b in pieces]
-            dst = pinned[i, c0:c1]
-            torch.cat(src, out=dst)
-            with torch.cuda.stream(h2d):
-                dev_rows[i, c0:c1].copy_(dst, non_blocking=True)
-        stream.wait_stream(h2d)
-        _native.wreduce([dev_rows[i, c0:c1] for i in range(n)], weights_f32, out[c0:c1], mode, stream)
-        if host is not None:
-            d2h.wait_stream(stream)
-            with torch.cuda.stream(d2h):
-                host[c0:c1].copy_(out[c0:c1], non_blocking=True)
+    _native.host_wreduce([[ps[k] for k in idx] for ps in all_params], weights_f32, pinned, dev_rows, out,
+                         host, mode, chunk, None, stream, h2d, d2h)
     STAGING.release(dev, dt, n, total, stream)
-    if host is not None:
-        out.record_stream(d2h)
-        stream.wait_stream(d2h)
     return host
 
 

@@ -228,6 +228,40 @@ int dlsim_wreduce_sharded(const void* const* d_slices, size_t slice_elems, int n
                           void* stream);
 
 /*
+ * dlsim_host_wreduce — the aggregate of N *host* models (the reference's own
+ * case: CPU modules, fedavg.py:20-25 run by functions.py:89-106), staged
+ * through pinned memory and reduced on the device, as one pipeline.
+ *
+ *   h_srcs[i * t + k]  host pointer of tensor k of model i (contiguous,
+ *                      numels[k] elements of dtype; any alignment)
+ *   h_staging, d_rows  n rows of row_stride elements each, page-locked host
+ *                      memory and device memory; 16-B aligned, row_stride a
+ *                      multiple of 8 elements, >= sum(numels)
+ *   d_out              device result, sum(numels) elements: the exact or fast
+ *                      reduce of the concatenated models (dlsim_wreduce rules)
+ *   h_out              page-locked host copy of the result, or NULL
+ *   chunk_elems        pipeline chunk of the parameter axis (rounded up to a
+ *                      multiple of 1024; 0 = one chunk)
+ *   threads            host threads packing the staging rows (the caller's
+ *                      own thread included; <= 1: the caller's thread only)
+ *   stream             the reduce; h2d_stream / d2h_stream the copies (may be
+ *                      `stream` itself or NULL = `stream`)
+ * Model i's share of chunk c is packed (memcpy, several threads) into its
+ * staging row and copied H2D on h2d_stream as soon as it is packed; once
+ * every model's share of chunk c is on the device, the chunk is reduced on
+ * `stream` and (h_out) copied back on d2h_stream, while later chunks are
+ * still being packed and copied. Returns after the pack and the queueing:
+ * the copies and kernels are stream-ordered and asynchronous, `stream` is
+ * ordered after all of them (synchronise it before reading h_out), and the
+ * staging buffers must not be reused before then. Results are bit-identical
+ * to dlsim_wreduce over the packed rows.
+ */
+int dlsim_host_wreduce(int n, int t, const void* const* h_srcs, const size_t* numels,
+                       const float* h_weights, void* h_staging, void* d_rows, size_t row_stride,
+                       void* d_out, void* h_out, int dtype, int mode, size_t chunk_elems, int threads,
+                       void* stream, void* h2d_stream, void* d2h_stream);
+
+/*
  * dlsim_shard_range — parameter-axis partition used by the sharded path.
  *
  * Splits [0, n_elems) into `world` contiguous slices whose boundaries are

@@ -33,6 +33,26 @@ class Shaped(nn.Module):
         self.ps = nn.ParameterList([nn.Parameter(torch.randn(*s, generator=g) * 0.05) for s in shapes])
 
 
+def chunk_plan(layout, dt, esz, chunk_bytes=16 << 20, max_chunks=8, align=1024):
+    """[(c0, c1, [(j, a, b)])]: the round-1 Python pipeline's chunks of the
+    dtype group's arena and the tensor pieces [a, b) that fill each."""
+    total = layout.totals[dt]
+    k = max(1, min(max_chunks, round(total * esz / chunk_bytes)))
+    bounds = [0]
+    for c in range(1, k):
+        b = (total * c // k) // align * align
+        if b > bounds[-1]:
+            bounds.append(b)
+    bounds.append(total)
+    offs, sizes = layout._group_offsets[dt], layout.split_sizes[dt]
+    plan = []
+    for c0, c1 in zip(bounds, bounds[1:]):
+        pieces = [(j, max(c0, off) - off, min(c1, off + sz) - off)
+                  for j, (off, sz) in enumerate(zip(offs, sizes)) if max(c0, off) < min(c1, off + sz)]
+        plan.append((c0, c1, pieces))
+    return plan
+
+
 def med(f, reps=15):
     f()
     torch.cuda.synchronize()
@@ -66,7 +86,7 @@ def main():
     res["pack_h2d_model"] = med(pack_h2d_model)
 
     layout = arena.ParamLayout(models[0])
-    plan = arena._chunk_plan(layout, torch.float32, 4)
+    plan = chunk_plan(layout, torch.float32, 4)
     sizes = layout.split_sizes[torch.float32]
     res["chunks"] = len(plan)
 

@@ -41,10 +41,12 @@ def main():
     out = {"n": n}
     for th in (4, 16):
         torch.set_num_threads(th)
-        for cb in (1 << 40, 16 << 20, 8 << 20, 4 << 20, 2 << 20):
+        for cb in (1 << 40, 16 << 20, 8 << 20, 4 << 20, 2 << 20, 1 << 20):
             arena.PIPELINE_CHUNK_BYTES = cb
             arena.PIPELINE_MAX_CHUNKS = 64
-            k = len(arena._chunk_plan(arena.ParamLayout(models[0]), torch.float32, 4))
+            total = arena.ParamLayout(models[0]).totals[torch.float32]
+            c = arena.pipeline_chunk_elems(total, 4)
+            k = -(-total // c) if c else 1
             out[f"t{th}_chunks{k}_ms"] = round(med(lambda: FedAvg.aggregate(models, None)), 3)
     print(json.dumps(out), flush=True)
 

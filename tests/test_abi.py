@@ -93,3 +93,29 @@ def test_zero_elements_is_a_noop():
     w = np.ones(2, dtype=np.float32)
     assert lib.dlsim_wreduce(ptrs, 2, w.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
                              ctypes.c_void_p(64), 0, 0, 0, None) == 0
+
+
+def _host_call(numels, stride=4096, staging=4096, rows=8192, out=16, srcs=None, dtype=0, mode=0, n=2):
+    lib = _native.load()
+    t = len(numels)
+    srcs = srcs if srcs is not None else [64] * (n * t)
+    w = np.ones(n, dtype=np.float32)
+    return lib.dlsim_host_wreduce(n, t, (ctypes.c_void_p * max(len(srcs), 1))(*srcs),
+                                  (ctypes.c_size_t * max(t, 1))(*numels),
+                                  w.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), staging, rows, stride,
+                                  out, None, dtype, mode, 0, 4, None, None, None)
+
+
+def test_host_wreduce_argument_errors_need_no_gpu():
+    """dlsim_host_wreduce rejects bad staging before any HIP call; zero
+    elements is a no-op."""
+    lib = _native.load()
+    assert _host_call([0, 0]) == 0
+    assert _host_call([10], dtype=5) == -2
+    assert _host_call([10], mode=4) == -3
+    assert _host_call([10], n=0) == -1
+    assert _host_call([100, 28], stride=64) == -1 and b"row_stride" in lib.dlsim_last_error()
+    assert _host_call([10], stride=12) == -1 and b"aligned" in lib.dlsim_last_error()
+    assert _host_call([10], staging=4100) == -1
+    assert _host_call([10], srcs=[64, 0]) == -1 and b"null source" in lib.dlsim_last_error()
+    assert _host_call([10], out=0) == -1

@@ -235,30 +235,18 @@ def test_staging_row_stride(numel, esz, expect):
     assert (s * esz) % 65536 != 0
 
 
-@pytest.mark.parametrize("chunk_bytes", [64, 4096, 1 << 20, 8 << 20])
-def test_host_pipeline_chunk_plan_covers_the_arena(monkeypatch, chunk_bytes):
-    """The host pipeline's chunks tile each dtype group's arena in order, start
-    on 1024-element boundaries (16-B aligned rows for the vector kernel) and
-    their pieces are exactly the tensors' elements."""
-    monkeypatch.setattr(arena, "PIPELINE_CHUNK_BYTES", chunk_bytes)
-    m = nn.Sequential(nn.Linear(300, 200), nn.Linear(200, 7), nn.Conv2d(3, 5, 3))
-    lay = arena.ParamLayout(m)
-    plan = arena._chunk_plan(lay, torch.float32, 4)
-    assert 1 <= len(plan) <= arena.PIPELINE_MAX_CHUNKS
-    assert plan[0][0] == 0 and plan[-1][1] == lay.totals[torch.float32]
-    seen = []
-    for (c0, c1, pieces), nxt in zip(plan, plan[1:] + [None]):
-        assert c0 % 1024 == 0 and c1 > c0
-        if nxt is not None:
-            assert nxt[0] == c1
-        assert sum(b - a for _, a, b in pieces) == c1 - c0
-        seen += [(j, a, b) for j, a, b in pieces]
-    # concatenating the pieces reproduces every tensor once, in order
-    per = {}
-    for j, a, b in seen:
-        assert per.get(j, 0) == a
-        per[j] = b
-    assert [per[j] for j in range(len(lay.split_sizes[torch.float32]))] == lay.split_sizes[torch.float32]
+@pytest.mark.parametrize("total,esz", [(1000, 4), (11_181_642, 4), (11_181_642, 2), (3 << 20, 4), (10 ** 9, 4)])
+def test_host_pipeline_chunk_elems(total, esz):
+    """The host pipeline cuts the parameter axis into at most
+    PIPELINE_MAX_CHUNKS chunks of about PIPELINE_CHUNK_BYTES per model
+    (0 = one chunk); the chunks cover the arena."""
+    c = arena.pipeline_chunk_elems(total, esz)
+    if c == 0:
+        assert total * esz < 1.5 * arena.PIPELINE_CHUNK_BYTES
+        return
+    k = -(-total // c)
+    assert 2 <= k <= arena.PIPELINE_MAX_CHUNKS and c * k >= total
+    assert k == arena.PIPELINE_MAX_CHUNKS or abs(c * esz - arena.PIPELINE_CHUNK_BYTES) < arena.PIPELINE_CHUNK_BYTES
 
 
 def test_module_params_matches_parameters():
