@@ -604,6 +604,57 @@ int rccl_fail(rccl_result_t r, const char* what) {
   return fail(DLSIM_E_RCCL, "%s: %s (ncclResult %d)", what, g_rccl.err ? g_rccl.err(r) : "?", r);
 }
 
+// ---- host staging pipelines (dlsim_host_wreduce, dlsim_host_chunk_mean) -------
+// Cross-stream ordering by events. Destroying a recorded event is deferred by
+// the runtime until it completes, so the destructor may run right away.
+struct StreamLinks {
+  std::vector<hipEvent_t> evs;
+  int rc = DLSIM_OK;
+  void link(hipStream_t from, hipStream_t to, const char* what) {
+    if (rc != DLSIM_OK || from == to) return;
+    hipEvent_t ev;
+    hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (e != hipSuccess) {
+      rc = hip_fail(e, what);
+      return;
+    }
+    evs.push_back(ev);
+    e = hipEventRecord(ev, from);
+    if (e == hipSuccess) e = hipStreamWaitEvent(to, ev, 0);
+    if (e != hipSuccess) rc = hip_fail(e, what);
+  }
+  ~StreamLinks() {
+    for (hipEvent_t ev : evs) (void)hipEventDestroy(ev);
+  }
+};
+
+// Pack `job` on `threads` host threads (the caller's included) and call
+// on_unit(u) for u = 0, 1, ... as each unit completes, in order, on this
+// thread. Below ~1 MiB of input the helpers stay asleep: their wake-up costs
+// more than they save.
+template <class F>
+void pack_and_dispatch(dlsim::PackJob& job, int threads, size_t in_bytes, F&& on_unit) {
+  const int helpers = in_bytes < (size_t{1} << 20) ? 0 : std::min(std::max(threads, 1), 64) - 1;
+  dlsim::PackPool& pool = dlsim::PackPool::get();
+  std::lock_guard<std::mutex> lk(pool.call_mutex());
+  if (helpers > 0) pool.start(&job, helpers);
+  for (size_t u = 0; u < job.units;) {
+    if (job.unit_done(u)) {
+      on_unit(u++);
+    } else if (!job.run_one()) {
+      std::this_thread::yield();
+    }
+  }
+  if (helpers > 0) pool.join();
+}
+
+// Staging layout of dlsim_host_chunk_mean: input rows back to back, each at
+// a 256-B aligned offset.
+size_t staged_row_elems(size_t n, size_t esz) {
+  const size_t al = 256 / esz;
+  return (n + al - 1) / al * al;
+}
+
 }  // namespace
 
 extern "C" {
@@ -883,68 +934,122 @@ int dlsim_host_wreduce(int n, int t, const void* const* h_srcs, const size_t* nu
     job.seal(n_chunks * n);
   }
 
-  // Events: `stream` -> copy streams before the first copy (earlier work on
-  // the rows), copy streams -> `stream` at the end; per chunk, H2D -> reduce
-  // and reduce -> D2H. Destroying a recorded event is deferred by the
-  // runtime until it completes.
-  int rc = DLSIM_OK;
-  std::vector<hipEvent_t> evs;
-  auto event_on = [&](hipStream_t from, hipStream_t to, const char* what) {
-    if (rc != DLSIM_OK || from == to) return;
-    hipEvent_t ev;
-    hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-    if (e != hipSuccess) { rc = hip_fail(e, what); return; }
-    evs.push_back(ev);
-    e = hipEventRecord(ev, from);
-    if (e == hipSuccess) e = hipStreamWaitEvent(to, ev, 0);
-    if (e != hipSuccess) rc = hip_fail(e, what);
-  };
-  event_on(st, h2d, "order H2D after stream");
-  if (h_out) event_on(st, d2h, "order D2H after stream");
-
+  // `stream` -> copy streams before the first copy (earlier work on the
+  // rows); per chunk, H2D -> reduce and reduce -> D2H; D2H -> `stream` at the
+  // end (every H2D is already ordered before its chunk's reduce).
+  StreamLinks ln;
+  ln.link(st, h2d, "order H2D after stream");
+  if (h_out) ln.link(st, d2h, "order D2H after stream");
   std::vector<const void*> ins(static_cast<size_t>(n));
-  auto dispatch_unit = [&](size_t u) {
-    if (rc != DLSIM_OK) return;
+  pack_and_dispatch(job, threads, total * esz * n, [&](size_t u) {
+    if (ln.rc != DLSIM_OK) return;
     const size_t c = u / n, i = u % n;
     const size_t c0 = c * chunk, c1 = std::min(total, c0 + chunk);
     const size_t o = i * row_bytes + c0 * esz;
     hipError_t e = hipMemcpyAsync(rows + o, stage + o, (c1 - c0) * esz, hipMemcpyHostToDevice, h2d);
-    if (e != hipSuccess) { rc = hip_fail(e, "staging H2D"); return; }
+    if (e != hipSuccess) {
+      ln.rc = hip_fail(e, "staging H2D");
+      return;
+    }
     if (i + 1 < static_cast<size_t>(n)) return;
-    event_on(h2d, st, "order reduce after H2D");
-    if (rc != DLSIM_OK) return;
+    ln.link(h2d, st, "order reduce after H2D");
+    if (ln.rc != DLSIM_OK) return;
     for (int r = 0; r < n; ++r) ins[r] = rows + r * row_bytes + c0 * esz;
-    rc = dispatch(ins.data(), n, h_weights, out + c0 * esz, c1 - c0, dtype, mode, st);
-    if (rc != DLSIM_OK || !h_out) return;
-    event_on(st, d2h, "order D2H after reduce");
-    if (rc != DLSIM_OK) return;
+    ln.rc = dispatch(ins.data(), n, h_weights, out + c0 * esz, c1 - c0, dtype, mode, st);
+    if (ln.rc != DLSIM_OK || !h_out) return;
+    ln.link(st, d2h, "order D2H after reduce");
+    if (ln.rc != DLSIM_OK) return;
     e = hipMemcpyAsync(static_cast<char*>(h_out) + c0 * esz, out + c0 * esz, (c1 - c0) * esz,
                        hipMemcpyDeviceToHost, d2h);
-    if (e != hipSuccess) rc = hip_fail(e, "result D2H");
-  };
+    if (e != hipSuccess) ln.rc = hip_fail(e, "result D2H");
+  });
+  if (h_out) ln.link(d2h, st, "order stream after D2H");
+  return ln.rc;
+}
 
-  // Below ~1 MiB of input the helpers' wake-up costs more than they save.
-  const size_t in_bytes = total * esz * n;
-  int helpers = in_bytes < (size_t{1} << 20) ? 0 : std::min(std::max(threads, 1), 64) - 1;
-  dlsim::PackPool& pool = dlsim::PackPool::get();
+int dlsim_host_chunk_mean(int b, const int* fan_in, const void* const* h_inputs, const size_t* n_elems,
+                          void* h_staging, void* d_staging, size_t staging_elems, void* const* d_outs,
+                          void* const* h_outs, int dtype, int cpu_threads, int threads, void* stream,
+                          void* h2d_stream, void* d2h_stream) {
+  g_err.clear();
+  if (b < 0) return fail(DLSIM_E_ARG, "b must be >= 0 (got %d)", b);
+  if (b == 0) return DLSIM_OK;
+  if (!fan_in || !h_inputs || !d_outs || !n_elems) return fail(DLSIM_E_ARG, "null array argument");
+  if (!known_dtype(dtype)) return fail(DLSIM_E_DTYPE, "unsupported dtype %d", dtype);
+  if (cpu_threads < 1) return fail(DLSIM_E_ARG, "cpu_threads must be >= 1 (got %d)", cpu_threads);
+  const size_t esz = elem_bytes(dtype);
+  size_t need = 0, rows_total = 0;
+  for (int t = 0; t < b; ++t) {
+    if (fan_in[t] < 1 || fan_in[t] > 65535) return fail(DLSIM_E_ARG, "task %d: fan-in %d not in [1, 65535]", t, fan_in[t]);
+    if (n_elems[t] * esz >= kMaxLaunchOutBytes)
+      return fail(DLSIM_E_ARG, "task %d: chunk of %zu elements is >= 2 GiB", t, n_elems[t]);
+    if (n_elems[t] > 0 && !d_outs[t]) return fail(DLSIM_E_ARG, "task %d: null output", t);
+    for (int i = 0; i < fan_in[t]; ++i)
+      if (n_elems[t] > 0 && !h_inputs[rows_total + i]) return fail(DLSIM_E_ARG, "task %d: null input %d", t, i);
+    need += static_cast<size_t>(fan_in[t]) * staged_row_elems(n_elems[t], esz);
+    rows_total += static_cast<size_t>(fan_in[t]);
+  }
+  if (need == 0) return DLSIM_OK;
+  if (!h_staging || !d_staging) return fail(DLSIM_E_ARG, "null staging");
+  if (!aligned16(h_staging) || !aligned16(d_staging)) return fail(DLSIM_E_ARG, "staging must be 16-B aligned");
+  if (staging_elems < need) return fail(DLSIM_E_ARG, "staging of %zu elements < %zu needed", staging_elems, need);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  hipStream_t h2d = h2d_stream ? static_cast<hipStream_t>(h2d_stream) : st;
+  hipStream_t d2h = d2h_stream ? static_cast<hipStream_t>(d2h_stream) : st;
+  char* hs = static_cast<char*>(h_staging);
+  char* ds = static_cast<char*>(d_staging);
+
+  // One unit per input row, in task order; row r sits at row_off[r].
+  std::vector<size_t> row_off(rows_total), row_task(rows_total);
+  dlsim::PackJob job;
   {
-    std::lock_guard<std::mutex> lk(pool.call_mutex());
-    if (helpers > 0) pool.start(&job, helpers);
-    // This thread packs too, and starts each unit's DMA (and each chunk's
-    // reduce) as soon as the unit is complete, in unit order.
-    for (size_t u = 0; u < job.units;) {
-      if (job.unit_done(u)) {
-        dispatch_unit(u++);
-      } else if (!job.run_one()) {
-        std::this_thread::yield();
+    size_t r = 0, o = 0;
+    for (int t = 0; t < b; ++t)
+      for (int i = 0; i < fan_in[t]; ++i, ++r) {
+        row_off[r] = o;
+        row_task[r] = static_cast<size_t>(t);
+        job.add(static_cast<uint32_t>(r), static_cast<const char*>(h_inputs[r]), hs + o * esz, n_elems[t] * esz);
+        o += staged_row_elems(n_elems[t], esz);
+      }
+    job.seal(rows_total);
+  }
+  StreamLinks ln;
+  ln.link(st, h2d, "order H2D after stream");
+  if (h_outs) ln.link(st, d2h, "order D2H after stream");
+  std::vector<const void*> ins;
+  size_t task_first = 0;  // first row of the current task
+  pack_and_dispatch(job, threads, need * esz, [&](size_t r) {
+    if (ln.rc != DLSIM_OK) return;
+    const int t = static_cast<int>(row_task[r]);
+    const size_t n = n_elems[t];
+    if (n > 0) {
+      hipError_t e = hipMemcpyAsync(ds + row_off[r] * esz, hs + row_off[r] * esz, n * esz, hipMemcpyHostToDevice, h2d);
+      if (e != hipSuccess) {
+        ln.rc = hip_fail(e, "staging H2D");
+        return;
       }
     }
-    if (helpers > 0) pool.join();
-  }
-  // (every H2D is already ordered before its chunk's reduce on `stream`)
-  if (h_out) event_on(d2h, st, "order stream after D2H");
-  for (hipEvent_t ev : evs) (void)hipEventDestroy(ev);
-  return rc;
+    if (r + 1 - task_first < static_cast<size_t>(fan_in[t])) return;
+    const size_t first = task_first;
+    task_first = r + 1;
+    if (n == 0) return;
+    // every row of task t is queued: its mean, then its D2H
+    ln.link(h2d, st, "order chunk mean after H2D");
+    if (ln.rc != DLSIM_OK) return;
+    ins.assign(static_cast<size_t>(fan_in[t]), nullptr);
+    for (int i = 0; i < fan_in[t]; ++i) ins[i] = ds + row_off[first + i] * esz;
+    void* out = d_outs[t];
+    ln.rc = with_mean_policy(dtype, [&](auto op) {
+      return run_chunk_mean<decltype(op)>(1, &fan_in[t], ins.data(), &out, &n_elems[t], cpu_threads, st);
+    });
+    if (ln.rc != DLSIM_OK || !h_outs || !h_outs[t]) return;
+    ln.link(st, d2h, "order D2H after chunk mean");
+    if (ln.rc != DLSIM_OK) return;
+    hipError_t e = hipMemcpyAsync(h_outs[t], out, n * esz, hipMemcpyDeviceToHost, d2h);
+    if (e != hipSuccess) ln.rc = hip_fail(e, "result D2H");
+  });
+  if (h_outs) ln.link(d2h, st, "order stream after D2H");
+  return ln.rc;
 }
 
 int dlsim_shard_range(size_t n_elems, int world, int rank, size_t align_elems, size_t* begin,

@@ -38,6 +38,7 @@ EXPORTS = (
     "dlsim_rccl_bind",
     "dlsim_wreduce_sharded",
     "dlsim_host_wreduce",
+    "dlsim_host_chunk_mean",
     "dlsim_shard_range",
     "dlsim_probe_copy",
     "dlsim_last_error",
@@ -109,6 +110,9 @@ def load() -> ctypes.CDLL:
                                            ctypes.POINTER(ctypes.c_float), vp, vp, sz, vp, vp, i, i, sz, i,
                                            vp, vp, vp]
         lib.dlsim_host_wreduce.restype = i
+        lib.dlsim_host_chunk_mean.argtypes = [i, ctypes.POINTER(i), ctypes.POINTER(vp), ctypes.POINTER(sz), vp, vp,
+                                              sz, ctypes.POINTER(vp), ctypes.POINTER(vp), i, i, i, vp, vp, vp]
+        lib.dlsim_host_chunk_mean.restype = i
         lib.dlsim_shard_range.argtypes = [sz, i, i, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)]
         lib.dlsim_shard_range.restype = i
         lib.dlsim_probe_copy.argtypes = [vp, vp, sz, vp]
@@ -366,6 +370,67 @@ def chunk_mean_batched(tasks, threads=None, stream=None):
            lib.dlsim_chunk_mean_batched(b, (ctypes.c_int * b)(*fan), (ctypes.c_void_p * len(ptrs))(*ptrs),
                                         (ctypes.c_void_p * b)(*outs), (ctypes.c_size_t * b)(*numels), dt,
                                         int(threads), _stream_handle(out0.device, stream)))
+    return [t[1] for t in tasks]
+
+
+def staged_rows_elems(numels, fan_in, esz: int) -> int:
+    """Staging size dlsim_host_chunk_mean needs: every input row at a 256-B
+    aligned offset."""
+    al = 256 // esz
+    return sum(f * ((k + al - 1) // al * al) for k, f in zip(numels, fan_in))
+
+
+def host_chunk_mean(tasks, staging, d_staging, host_outs=None, threads=None, cpu_threads=None, stream=None,
+                    h2d_stream=None, d2h_stream=None):
+    """dlsim_host_chunk_mean. tasks: sequence of (host inputs, device out);
+    `staging` (pinned) and `d_staging` (device) hold staged_rows_elems()
+    elements; host_outs: None or per task a pinned host tensor (or None).
+    Returns after packing; synchronise `stream` before reading host_outs or
+    freeing the staging."""
+    import torch
+    lib = load()
+    b = len(tasks)
+    if b == 0:
+        return []
+    out0 = tasks[0][1]
+    dt = out0.dtype
+    fan, ptrs, outs, numels, keep = [], [], [], [], []
+    for inputs, out in tasks:
+        if len(inputs) < 1:
+            raise IndexError("list index out of range")
+        if not out.is_cuda or out.dtype != dt or not out.is_contiguous() or out.device != out0.device:
+            raise ValueError("outputs: contiguous device tensors of one dtype, one device")
+        for x in inputs:
+            if x.get_device() != -1 or x.dtype is not dt or x.numel() != out.numel():
+                raise ValueError("inputs: host tensors of the output's dtype and size")
+            if not x.is_contiguous():
+                x = x.contiguous()
+                keep.append(x)
+            ptrs.append(x.data_ptr())
+        fan.append(len(inputs))
+        outs.append(out.data_ptr())
+        numels.append(out.numel())
+    need = staged_rows_elems(numels, fan, out0.element_size())
+    if staging.numel() < need or d_staging.numel() < need or staging.dtype != dt or d_staging.dtype != dt \
+            or staging.is_cuda or not d_staging.is_cuda:
+        raise ValueError(f"staging: a pinned host and a device buffer of >= {need} elements of the dtype")
+    hptrs = None
+    if host_outs is not None:
+        hp = []
+        for h, (_, out) in zip(host_outs, tasks):
+            if h is not None and (h.is_cuda or h.dtype != dt or h.numel() != out.numel()):
+                raise ValueError("host_outs: host tensors of the outputs' dtype and size")
+            hp.append(None if h is None else h.data_ptr())
+        hptrs = (ctypes.c_void_p * b)(*hp)
+    _check("dlsim_host_chunk_mean",
+           lib.dlsim_host_chunk_mean(b, (ctypes.c_int * b)(*fan), (ctypes.c_void_p * len(ptrs))(*ptrs),
+                                     (ctypes.c_size_t * b)(*numels), staging.data_ptr(), d_staging.data_ptr(),
+                                     min(staging.numel(), d_staging.numel()), (ctypes.c_void_p * b)(*outs), hptrs,
+                                     dtype_code(dt), int(torch.get_num_threads() if cpu_threads is None else cpu_threads),
+                                     int(torch.get_num_threads() if threads is None else threads),
+                                     _stream_handle(out0.device, stream),
+                                     None if h2d_stream is None else h2d_stream.cuda_stream,
+                                     None if d2h_stream is None else d2h_stream.cuda_stream))
     return [t[1] for t in tasks]
 
 

@@ -30,7 +30,7 @@ import torch
 from torch import nn
 
 from . import _native
-from .arena import _target_device
+from .arena import _side_streams, _target_device
 
 
 class ChunkManager:
@@ -57,11 +57,12 @@ class ChunkManager:
 
     @staticmethod
     def mean_chunk_indices(chunks: List[List[torch.Tensor]], device=None) -> List[torch.Tensor]:
-        """[torch.mean(torch.stack(cs), dim=0) for cs in chunks], every chunk
-        index in one batched launch per dtype (dlsim_chunk_mean_batched). Device
-        chunks are read in place; host chunks (the reference's case) are staged
-        into one pinned buffer, copied with one H2D, and the means come back
-        with one D2H. Each result lives where its first chunk lives."""
+        """[torch.mean(torch.stack(cs), dim=0) for cs in chunks]. Device chunks
+        are read in place, every chunk index in one batched launch per dtype
+        (dlsim_chunk_mean_batched); host chunks (the reference's case) go
+        through dlsim_host_chunk_mean (threaded pack into pinned staging,
+        per-row H2D, per-index mean and D2H, overlapped). Each result lives
+        where its first chunk lives."""
         for cs in chunks:
             first = cs[0]
             for c in cs:
@@ -97,44 +98,33 @@ class ChunkManager:
                             tasks.append(([c.reshape(-1).contiguous() for c in chunks[ci]], out))
                     _native.chunk_mean_batched(tasks)
                     continue
-                # host (or mixed) chunks: rows at 256-B aligned offsets of one
-                # pinned staging buffer, outputs in one device buffer
-                in_off, n_in = [], 0
-                for ci, k in zip(idxs, sizes):
-                    offs = []
-                    for _ in chunks[ci]:
-                        offs.append(n_in)
-                        n_in += rnd(k)
-                    in_off.append(offs)
-                stage = torch.empty(max(n_in, 1), dtype=dt, pin_memory=True)
-                d_in = torch.empty(max(n_in, 1), dtype=dt, device=dev)
-                for ci, offs in zip(idxs, in_off):
-                    for c, o in zip(chunks[ci], offs):
-                        k = c.numel()
-                        stage[o:o + k].copy_(c.reshape(-1))
-                        # this row's DMA overlaps the staging of the next one
-                        d_in[o:o + k].copy_(stage[o:o + k], non_blocking=True)
-                d_out = torch.empty(max(n_out, 1), dtype=dt, device=dev)
-                tasks = []
-                for ci, offs, o in zip(idxs, in_off, out_off):
-                    k = chunks[ci][0].numel()
-                    if k:
-                        tasks.append(([d_in[x:x + k] for x in offs], d_out[o:o + k]))
-                _native.chunk_mean_batched(tasks)
-                # the host result is always back to back (reconstruct_model
-                # then uses it without a cat): one D2H when the device
-                # layout is tight too, else one per chunk index
+                host_out_size = sum(sizes)
+                host = torch.empty(max(host_out_size, 1), dtype=dt, pin_memory=True)
                 host_off = [0]
                 for k in sizes:
                     host_off.append(host_off[-1] + k)
-                host = torch.empty(max(host_off[-1], 1), dtype=dt, pin_memory=True)
-                if tight:
-                    host.copy_(d_out, non_blocking=True)
+                d_out = torch.empty(max(n_out, 1), dtype=dt, device=dev)
+                stream = torch.cuda.current_stream(dev)
+                if all(c.get_device() == -1 for ci in idxs for c in chunks[ci]):
+                    # host chunks (the reference's case): dlsim_host_chunk_mean
+                    # packs the rows on the library's threads, starts each
+                    # row's H2D as soon as it is packed, runs each index's mean
+                    # once its rows are on the device and copies it back, the
+                    # host result back to back (reconstruct_model then uses it
+                    # without a cat)
+                    fan = [len(chunks[ci]) for ci in idxs]
+                    need = _native.staged_rows_elems(sizes, fan, esz)
+                    stage = torch.empty(max(need, 1), dtype=dt, pin_memory=True)
+                    d_in = torch.empty(max(need, 1), dtype=dt, device=dev)
+                    big = need * esz >= PIPELINE_SIDE_STREAM_BYTES
+                    h2d, d2h = _side_streams(dev) if big else (None, None)
+                    _native.host_chunk_mean(
+                        [(chunks[ci], d_out[o:o + k]) for ci, k, o in zip(idxs, sizes, out_off)],
+                        stage, d_in, host_outs=[host[h:h + k] for k, h in zip(sizes, host_off)],
+                        stream=stream, h2d_stream=h2d, d2h_stream=d2h)
+                    stream.synchronize()
                 else:
-                    for k, o, h in zip(sizes, out_off, host_off):
-                        if k:
-                            host[h:h + k].copy_(d_out[o:o + k], non_blocking=True)
-                torch.cuda.current_stream(dev).synchronize()
+                    _mixed_means(chunks, idxs, sizes, out_off, host, host_off, d_out, dt, dev, rnd, tight)
                 for ci, o, h in zip(idxs, out_off, host_off):
                     first = chunks[ci][0]
                     src = host[h:h + first.numel()] if not first.is_cuda else d_out[o:o + first.numel()]
@@ -188,3 +178,42 @@ def _span(ts: List[torch.Tensor]):
         nxt += t.numel() * t.element_size()
         total += t.numel()
     return t0.as_strided((total,), (1,))
+
+
+# Host chunk means go through the side copy streams above this many staged
+# bytes (below it the events cost more than the overlap saves).
+PIPELINE_SIDE_STREAM_BYTES = 4 << 20
+
+
+def _mixed_means(chunks, idxs, sizes, out_off, host, host_off, d_out, dt, dev, rnd, tight):
+    """Chunk means when some contributors are on a device and some on the
+    host: rows at 256-B aligned offsets of one pinned staging buffer (a CUDA
+    row copies through it), one H2D per row, one batched launch, then the
+    back-to-back host result."""
+    in_off, n_in = [], 0
+    for ci, k in zip(idxs, sizes):
+        offs = []
+        for _ in chunks[ci]:
+            offs.append(n_in)
+            n_in += rnd(k)
+        in_off.append(offs)
+    stage = torch.empty(max(n_in, 1), dtype=dt, pin_memory=True)
+    d_in = torch.empty(max(n_in, 1), dtype=dt, device=dev)
+    for ci, offs in zip(idxs, in_off):
+        for c, o in zip(chunks[ci], offs):
+            k = c.numel()
+            stage[o:o + k].copy_(c.reshape(-1))
+            d_in[o:o + k].copy_(stage[o:o + k], non_blocking=True)
+    tasks = []
+    for ci, offs, o in zip(idxs, in_off, out_off):
+        k = chunks[ci][0].numel()
+        if k:
+            tasks.append(([d_in[x:x + k] for x in offs], d_out[o:o + k]))
+    _native.chunk_mean_batched(tasks)
+    if tight:
+        host.copy_(d_out, non_blocking=True)
+    else:
+        for k, o, h in zip(sizes, out_off, host_off):
+            if k:
+                host[h:h + k].copy_(d_out[o:o + k], non_blocking=True)
+    torch.cuda.current_stream(dev).synchronize()

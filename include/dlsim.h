@@ -262,6 +262,30 @@ int dlsim_host_wreduce(int n, int t, const void* const* h_srcs, const size_t* nu
                        void* stream, void* h2d_stream, void* d2h_stream);
 
 /*
+ * dlsim_host_chunk_mean — dlsim_chunk_mean_batched for *host* chunks (the
+ * reference's case: ChunkManager.reconstruct_model over chunks received from
+ * peers, chunk_manager.py:38-40), staged and pipelined like
+ * dlsim_host_wreduce.
+ *   h_inputs       the host chunks, task by task (fan_in[t] each, n_elems[t]
+ *                  elements; contiguous, any alignment)
+ *   h_staging,     page-locked host / device staging of staging_elems
+ *   d_staging      elements, 16-B aligned; the library puts input row r at a
+ *                  256-B aligned offset, so staging_elems must be at least
+ *                  sum_t fan_in[t] * round_up(n_elems[t], 256 / sizeof(elem))
+ *   d_outs[t]      device mean of task t (16-B aligned for the vector path)
+ *   h_outs         NULL, or per task a page-locked host destination (or NULL)
+ * Rows are packed on `threads` host threads; each row goes H2D as soon as it
+ * is packed, each task's mean runs on `stream` once its rows are on the
+ * device (in PyTorch's CPU order at cpu_threads, as dlsim_chunk_mean_batched),
+ * and its result goes back on d2h_stream. Returns after packing and
+ * queueing; `stream` is ordered after everything.
+ */
+int dlsim_host_chunk_mean(int b, const int* fan_in, const void* const* h_inputs, const size_t* n_elems,
+                          void* h_staging, void* d_staging, size_t staging_elems, void* const* d_outs,
+                          void* const* h_outs, int dtype, int cpu_threads, int threads, void* stream,
+                          void* h2d_stream, void* d2h_stream);
+
+/*
  * dlsim_shard_range — parameter-axis partition used by the sharded path.
  *
  * Splits [0, n_elems) into `world` contiguous slices whose boundaries are

@@ -119,3 +119,25 @@ def test_host_wreduce_argument_errors_need_no_gpu():
     assert _host_call([10], staging=4100) == -1
     assert _host_call([10], srcs=[64, 0]) == -1 and b"null source" in lib.dlsim_last_error()
     assert _host_call([10], out=0) == -1
+
+
+def test_host_chunk_mean_argument_errors_need_no_gpu():
+    lib = _native.load()
+
+    def call(fan, numels, staging_elems=1 << 20, dtype=0, cpu_threads=4, staging=4096, outs=None):
+        b = len(fan)
+        ins = (ctypes.c_void_p * max(sum(fan), 1))(*([64] * max(sum(fan), 1)))
+        outs = outs if outs is not None else [128] * b
+        return lib.dlsim_host_chunk_mean(b, (ctypes.c_int * b)(*fan), ins, (ctypes.c_size_t * b)(*numels),
+                                         staging, 8192, staging_elems, (ctypes.c_void_p * b)(*outs), None,
+                                         dtype, cpu_threads, 4, None, None, None)
+    assert call([], []) == 0
+    assert call([2], [0]) == 0  # nothing to stage
+    assert call([2], [10], dtype=9) == -2
+    assert call([2], [10], cpu_threads=0) == -1
+    assert call([0], [10]) == -1 and b"fan-in" in lib.dlsim_last_error()
+    assert call([2, 3], [100, 7], staging_elems=100) == -1 and b"needed" in lib.dlsim_last_error()
+    assert _native.staged_rows_elems([100, 7], [2, 3], 4) == 2 * 128 + 3 * 64
+    assert call([2, 3], [100, 7], staging_elems=2 * 128 + 3 * 64 - 1) == -1
+    assert call([2], [10], staging=4100) == -1 and b"aligned" in lib.dlsim_last_error()
+    assert call([2], [10], outs=[0]) == -1 and b"null output" in lib.dlsim_last_error()

@@ -233,3 +233,56 @@ def test_chunk_mean_errors():
         _native.chunk_mean_batched([([], x)])
     with pytest.raises(RuntimeError, match="cpu_threads"):
         _native.chunk_mean_batched([([x], torch.empty(8, device=dev()))], threads=0)
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16"])
+@pytest.mark.parametrize("threads,cpu_threads,side", [(1, 1, False), (4, 4, True), (8, 8, True), (3, 16, False)])
+def test_host_chunk_mean_matches_torch_order(dtype, threads, cpu_threads, side):
+    """dlsim_host_chunk_mean (host chunks packed on `threads` library threads,
+    per-row H2D, per-task mean and D2H): every task bit-identical to the
+    order-exact oracle at cpu_threads, including empty tasks, one-element
+    chunks, fan-in 1 and 40, host inputs at odd offsets, with and without the
+    side copy streams."""
+    from dasklearn_amd.arena import _side_streams
+    rng = np.random.default_rng(threads * 100 + cpu_threads)
+    tasks, exp, hosts = [], [], []
+    for m, n in [(4, 300_001), (1, 7), (40, 4099), (3, 0), (17, 1), (2, 65), (9, 1_000_003), (5, 33)]:
+        x = (rng.standard_normal((m, n)) * 0.1).astype(np.float32)
+        rows = orc.f32_to_bf16_bits(x) if dtype == "bf16" else orc.f32_to_f16_bits(x) if dtype == "f16" else x
+        ts = []
+        for i, r in enumerate(rows):
+            if dtype == "f32":
+                h = torch.from_numpy(r.copy())
+            else:
+                h = torch.from_numpy(r.view(np.int16).copy()).view(torch.bfloat16 if dtype == "bf16" else torch.float16)
+            if i % 2:  # an odd offset into a larger host buffer
+                buf = torch.empty(n + 1, dtype=h.dtype)
+                buf[1:].copy_(h)
+                h = buf[1:]
+            ts.append(h)
+        out = torch.empty(n + 64, dtype=ts[0].dtype, device=dev())[:n]
+        tasks.append((ts, out))
+        hosts.append(torch.empty(n, dtype=ts[0].dtype, pin_memory=True))
+        exp.append(orc.chunk_mean(list(rows), dtype, cpu_threads) if n else None)
+    esz = tasks[0][1].element_size()
+    need = _native.staged_rows_elems([t[1].numel() for t in tasks], [len(t[0]) for t in tasks], esz)
+    stage = torch.empty(need, dtype=tasks[0][1].dtype, pin_memory=True)
+    d_in = torch.empty(need, dtype=tasks[0][1].dtype, device=dev())
+    h2d, d2h = _side_streams(dev()) if side else (None, None)
+    stream = torch.cuda.current_stream(dev())
+    _native.host_chunk_mean(tasks, stage, d_in, host_outs=hosts, threads=threads, cpu_threads=cpu_threads,
+                            stream=stream, h2d_stream=h2d, d2h_stream=d2h)
+    stream.synchronize()
+    for (ts, out), h, e in zip(tasks, hosts, exp):
+        if e is None:
+            continue
+        assert orc.same_bits(_bits(out), e), (len(ts), out.numel())
+        assert orc.same_bits(_bits(h), e), (len(ts), out.numel())
+
+
+def test_host_chunk_mean_rejects_small_staging():
+    x = [torch.zeros(100), torch.zeros(100)]
+    out = torch.empty(100, device=dev())
+    stage = torch.empty(64, pin_memory=True)
+    with pytest.raises(ValueError):
+        _native.host_chunk_mean([(x, out)], stage, torch.empty(64, device=dev()))
