@@ -9,6 +9,9 @@ shapes, dtypes, alignments, weights and special values, for a time budget.
               parameters, buffers, host or device) vs the oracle per dtype group
   reconstruct ChunkManager.reconstruct_model on random models and chunkings vs
               the reference's own arithmetic (torch.mean of torch.stack on the CPU)
+  host_reduce dlsim_host_wreduce (random host tensors at odd offsets, pipeline
+              chunks, pack threads, side streams or not) vs the oracle
+  host_chunk  dlsim_host_chunk_mean (random tasks, threads) vs PyTorch's CPU order
 
 Prints one JSON line with the case counts and the first failures (if any).
 
@@ -61,6 +64,20 @@ def to_dev(rows, dtype, offset):
         buf = torch.empty(h.numel() + offset, dtype=h.dtype, device="cuda")
         buf[offset:].copy_(h)
         out.append(buf[offset:])
+    return out
+
+
+def to_host(rows, dtype):
+    """Host tensors of the rows, every other one at an odd element offset."""
+    out = []
+    for i, r in enumerate(rows):
+        h = torch.from_numpy(np.ascontiguousarray(r).view(np.int16).copy()).view(DT[dtype]) if dtype != "f32" \
+            else torch.from_numpy(np.ascontiguousarray(r).copy())
+        if i % 2:
+            buf = torch.empty(h.numel() + 1, dtype=h.dtype)
+            buf[1:].copy_(h)
+            h = buf[1:]
+        out.append(h)
     return out
 
 
@@ -128,7 +145,7 @@ def main():
     a = ap.parse_args()
     rng = np.random.default_rng(a.seed)
     counts = {"reduce": 0, "reduce_fast": 0, "tensors": 0, "batched": 0, "chunk_mean": 0, "modules": 0,
-              "reconstruct": 0}
+              "reconstruct": 0, "host_reduce": 0, "host_chunk": 0}
     fails = []
     t_end = time.time() + a.seconds
     t_note = time.time() + 20
@@ -137,8 +154,9 @@ def main():
             print(json.dumps({"progress": counts, "failures": len(fails)}), file=sys.stderr, flush=True)
             t_note = time.time() + 20
         dtype = rng.choice(["f32", "bf16", "f16"])
-        which = rng.choice(["reduce", "tensors", "batched", "chunk_mean", "modules", "reconstruct"],
-                           p=[0.3, 0.1, 0.15, 0.25, 0.1, 0.1])
+        which = rng.choice(["reduce", "tensors", "batched", "chunk_mean", "modules", "reconstruct",
+                            "host_reduce", "host_chunk"],
+                           p=[0.25, 0.1, 0.1, 0.2, 0.1, 0.1, 0.1, 0.05])
         try:
             if which == "reduce":
                 n = int(rng.choice([1, 2, 3, 5, 8, 9, 14, 15, 16, 17, 33, 128, 129, 200]))
@@ -253,6 +271,67 @@ def main():
                 ok = orc.same_bits(got.numpy(), expect.numpy())
                 counts["reconstruct"] += 1
                 case = dict(kind="reconstruct", k=k, peers=n_peers, threads=threads, device=on_dev)
+            elif which == "host_reduce":
+                from dasklearn_amd.arena import _side_streams
+                n = int(rng.choice([1, 2, 3, 8, 9, 17]))
+                sizes = [int(s) for s in rng.integers(0, int(rng.choice([10, 5000, 200_000])),
+                                                     size=int(rng.integers(1, 30)))]
+                p = sum(sizes)
+                rows = rand_values(rng, n, p, dtype)
+                offs = np.cumsum([0] + sizes[:-1])
+                by_model = [[t[o:o + s].clone() for o, s in zip(offs, sizes)] for t in
+                            [torch.from_numpy(np.ascontiguousarray(r).view(np.int16).copy()).view(DT[dtype])
+                             if dtype != "f32" else torch.from_numpy(np.ascontiguousarray(r).copy()) for r in rows]]
+                for i, ts in enumerate(by_model):  # odd host offsets
+                    if i % 2:
+                        by_model[i] = [torch.cat([t.new_zeros(1), t])[1:] for t in ts]
+                stride = (p + 63) // 64 * 64 + 64
+                stage = torch.empty((n, stride), dtype=DT[dtype], pin_memory=True)
+                d_rows = torch.empty((n, stride), dtype=DT[dtype], device="cuda")
+                out = torch.empty(max(p, 1), dtype=DT[dtype], device="cuda")[:p]
+                host = torch.empty(p, dtype=DT[dtype], pin_memory=True) if rng.random() < 0.7 else None
+                chunk = int(rng.choice([0, 1024, 5000, 65536]))
+                threads = int(rng.choice([1, 2, 4, 8]))
+                side = bool(rng.random() < 0.5)
+                h2d, d2h = _side_streams(torch.device("cuda", 0)) if side else (None, None)
+                w = rand_weights(rng, n)
+                _native.host_wreduce(by_model, w, stage, d_rows, out, host, _native.DLSIM_EXACT, chunk, threads,
+                                     None, h2d, d2h)
+                torch.cuda.current_stream().synchronize()
+                exp = orc.wreduce(list(rows), w, dtype)
+                ok = p == 0 or orc.same_bits(bits(out), exp)
+                ok = ok and (host is None or p == 0 or orc.same_bits(bits(host), exp))
+                counts["host_reduce"] += 1
+                case = dict(kind="host_reduce", dtype=dtype, n=n, p=p, tensors=len(sizes), chunk=chunk,
+                            threads=threads, side=side)
+            elif which == "host_chunk":
+                from dasklearn_amd.arena import _side_streams
+                cpu_threads = int(rng.choice([1, 2, 4, 8, 16]))
+                tasks, exps, hosts = [], [], []
+                for _ in range(int(rng.integers(1, 16))):
+                    m = int(rng.choice([1, 2, 3, 4, 9, 16, 17, 33, 100]))
+                    n = int(rng.choice([0, 1, 2, 7, 8, 33, 1000, 8193, 100_003]))
+                    if m * n > 1_000_000:
+                        n = int(rng.choice([1, 7, 33, 1000]))
+                    rows = rand_values(rng, m, n, dtype)
+                    tasks.append((to_host(rows, dtype), torch.empty(n + 8, dtype=DT[dtype], device="cuda")[:n]))
+                    hosts.append(torch.empty(n, dtype=DT[dtype], pin_memory=True))
+                    exps.append(orc.chunk_mean(list(rows), dtype, cpu_threads) if n else None)
+                esz = tasks[0][1].element_size()
+                need = _native.staged_rows_elems([t[1].numel() for t in tasks], [len(t[0]) for t in tasks], esz)
+                stage = torch.empty(max(need, 1), dtype=DT[dtype], pin_memory=True)
+                d_in = torch.empty(max(need, 1), dtype=DT[dtype], device="cuda")
+                side = bool(rng.random() < 0.5)
+                h2d, d2h = _side_streams(torch.device("cuda", 0)) if side else (None, None)
+                threads = int(rng.choice([1, 2, 4, 8]))
+                _native.host_chunk_mean(tasks, stage, d_in, host_outs=hosts, threads=threads,
+                                        cpu_threads=cpu_threads, h2d_stream=h2d, d2h_stream=d2h)
+                torch.cuda.current_stream().synchronize()
+                ok = all(e is None or (orc.same_bits(bits(t[1]), e) and orc.same_bits(bits(h), e))
+                         for t, h, e in zip(tasks, hosts, exps))
+                counts["host_chunk"] += 1
+                case = dict(kind="host_chunk", dtype=dtype, tasks=len(tasks), threads=threads,
+                            cpu_threads=cpu_threads, side=side)
             else:
                 threads = int(rng.choice([1, 2, 4, 8, 16]))
                 tasks, exps = [], []
