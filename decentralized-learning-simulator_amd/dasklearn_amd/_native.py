@@ -412,13 +412,14 @@ def host_chunk_mean(tasks, staging, d_staging, host_outs=None, threads=None, cpu
         numels.append(out.numel())
     need = staged_rows_elems(numels, fan, out0.element_size())
     if staging.numel() < need or d_staging.numel() < need or staging.dtype != dt or d_staging.dtype != dt \
-            or staging.is_cuda or not d_staging.is_cuda:
+            or staging.is_cuda or not d_staging.is_cuda or not staging.is_contiguous() \
+            or not d_staging.is_contiguous():
         raise ValueError(f"staging: a pinned host and a device buffer of >= {need} elements of the dtype")
     hptrs = None
     if host_outs is not None:
         hp = []
         for h, (_, out) in zip(host_outs, tasks):
-            if h is not None and (h.is_cuda or h.dtype != dt or h.numel() != out.numel()):
+            if h is not None and (h.is_cuda or h.dtype != dt or h.numel() != out.numel() or not h.is_contiguous()):
                 raise ValueError("host_outs: host tensors of the outputs' dtype and size")
             hp.append(None if h is None else h.data_ptr())
         hptrs = (ctypes.c_void_p * b)(*hp)
@@ -552,10 +553,13 @@ def host_wreduce(inputs_by_model, weights_f32, staging, rows, out, host_out=None
     total = sum(numels)
     if out.numel() != total or not out.is_cuda or not out.is_contiguous():
         raise ValueError("out must be a contiguous device tensor of the models' size")
-    if staging.shape[0] < n or rows.shape[0] < n or staging.stride(0) != rows.stride(0) \
+    if staging.dim() != 2 or rows.dim() != 2 or staging.shape[0] < n or rows.shape[0] < n \
+            or staging.stride(0) != rows.stride(0) or staging.stride(1) != 1 or rows.stride(1) != 1 \
+            or staging.is_cuda or not rows.is_cuda \
             or staging.dtype != dt or rows.dtype != dt or rows.device != out.device:
         raise ValueError("staging/rows: [n, >= total] buffers of the output's dtype, equal strides")
-    if host_out is not None and (host_out.numel() != total or host_out.dtype != dt or host_out.is_cuda):
+    if host_out is not None and (host_out.numel() != total or host_out.dtype != dt or host_out.is_cuda
+                                 or not host_out.is_contiguous()):
         raise ValueError("host_out must be a host tensor of the output's size and dtype")
     w = np.ascontiguousarray(weights_f32, dtype=np.float32)
     if w.size != n:
