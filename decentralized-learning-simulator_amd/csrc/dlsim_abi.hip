@@ -1052,6 +1052,26 @@ int dlsim_host_chunk_mean(int b, const int* fan_in, const void* const* h_inputs,
   return ln.rc;
 }
 
+int dlsim_host_pack(int t, const void* const* h_srcs, const size_t* nbytes, const size_t* dst_off, void* h_dst,
+                    int threads) {
+  g_err.clear();
+  if (t < 0) return fail(DLSIM_E_ARG, "t must be >= 0 (got %d)", t);
+  if (t == 0) return DLSIM_OK;
+  if (!h_srcs || !nbytes || !dst_off || !h_dst) return fail(DLSIM_E_ARG, "null argument");
+  dlsim::PackJob job;
+  size_t total = 0;
+  char* dst = static_cast<char*>(h_dst);
+  for (int j = 0; j < t; ++j) {
+    if (nbytes[j] == 0) continue;
+    if (!h_srcs[j]) return fail(DLSIM_E_ARG, "null source pointer at index %d", j);
+    job.add(0, static_cast<const char*>(h_srcs[j]), dst + dst_off[j], nbytes[j]);
+    total += nbytes[j];
+  }
+  job.seal(1);
+  pack_and_dispatch(job, threads, total, [](size_t) {});
+  return DLSIM_OK;
+}
+
 int dlsim_shard_range(size_t n_elems, int world, int rank, size_t align_elems, size_t* begin,
                       size_t* end) {
   g_err.clear();

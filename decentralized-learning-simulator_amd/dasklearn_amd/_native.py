@@ -39,6 +39,7 @@ EXPORTS = (
     "dlsim_wreduce_sharded",
     "dlsim_host_wreduce",
     "dlsim_host_chunk_mean",
+    "dlsim_host_pack",
     "dlsim_shard_range",
     "dlsim_probe_copy",
     "dlsim_last_error",
@@ -113,6 +114,8 @@ def load() -> ctypes.CDLL:
         lib.dlsim_host_chunk_mean.argtypes = [i, ctypes.POINTER(i), ctypes.POINTER(vp), ctypes.POINTER(sz), vp, vp,
                                               sz, ctypes.POINTER(vp), ctypes.POINTER(vp), i, i, i, vp, vp, vp]
         lib.dlsim_host_chunk_mean.restype = i
+        lib.dlsim_host_pack.argtypes = [i, ctypes.POINTER(vp), ctypes.POINTER(sz), ctypes.POINTER(sz), vp, i]
+        lib.dlsim_host_pack.restype = i
         lib.dlsim_shard_range.argtypes = [sz, i, i, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)]
         lib.dlsim_shard_range.restype = i
         lib.dlsim_probe_copy.argtypes = [vp, vp, sz, vp]
@@ -574,6 +577,30 @@ def host_wreduce(inputs_by_model, weights_f32, staging, rows, out, host_out=None
         None if d2h_stream is None else d2h_stream.cuda_stream)
     _check("dlsim_host_wreduce", rc)
     return out
+
+
+def host_pack(srcs, dst_offsets, dst, threads: Optional[int] = None):
+    """dlsim_host_pack: copy host tensors srcs[j] (contiguous) into the host
+    tensor `dst` at byte offsets dst_offsets[j], on the library's threads."""
+    import torch
+    if dst.is_cuda or not dst.is_contiguous():
+        raise ValueError("dst must be a contiguous host tensor")
+    cap = dst.numel() * dst.element_size()
+    ptrs, nb = [], []
+    for x, o in zip(srcs, dst_offsets):
+        if x.get_device() != -1 or not x.is_contiguous():
+            raise ValueError("sources must be contiguous host tensors")
+        b = x.numel() * x.element_size()
+        if o < 0 or o + b > cap:
+            raise ValueError("source does not fit dst at its offset")
+        ptrs.append(x.data_ptr())
+        nb.append(b)
+    t = len(ptrs)
+    _check("dlsim_host_pack",
+           load().dlsim_host_pack(t, (ctypes.c_void_p * max(t, 1))(*ptrs), (ctypes.c_size_t * max(t, 1))(*nb),
+                                  (ctypes.c_size_t * max(t, 1))(*dst_offsets), dst.data_ptr(),
+                                  int(torch.get_num_threads() if threads is None else threads)))
+    return dst
 
 
 def probe_copy(src, dst, stream=None) -> None:

@@ -85,6 +85,17 @@ class RoundExecutor:
             return {k: self._resolve(x) for k, x in v.items()}
         return v
 
+    def _layout_for(self, m: nn.Module) -> ParamLayout:
+        """m's ParamLayout; a model of a class seen before reuses that layout
+        when the parameter signature matches (no per-model ParamLayout build)."""
+        known = self._layouts.get(type(m))
+        ps = module_params(m)
+        if known is not None and _same_signature(ps, known._signature):
+            return known.rebind(ps)
+        layout = ParamLayout(m)
+        self._layouts[type(m)] = layout
+        return layout
+
     def _arena_of(self, m: nn.Module, cache: dict):
         """(layout over m's parameters, {dtype: flat device arena}) for one
         model, once per wave (`cache` keeps the model alive, so its id cannot
@@ -97,15 +108,7 @@ class RoundExecutor:
             layout, ar = reg
             views = {dt: [ar[dt]] for dt in layout.groups}
         else:
-            # a model of a class seen before reuses that layout when the
-            # parameter signature matches (no per-model ParamLayout build)
-            known = self._layouts.get(type(m))
-            ps = module_params(m)
-            if known is not None and _same_signature(ps, known._signature):
-                layout = known.rebind(ps)
-            else:
-                layout = ParamLayout(m)
-                self._layouts[type(m)] = layout
+            layout = self._layout_for(m)
             views = {dt: None if (v := layout.arena_view(layout.params, dt)) is None else [v]
                      for dt in layout.groups}
         params = [layout.params]
@@ -120,13 +123,56 @@ class RoundExecutor:
         cache[id(m)] = (m, layout, arenas)
         return layout, arenas
 
+    def _upload_host_models(self, models, cache: dict) -> None:
+        """Every host model of a wave (the reference's CPU-trained models) to
+        one device buffer: the library's threads pack all their parameters
+        into one pinned buffer (dlsim_host_pack; one arena per model and
+        dtype at 256-B aligned offsets), then one H2D. Fills `cache` as
+        _arena_of would (instead of one small H2D per parameter tensor)."""
+        pending, seen = [], set()
+        for m in models:
+            if id(m) in seen or (id(m) in cache and cache[id(m)][0] is m) or registered_arenas(m) is not None:
+                continue
+            seen.add(id(m))
+            ps = module_params(m)
+            if not ps or any(p.get_device() != -1 for p in ps):
+                continue
+            pending.append((m, self._layout_for(m)))
+        if not pending:
+            return
+        dev = _target_device(pending[0][1].params, self.device)
+        srcs, offs, spans, off = [], [], [], 0
+        for m, layout in pending:
+            span = {}
+            for dt, idx in layout.groups.items():
+                esz = layout.params[idx[0]].element_size()
+                span[dt] = (off, layout.totals[dt], esz)
+                for k in idx:
+                    p = layout.params[k]
+                    srcs.append(p.detach() if p.is_contiguous() else p.detach().contiguous())
+                    offs.append(off)
+                    off += p.numel() * esz
+                off = (off + 255) // 256 * 256
+            spans.append(span)
+        stage = torch.empty(max(off, 1), dtype=torch.uint8, pin_memory=True)
+        _native.host_pack(srcs, offs, stage)
+        buf = torch.empty(max(off, 1), dtype=torch.uint8, device=dev)
+        buf.copy_(stage, non_blocking=True)  # torch keeps `stage` until the copy is done
+        for (m, layout), span in zip(pending, spans):
+            arenas = {dt: buf[o:o + n * esz].view(dt) for dt, (o, n, esz) in span.items()}
+            cache[id(m)] = (m, layout, arenas)
+
     def _aggregate_wave(self, aggs) -> List[nn.Module]:
         cache: dict = {}
         prepared = []
+        resolved = []
         for name, _, data in aggs:
             d = self._resolve(data)
             models = d["models"]
             w32 = _resolve(models, d.get("weights"))  # fedavg.py:14-17 rules and exceptions
+            resolved.append((models, w32))
+        self._upload_host_models([m for models, _ in resolved for m in models], cache)
+        for models, w32 in resolved:
             ents = [self._arena_of(m, cache) for m in models]
             layout0 = ents[0][0]
             sig = layout0._signature

@@ -21,7 +21,9 @@
  *     return; nothing synchronises the device.
  *   - Return value: 0 on success, a negative DLSIM_E* code otherwise;
  *     dlsim_last_error() gives a message (thread-local).
- *   - No global state besides a per-thread error string.
+ *   - No global state besides a per-thread error string and the host pack
+ *     thread pool of the host entry points (created on first use, idle
+ *     between calls).
  */
 #ifndef DLSIM_H_
 #define DLSIM_H_
@@ -284,6 +286,17 @@ int dlsim_host_chunk_mean(int b, const int* fan_in, const void* const* h_inputs,
                           void* h_staging, void* d_staging, size_t staging_elems, void* const* d_outs,
                           void* const* h_outs, int dtype, int cpu_threads, int threads, void* stream,
                           void* h2d_stream, void* d2h_stream);
+
+/*
+ * dlsim_host_pack — host-only gather: copy t host buffers (h_srcs[j],
+ * nbytes[j] bytes) to h_dst + dst_off[j] on `threads` host threads (the
+ * caller's included), with the pack of dlsim_host_wreduce (streaming stores).
+ * Synchronous; no GPU call. Used to stage many host models for one H2D (the
+ * round executor's upload of a wave's host-trained models; worker.py:24 ->
+ * functions.py:89-106 receive them as CPU modules).
+ */
+int dlsim_host_pack(int t, const void* const* h_srcs, const size_t* nbytes, const size_t* dst_off, void* h_dst,
+                    int threads);
 
 /*
  * dlsim_shard_range — parameter-axis partition used by the sharded path.

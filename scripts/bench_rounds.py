@@ -11,9 +11,12 @@ Three ways of running the same aggregate tasks:
   cpu_ref     the reference's FedAvg.aggregate op sequence (oracle restatement)
               per task on host models at the worker's 4 threads (broker.py:31)
 The train task is a synthetic device-side perturbation (the real one needs
-network datasets; out of scope) and is not counted.
+network datasets; out of scope) and is not counted. With --host it returns a
+host model instead (the reference's CPU training, model_trainer.py:129), so
+every aggregate reads host models: the executor uploads each wave's models
+once, the sequential worker loop stages them per task.
 
-    python scripts/bench_rounds.py [--peers 100] [--rounds 4]
+    python scripts/bench_rounds.py [--peers 100] [--rounds 4] [--host]
 """
 from __future__ import annotations
 
@@ -84,6 +87,14 @@ def train(settings, params):
     return [out]
 
 
+def train_host(settings, params):
+    out = copy.deepcopy(params["model"]).cpu()
+    with torch.no_grad():
+        for p in out.parameters():
+            p.add_(1e-3 * (params["peer"] + 1))
+    return [out]
+
+
 def resolve(results, v):
     if isinstance(v, tuple) and len(v) == 2 and isinstance(v[0], str):
         return results[v[0]][v[1]]
@@ -92,8 +103,9 @@ def resolve(results, v):
     return v
 
 
-def sequential(tasks, agg_fn, init, sync):
+def sequential(tasks, agg_fn, init, sync, train_fn=None):
     """The worker's one-task-at-a-time loop; only aggregate calls are timed."""
+    train_fn = train_fn or train
     results = {"init": [init]}
     t_agg, n_agg = 0.0, 0
     for name, f, data in tasks:
@@ -106,7 +118,7 @@ def sequential(tasks, agg_fn, init, sync):
             t_agg += time.perf_counter() - t0
             n_agg += 1
         else:
-            results[name] = train(Settings(), d)
+            results[name] = train_fn(Settings(), d)
     return t_agg, n_agg
 
 
@@ -115,6 +127,7 @@ def main():
     ap.add_argument("--peers", type=int, default=100)
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--cpu-rounds", type=int, default=2)
+    ap.add_argument("--host", action="store_true", help="train returns host models (CPU training)")
     ap.add_argument("--profile", default=None, help="cProfile the batched run into this file")
     ap.add_argument("--profile-seq", default=None, help="cProfile the sequential run into this file")
     a = ap.parse_args()
@@ -131,35 +144,38 @@ def main():
     task_bytes = (fan + 1) * p * 4
     sync = torch.cuda.synchronize
 
-    # warm-up (library load, allocator, kernels)
-    wt, _ = dag(min(a.peers, 8), 1)
-    RoundExecutor({"train": train}, Settings()).run(wt, seed={"init": [init_d]})
-    sequential(wt, aggregate, init_d, sync)
+    tr = train_host if a.host else train
+    init_x = init_h if a.host else init_d
+    # warm-up at full size (library load, kernels, and the device and pinned
+    # allocator caches for a wave's buffers, so the timed rounds are steady state)
+    wt, _ = dag(a.peers, 1)
+    RoundExecutor({"train": tr}, Settings(), device=dev).run(wt, seed={"init": [init_x]})
+    sequential(wt, aggregate, init_x, sync, tr)
 
-    ex = RoundExecutor({"train": train}, Settings(), timing=True)
+    ex = RoundExecutor({"train": tr}, Settings(), device=dev, timing=True)
     if a.profile:
         import cProfile
         import pstats
         prof = cProfile.Profile()
         prof.enable()
-        ex.run(tasks, seed={"init": [init_d]})
+        ex.run(tasks, seed={"init": [init_x]})
         prof.disable()
         with open(a.profile, "w") as f:
             pstats.Stats(prof, stream=f).sort_stats("tottime").print_stats(45)
     else:
-        ex.run(tasks, seed={"init": [init_d]})
+        ex.run(tasks, seed={"init": [init_x]})
     bt, bn = ex.stats["aggregate"], ex.stats["aggregate_tasks"]
     if a.profile_seq:
         import cProfile
         import pstats
         prof = cProfile.Profile()
         prof.enable()
-        st, sn = sequential(tasks, aggregate, init_d, sync)
+        st, sn = sequential(tasks, aggregate, init_x, sync, tr)
         prof.disable()
         with open(a.profile_seq, "w") as f:
             pstats.Stats(prof, stream=f).sort_stats("tottime").print_stats(45)
     else:
-        st, sn = sequential(tasks, aggregate, init_d, sync)
+        st, sn = sequential(tasks, aggregate, init_x, sync, tr)
 
     def cpu_agg(settings, d):
         return [fedavg_torch.aggregate_modules(d["models"], d.get("weights"))]
@@ -169,7 +185,7 @@ def main():
     ct, cn = sequential(ctasks, cpu_agg, init_h, lambda: None)
 
     def line(kind, t, n):
-        return {"kind": kind, "peers": a.peers, "fan_in": fan, "tasks": n, "params": p,
+        return {"kind": kind + ("_host_models" if a.host and not kind.startswith("cpu") else ""), "peers": a.peers, "fan_in": fan, "tasks": n, "params": p,
                 "ms_per_round": round(t / n * a.peers * 1e3, 3), "us_per_task": round(t / n * 1e6, 1),
                 "GBps_algorithmic": round(task_bytes * n / t / 1e9, 2)}
 

@@ -54,3 +54,44 @@ def test_round_executor_reports_unresolvable_inputs():
     ex = RoundExecutor({}, Settings())
     with pytest.raises(RuntimeError, match="unresolvable"):
         ex.run([("agg_0", "aggregate", {"models": [("missing", 0)], "round": 1, "peer": 0})])
+
+
+def host_train(settings, params):
+    """device_agnostic_train that always returns a host model (the reference's
+    CPU training): every wave's aggregates read host models."""
+    return [device_agnostic_train(settings, {**params, "model": params["model"].cpu()})[0].cpu()]
+
+
+class MixedShaped(torch.nn.Module):
+    """GNLeNet shapes with some tensors in bf16 and fp16 (three dtype groups)."""
+
+    def __init__(self):
+        super().__init__()
+        dts = [torch.float32, torch.bfloat16, torch.float16]
+        self.ps = torch.nn.ParameterList([torch.nn.Parameter(torch.randn(*s).to(dts[i % 3]) * 0.05)
+                                          for i, s in enumerate(GNLENET)])
+
+
+@pytest.mark.parametrize("mixed", [False, True])
+def test_round_executor_host_trained_models(mixed):
+    """Host models in every wave go to the device in one dlsim_host_pack + H2D
+    per wave (one arena per model and dtype): bit-identical to the sequential
+    oracle replay, for one and for three dtype groups."""
+    from dasklearn_amd.arena import module_params
+    torch.manual_seed(23)
+    init = MixedShaped() if mixed else Shaped(GNLENET)
+    tasks, nb = build_dag(6, 2)
+    ex = RoundExecutor({"train": host_train}, Settings())
+    got = ex.run(tasks, seed={"init": [init]})
+    exp = replay(tasks, {"aggregate": oracle_aggregate, "train": host_train}, init)
+    for p in range(6):
+        a = got[f"agg_{p}_2"][0]
+        b = exp[f"agg_{p}_2"][0]
+        assert all(q.is_cuda for q in a.parameters())
+        for dt in (torch.float32, torch.bfloat16, torch.float16):
+            ga = [q.detach().reshape(-1).cpu() for q in module_params(a) if q.dtype == dt]
+            gb = [q.detach().reshape(-1).cpu() for q in module_params(b) if q.dtype == dt]
+            if ga:
+                x, y = torch.cat(ga), torch.cat(gb)
+                assert torch.equal(x.view(torch.int16) if x.element_size() == 2 else x.view(torch.int32),
+                                   y.view(torch.int16) if y.element_size() == 2 else y.view(torch.int32)), (p, dt)
