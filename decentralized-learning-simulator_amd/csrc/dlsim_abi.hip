@@ -1,6 +1,7 @@
 // dlsim_abi.hip — the C ABI of include/dlsim.h over the gfx950 kernels of
 // wreduce_kernels.hpp. Host-side dispatch only: argument checks, choice of
-// vector vs scalar kernel, kernarg packing, multi-pass for n > 128.
+// vector vs scalar kernel, launch shape, kernarg or device-table fan-in, batching
+// and its hazard checks, host staging pipelines.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
@@ -12,6 +13,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "dlsim.h"
@@ -66,49 +68,63 @@ template <class Op> constexpr int max_fixed_fan_in() { return Op::kBytes == 4 ? 
 template <class Op> constexpr int group_size() { return Op::kBytes == 4 ? 8 : 4; }
 
 // Launch shape of the fixed fan-in kernels, chosen by the per-stream size
-// (size sweep: profiles/r01_tune_shape_sweep.log, arena rows as in bench.py):
-//   fp32  < 5 M elements   : block map, sc1 stores   (1-4% over the wave map at 1-4 M)
-//   fp32 >= 5 M            : wave map,  sc1 stores   (~1% at 6-11 M)
-//   bf16  < 48 M elements  : VPT 1, wave map, sc1    (+7-12% at 4-33 M for n = 2)
-//   bf16 >= 48 M           : VPT 4, block map, nt    (+1.5-2.5% at 64-125 M)
+// class (size sweeps with arena rows as in bench.py and >= 1 GiB of rotating
+// inputs: profiles/r01_tune_shape_sweep.log, profiles/r02_tune_slices/):
+//   fp32  < 2 M elements   : VPT 2, block map, sc1 (+7% at the 8-rank slice
+//                            of the north star, 1.4 M: 9.85 vs 10.57 us)
+//   fp32  2 M .. 5 M       : VPT 4, block map, sc1 (1-4% over the wave map)
+//   fp32 >= 5 M            : VPT 4, wave map,  sc1 (~1% at 6-11 M)
+//   bf16  < 48 M elements  : VPT 1, wave map, sc1  (+7-12% at 4-33 M for n = 2)
+//   bf16 >= 48 M           : VPT 4, block map, nt  (+1.5-2.5% at 64-125 M)
 struct Shape {
   int vpt;
   int store;
   bool wave;
 };
-template <class Op, bool Small> constexpr Shape fixed_shape() {
-  if constexpr (Op::kBytes == 4) return Small ? Shape{4, kStore, false} : Shape{4, kStore, true};
-  else return Small ? Shape{1, kStore, true} : Shape{4, dlsim::kStNT, false};
+template <class Op, int C> constexpr Shape fixed_shape() {
+  if constexpr (Op::kBytes == 4) {
+    if constexpr (C == 0) return Shape{2, kStore, false};
+    else if constexpr (C == 1) return Shape{4, kStore, false};
+    else return Shape{4, kStore, true};
+  } else {
+    if constexpr (C < 2) return Shape{1, kStore, true};
+    else return Shape{4, dlsim::kStNT, false};
+  }
 }
-template <class Op> constexpr size_t small_shape_below() { return Op::kBytes == 4 ? 5000000 : 48000000; }
+template <class Op> int size_class(size_t nelem) {
+  if constexpr (Op::kBytes == 4) return nelem < 2000000 ? 0 : nelem < 5000000 ? 1 : 2;
+  else return nelem < 48000000 ? 0 : 2;
+}
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
-template <class Op, int NB, int NF, int VPT, int STP, bool WAVE>
-hipError_t launch_shape(const dlsim::Slots<NB>& s, int n, const void* acc_in, void* out, size_t nelem,
-                        hipStream_t st) {
+template <class Op, class S, int NF, int VPT, int STP, bool WAVE>
+hipError_t launch_shape(const S& s, int n, void* out, size_t nelem, hipStream_t st) {
   const size_t nvec = nelem / Op::E;
   const size_t tile = static_cast<size_t>(dlsim::kBlock) * VPT;
   const size_t blocks = nvec / tile + 1;  // full tiles + one block for the ragged end
   if (blocks > 0x7fffffffu) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((dlsim::k_wreduce_tiles<Op, NB, NF, group_size<Op>(), VPT, kNT, STP, WAVE>),
-                     dim3(static_cast<unsigned>(blocks)), dim3(dlsim::kBlock), 0, st, s, n, acc_in, out,
-                     nvec, nelem);
+  hipLaunchKernelGGL((dlsim::k_wreduce_tiles<Op, S, NF, group_size<Op>(), VPT, kNT, STP, WAVE>),
+                     dim3(static_cast<unsigned>(blocks)), dim3(dlsim::kBlock), 0, st, s, n, out, nvec, nelem);
   return hipGetLastError();
 }
 
-template <class Op, int NB, int NF>
-hipError_t launch_tiles(const dlsim::Slots<NB>& s, int n, const void* acc_in, void* out, size_t nelem,
-                        hipStream_t st) {
+template <class Op, class S, int NF, int C>
+hipError_t launch_class(const S& s, int n, void* out, size_t nelem, hipStream_t st) {
+  constexpr Shape k = fixed_shape<Op, C>();
+  return launch_shape<Op, S, NF, k.vpt, k.store, k.wave>(s, n, out, nelem, st);
+}
+
+template <class Op, class S, int NF>
+hipError_t launch_tiles(const S& s, int n, void* out, size_t nelem, hipStream_t st) {
   if constexpr (NF > 0) {
-    if (nelem < small_shape_below<Op>()) {
-      constexpr Shape k = fixed_shape<Op, true>();
-      return launch_shape<Op, NB, NF, k.vpt, k.store, k.wave>(s, n, acc_in, out, nelem, st);
+    switch (size_class<Op>(nelem)) {
+      case 0: return launch_class<Op, S, NF, 0>(s, n, out, nelem, st);
+      case 1: return launch_class<Op, S, NF, 1>(s, n, out, nelem, st);
+      default: return launch_class<Op, S, NF, 2>(s, n, out, nelem, st);
     }
-    constexpr Shape k = fixed_shape<Op, false>();
-    return launch_shape<Op, NB, NF, k.vpt, k.store, k.wave>(s, n, acc_in, out, nelem, st);
   } else {
-    return launch_shape<Op, NB, 0, kVpt, store_policy<Op>(), wave_map<Op>()>(s, n, acc_in, out, nelem, st);
+    return launch_shape<Op, S, 0, kVpt, store_policy<Op>(), wave_map<Op>()>(s, n, out, nelem, st);
   }
 }
 
@@ -117,53 +133,80 @@ hipError_t launch_fixed_k(const dlsim::Slots<16>& s, int n, void* out, size_t ne
   if constexpr (K > max_fixed_fan_in<Op>()) {
     return hipErrorInvalidValue;
   } else {
-    if (n == K) return launch_tiles<Op, 16, K>(s, n, nullptr, out, nelem, st);
+    if (n == K) return launch_tiles<Op, dlsim::Slots<16>, K>(s, n, out, nelem, st);
     return launch_fixed_k<Op, K + 1>(s, n, out, nelem, st);
   }
 }
 
-template <class Op>
-hipError_t launch_fixed(const dlsim::Slots<16>& s, int n, void* out, size_t nelem, hipStream_t st) {
-  return launch_fixed_k<Op, 1>(s, n, out, nelem, st);
-}
-
-template <class Op, int NB>
-hipError_t launch_pass(const dlsim::Slots<NB>& s, int n, const void* acc_in, void* out,
-                       size_t nelem, bool vec, hipStream_t st) {
+template <class Op, class S>
+hipError_t launch_any(const S& s, int n, void* out, size_t nelem, bool vec, hipStream_t st) {
   if (vec) {
-    if constexpr (NB == 16) {
-      if (!acc_in && n <= max_fixed_fan_in<Op>()) return launch_fixed<Op>(s, n, out, nelem, st);
+    if constexpr (std::is_same<S, dlsim::Slots<16>>::value) {
+      if (n <= max_fixed_fan_in<Op>()) return launch_fixed_k<Op, 1>(s, n, out, nelem, st);
     }
-    return launch_tiles<Op, NB, 0>(s, n, acc_in, out, nelem, st);
+    return launch_tiles<Op, S, 0>(s, n, out, nelem, st);
   }
   const size_t blocks = (nelem + dlsim::kBlock - 1) / dlsim::kBlock;
   if (blocks > 0x7fffffffu) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((dlsim::k_wreduce_scalar<Op, NB>), dim3(static_cast<unsigned>(blocks)),
-                     dim3(dlsim::kBlock), 0, st, s, n, acc_in, out, nelem);
+  hipLaunchKernelGGL((dlsim::k_wreduce_scalar<Op, S>), dim3(static_cast<unsigned>(blocks)), dim3(dlsim::kBlock), 0,
+                     st, s, n, out, nelem);
   return hipGetLastError();
 }
 
-// Packs up to NB inputs into kernel arguments and launches one pass.
-template <class Op, int NB>
-hipError_t pass_nb(const void* const* in, const float* w, int cnt, const void* acc_in, void* out,
-                   size_t nelem, bool vec, float div, hipStream_t st) {
-  dlsim::Slots<NB> s;
+template <int NB>
+void fill_slots(dlsim::Slots<NB>& s, const void* const* in, const float* w, int n, float div) {
   std::memset(&s, 0, sizeof(s));
-  for (int i = 0; i < cnt; ++i) {
+  for (int i = 0; i < n; ++i) {
     s.p[i] = in[i];
     s.w[i] = w ? w[i] : 1.0f;
   }
   s.div = div;
-  return launch_pass<Op, NB>(s, cnt, acc_in, out, nelem, vec, st);
 }
 
+// One launch over [0, nelem) of n inputs: every output element is written
+// once, after all n of its terms are folded in input order. Up to
+// DLSIM_MAX_FUSED_INPUTS inputs travel as kernel arguments; above that the
+// pointer/weight table goes to a stream-ordered device buffer (the pageable
+// host copy is staged by the runtime before hipMemcpyAsync returns).
+// div: final divisor (the mean policies; 1 for the weighted reduce).
 template <class Op>
-int run_range(const void* const* in, int n, const float* w, void* out, size_t nelem, bool vec,
-              float div, hipStream_t st);
+int run_range(const void* const* in, int n, const float* w, void* out, size_t nelem, bool vec, float div,
+              hipStream_t st) {
+  hipError_t e;
+  if (n <= 16) {
+    dlsim::Slots<16> s;
+    fill_slots(s, in, w, n, div);
+    e = launch_any<Op>(s, n, out, nelem, vec, st);
+  } else if (n <= DLSIM_MAX_FUSED_INPUTS) {
+    dlsim::Slots<DLSIM_MAX_FUSED_INPUTS> s;
+    fill_slots(s, in, w, n, div);
+    e = launch_any<Op>(s, n, out, nelem, vec, st);
+  } else {
+    const size_t pbytes = static_cast<size_t>(n) * sizeof(void*);
+    std::vector<unsigned char> h(pbytes + static_cast<size_t>(n) * sizeof(float));
+    std::memcpy(h.data(), in, pbytes);
+    for (int i = 0; i < n; ++i) {
+      const float wi = w ? w[i] : 1.0f;
+      std::memcpy(h.data() + pbytes + static_cast<size_t>(i) * sizeof(float), &wi, sizeof(float));
+    }
+    void* d = nullptr;
+    e = hipMallocAsync(&d, h.size(), st);
+    if (e != hipSuccess) return hip_fail(e, "fan-in table alloc");
+    e = hipMemcpyAsync(d, h.data(), h.size(), hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) {
+      const dlsim::DevSlots s{static_cast<const void* const*>(d),
+                              reinterpret_cast<const float*>(static_cast<unsigned char*>(d) + pbytes), div};
+      e = launch_any<Op>(s, n, out, nelem, vec, st);
+    }
+    const hipError_t e2 = hipFreeAsync(d, st);
+    if (e == hipSuccess) e = e2;
+  }
+  if (e != hipSuccess) return hip_fail(e, "kernel launch");
+  return DLSIM_OK;
+}
 
 // Elements are independent: an output longer than one launch's 2 GiB store
 // window is reduced as consecutive ranges (pointers offset by the range start).
-// div: final divisor (the mean policies; 1 for the weighted reduce).
 template <class Op>
 int run(const void* const* in, int n, const float* w, void* out, size_t nelem, hipStream_t st,
         float div = 1.0f) {
@@ -182,24 +225,43 @@ int run(const void* const* in, int n, const float* w, void* out, size_t nelem, h
   return DLSIM_OK;
 }
 
-template <class Op>
-int run_range(const void* const* in, int n, const float* w, void* out, size_t nelem, bool vec,
-              float div, hipStream_t st) {
-  // Passes of <= DLSIM_MAX_FUSED_INPUTS inputs; pass k > 0 continues the sum
-  // held in `out` (stored exactly: fp32, or bf16-valued in EXACT bf16); only
-  // the last pass applies the divisor.
-  for (int i0 = 0; i0 < n; i0 += DLSIM_MAX_FUSED_INPUTS) {
-    const int cnt = std::min(DLSIM_MAX_FUSED_INPUTS, n - i0);
-    const void* acc_in = (i0 == 0) ? nullptr : out;
-    const float* wp = w ? w + i0 : nullptr;
-    const float d = (i0 + cnt >= n) ? div : 1.0f;
-    hipError_t e = (cnt <= 16)
-                       ? pass_nb<Op, 16>(in + i0, wp, cnt, acc_in, out, nelem, vec, d, st)
-                       : pass_nb<Op, DLSIM_MAX_FUSED_INPUTS>(in + i0, wp, cnt, acc_in, out,
-                                                             nelem, vec, d, st);
-    if (e != hipSuccess) return hip_fail(e, "kernel launch");
+// ---- cross-task hazards of the batched entry points ---------------------------
+// A batched launch runs its tasks concurrently; b separate calls run them in
+// order. They agree unless one task writes bytes another task reads or
+// writes. Detected in O((inputs + b) log b): the output spans are sorted (any
+// overlap among them shows between neighbours), then each input span is
+// looked up among them. A task's exact in-place alias of its own input is
+// fine (one lane reads every term of an element before writing it).
+struct Span {
+  uintptr_t a, b;
+  int task;
+};
+
+bool cross_task_overlap(int nt, const int* fan_in, const void* const* in, void* const* outs, const size_t* nelem,
+                        size_t esz) {
+  std::vector<Span> wr;
+  wr.reserve(static_cast<size_t>(nt));
+  for (int t = 0; t < nt; ++t) {
+    if (nelem[t] == 0) continue;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(outs[t]);
+    wr.push_back({a, a + nelem[t] * esz, t});
   }
-  return DLSIM_OK;
+  std::sort(wr.begin(), wr.end(), [](const Span& x, const Span& y) { return x.a < y.a; });
+  for (size_t k = 1; k < wr.size(); ++k)
+    if (wr[k].a < wr[k - 1].b) return true;  // two outputs overlap (disjoint otherwise: ends sorted too)
+  size_t off = 0;
+  for (int t = 0; t < nt; ++t) {
+    const size_t bytes = nelem[t] * esz;
+    for (int i = 0; i < fan_in[t]; ++i) {
+      if (bytes == 0) continue;
+      const uintptr_t a = reinterpret_cast<uintptr_t>(in[off + i]), b = a + bytes;
+      auto it = std::upper_bound(wr.begin(), wr.end(), a, [](uintptr_t v, const Span& x) { return v < x.b; });
+      for (; it != wr.end() && it->a < b; ++it)
+        if (it->task != t) return true;
+    }
+    off += static_cast<size_t>(fan_in[t]);
+  }
+  return false;
 }
 
 // ---- batched launches ---------------------------------------------------------
@@ -261,6 +323,15 @@ int run_batched(int b, const int* fan_in, const void* const* in, const float* w,
                 const size_t* nelem, hipStream_t st, const float* divs = nullptr) {
   std::vector<size_t> off(static_cast<size_t>(b) + 1, 0);
   for (int t = 0; t < b; ++t) off[t + 1] = off[t] + static_cast<size_t>(fan_in[t]);
+  if (cross_task_overlap(b, fan_in, in, outs, nelem, Op::kBytes)) {
+    // A task reads or writes another task's output: keep the semantics of b
+    // separate calls by running the tasks one launch each, in order.
+    for (int t = 0; t < b; ++t) {
+      int rc = run<Op>(in + off[t], fan_in[t], w + off[t], outs[t], nelem[t], st, divs ? divs[t] : 1.0f);
+      if (rc != DLSIM_OK) return rc;
+    }
+    return DLSIM_OK;
+  }
   const size_t tile = static_cast<size_t>(dlsim::kBlock) * kVpt;
   auto batchable = [&](int t) {
     if (nelem[t] == 0 || fan_in[t] > 16) return false;
@@ -270,7 +341,8 @@ int run_batched(int b, const int* fan_in, const void* const* in, const float* w,
       if (!aligned16(in[off[t] + i])) return false;
     return true;
   };
-  // Tasks that cannot ride in a batch (large fan-in, misaligned, > 2 GiB) go alone.
+  // Tasks that cannot ride in a batch (large fan-in, misaligned, > 2 GiB) go
+  // alone (no task touches another's output, so the order is free).
   std::vector<int> group;
   for (int t = 0; t < b; ++t) {
     if (batchable(t)) {
@@ -354,6 +426,10 @@ int table_fill(int b, const int* fan_in, const void* const* in, const float* w, 
   TableLayout L;
   if (!table_layout<Op>(b, fan_in, nelem, &L)) return fail(DLSIM_E_ARG, "batch too large");
   if (bytes < L.bytes) return fail(DLSIM_E_ARG, "table buffer too small (%zu < %zu)", bytes, L.bytes);
+  if (cross_task_overlap(b, fan_in, in, outs, nelem, Op::kBytes))
+    return fail(DLSIM_E_ARG,
+                "a task's output overlaps another task's input or output: one table launch runs all tasks "
+                "concurrently (use separate calls, or dlsim_wreduce_batched, which orders them)");
   unsigned char* base = static_cast<unsigned char*>(h_table);
   std::memset(base, 0, L.bytes);
   auto* h = reinterpret_cast<dlsim::BatchTableHeader*>(base);
@@ -458,8 +534,9 @@ int check_args(const void* const* in, int n, const float* w, const void* out, si
   for (int i = 0; i < n; ++i) {
     if (!in[i]) return fail(DLSIM_E_ARG, "null input pointer at index %d", i);
     const uintptr_t a0 = reinterpret_cast<uintptr_t>(in[i]), a1 = a0 + bytes;
-    // Exact aliasing (out == in[i]) is safe: a lane reads every input of an
-    // element before it writes that element. Partial overlap is not.
+    // Exact aliasing (out == in[i]) is safe for every i: the reduce is one
+    // pass, and a lane reads all n terms of an element before writing it.
+    // Partial overlap is not.
     if (a0 != o0 && a0 < o1 && o0 < a1)
       return fail(DLSIM_E_ARG, "output partially overlaps input %d", i);
   }
@@ -511,6 +588,14 @@ int run_chunk_mean(int b, const int* fan_in, const void* const* in, void* const*
   constexpr size_t tile = static_cast<size_t>(dlsim::kBlock) * CmDefault::VPT;
   std::vector<size_t> off(static_cast<size_t>(b) + 1, 0);
   for (int t = 0; t < b; ++t) off[t + 1] = off[t] + static_cast<size_t>(fan_in[t]);
+  if (b > 1 && cross_task_overlap(b, fan_in, in, outs, nelem, Op::kBytes)) {
+    // tasks touch each other's outputs: one launch per task, in order
+    for (int t = 0; t < b; ++t) {
+      int rc = run_chunk_mean<Op>(1, fan_in + t, in + off[t], outs + t, nelem + t, threads, st);
+      if (rc != DLSIM_OK) return rc;
+    }
+    return DLSIM_OK;
+  }
   auto task_flags = [&](int t) {
     bool vec = aligned16(outs[t]);
     for (int i = 0; i < fan_in[t] && vec; ++i) vec = aligned16(in[off[t] + i]);
@@ -901,6 +986,11 @@ int dlsim_host_wreduce(int n, int t, const void* const* h_srcs, const size_t* nu
   if (!aligned16(h_staging) || !aligned16(d_rows) || row_stride % 8 != 0)
     return fail(DLSIM_E_ARG, "staging rows must be 16-B aligned with a stride that is a multiple of 8");
   if (row_stride < total) return fail(DLSIM_E_ARG, "row_stride %zu < %zu elements", row_stride, total);
+  {
+    const uintptr_t r0 = reinterpret_cast<uintptr_t>(d_rows), r1 = r0 + static_cast<size_t>(n) * row_stride * esz;
+    const uintptr_t o0 = reinterpret_cast<uintptr_t>(d_out), o1 = o0 + total * esz;
+    if (o0 < r1 && r0 < o1) return fail(DLSIM_E_ARG, "d_out overlaps the device staging rows");
+  }
   for (size_t j = 0; j < static_cast<size_t>(n) * t; ++j)
     if (!h_srcs[j] && numels[j % t] > 0) return fail(DLSIM_E_ARG, "null source pointer at index %zu", j);
   const size_t chunk = chunk_elems == 0 || chunk_elems >= total ? total : (chunk_elems + 1023) / 1024 * 1024;
@@ -993,6 +1083,13 @@ int dlsim_host_chunk_mean(int b, const int* fan_in, const void* const* h_inputs,
   if (!h_staging || !d_staging) return fail(DLSIM_E_ARG, "null staging");
   if (!aligned16(h_staging) || !aligned16(d_staging)) return fail(DLSIM_E_ARG, "staging must be 16-B aligned");
   if (staging_elems < need) return fail(DLSIM_E_ARG, "staging of %zu elements < %zu needed", staging_elems, need);
+  {
+    const uintptr_t s0 = reinterpret_cast<uintptr_t>(d_staging), s1 = s0 + need * esz;
+    for (int t = 0; t < b; ++t) {
+      const uintptr_t o0 = reinterpret_cast<uintptr_t>(d_outs[t]), o1 = o0 + n_elems[t] * esz;
+      if (n_elems[t] > 0 && o0 < s1 && s0 < o1) return fail(DLSIM_E_ARG, "task %d: output overlaps the device staging", t);
+    }
+  }
   hipStream_t st = static_cast<hipStream_t>(stream);
   hipStream_t h2d = h2d_stream ? static_cast<hipStream_t>(h2d_stream) : st;
   hipStream_t d2h = d2h_stream ? static_cast<hipStream_t>(d2h_stream) : st;
@@ -1097,12 +1194,14 @@ int dlsim_probe_copy(const void* d_src, void* d_dst, size_t bytes, void* stream)
     return fail(DLSIM_E_ARG, "probe_copy needs 16-byte aligned sizes and pointers");
   const size_t nvec = bytes / 16;
   if (nvec == 0) return DLSIM_OK;
-  constexpr int VPT = 4;
-  const size_t blocks = (nvec + dlsim::kBlock * VPT - 1) / (dlsim::kBlock * VPT);
-  hipLaunchKernelGGL((dlsim::k_copy16<VPT>), dim3(static_cast<unsigned>(blocks)), dim3(dlsim::kBlock), 0,
-                     static_cast<hipStream_t>(stream), static_cast<const dlsim::u32x4*>(d_src),
-                     static_cast<dlsim::u32x4*>(d_dst), nvec);
-  hipError_t e = hipGetLastError();
+  dlsim::Slots<16> s;
+  std::memset(&s, 0, sizeof(s));
+  s.p[0] = d_src;
+  s.w[0] = 1.0f;
+  s.div = 1.0f;
+  if (bytes > kMaxLaunchOutBytes) return fail(DLSIM_E_ARG, "probe_copy is limited to < 2 GiB");
+  hipError_t e =
+      launch_tiles<dlsim::CopyProbe, dlsim::Slots<16>, 1>(s, 1, d_dst, nvec * 4, static_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(e, "probe_copy launch");
   return DLSIM_OK;
 }

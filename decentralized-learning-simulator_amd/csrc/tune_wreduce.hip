@@ -109,7 +109,7 @@ __global__ __launch_bounds__(BLOCK) void k_tiles_block(const Slots<128> s, int n
   const size_t t = blockIdx.x - 1;
   if (t >= full) return;
   const size_t lane_off = (threadIdx.x >> 6) * 64 * VPT + (threadIdx.x & 63);
-  reduce_tile<Op, Slots<128>, NF, 8, VPT, 1, false, 16, 64>(s, n, nullptr, o, t * kT + lane_off, nvec);
+  reduce_tile<Op, Slots<128>, NF, 8, VPT, 1, false, 16, 64>(s, n, o, t * kT + lane_off, nvec);
 }
 
 // XCD-aware tile map experiment: workgroups are dispatched round-robin over
@@ -126,7 +126,7 @@ __global__ __launch_bounds__(kBlock) void k_tiles_xcd(const Slots<128> s, int n,
   const size_t t = (k & 7) * per + (k >> 3);
   if (t >= nvec / kT) return;
   const size_t lane_off = (threadIdx.x >> 6) * 64 * VPT + (threadIdx.x & 63);
-  reduce_tile<Op, Slots<128>, NF, 8, VPT, 1, false, 16, 64>(s, n, nullptr, o, t * kT + lane_off, nvec);
+  reduce_tile<Op, Slots<128>, NF, 8, VPT, 1, false, 16, 64>(s, n, o, t * kT + lane_off, nvec);
 }
 }  // namespace dlsim
 
@@ -169,8 +169,8 @@ void launch_t(const Slots<128>& s, int n, void* out, size_t nvec, size_t nelem, 
   const size_t full = nvec / tile;
   size_t grid = full + 1;
   if (gm > 0) grid = std::min<size_t>(grid, (size_t)gm * 256);
-  hipLaunchKernelGGL((k_wreduce_tiles<Op, 128, NF, G, VPT, NT>), dim3((unsigned)grid), dim3(kBlock), 0,
-                     st, s, n, nullptr, out, nvec, nelem);
+  hipLaunchKernelGGL((k_wreduce_tiles<Op, Slots<128>, NF, G, VPT, NT>), dim3((unsigned)grid), dim3(kBlock), 0,
+                     st, s, n, out, nvec, nelem);
 }
 
 template <class Op, int NF, int G, int VPT, int NT, int NTS, bool WM = false>
@@ -183,8 +183,8 @@ void launch_ts(const Slots<128>& s, int n, void* out, size_t nvec, size_t nelem,
   size_t lds = 0;
   if (gm > 0) grid = std::min<size_t>(grid, (size_t)gm * 256);
   if (gm < 0) lds = (160 * 1024) / (size_t)(-gm) - 512;
-  hipLaunchKernelGGL((k_wreduce_tiles<Op, 128, NF, G, VPT, NT, NTS, WM>), dim3((unsigned)grid), dim3(kBlock), lds,
-                     st, s, n, nullptr, out, nvec, nelem);
+  hipLaunchKernelGGL((k_wreduce_tiles<Op, Slots<128>, NF, G, VPT, NT, NTS, WM>), dim3((unsigned)grid), dim3(kBlock), lds,
+                     st, s, n, out, nvec, nelem);
 }
 
 // LDS-DMA body over full tiles; ragged end by the tiled kernel's last block
@@ -240,8 +240,8 @@ template <class Op, int NF>
 void launch_probe(const Slots<128>& s, int n, void* out, size_t nvec, size_t nelem, hipStream_t st, int) {
   if constexpr (Op::kBytes == 4) {
     const size_t full = nvec / ((size_t)kBlock * 4);
-    hipLaunchKernelGGL((k_wreduce_tiles<XorProbe, 128, NF, 8, 4, 1, 16, true>), dim3((unsigned)(full + 1)),
-                       dim3(kBlock), 0, st, s, n, nullptr, out, nvec, nelem);
+    hipLaunchKernelGGL((k_wreduce_tiles<XorProbe, Slots<128>, NF, 8, 4, 1, 16, true>), dim3((unsigned)(full + 1)),
+                       dim3(kBlock), 0, st, s, n, out, nvec, nelem);
   }
 }
 
@@ -257,14 +257,14 @@ __global__ __launch_bounds__(kBlock) void k_tiles_contig(const Slots<128> s, int
   const size_t B = gridDim.x;
   if (blockIdx.x == 0) {
     if (full * kTile < nvec)
-      reduce_tile<Op, Slots<128>, NF, 8, 4, 1, true, 16>(s, n, nullptr, o, full * kTile + threadIdx.x, nvec);
+      reduce_tile<Op, Slots<128>, NF, 8, 4, 1, true, 16>(s, n, o, full * kTile + threadIdx.x, nvec);
     const size_t j = nvec * Op::E + threadIdx.x;
-    if (j < nelem) fold_scalar<Op, Slots<128>>(s, n, nullptr, out, j);
+    if (j < nelem) fold_scalar<Op, Slots<128>>(s, n, out, j);
   }
   const size_t t0 = full * blockIdx.x / B, t1 = full * (blockIdx.x + 1) / B;
   const size_t lo = (threadIdx.x >> 6) * 64 * 4 + (threadIdx.x & 63);
   for (size_t t = t0; t < t1; ++t)
-    reduce_tile<Op, Slots<128>, NF, 8, 4, 1, false, 16, 64>(s, n, nullptr, o, t * kTile + lo, nvec);
+    reduce_tile<Op, Slots<128>, NF, 8, 4, 1, false, 16, 64>(s, n, o, t * kTile + lo, nvec);
 }
 
 template <class Op, int NF>
@@ -287,19 +287,19 @@ __global__ __launch_bounds__(kBlock) void k_tiles_split(const Slots<128> s, int 
   const size_t small_full = (nvec - base) / kSm;
   if (blockIdx.x == 0) {
     if (base + small_full * kSm < nvec)
-      reduce_tile<Op, Slots<128>, NF, 8, VSM, 1, true, 16>(s, n, nullptr, o, base + small_full * kSm + threadIdx.x,
+      reduce_tile<Op, Slots<128>, NF, 8, VSM, 1, true, 16>(s, n, o, base + small_full * kSm + threadIdx.x,
                                                          nvec);
     const size_t j = nvec * Op::E + threadIdx.x;
-    if (j < nelem) fold_scalar<Op, Slots<128>>(s, n, nullptr, out, j);
+    if (j < nelem) fold_scalar<Op, Slots<128>>(s, n, out, j);
     return;
   }
   const size_t b = blockIdx.x - 1;
   if (b < big_tiles) {
     const size_t lo = (threadIdx.x >> 6) * 64 * VB + (threadIdx.x & 63);
-    reduce_tile<Op, Slots<128>, NF, 8, VB, 1, false, 16, 64>(s, n, nullptr, o, b * kBig + lo, nvec);
+    reduce_tile<Op, Slots<128>, NF, 8, VB, 1, false, 16, 64>(s, n, o, b * kBig + lo, nvec);
   } else {
     const size_t lo = (threadIdx.x >> 6) * 64 * VSM + (threadIdx.x & 63);
-    reduce_tile<Op, Slots<128>, NF, 8, VSM, 1, false, 16, 64>(s, n, nullptr, o, base + (b - big_tiles) * kSm + lo,
+    reduce_tile<Op, Slots<128>, NF, 8, VSM, 1, false, 16, 64>(s, n, o, base + (b - big_tiles) * kSm + lo,
                                                             nvec);
   }
 }
@@ -342,6 +342,20 @@ void add_nf(std::vector<Variant>& vs, int n) {
   vs.push_back({p + "_split95_V1", launch_split<Op, NF, 4, 1>, 95});
   vs.push_back({p + "_split90_V2", launch_split<Op, NF, 4, 2>, 90});
   vs.push_back({p + "_split97_V1", launch_split<Op, NF, 4, 1>, 97});
+  // small-launch shapes (strong-scaling slices): block map at VPT 1/2,
+  // grid-stride grids of k*256 blocks, nt stores
+  vs.push_back({p + "_V2_sc1_blk", launch_ts<Op, NF, 8, 2, 1, 16, false>, 0});
+  vs.push_back({p + "_V1_sc1_g1", launch_ts<Op, NF, 8, 1, 1, 16, true>, 1});
+  vs.push_back({p + "_V1_sc1_g2", launch_ts<Op, NF, 8, 1, 1, 16, true>, 2});
+  vs.push_back({p + "_V1_sc1_g4", launch_ts<Op, NF, 8, 1, 1, 16, true>, 4});
+  vs.push_back({p + "_V2_sc1_g1", launch_ts<Op, NF, 8, 2, 1, 16, true>, 1});
+  vs.push_back({p + "_V2_sc1_g2", launch_ts<Op, NF, 8, 2, 1, 16, true>, 2});
+  vs.push_back({p + "_V4_sc1_g1", launch_ts<Op, NF, 8, 4, 1, 16, true>, 1});
+  vs.push_back({p + "_V1_nt", launch_ts<Op, NF, 8, 1, 1, kStNT, true>, 0});
+  vs.push_back({p + "_V2_nt_wave", launch_ts<Op, NF, 8, 2, 1, kStNT, true>, 0});
+  vs.push_back({p + "_V4_nt_wave", launch_ts<Op, NF, 8, 4, 1, kStNT, true>, 0});
+  vs.push_back({p + "_V1_plain", launch_ts<Op, NF, 8, 1, 1, kStPlain, true>, 0});
+  vs.push_back({p + "_V1_sc1_ldplain", launch_ts<Op, NF, 8, 1, 0, 16, true>, 0});
 }
 
 template <class Op>
@@ -361,8 +375,12 @@ std::vector<Variant> variants(int n) {
 
 template <class Op>
 int run(int n, size_t P, int reps, double peak_gbs) {
-  const int sets = 3;
   const size_t bytes = P * Op::kBytes;
+  // enough rotating input sets that their footprint is >= 1 GiB (4x the
+  // 256 MiB Infinity Cache): small slices must not be served from it
+  const double set_bytes = (double)(n + 1) * bytes;
+  const int sets = std::max(3, std::min(64, (int)((1ull << 30) / set_bytes) + 1));
+  printf("sets=%d footprint=%.0fMB\n", sets, sets * set_bytes / 1e6);
   const size_t nvec = P / Op::E;
   std::vector<void*> in((size_t)sets * n);
   std::vector<void*> out(sets);
@@ -469,31 +487,40 @@ int run(int n, size_t P, int reps, double peak_gbs) {
     printf("variant=%-16s n=%d P=%zu bytes=%.1fMB median_us=%.2f GBps=%.0f frac=%.3f batch_us=%.2f batch_GBps=%.0f bfrac=%.3f same=%d\n",
            vs[v].name.c_str(), n, P, alg_bytes / 1e6, us, gbs, gbs / peak_gbs, bus, bgbs, bgbs / peak_gbs, (int)same);
   }
-  // copy ceiling on the same footprint
+  // copy ceiling on the same per-launch footprint, rotating >= 1 GiB of
+  // buffers like the inputs (a fixed pair would be served from the MALL)
   {
     const size_t cbytes = (size_t)(alg_bytes / 2) & ~(size_t)15;
-    void *a, *b;
-    CK(hipMalloc(&a, cbytes));
-    CK(hipMalloc(&b, cbytes));
-    CK(hipMemset(a, 1, cbytes));
-    std::vector<double> t;
-    for (int k = 0; k < reps; ++k) {
-      CK(hipEventRecord(ev[0], st));
-      const size_t nv = cbytes / 16;
-      hipLaunchKernelGGL((k_copy16<4>), dim3((unsigned)((nv + 1023) / 1024)), dim3(256), 0, st,
-                         (const u32x4*)a, (u32x4*)b, nv);
-      CK(hipEventRecord(ev[1], st));
-      CK(hipEventSynchronize(ev[1]));
-      float ms;
-      CK(hipEventElapsedTime(&ms, ev[0], ev[1]));
-      t.push_back(ms * 1e3);
+    const int csets = std::max(2, std::min(64, (int)((1ull << 30) / (2.0 * cbytes)) + 1));
+    std::vector<void*> ca(csets), cb(csets);
+    for (int k = 0; k < csets; ++k) {
+      CK(hipMalloc(&ca[k], cbytes));
+      CK(hipMalloc(&cb[k], cbytes));
+      CK(hipMemset(ca[k], 1, cbytes));
     }
-    std::sort(t.begin(), t.end());
-    const double us = t[t.size() / 2];
-    printf("copy16 bytes_moved=%.1fMB median_us=%.2f GBps=%.0f frac=%.3f\n", 2.0 * cbytes / 1e6, us,
+    const size_t nv = cbytes / 16;
+    auto launch_copy = [&](int k) {
+      Slots<128> cs;
+      memset(&cs, 0, sizeof(cs));
+      cs.p[0] = ca[k % csets];
+      cs.w[0] = 1.0f;
+      cs.div = 1.0f;
+      launch_ts<CopyProbe, 1, 8, 4, 1, 16, true>(cs, 1, cb[k % csets], nv, nv * 4, st, 0);
+    };
+    for (int k = 0; k < 10; ++k) launch_copy(k);
+    CK(hipEventRecord(ev[0], st));
+    for (int k = 0; k < reps; ++k) launch_copy(k);
+    CK(hipEventRecord(ev[1], st));
+    CK(hipEventSynchronize(ev[1]));
+    float ms;
+    CK(hipEventElapsedTime(&ms, ev[0], ev[1]));
+    const double us = ms * 1e3 / reps;
+    printf("copy16 sets=%d bytes_moved=%.1fMB batch_us=%.2f GBps=%.0f frac=%.3f\n", csets, 2.0 * cbytes / 1e6, us,
            2.0 * cbytes / (us * 1e-6) / 1e9, 2.0 * cbytes / (us * 1e-6) / 1e9 / peak_gbs);
-    CK(hipFree(a));
-    CK(hipFree(b));
+    for (int k = 0; k < csets; ++k) {
+      CK(hipFree(ca[k]));
+      CK(hipFree(cb[k]));
+    }
   }
   if (arena) CK(hipFree(arena));
   else

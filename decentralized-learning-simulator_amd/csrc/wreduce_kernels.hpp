@@ -374,7 +374,21 @@ template <int NB>
 struct Slots {
   const void* p[NB];
   float w[NB];
-  float div;  // final divisor of the mean policies (1 elsewhere / between passes)
+  float div;  // final divisor of the mean policies (1 for the weighted reduce)
+  __device__ const void* ptr(int i) const { return p[i]; }
+  __device__ float wt(int i) const { return w[i]; }
+  __device__ float divisor() const { return div; }
+};
+
+// Fan-in above the kernarg slots (n > DLSIM_MAX_FUSED_INPUTS): the pointers
+// and weights sit in a small device array the host uploads on the launch
+// stream (read with scalar loads like the kernargs), so every n is one pass
+// over the inputs: each output element is written once, after all n of its
+// terms are folded.
+struct DevSlots {
+  const void* const* p;
+  const float* w;
+  float div;
   __device__ const void* ptr(int i) const { return p[i]; }
   __device__ float wt(int i) const { return w[i]; }
   __device__ float divisor() const { return div; }
@@ -382,18 +396,16 @@ struct Slots {
 
 // Scalar fold of one element over all n inputs (tail / misaligned path).
 template <class Op, class S>
-__device__ __forceinline__ void fold_scalar(const S& s, int n, const void* acc_in,
-                                            void* out, size_t j) {
-  // Every load of a chunk of 8 inputs (and the pass accumulator) issues
-  // before its first use: one HBM round trip per chunk, not one per input.
-  // The first input doubles as the x0*0 seed (n >= 1).
-  const float acc0 = acc_in ? load_elem<Op>(acc_in, j) : 0.0f;
+__device__ __forceinline__ void fold_scalar(const S& s, int n, void* out, size_t j) {
+  // Every load of a chunk of 8 inputs issues before its first use: one HBM
+  // round trip per chunk, not one per input. The first input doubles as the
+  // x0*0 seed (n >= 1).
   float a = 0.0f;
   for (int i = 0; i < n; i += 8) {
     float x[8];
 #pragma unroll
     for (int g = 0; g < 8; ++g) x[g] = (i + g < n) ? load_elem<Op>(s.ptr(i + g), j) : 0.0f;
-    if (i == 0) a = acc_in ? acc0 : Op::init(x[0]);
+    if (i == 0) a = Op::init(x[0]);
 #pragma unroll
     for (int g = 0; g < 8; ++g)
       if (i + g < n) a = Op::step(a, s.wt(i + g), x[g]);
@@ -402,13 +414,11 @@ __device__ __forceinline__ void fold_scalar(const S& s, int n, const void* acc_i
 }
 
 // Scalar kernel: any alignment, one element per thread.
-template <class Op, int NB>
-__global__ __launch_bounds__(kBlock) void k_wreduce_scalar(const Slots<NB> s, int n,
-                                                           const void* __restrict__ acc_in,
-                                                           void* __restrict__ out,
+template <class Op, class S>
+__global__ __launch_bounds__(kBlock) void k_wreduce_scalar(const S s, int n, void* __restrict__ out,
                                                            size_t nelem) {
   const size_t j = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x;
-  if (j < nelem) fold_scalar<Op, Slots<NB>>(s, n, acc_in, out, j);
+  if (j < nelem) fold_scalar<Op, S>(s, n, out, j);
 }
 
 // ---- tiled kernel ------------------------------------------------------------
@@ -418,9 +428,9 @@ __global__ __launch_bounds__(kBlock) void k_wreduce_scalar(const Slots<NB> s, in
 // partial tile and the < E scalar tail go to the grid's last block, which
 // holds the fewest full tiles under the grid-stride deal below.
 //
-// NF > 0: the fan-in n == NF is a compile-time constant (single pass, no
-// acc_in): every input's loads are issued back to back with no group
-// branches. NF == 0: runtime n in groups of G (first group peeled).
+// NF > 0: the fan-in n == NF is a compile-time constant: every input's loads
+// are issued back to back with no group branches. NF == 0: runtime n in
+// groups of G (first group peeled).
 template <class Op, int VPT, int NT, bool CHECK, int VS = kBlock>
 __device__ __forceinline__ void load_tile(const void* src, size_t v0, size_t nvec,
                                           u32x4 (&r)[VPT]) {
@@ -459,8 +469,7 @@ __device__ __forceinline__ void init_tile(float (&a)[VPT][Op::E], const u32x4 (&
 }
 
 template <class Op, class S, int NF, int G, int VPT, int NT, bool CHECK, int STP, int VS = kBlock>
-__device__ __forceinline__ void reduce_tile(const S& s, int n, const void* acc_in,
-                                            const OutRef& out, size_t v0, size_t nvec) {
+__device__ __forceinline__ void reduce_tile(const S& s, int n, const OutRef& out, size_t v0, size_t nvec) {
   float a[VPT][Op::E];
   if constexpr (NF > 0) {
     u32x4 r[NF][VPT];
@@ -470,17 +479,14 @@ __device__ __forceinline__ void reduce_tile(const S& s, int n, const void* acc_i
 #pragma unroll
     for (int i = 0; i < NF; ++i) fold_tile<Op, VPT>(a, s.wt(i), r[i]);
   } else {
-    // first group: acc (if continuing a previous pass) + up to G inputs
+    // first group: up to G inputs, input 0 seeding acc = x0 * 0
     {
-      u32x4 racc[VPT];
       u32x4 r[G][VPT];
       const int cnt = n < G ? n : G;
-      if (acc_in) load_tile<Op, VPT, NT, CHECK, VS>(acc_in, v0, nvec, racc);
 #pragma unroll
       for (int g = 0; g < G; ++g)
         if (g < cnt) load_tile<Op, VPT, NT, CHECK, VS>(s.ptr(g), v0, nvec, r[g]);
-      if (acc_in) init_tile<Op, VPT>(a, racc, true);
-      else init_tile<Op, VPT>(a, r[0], false);
+      init_tile<Op, VPT>(a, r[0], false);
 #pragma unroll
       for (int g = 0; g < G; ++g)
         if (g < cnt) fold_tile<Op, VPT>(a, s.wt(g), r[g]);
@@ -514,11 +520,9 @@ __device__ __forceinline__ void reduce_tile(const S& s, int n, const void* acc_i
 // measured and did not pay: profiles/r01_tune_ragged.log.)
 // WAVEMAP: lane l of wave w reads vectors w*64*VPT + l + k*64 of a tile (each
 // wave sweeps VPT contiguous KiB per stream) instead of l' + k*kBlock.
-template <class Op, int NB, int NF, int G, int VPT, int NT, int STP = (NT ? kStNT : kStPlain),
+template <class Op, class S, int NF, int G, int VPT, int NT, int STP = (NT ? kStNT : kStPlain),
           bool WAVEMAP = false>
-__global__ __launch_bounds__(kBlock) void k_wreduce_tiles(const Slots<NB> s, int n,
-                                                          const void* __restrict__ acc_in,
-                                                          void* __restrict__ out, size_t nvec,
+__global__ __launch_bounds__(kBlock) void k_wreduce_tiles(const S s, int n, void* __restrict__ out, size_t nvec,
                                                           size_t nelem) {
   constexpr size_t kTile = static_cast<size_t>(kBlock) * VPT;
   const size_t full = nvec / kTile;
@@ -526,9 +530,9 @@ __global__ __launch_bounds__(kBlock) void k_wreduce_tiles(const Slots<NB> s, int
   const size_t nb = gridDim.x;
   if (blockIdx.x == 0) {
     if (full * kTile < nvec)
-      reduce_tile<Op, Slots<NB>, NF, G, VPT, NT, true, STP>(s, n, acc_in, o, full * kTile + threadIdx.x, nvec);
+      reduce_tile<Op, S, NF, G, VPT, NT, true, STP>(s, n, o, full * kTile + threadIdx.x, nvec);
     const size_t j = nvec * Op::E + threadIdx.x;
-    if (j < nelem) fold_scalar<Op, Slots<NB>>(s, n, acc_in, out, j);
+    if (j < nelem) fold_scalar<Op, S>(s, n, out, j);
     if (nb > 1) return;
   }
   const size_t workers = nb > 1 ? nb - 1 : 1;
@@ -536,10 +540,10 @@ __global__ __launch_bounds__(kBlock) void k_wreduce_tiles(const Slots<NB> s, int
   if constexpr (WAVEMAP) {
     const size_t lane_off = (threadIdx.x >> 6) * 64 * VPT + (threadIdx.x & 63);
     for (size_t t = first; t < full; t += workers)
-      reduce_tile<Op, Slots<NB>, NF, G, VPT, NT, false, STP, 64>(s, n, acc_in, o, t * kTile + lane_off, nvec);
+      reduce_tile<Op, S, NF, G, VPT, NT, false, STP, 64>(s, n, o, t * kTile + lane_off, nvec);
   } else {
     for (size_t t = first; t < full; t += workers)
-      reduce_tile<Op, Slots<NB>, NF, G, VPT, NT, false, STP>(s, n, acc_in, o, t * kTile + threadIdx.x, nvec);
+      reduce_tile<Op, S, NF, G, VPT, NT, false, STP>(s, n, o, t * kTile + threadIdx.x, nvec);
   }
 }
 
@@ -590,12 +594,12 @@ __global__ __launch_bounds__(kBlock) void k_wreduce_batch(const BatchSlots s) {
   const uint32_t local = bid - s.block_start[t];
   if (local == 0) {
     if (full * kTile < nvec)
-      reduce_tile<Op, TaskArgs, NF, G, VPT, NT, true, STP>(a, n, nullptr, o, full * kTile + threadIdx.x, nvec);
+      reduce_tile<Op, TaskArgs, NF, G, VPT, NT, true, STP>(a, n, o, full * kTile + threadIdx.x, nvec);
     const size_t j = nvec * Op::E + threadIdx.x;
-    if (j < s.nelem[t]) fold_scalar<Op, TaskArgs>(a, n, nullptr, s.out[t], j);
+    if (j < s.nelem[t]) fold_scalar<Op, TaskArgs>(a, n, s.out[t], j);
     return;
   }
-  reduce_tile<Op, TaskArgs, NF, G, VPT, NT, false, STP>(a, n, nullptr, o, (local - 1) * kTile + threadIdx.x, nvec);
+  reduce_tile<Op, TaskArgs, NF, G, VPT, NT, false, STP>(a, n, o, (local - 1) * kTile + threadIdx.x, nvec);
 }
 
 // ---- batched launch from a device descriptor table ----------------------------
@@ -648,30 +652,27 @@ __global__ __launch_bounds__(kBlock) void k_wreduce_batch_table(const unsigned c
   const uint32_t local = blockIdx.x - d.block_start;
   if (local == 0) {
     if (full * kTile < nvec)
-      reduce_tile<Op, TableArgs, NF, G, VPT, NT, true, STP>(a, n, nullptr, o, full * kTile + threadIdx.x, nvec);
+      reduce_tile<Op, TableArgs, NF, G, VPT, NT, true, STP>(a, n, o, full * kTile + threadIdx.x, nvec);
     const size_t j = nvec * Op::E + threadIdx.x;
-    if (j < d.nelem) fold_scalar<Op, TableArgs>(a, n, nullptr, d.out, j);
+    if (j < d.nelem) fold_scalar<Op, TableArgs>(a, n, d.out, j);
     return;
   }
-  reduce_tile<Op, TableArgs, NF, G, VPT, NT, false, STP>(a, n, nullptr, o, (local - 1) * kTile + threadIdx.x, nvec);
+  reduce_tile<Op, TableArgs, NF, G, VPT, NT, false, STP>(a, n, o, (local - 1) * kTile + threadIdx.x, nvec);
 }
 
-// Copy probe: the achievable streaming ceiling on this device.
-template <int VPT>
-__global__ __launch_bounds__(kBlock) void k_copy16(const u32x4* __restrict__ src,
-                                                   u32x4* __restrict__ dst, size_t nvec) {
-  const size_t base = static_cast<size_t>(blockIdx.x) * (kBlock * VPT) + threadIdx.x;
-  u32x4 r[VPT];
-#pragma unroll
-  for (int v = 0; v < VPT; ++v) {
-    const size_t i = base + static_cast<size_t>(v) * kBlock;
-    if (i < nvec) r[v] = src[i];
-  }
-#pragma unroll
-  for (int v = 0; v < VPT; ++v) {
-    const size_t i = base + static_cast<size_t>(v) * kBlock;
-    if (i < nvec) dst[i] = r[v];
-  }
-}
+// Copy probe: the streaming ceiling of the reduce's own access pattern.
+// With n = 1 the tiled kernel reads one stream and writes one (same grid,
+// lane map, nt loads and sc1 stores as the fp32 reduce): a bit-exact copy of
+// 16-byte vectors (dlsim_probe_copy), so a 1:1 read/write stream is timed
+// with exactly the machinery the reduce uses.
+struct CopyProbe {
+  static constexpr int E = 4;
+  static constexpr int kBytes = 4;
+  static constexpr int kFmt = kFmtF32;
+  __device__ static float init(float x) { return x; }
+  __device__ static float step(float acc, float, float) { return acc; }
+  __device__ static void step2(float&, float&, float, float, float) {}
+  __device__ static float finish(float a, float) { return a; }
+};
 
 }  // namespace dlsim

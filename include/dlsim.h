@@ -63,9 +63,11 @@ enum dlsim_mode {
 #define DLSIM_E_RCCL (-4)     /* RCCL not bound, or an RCCL call failed       */
 #define DLSIM_E_HIP (-100)    /* a HIP call failed: code = -100 - hipError_t  */
 
-/* Maximum inputs fused into one kernel launch; larger n is processed in
- * passes of this many inputs that continue the running sum in `d_out`
- * (same rounding sequence, so EXACT results do not depend on it). */
+/* Fan-in carried in kernel arguments. Larger n (any n >= 1) reads its
+ * pointer/weight table from a small device buffer the call allocates and
+ * uploads on `stream` (hipMallocAsync / hipMemcpyAsync / hipFreeAsync; do not
+ * capture such a call in a graph). Either way the reduce is ONE pass: every
+ * output element is written once, after all n of its terms are folded. */
 #define DLSIM_MAX_FUSED_INPUTS 128
 
 /*
@@ -79,7 +81,10 @@ enum dlsim_mode {
  *   h_weights  host array of n fp32 weights (already rounded to fp32 — the
  *              reference's `w * p1` converts its Python float with RNE,
  *              fedavg.py:25); uniform 1/n is the caller's job (fedavg.py:14-15)
- *   d_out      device buffer of n_elems; must not alias any input
+ *   d_out      device buffer of n_elems. It may BE an input (d_out ==
+ *              d_inputs[i], any i: an in-place update; every term of an
+ *              element is read before the element is written); any other
+ *              overlap with an input is rejected (DLSIM_E_ARG)
  *   stream     hipStream_t
  * Any alignment is accepted; 16-byte-aligned buffers take the vector path.
  */
@@ -114,10 +119,13 @@ int dlsim_wreduce_tensors(const void* const* d_inputs, int n, int t,
  * Task t has fan_in[t] inputs: d_inputs[o_t .. o_t + fan_in[t]) with weights
  * h_weights[o_t ..], o_t = fan_in[0] + ... + fan_in[t-1]; it writes
  * n_elems[t] elements to d_outs[t]. Every task follows dlsim_wreduce's rules
- * and rounding (results are bit-identical to b separate dlsim_wreduce calls).
- * Replaces b separate `aggregate` tasks scheduled by the broker
- * (broker.py:261-275 -> functions.py:89-106); up to 32 tasks / 192 inputs
- * share one launch, tasks with fan-in > 16 run alone.
+ * and rounding, and the results are bit-identical to b separate dlsim_wreduce
+ * calls made in task order, also when tasks depend on each other: if any
+ * task's output overlaps another task's input or output (task 1 reads what
+ * task 0 writes), the tasks run one launch each, in order; otherwise up to
+ * 32 tasks / 192 inputs share one launch and tasks with fan-in > 16 run
+ * alone. Replaces b separate `aggregate` tasks scheduled by the broker
+ * (broker.py:261-275 -> functions.py:89-106).
  */
 int dlsim_wreduce_batched(int b, const int* fan_in, const void* const* d_inputs,
                           const float* h_weights, void* const* d_outs, const size_t* n_elems,
@@ -132,7 +140,10 @@ int dlsim_wreduce_batched(int b, const int* fan_in, const void* const* d_inputs,
  *   dlsim_batch_table_bytes   size of the table for these tasks
  *   dlsim_batch_table_fill    write it into caller host memory h_table
  *                             (every task: fan-in <= 128, 16-B aligned
- *                             buffers, output < 2 GiB; else DLSIM_E_ARG)
+ *                             buffers, output < 2 GiB, and no task's output
+ *                             overlapping another task's input or output —
+ *                             the launch runs all tasks concurrently; else
+ *                             DLSIM_E_ARG)
  *   (caller copies h_table to d_table, e.g. hipMemcpyAsync on `stream`)
  *   dlsim_batch_table_launch  one launch over every task; reads the grid size
  *                             from h_table and the descriptors from d_table
@@ -155,12 +166,12 @@ int dlsim_batch_table_launch(const void* h_table, const void* d_table, int dtype
  *
  * Replaces `torch.mean(torch.stack(chunks_at_idx), dim=0)` of
  * ChunkManager.reconstruct_model (simulation/conflux/chunk_manager.py:38-40),
- * which PyTorch computes as a sum over dim 0 followed by div_(n): the sum is
- * folded in input order from +0 and divided once (IEEE division). bf16: the
- * fp32 sum is rounded to bf16, then divided and rounded again. Bit-identical
- * to the reference while PyTorch's CPU dim-0 reduction is sequential (n <= 4);
- * for larger n PyTorch's order depends on sizes and thread count, so parity
- * is a tolerance. Same buffer and stream rules as dlsim_wreduce.
+ * which PyTorch computes as a sum over dim 0 followed by div_(n): here the
+ * sum is folded in input order from +0 in fp32 and divided once (IEEE
+ * division); bf16/f16 inputs are summed in fp32, divided and rounded once,
+ * for every n. PyTorch's own CPU order (cascade_sum) is
+ * dlsim_chunk_mean_batched; this input-order mean is off the reference path.
+ * Same buffer and stream rules as dlsim_wreduce.
  */
 int dlsim_mean(const void* const* d_inputs, int n, void* d_out, size_t n_elems, int dtype,
                void* stream);
@@ -173,7 +184,8 @@ int dlsim_mean(const void* const* d_inputs, int n, void* d_out, size_t n_elems, 
  * of fan_in. Replaces the per-chunk-index loop of
  * ChunkManager.reconstruct_model (simulation/conflux/chunk_manager.py:38-40):
  * every chunk index of one reconstruction (or of many) in one launch.
- * Results are bit-identical to b separate dlsim_mean calls.
+ * Results are bit-identical to b separate dlsim_mean calls in task order
+ * (cross-task overlaps are ordered as in dlsim_wreduce_batched).
  */
 int dlsim_mean_batched(int b, const int* fan_in, const void* const* d_inputs, void* const* d_outs,
                        const size_t* n_elems, int dtype, void* stream);
@@ -189,7 +201,8 @@ int dlsim_mean_batched(int b, const int* fan_in, const void* const* d_inputs, vo
  * ATen's cascade_sum (chunk_mean_kernels.hpp); bf16 chunks are summed in
  * fp32, divided and rounded once. Any fan-in up to 65535: up to 192 inputs
  * per launch travel as kernel arguments, larger ones through a stream-ordered
- * device array (hipMallocAsync / hipFreeAsync on `stream`).
+ * device array (hipMallocAsync / hipFreeAsync on `stream`). Tasks whose
+ * outputs overlap another task's buffers run one launch each, in order.
  * Replaces the per-index loop of ChunkManager.reconstruct_model.
  */
 int dlsim_chunk_mean_batched(int b, const int* fan_in, const void* const* d_inputs, void* const* d_outs,
@@ -311,8 +324,10 @@ int dlsim_shard_range(size_t n_elems, int world, int rank, size_t align_elems,
                       size_t* begin, size_t* end);
 
 /*
- * dlsim_probe_copy — streaming copy kernel (16 B/lane), used to measure the
- * device's achievable HBM copy ceiling next to the reduce. bytes % 16 == 0.
+ * dlsim_probe_copy — bit-exact copy through the reduce's own tile kernel
+ * (n = 1, same grid, lane map, nt loads and sc1 stores as the fp32 reduce of
+ * that size): the 1:1 read/write streaming ceiling of the access pattern,
+ * reported next to the reduce. bytes % 16 == 0, 16-B aligned, < 2 GiB.
  */
 int dlsim_probe_copy(const void* d_src, void* d_dst, size_t bytes, void* stream);
 
