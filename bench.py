@@ -1,30 +1,42 @@
 """bench.py — device-resident GB/s of the N-way weighted model-tensor reduce.
 
 Metric (BASELINE.json): "device-resident GB/s, N-way weighted model-tensor
-reduce; 1/2/4/8 MI355X". A step is one aggregate of one batch: one launch of
-the fused HIP reduce over N flat parameter arenas already resident in HBM
-(the arithmetic of FedAvg.aggregate, dasklearn/gradient_aggregation/fedavg.py:12-26).
+reduce; 1/2/4/8 MI355X". A step is one aggregate: one launch of the fused HIP
+reduce over N flat parameter arenas already resident in HBM (the arithmetic of
+FedAvg.aggregate, dasklearn/gradient_aggregation/fedavg.py:12-26).
 
 Workload (default, --config north_star): 8 models x 11,181,642 fp32 params
-(ResNet-18/CIFAR-10 size), Dirichlet(1) weights, DLSIM_EXACT (bit-identical
-to the reference). Multi-GPU: one process per GPU (torchrun); the parameter
-axis is sharded — each rank owns an 11,181,642-element slice of every model
-(weak scaling: the global parameter count grows with N) and reduces it with
-no data-path collective; `value` = bytes all ranks processed / max-over-ranks
-time. The RCCL all-gather that would materialise the full output is timed
-separately (`allgather`), never inside `value`.
+(ResNet-18/CIFAR-10 size), Dirichlet(1) weights, DLSIM_EXACT (bit-identical to
+the reference).
 
-Bytes per step per rank = (N_models + 1) * P * sizeof(dtype) (read N, write 1).
-Inputs rotate over 3 disjoint sets so the 256 MiB Infinity Cache cannot serve
-re-reads.
+Multi-GPU (one process per GPU). `python bench.py --gpus N` spawns its N rank
+processes itself (fresh interpreters started before anything touches the GPU,
+127.0.0.1 rendezvous); under torchrun the ranks come from the environment
+instead. The default is STRONG scaling of the named config: the parameter axis
+of the same aggregate is split into N contiguous 64-element-aligned slices
+(dlsim_shard_range), rank r reduces slice r of all N models with no data-path
+collective. `value` = the config's bytes x K / the max over ranks of each
+rank's HIP-event time around its K launches; the barriers that line the ranks
+up sit outside that window. The line carries the speed-up over the same
+config on one GPU (rank 0 times it alone, same K, same timing) and, in their
+own fields, the RCCL all-gather that would materialise the full output and
+the C ABI's sharded entry point (local reduce + grouped in-place broadcasts).
+--weak instead gives every rank the config's full parameter count.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config NAME]
+Bytes per step per rank = (N_models + 1) * P_rank * sizeof(dtype) (read N,
+write 1). Input sets rotate, with enough sets that their footprint is >= 1 GiB,
+so the 256 MiB Infinity Cache cannot serve re-reads (small slices included).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config NAME] [--weak]
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -35,12 +47,13 @@ for _p in (ROOT, PKG_ROOT):
         sys.path.insert(0, _p)
 
 import numpy as np  # noqa: E402
-import torch  # noqa: E402
+import torch  # noqa: E402  (importing torch does not initialise the GPU)
 import torch.distributed as dist  # noqa: E402
 
 METRIC = "device-resident GB/s, N-way weighted model-tensor reduce; 1/2/4/8 MI355X"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 RESNET18_P = 11_181_642
+MIN_SET_FOOTPRINT = 1 << 30  # rotate >= 1 GiB of inputs: 4x the 256 MiB Infinity Cache
 
 GNLENET_SHAPES = [(32, 3, 5, 5), (32,), (32,), (32,), (32, 32, 5, 5), (32,), (32,), (32,),
                   (64, 32, 5, 5), (64,), (64,), (64,), (10, 576), (10,)]
@@ -65,10 +78,10 @@ def resnet18_shapes():
 LAYOUTS = {"north_star": resnet18_shapes, "cfg3": resnet18_shapes, "cfg5": resnet18_shapes,
            "cfg2_gnlenet": lambda: GNLENET_SHAPES}
 
-# name: (n_models, params per rank, dtype, weights, description)
+# name: (n_models, params, dtype, weights, description)
 CONFIGS = {
     "north_star": (8, RESNET18_P, "f32", "dirichlet",
-                   "8-way Dirichlet-weighted fp32 reduce, 11,181,642 params/rank (ResNet-18/CIFAR-10)"),
+                   "8-way Dirichlet-weighted fp32 reduce, 11,181,642 params (ResNet-18/CIFAR-10)"),
     "cfg2": (8, 1_048_576, "f32", "uniform",
              "8-way unweighted fp32 average, 1,048,576 params (CIFAR-10 model, ~1 M label)"),
     "cfg2_gnlenet": (8, 85_354, "f32", "uniform",
@@ -76,40 +89,109 @@ CONFIGS = {
     "cfg3": (17, RESNET18_P, "f32", "dirichlet",
              "D-PSGD k=16 weighted neighbour mix, 17 x 11,181,642 fp32"),
     "cfg4": (2, 125_000_000, "bf16", "age",
-             "gossip 2-way bf16 merge, 125,000,000 params/rank, age weights [3/8, 5/8]"),
+             "gossip 2-way bf16 merge, 125,000,000 params, age weights [3/8, 5/8]"),
     "cfg5": (100, RESNET18_P, "f32", "dirichlet",
-             "FedAvg 100-client weighted fp32 reduce, 11,181,642 params/rank"),
+             "FedAvg 100-client weighted fp32 reduce, 11,181,642 params"),
     # not a BASELINE.json config: fp16 models through the same path
     "cfg4_f16": (2, 125_000_000, "f16", "age",
-                 "gossip 2-way fp16 merge, 125,000,000 params/rank, age weights [3/8, 5/8]"),
+                 "gossip 2-way fp16 merge, 125,000,000 params, age weights [3/8, 5/8]"),
 }
 
 TORCH_DTYPE = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16}
 ELEM_BYTES = {"f32": 4, "bf16": 2, "f16": 2}
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="north_star", choices=sorted(CONFIGS))
     ap.add_argument("--mode", default="exact", choices=["exact", "fast"])
-    ap.add_argument("--strong", action="store_true",
-                    help="strong scaling: split the config's params over ranks instead of per rank")
+    ap.add_argument("--weak", action="store_true",
+                    help="weak scaling: every rank reduces the config's full parameter count "
+                         "(default: strong scaling, the config's parameters split over the ranks)")
+    ap.add_argument("--strong", action="store_true", help="strong scaling (the default; kept for old scripts)")
     ap.add_argument("--slice-of", type=int, default=1,
                     help="1 GPU only: run rank 0's slice of a strong split over this many ranks "
-                         "(the per-rank work of --strong at that world size, without the other ranks)")
+                         "(the per-rank work of the strong split at that world size, without the other ranks)")
     ap.add_argument("--batch", type=int, default=1,
                     help="B independent aggregates of the config per step, in batched launches "
-                         "(dlsim_wreduce_batched; a simulated round's per-peer tasks)")
+                         "(a simulated round's per-peer tasks)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend: nccl (= RCCL over xGMI, the real path); gloo only "
                          "to rehearse the multi-process flow on a box with fewer GPUs than ranks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-single-gpu-reference", action="store_true",
+                    help="N > 1: skip rank 0's timing of the whole config alone (the speed-up base)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="budget for the CPU baseline sample (rank 0, N=1 only)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+# ---- process launch ----------------------------------------------------------------
+
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv, script: str = None) -> int:
+    """Start N rank processes of this script (fresh interpreters: this parent
+    never touches the GPU, and nothing is exec'd over it), wait for them and
+    return the first failing exit code (0 if all succeed). If one rank fails,
+    the others are stopped after a grace period instead of waiting forever in
+    a collective."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__), *argv], env=env))
+    rc, failed_at = 0, None
+    while True:
+        codes = [p.poll() for p in procs]
+        for c in codes:
+            if c not in (None, 0) and rc == 0:
+                rc, failed_at = c, time.monotonic()
+        if all(c is not None for c in codes):
+            return rc
+        if failed_at is not None and time.monotonic() - failed_at > 30:
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+            for p in procs:
+                p.wait()
+            return rc
+        time.sleep(0.05)
+
+
+# ---- timing ----------------------------------------------------------------------
+
+def time_steps(launch, k_steps: int, sync, barrier, new_event):
+    """Time exactly k_steps launches. The barrier that lines the ranks up and
+    a device sync come BEFORE the window; the window is two events on the
+    launch stream around the launches (plus a host clock from the first
+    launch to the sync after the last); the closing barrier comes AFTER the
+    window is read. Returns (event_ms, wall_ms) for all k_steps."""
+    barrier()
+    sync()
+    e0, e1 = new_event(), new_event()
+    t0 = time.perf_counter()
+    e0.record()
+    for k in range(k_steps):
+        launch(k)
+    e1.record()
+    sync()
+    wall_ms = (time.perf_counter() - t0) * 1e3
+    ev_ms = e0.elapsed_time(e1)
+    barrier()
+    return ev_ms, wall_ms
+
+
+def n_sets(bytes_per_set: int) -> int:
+    return max(3, min(256, math.ceil(MIN_SET_FOOTPRINT / max(1, bytes_per_set))))
 
 
 def weights_for(kind: str, n: int) -> list:
@@ -120,22 +202,86 @@ def weights_for(kind: str, n: int) -> list:
     return [float(1.0 / n)] * n  # fedavg.py:14-15
 
 
-def pmc_traffic(config: str, mode: str):
-    """Per-launch HBM bytes for this config from the committed PMC summary
-    (profiles/*pmc*.json, made by scripts/pmc_summary.py from rocprofv3 --pmc
-    runs of this same command; FETCH_SIZE doubled per the gfx950 rule)."""
+class ReduceWorkload:
+    """Rotating input sets and prepared launches of one config's aggregate on
+    one device: `launch(k)` runs step k (set k mod S)."""
+
+    def __init__(self, n, p, dtype, w32, mode, batch, dev, seed, stream):
+        from dasklearn_amd import _native
+        from dasklearn_amd.arena import row_stride
+        tdt = TORCH_DTYPE[dtype]
+        esz = ELEM_BYTES[dtype]
+        self.stream = stream
+        self.bytes_per_step = (n + 1) * p * esz * batch
+        self.sets = n_sets(self.bytes_per_step)
+        g = torch.Generator(device=dev).manual_seed(seed)
+        # rows padded to 256 B so every model's arena starts 16-byte aligned
+        # (the vector kernel's requirement), at the staging arena's stride
+        p_pad = row_stride(p, esz)
+        self.plans, self.probe_plans, self.outs, self._keep = [], [], [], []
+        for s in range(self.sets):
+            if batch == 1:
+                x = torch.empty((n, p_pad), dtype=tdt, device=dev)
+                x[:, :p].copy_((torch.randn((n, p), generator=g, device=dev) * 0.05).to(tdt))
+                out = torch.empty(p, dtype=tdt, device=dev)
+                plan = _native.ReducePlan([x[i, :p] for i in range(n)], w32, out, mode)
+                assert all(t.data_ptr() % 16 == 0 for t in plan._keep[0]), "arena rows must be 16-B aligned"
+                self.outs.append(out)
+            else:
+                x = torch.empty((batch, n, p_pad), dtype=tdt, device=dev)
+                x[:, :, :p].copy_((torch.randn((batch, n, p), generator=g, device=dev) * 0.05).to(tdt))
+                ob = torch.empty((batch, p_pad), dtype=tdt, device=dev)
+                plan = _native.BatchPlan([([x[b, i, :p] for i in range(n)], w32, ob[b, :p]) for b in range(batch)],
+                                         mode)
+                self.outs.append(ob[0, :p])
+            self.plans.append(plan)
+            if batch == 1:
+                self.probe_plans.append(_native.ReducePlan([x[i, :p] for i in range(n)], w32, out, mode, probe=True))
+            self._keep.append(x)
+        self.kernel = "dlsim::k_wreduce_tiles" if batch == 1 else "dlsim::k_wreduce_batch_table"
+
+    def launch(self, k):
+        self.plans[k % self.sets].launch(self.stream)
+
+    def launch_probe(self, k):
+        self.probe_plans[k % self.sets].launch(self.stream)
+
+
+def pattern_ceiling(wl, k_steps: int, sync, new_event, achieved_gbps: float):
+    """dlsim_probe_pattern over the same rotating sets: the reduce's own
+    dispatch (kernel, launch shape, nt loads, store policy) with the weighted
+    fold replaced by a bitwise XOR — what the memory system allows for exactly
+    this read/write mix, measured in the same run."""
+    for k in range(10):
+        wl.launch_probe(k)
+    ev_ms, _ = time_steps(wl.launch_probe, k_steps, sync, lambda: None, new_event)
+    us = ev_ms * 1e3 / k_steps
+    gbps = wl.bytes_per_step / (us * 1e-6) / 1e9
+    return {"GBps": round(gbps, 1), "frac": round(gbps / HBM_PEAK_GBPS, 4), "us_per_launch": round(us, 3),
+            "reduce_over_probe": round(achieved_gbps / gbps, 4),
+            "kernel": "dlsim_probe_pattern: same dispatch and shapes, XOR fold (memory only)"}
+
+
+def pmc_traffic(config: str, mode: str, split: int):
+    """Per-launch HBM bytes for this config (and strong split) from the
+    committed PMC summaries (profiles/*pmc*.json, scripts/pmc_summary.py over
+    rocprofv3 --pmc runs of this same command; FETCH_SIZE doubled per the
+    gfx950 rule). Returns (bytes, source file) or (None, reason)."""
     import glob
-    best = None
+    best, src = None, None
+    key = config if split <= 1 else f"{config}@slice{split}"
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
         try:
             with open(path) as f:
                 d = json.load(f)
         except Exception:
             continue
-        ent = d.get(config, {}).get(mode)
+        ent = d.get(key, {}).get(mode)
         if ent and "hbm_bytes_per_launch" in ent:
-            best = ent["hbm_bytes_per_launch"]
-    return best
+            best, src = ent["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
+    if best is None:
+        return None, f"no committed rocprofv3 --pmc summary for {key}/{mode}"
+    return best, src + " (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, separate passes; not measured in this run)"
 
 
 def _host_threads() -> int:
@@ -149,11 +295,11 @@ def _host_threads() -> int:
 def cpu_baseline(config, n, p, dtype, weights, budget_s):
     """The reference's aggregate as it runs in the simulator's worker: the
     op-for-op PyTorch-CPU restatement of FedAvg.aggregate (oracle/, validated
-    bit-identical to the reference) on N host modules with the workload's real
-    parameter layout (ResNet-18: 62 tensors), including the deepcopy of
-    models[0], at the worker's 4 threads (broker.py:31, session_settings.py:52).
-    A second, shorter sample at every host core this job may use goes under
-    "all_cores" (SURVEY.md §8d asks for both)."""
+    bit-identical to the reference and timed against it, profiles/r02_cpu_port_vs_reference.json)
+    on N host modules with the workload's real parameter layout (ResNet-18: 62
+    tensors), including the deepcopy of models[0], at the worker's 4 threads
+    (broker.py:31, session_settings.py:52). A second, shorter sample at every
+    host core this job may use goes under "all_cores" (SURVEY.md §8d)."""
     from torch import nn
     from oracle import fedavg_torch
     tdt = TORCH_DTYPE[dtype]
@@ -203,20 +349,16 @@ def cpu_baseline(config, n, p, dtype, weights, budget_s):
     return out
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus != 1:
-            print(f"bench.py: --gpus {args.gpus} needs torchrun with that many ranks", file=sys.stderr)
-            sys.exit(2)
+# ---- one rank -------------------------------------------------------------------
+
+def run_rank(args, rank: int, world: int, local: int):
+    from dasklearn_amd import _native
+
     ndev = torch.cuda.device_count()
     if args.backend == "nccl" and world > ndev:
-        print(f"bench.py: {world} ranks but {ndev} GPUs visible", file=sys.stderr)
-        sys.exit(2)
-    local_dev = local % max(1, ndev)  # gloo rehearsal may share a GPU
+        print(f"bench.py: {world} ranks but {ndev} GPUs visible (use --backend gloo to rehearse)", file=sys.stderr)
+        return 2
+    local_dev = local % max(1, ndev)  # a gloo rehearsal may share a GPU
     torch.cuda.set_device(local_dev)
     dev = torch.device("cuda", local_dev)
     backend_note = None
@@ -231,146 +373,82 @@ def main():
                 dist.init_process_group("gloo")
         else:
             dist.init_process_group("gloo")
-    # small control-plane tensors live where the backend can reduce them
-    cdev = dev if args.backend == "nccl" else torch.device("cpu")
-
-    from dasklearn_amd import _native
+    cdev = dev if args.backend == "nccl" else torch.device("cpu")  # control-plane tensors
+    barrier = (lambda: dist.barrier()) if world > 1 else (lambda: None)
 
     n, p_cfg, dtype, wkind, desc = CONFIGS[args.config]
-    if args.strong and world > 1:
-        b, e = _native.shard_range(p_cfg, world, rank, 64)
-        p = e - b
-    elif args.slice_of > 1 and world == 1:
-        b, e = _native.shard_range(p_cfg, args.slice_of, 0, 64)
-        p = e - b
-    else:
-        p = p_cfg
-    tdt = TORCH_DTYPE[dtype]
+    strong = world > 1 and not args.weak
+    split = world if strong else (args.slice_of if world == 1 else 1)
+    b0, e0 = _native.shard_range(p_cfg, split, rank if strong else 0, 64) if split > 1 else (0, p_cfg)
+    p = e0 - b0
     esz = ELEM_BYTES[dtype]
     mode = _native.DLSIM_EXACT if args.mode == "exact" else _native.DLSIM_FAST
     weights = weights_for(wkind, n)
     w32 = _native.fp32_weights(weights)
-
-    # 3 rotating input sets (each > 256 MiB Infinity Cache for the large configs)
-    sets = 3
-    g = torch.Generator(device=dev).manual_seed(1234 + rank)
-    arenas = []
-    # rows padded to 256 B so every model's arena starts 16-byte aligned
-    # (the vector kernel's requirement; unaligned rows would take the scalar
-    # path), at the staging arena's stride (4 KiB more at power-of-two strides)
-    from dasklearn_amd.arena import row_stride
-    p_pad = row_stride(p, esz)
-    for s in range(sets):
-        x = torch.empty((n, p_pad), dtype=tdt, device=dev)
-        for i in range(n):
-            x[i, :p].copy_(torch.randn(p, generator=g, device=dev) * 0.05)
-        arenas.append(x)
     B = max(1, args.batch)
-    if B == 1:
-        outs = [torch.empty(p, dtype=tdt, device=dev) for _ in range(sets)]
-        plans = [_native.ReducePlan([arenas[s][i, :p] for i in range(n)], w32, outs[s], mode)
-                 for s in range(sets)]
-        assert all(t.data_ptr() % 16 == 0 for t in plans[0]._keep[0]), "arena rows must be 16-B aligned"
-    else:
-        # B tasks per step, each with its own N input models (rows of a bigger
-        # arena block) and output; sets rotate as above
-        blocks = []
-        for s in range(sets):
-            x = torch.empty((B, n, p_pad), dtype=tdt, device=dev)
-            x.copy_(arenas[s].unsqueeze(0).expand(B, n, p_pad))
-            x.add_(torch.randn((B, 1, 1), generator=g, device=dev).to(tdt) * 0.01)
-            blocks.append(x)
-        del arenas
-        outs_b = [torch.empty((B, p_pad), dtype=tdt, device=dev) for _ in range(sets)]
-        plans = [_native.BatchPlan([([blocks[s][b, i, :p] for i in range(n)], w32, outs_b[s][b, :p])
-                                    for b in range(B)], mode) for s in range(sets)]
-        outs = [o[0, :p] for o in outs_b]
     stream = torch.cuda.current_stream(dev)
+    new_event = lambda: _StreamEvent(stream)  # noqa: E731
+    sync = lambda: torch.cuda.synchronize(dev)  # noqa: E731
 
+    wl = ReduceWorkload(n, p, dtype, w32, mode, B, dev, 1234 + rank, stream)
     for k in range(args.warmup):
-        plans[k % sets].launch(stream)
-    torch.cuda.synchronize(dev)
-
+        wl.launch(k)
     K = args.steps
-    # HIP events on the launch stream bracket the whole timed region: the
-    # per-launch kernel time is (elapsed / K), which includes the ~1-2 us
-    # launch boundaries between back-to-back kernels (so it is an upper bound
-    # of the rocprofv3 per-dispatch duration).
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for k in range(K):
-        plans[k % sets].launch(stream)
-    ev1.record(stream)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    kern_avg_ms = ev0.elapsed_time(ev1) / K
+    ev_ms, wall_ms = time_steps(wl.launch, K, sync, barrier, new_event)
 
-    bytes_per_launch = (n + 1) * p * esz * B
-    el_t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
-    tot_b = torch.tensor([bytes_per_launch * K], dtype=torch.float64, device=cdev)
+    stats = torch.tensor([ev_ms, wall_ms, float(wl.bytes_per_step) * K], dtype=torch.float64, device=cdev)
+    per_rank_us = torch.tensor([ev_ms / K * 1e3], dtype=torch.float64, device=cdev)
     if world > 1:
-        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
-        dist.all_reduce(tot_b, op=dist.ReduceOp.SUM)
-    max_el = float(el_t.item())
-    total_bytes = float(tot_b.item())
-    value = total_bytes / max_el / 1e9
+        mx = stats[:2].clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        tot = stats[2:].clone()
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        gathered = [torch.zeros_like(per_rank_us) for _ in range(world)]
+        dist.all_gather(gathered, per_rank_us)
+        max_ev, max_wall, total_bytes = float(mx[0]), float(mx[1]), float(tot[0])
+        rank_us = [round(float(t.item()), 3) for t in gathered]
+    else:
+        max_ev, max_wall, total_bytes = ev_ms, wall_ms, float(wl.bytes_per_step) * K
+        rank_us = [round(ev_ms / K * 1e3, 3)]
+    value = total_bytes / (max_ev * 1e-3) / 1e9
 
-    # copy ceiling on this device (same footprint as one step), reported beside
-    cb = min(bytes_per_launch // 2, 1 << 30) & ~15
-    src = torch.empty(cb, dtype=torch.uint8, device=dev).fill_(1)
-    dst = torch.empty_like(src)
-    for _ in range(5):
-        _native.probe_copy(src, dst)
-    c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    c0.record(stream)
-    for _ in range(20):
-        _native.probe_copy(src, dst)
-    c1.record(stream)
-    torch.cuda.synchronize(dev)
-    copy_gbps = 2 * cb * 20 / (c0.elapsed_time(c1) * 1e-3) / 1e9
-    del src, dst
-
-    allgather = None
+    # ---- N > 1: the output all-gather, in its own fields -----------------------
+    gather = None
     if world > 1:
-        # slices can differ by one 64-element unit under --strong: pad to the widest
-        width = p
-        if args.strong:
-            width = max(e - b for b, e in (_native.shard_range(p_cfg, world, r, 64) for r in range(world)))
-        shard = torch.zeros(width, dtype=tdt, device=dev)
-        shard[:p].copy_(outs[0])
-        if args.backend != "nccl":
-            shard = shard.cpu()
-        full = torch.empty(width * world, dtype=tdt, device=shard.device)
-        for _ in range(3):
-            dist.all_gather_into_tensor(full, shard)
-        torch.cuda.synchronize(dev)
-        dist.barrier()
-        a0 = time.perf_counter()
-        reps = 10
-        for _ in range(reps):
-            dist.all_gather_into_tensor(full, shard)
-        torch.cuda.synchronize(dev)
-        ag_ms = (time.perf_counter() - a0) / reps * 1e3
-        agt = torch.tensor([ag_ms], dtype=torch.float64, device=cdev)
-        dist.all_reduce(agt, op=dist.ReduceOp.MAX)
-        allgather = {"ms": round(float(agt.item()), 4),
-                     "bytes_out_per_rank": width * esz * world,
-                     "note": ("RCCL" if args.backend == "nccl" else "gloo (rehearsal)")
-                             + " all_gather_into_tensor of the reduced shards (not in value)"}
+        gather = _time_gathers(args, wl, rank, world, p_cfg, p, n, w32, mode, dtype, dev, cdev, stream, strong, barrier)
+
+    # ---- N > 1 strong: the same config on one GPU (rank 0 alone) ----------------
+    single = None
+    if strong and not args.no_single_gpu_reference:
+        barrier()
+        if rank == 0:
+            full = ReduceWorkload(n, p_cfg, dtype, w32, mode, B, dev, 99, stream)
+            for k in range(args.warmup):
+                full.launch(k)
+            t1_ms, _ = time_steps(full.launch, K, sync, lambda: None, new_event)
+            single = {"ms_per_step": round(t1_ms / K, 6),
+                      "speedup": round((t1_ms / K) / (max_ev / K), 3),
+                      "note": f"T1 = the whole {args.config} aggregate on rank 0's GPU alone, {K} launches, "
+                              f"same event timing; speedup = T1 / T{world} (max over ranks)"}
+            del full
+        barrier()
 
     result = None
     if rank == 0:
-        achieved = bytes_per_launch / (kern_avg_ms * 1e-3) / 1e9
-        # PMC bytes were profiled for the plain single-task, per-rank-shard run
-        traffic = pmc_traffic(args.config, args.mode) if (B == 1 and not args.strong and args.slice_of <= 1) \
-            else None
+        achieved = wl.bytes_per_step / (ev_ms / K * 1e-3) / 1e9
+        traffic, traffic_src = (pmc_traffic(args.config, args.mode, split) if B == 1
+                                else (None, "no committed PMC summary for batched launches"))
+        probe = pattern_ceiling(wl, K, sync, new_event, achieved) if B == 1 else None
+        scaling = "weak" if args.weak and world > 1 else "strong"
+        workload = args.config + ": " + desc
+        if B > 1:
+            workload += f" x {B} tasks per launch"
+        if strong:
+            workload += f" (strong scaling: {p_cfg} params split over {world} ranks)"
+        elif args.weak and world > 1:
+            workload += f" (weak scaling: {p_cfg} params per rank)"
+        elif split > 1:
+            workload += f" (rank 0's slice of a {split}-rank strong split, alone on 1 GPU)"
         result = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -378,33 +456,35 @@ def main():
             "n_gpus": world,
             "steps": K,
             "warmup": args.warmup,
-            "ms_per_step": round(max_el / K * 1e3, 5),
+            "ms_per_step": round(max_ev / K, 6),
             "higher_is_better": True,
-            "scaling": "strong" if (args.strong and world > 1) else "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": dtype,
-            "data": "synthetic: torch.randn*0.05 on device, 3 rotating input sets; "
-                    f"{wkind} weights",
-            "config": {"workload": args.config + ": " + desc + (f" x {B} tasks per launch" if B > 1 else "")
-                       + (f" (strong scaling: {p_cfg} params split over {world} ranks)" if args.strong and world > 1 else "")
-                       + (f" (rank 0's slice of a {args.slice_of}-rank strong split, alone on 1 GPU)"
-                          if args.slice_of > 1 and world == 1 else ""),
+            "data": f"synthetic: torch.randn*0.05 on device, {wl.sets} rotating input sets "
+                    f"(>= 1 GiB); {wkind} weights",
+            "config": {"workload": workload,
                        "backend": (backend_note or args.backend) if world > 1 else None,
-                       "n_models": n, "params_per_rank": p, "tasks_per_step": B,
-                       "mode": args.mode, "parallelism": f"param-shard x{world}",
-                       "bytes_per_step_per_rank": bytes_per_launch},
+                       "n_models": n, "params_total": p_cfg if strong or split > 1 else p * world,
+                       "params_rank0": p, "tasks_per_step": B, "mode": args.mode,
+                       "parallelism": f"param-shard x{world}",
+                       "bytes_per_step_rank0": wl.bytes_per_step},
+            "timing": {"value_from": "HIP events around the K launches on each rank's launch stream; "
+                                     "value = all ranks' bytes / max over ranks; barriers outside the window",
+                       "kernel_avg_us_per_rank": rank_us,
+                       "wall_ms_per_step_max": round(max_wall / K, 6)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                         "traffic": traffic,
-                         "kernel": "dlsim::k_wreduce_tiles" if B == 1 else "dlsim::k_wreduce_batch",
-                         "kernel_avg_us": round(kern_avg_ms * 1e3, 2),
-                         "timing": "HIP events around the K timed launches on the launch stream"},
-            "copy_ceiling_GBps": round(copy_gbps, 1),
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "kernel": wl.kernel, "kernel_avg_us": round(ev_ms / K * 1e3, 3),
+                         "timing": "rank 0: HIP events around the K timed launches on the launch stream"},
+            "pattern_ceiling": probe,
         }
-        if allgather:
-            result["allgather"] = allgather
-    if world > 1:
-        dist.barrier()
+        if single:
+            result["single_gpu_reference"] = single
+        if gather:
+            result["allgather"] = gather
+    barrier()
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(args.config, n, p, dtype, weights, args.cpu_seconds)
@@ -413,7 +493,99 @@ def main():
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
+
+
+class _StreamEvent:
+    """A timing event recorded on a given stream (torch.cuda.Event.record()
+    without an argument would use the current stream)."""
+
+    def __init__(self, stream):
+        self.stream = stream
+        self.ev = torch.cuda.Event(enable_timing=True)
+
+    def record(self):
+        self.ev.record(self.stream)
+
+    def elapsed_time(self, other):
+        return self.ev.elapsed_time(other.ev)
+
+
+def _time_gathers(args, wl, rank, world, p_cfg, p, n, w32, mode, dtype, dev, cdev, stream, strong, barrier):
+    """The collective that would materialise the full output, timed apart
+    from `value`: (a) RCCL all_gather_into_tensor of width-padded slices
+    (torch), (b) on an RCCL group, the C ABI's dlsim_wreduce_sharded end to
+    end (this rank's reduce into the full buffer + grouped in-place
+    ncclBroadcast of every rank's slice, a variable-size all-gather)."""
+    from dasklearn_amd import _native
+    tdt = TORCH_DTYPE[dtype]
+    esz = ELEM_BYTES[dtype]
+    width = max(e - b for b, e in (_native.shard_range(p_cfg, world, r, 64) for r in range(world))) \
+        if strong else p
+    shard = torch.zeros(width, dtype=tdt, device=dev)
+    shard[:p].copy_(wl.outs[0])
+    if args.backend != "nccl":
+        shard = shard.cpu()
+    full = torch.empty(width * world, dtype=tdt, device=shard.device)
+    reps = 20
+    for _ in range(3):
+        dist.all_gather_into_tensor(full, shard)
+    torch.cuda.synchronize(dev)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        dist.all_gather_into_tensor(full, shard)
+    torch.cuda.synchronize(dev)
+    ag_ms = (time.perf_counter() - t0) / reps * 1e3
+    out = {"all_gather_into_tensor_ms": ag_ms,
+           "bytes_out_per_rank": width * esz * world,
+           "note": ("RCCL" if args.backend == "nccl" else "gloo (rehearsal)")
+                   + " collectives of the reduced slices; host clock over 20 back-to-back ops after a sync; "
+                     "not in value"}
+    if args.backend == "nccl" and strong:
+        try:
+            pg = dist.distributed_c10d._get_default_group()
+            comm = int(pg._get_backend(dev)._comm_ptr())
+            slices = [wl.plans[0]._keep[0][i] for i in range(n)]
+            fullout = torch.empty(p_cfg, dtype=tdt, device=dev)
+            for _ in range(3):
+                _native.wreduce_sharded(slices, w32, fullout, comm, True, mode, stream)
+            torch.cuda.synchronize(dev)
+            barrier()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(reps):
+                _native.wreduce_sharded(slices, w32, fullout, comm, True, mode, stream)
+            e1.record(stream)
+            torch.cuda.synchronize(dev)
+            out["dlsim_wreduce_sharded_gather_ms"] = e0.elapsed_time(e1) / reps
+            out["sharded_note"] = ("dlsim_wreduce_sharded(gather=1) on the group's RCCL communicator: local reduce "
+                                   "+ grouped in-place ncclBroadcast, HIP events on the launch stream")
+        except Exception as e:  # report, do not fail the bench line
+            out["dlsim_wreduce_sharded_error"] = f"{type(e).__name__}: {e}"[:300]
+    t = torch.tensor([out["all_gather_into_tensor_ms"], out.get("dlsim_wreduce_sharded_gather_ms", 0.0)],
+                     dtype=torch.float64, device=cdev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    out["all_gather_into_tensor_ms"] = round(float(t[0]), 4)
+    if "dlsim_wreduce_sharded_gather_ms" in out:
+        out["dlsim_wreduce_sharded_gather_ms"] = round(float(t[1]), 4)
+    return out
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # self-launch: one fresh process per GPU, started before any GPU call
+        return spawn_ranks(args.gpus, argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        return 2
+    return run_rank(args, rank, world, local)
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

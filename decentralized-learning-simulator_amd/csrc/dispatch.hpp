@@ -1,0 +1,646 @@
+// dispatch.hpp — host-side dispatch of the reduce kernels (launch shapes,
+// fan-in slots, size classes, batches, descriptor tables, chunk-mean tasks),
+// shared by the C ABI (dlsim_abi.hip) and the per-policy instantiation units
+// (inst_*.hip). The ABI unit declares every per-policy entry `extern
+// template`; each inst_*.hip instantiates the ones of its element policies,
+// so the device code of the policies compiles in parallel translation units.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <type_traits>
+#include <vector>
+
+#include "dlsim.h"
+#include "wreduce_kernels.hpp"
+#include "chunk_mean_kernels.hpp"
+
+namespace dlsim_host __attribute__((visibility("hidden"))) {
+
+// error reporting of the ABI (dlsim_abi.hip): set the thread's message, return code
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int hip_fail(hipError_t e, const char* what);
+
+// Launch shape (tuned on MI355X with csrc/tune_wreduce.hip):
+// 4 vectors of 16 B per lane (a 16 KiB tile per stream per block), one tile
+// per block, non-temporal loads and stores. Small fan-in runs a kernel
+// specialised on n (all n*4 loads issued back to back, fewer VGPRs than the
+// grouped loop); larger n folds groups of G inputs. The specialised kernels
+// are used only while they fit in 256 VGPRs (two waves per SIMD): past that
+// the measured rate drops by up to 20% (profiles/r01_sweep_fanin_*.jsonl).
+constexpr int kVpt = 4;
+constexpr bool kNT = true;
+// Output stores are buffer_store_dwordx4 with sc1 (write-through): no dirty
+// output lines are left in L2 for the kernel-boundary writeback, which was
+// worth 3-4% per launch on the north star (profiles/r01_tune_store_*.log).
+// The buffer's 32-bit byte offsets cap one launch's output at 2 GiB; longer
+// outputs are split into independent launches over element ranges.
+constexpr int kStore = 16;  // sc1
+// Per element type (profiles/r01_tune_*): fp32 takes sc1 write-through stores
+// and the wave-contiguous lane map (each wave sweeps 4 KiB per stream, +1.3%
+// on the north star); bf16, whose output is a third of the traffic in the
+// 2-way merge, keeps non-temporal stores (+2% there) and the block map.
+// These are the policies of the grouped (runtime fan-in) kernel and of the
+// batched kernels.
+// fp64 elements take the fp32 shapes (a 16-byte vector is 4 VGPRs in both).
+template <class Op> constexpr int store_policy() { return Op::kBytes >= 4 ? kStore : dlsim::kStNT; }
+template <class Op> constexpr bool wave_map() { return Op::kBytes >= 4; }
+constexpr size_t kMaxLaunchOutBytes = (size_t{1} << 31) - (size_t{1} << 20);
+template <class Op> constexpr int max_fixed_fan_in() { return Op::kBytes >= 4 ? 14 : 9; }
+template <class Op> constexpr int group_size() { return Op::kBytes >= 4 ? 8 : 4; }
+
+// Launch shape of the fixed fan-in kernels, chosen by the per-stream size
+// class (size sweeps with arena rows as in bench.py and >= 1 GiB of rotating
+// inputs: profiles/r01_tune_shape_sweep.log, profiles/r02_tune_slices/):
+//   fp32  < 2 M elements   : VPT 2, block map, sc1 (+7% at the 8-rank slice
+//                            of the north star, 1.4 M: 9.85 vs 10.57 us)
+//   fp32  2 M .. 5 M       : VPT 4, block map, sc1 (1-4% over the wave map)
+//   fp32 >= 5 M            : VPT 4, wave map,  sc1 (~1% at 6-11 M)
+//   bf16  < 48 M elements  : VPT 1, wave map, sc1  (+7-12% at 4-33 M for n = 2)
+//   bf16 >= 48 M           : VPT 4, block map, nt  (+1.5-2.5% at 64-125 M)
+struct Shape {
+  int vpt;
+  int store;
+  bool wave;
+};
+template <class Op, int C> constexpr Shape fixed_shape() {
+  if constexpr (Op::kBytes >= 4) {
+    if constexpr (C == 0) return Shape{2, kStore, false};
+    else if constexpr (C == 1) return Shape{4, kStore, false};
+    else return Shape{4, kStore, true};
+  } else {
+    if constexpr (C < 2) return Shape{1, kStore, true};
+    else return Shape{4, dlsim::kStNT, false};
+  }
+}
+template <class Op> int size_class(size_t nelem) {
+  const size_t bytes = nelem * Op::kBytes;  // per stream
+  if constexpr (Op::kBytes >= 4) return bytes < 8000000 ? 0 : bytes < 20000000 ? 1 : 2;
+  else return bytes < 96000000 ? 0 : 2;
+}
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+template <class Op, class S, int NF, int VPT, int STP, bool WAVE>
+hipError_t launch_shape(const S& s, int n, void* out, size_t nelem, hipStream_t st) {
+  const size_t nvec = nelem / Op::E;
+  const size_t tile = static_cast<size_t>(dlsim::kBlock) * VPT;
+  const size_t blocks = nvec / tile + 1;  // full tiles + one block for the ragged end
+  if (blocks > 0x7fffffffu) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((dlsim::k_wreduce_tiles<Op, S, NF, group_size<Op>(), VPT, kNT, STP, WAVE>),
+                     dim3(static_cast<unsigned>(blocks)), dim3(dlsim::kBlock), 0, st, s, n, out, nvec, nelem);
+  return hipGetLastError();
+}
+
+template <class Op, class S, int NF, int C>
+hipError_t launch_class(const S& s, int n, void* out, size_t nelem, hipStream_t st) {
+  constexpr Shape k = fixed_shape<Op, C>();
+  return launch_shape<Op, S, NF, k.vpt, k.store, k.wave>(s, n, out, nelem, st);
+}
+
+template <class Op, class S, int NF>
+hipError_t launch_tiles(const S& s, int n, void* out, size_t nelem, hipStream_t st) {
+  if constexpr (NF > 0) {
+    switch (size_class<Op>(nelem)) {
+      case 0: return launch_class<Op, S, NF, 0>(s, n, out, nelem, st);
+      case 1: return launch_class<Op, S, NF, 1>(s, n, out, nelem, st);
+      default: return launch_class<Op, S, NF, 2>(s, n, out, nelem, st);
+    }
+  } else {
+    return launch_shape<Op, S, 0, kVpt, store_policy<Op>(), wave_map<Op>()>(s, n, out, nelem, st);
+  }
+}
+
+template <class Op, int K>
+hipError_t launch_fixed_k(const dlsim::Slots<16, dlsim::wt_t<Op>>& s, int n, void* out, size_t nelem,
+                          hipStream_t st) {
+  if constexpr (K > max_fixed_fan_in<Op>()) {
+    return hipErrorInvalidValue;
+  } else {
+    if (n == K) return launch_tiles<Op, dlsim::Slots<16, dlsim::wt_t<Op>>, K>(s, n, out, nelem, st);
+    return launch_fixed_k<Op, K + 1>(s, n, out, nelem, st);
+  }
+}
+
+template <class Op, class S>
+hipError_t launch_any(const S& s, int n, void* out, size_t nelem, bool vec, hipStream_t st) {
+  if (vec) {
+    if constexpr (std::is_same<S, dlsim::Slots<16, dlsim::wt_t<Op>>>::value) {
+      if (n <= max_fixed_fan_in<Op>()) return launch_fixed_k<Op, 1>(s, n, out, nelem, st);
+    }
+    return launch_tiles<Op, S, 0>(s, n, out, nelem, st);
+  }
+  const size_t blocks = (nelem + dlsim::kBlock - 1) / dlsim::kBlock;
+  if (blocks > 0x7fffffffu) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((dlsim::k_wreduce_scalar<Op, S>), dim3(static_cast<unsigned>(blocks)), dim3(dlsim::kBlock), 0,
+                     st, s, n, out, nelem);
+  return hipGetLastError();
+}
+
+template <int NB, class W>
+void fill_slots(dlsim::Slots<NB, W>& s, const void* const* in, const W* w, int n, float div) {
+  std::memset(&s, 0, sizeof(s));
+  for (int i = 0; i < n; ++i) {
+    s.p[i] = in[i];
+    s.w[i] = w ? w[i] : 1.0f;
+  }
+  s.div = div;
+}
+
+// One launch over [0, nelem) of n inputs: every output element is written
+// once, after all n of its terms are folded in input order. Up to
+// DLSIM_MAX_FUSED_INPUTS inputs travel as kernel arguments; above that the
+// pointer/weight table goes to a stream-ordered device buffer (the pageable
+// host copy is staged by the runtime before hipMemcpyAsync returns).
+// div: final divisor (the mean policies; 1 for the weighted reduce).
+template <class Op>
+int run_range(const void* const* in, int n, const dlsim::wt_t<Op>* w, void* out, size_t nelem, bool vec, float div,
+              hipStream_t st) {
+  using W = dlsim::wt_t<Op>;
+  hipError_t e;
+  if (n <= 16) {
+    dlsim::Slots<16, W> s;
+    fill_slots(s, in, w, n, div);
+    e = launch_any<Op>(s, n, out, nelem, vec, st);
+  } else if (n <= DLSIM_MAX_FUSED_INPUTS) {
+    dlsim::Slots<DLSIM_MAX_FUSED_INPUTS, W> s;
+    fill_slots(s, in, w, n, div);
+    e = launch_any<Op>(s, n, out, nelem, vec, st);
+  } else {
+    const size_t pbytes = static_cast<size_t>(n) * sizeof(void*);
+    std::vector<unsigned char> h(pbytes + static_cast<size_t>(n) * sizeof(W));
+    std::memcpy(h.data(), in, pbytes);
+    for (int i = 0; i < n; ++i) {
+      const W wi = w ? w[i] : W(1);
+      std::memcpy(h.data() + pbytes + static_cast<size_t>(i) * sizeof(W), &wi, sizeof(W));
+    }
+    void* d = nullptr;
+    e = hipMallocAsync(&d, h.size(), st);
+    if (e != hipSuccess) return hip_fail(e, "fan-in table alloc");
+    e = hipMemcpyAsync(d, h.data(), h.size(), hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) {
+      const dlsim::DevSlots<W> s{static_cast<const void* const*>(d),
+                                 reinterpret_cast<const W*>(static_cast<unsigned char*>(d) + pbytes), div};
+      e = launch_any<Op>(s, n, out, nelem, vec, st);
+    }
+    const hipError_t e2 = hipFreeAsync(d, st);
+    if (e == hipSuccess) e = e2;
+  }
+  if (e != hipSuccess) return hip_fail(e, "kernel launch");
+  return DLSIM_OK;
+}
+
+// Elements are independent: an output longer than one launch's 2 GiB store
+// window is reduced as consecutive ranges (pointers offset by the range start).
+template <class Op>
+int run(const void* const* in, int n, const dlsim::wt_t<Op>* w, void* out, size_t nelem, hipStream_t st,
+        float div = 1.0f) {
+  if (nelem == 0) return DLSIM_OK;
+  bool vec = aligned16(out);
+  for (int i = 0; i < n && vec; ++i) vec = aligned16(in[i]);
+  const size_t chunk = kMaxLaunchOutBytes / Op::kBytes;  // multiple of every tile size
+  if (!vec || nelem <= chunk) return run_range<Op>(in, n, w, out, nelem, vec, div, st);
+  std::vector<const void*> sub(static_cast<size_t>(n));
+  for (size_t b = 0; b < nelem; b += chunk) {
+    const size_t len = std::min(chunk, nelem - b);
+    for (int i = 0; i < n; ++i) sub[i] = static_cast<const char*>(in[i]) + b * Op::kBytes;
+    int rc = run_range<Op>(sub.data(), n, w, static_cast<char*>(out) + b * Op::kBytes, len, vec, div, st);
+    if (rc != DLSIM_OK) return rc;
+  }
+  return DLSIM_OK;
+}
+
+// ---- cross-task hazards of the batched entry points ---------------------------
+// A batched launch runs its tasks concurrently; b separate calls run them in
+// order. They agree unless one task writes bytes another task reads or
+// writes. Detected in O((inputs + b) log b): the output spans are sorted (any
+// overlap among them shows between neighbours), then each input span is
+// looked up among them. A task's exact in-place alias of its own input is
+// fine (one lane reads every term of an element before writing it).
+struct Span {
+  uintptr_t a, b;
+  int task;
+};
+
+inline bool cross_task_overlap(int nt, const int* fan_in, const void* const* in, void* const* outs, const size_t* nelem,
+                        size_t esz) {
+  std::vector<Span> wr;
+  wr.reserve(static_cast<size_t>(nt));
+  for (int t = 0; t < nt; ++t) {
+    if (nelem[t] == 0) continue;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(outs[t]);
+    wr.push_back({a, a + nelem[t] * esz, t});
+  }
+  std::sort(wr.begin(), wr.end(), [](const Span& x, const Span& y) { return x.a < y.a; });
+  for (size_t k = 1; k < wr.size(); ++k)
+    if (wr[k].a < wr[k - 1].b) return true;  // two outputs overlap (disjoint otherwise: ends sorted too)
+  size_t off = 0;
+  for (int t = 0; t < nt; ++t) {
+    const size_t bytes = nelem[t] * esz;
+    for (int i = 0; i < fan_in[t]; ++i) {
+      if (bytes == 0) continue;
+      const uintptr_t a = reinterpret_cast<uintptr_t>(in[off + i]), b = a + bytes;
+      auto it = std::upper_bound(wr.begin(), wr.end(), a, [](uintptr_t v, const Span& x) { return v < x.b; });
+      for (; it != wr.end() && it->a < b; ++it)
+        if (it->task != t) return true;
+    }
+    off += static_cast<size_t>(fan_in[t]);
+  }
+  return false;
+}
+
+// ---- batched launches ---------------------------------------------------------
+template <class Op, int NF>
+hipError_t launch_batch_nf(const dlsim::BatchSlots& s, unsigned blocks, hipStream_t st) {
+  hipLaunchKernelGGL((dlsim::k_wreduce_batch<Op, NF, group_size<Op>(), kVpt, kNT, store_policy<Op>()>), dim3(blocks),
+                     dim3(dlsim::kBlock), 0, st, s);
+  return hipGetLastError();
+}
+
+template <class Op, int K>
+hipError_t launch_batch_fixed(const dlsim::BatchSlots& s, int n, unsigned blocks, hipStream_t st) {
+  if constexpr (K > max_fixed_fan_in<Op>()) {
+    return launch_batch_nf<Op, 0>(s, blocks, st);
+  } else {
+    if (n == K) return launch_batch_nf<Op, K>(s, blocks, st);
+    return launch_batch_fixed<Op, K + 1>(s, n, blocks, st);
+  }
+}
+
+// Fill and launch BatchSlots with tasks [t0, t1); all tasks vector-eligible.
+// divs: per-task final divisor (the mean policies), nullptr = 1.
+template <class Op>
+hipError_t launch_batch(const int* fan_in, const size_t* in_off, const void* const* in, const float* w,
+                        const float* divs, void* const* outs, const size_t* nelem, int t0, int t1,
+                        hipStream_t st) {
+  dlsim::BatchSlots s;
+  std::memset(&s, 0, sizeof(s));
+  const size_t tile = static_cast<size_t>(dlsim::kBlock) * kVpt;
+  uint32_t blocks = 0;
+  int ptrs = 0;
+  bool uniform = true;
+  for (int t = t0; t < t1; ++t) {
+    const int k = t - t0;
+    const size_t nvec = nelem[t] / Op::E;
+    s.out[k] = outs[t];
+    s.nvec[k] = nvec;
+    s.nelem[k] = nelem[t];
+    s.block_start[k] = blocks;
+    s.ptr_off[k] = static_cast<uint16_t>(ptrs);
+    s.fan_in[k] = static_cast<uint16_t>(fan_in[t]);
+    s.div[k] = divs ? divs[t] : 1.0f;
+    for (int i = 0; i < fan_in[t]; ++i) {
+      s.p[ptrs + i] = in[in_off[t] + i];
+      s.w[ptrs + i] = w[in_off[t] + i];
+    }
+    ptrs += fan_in[t];
+    blocks += static_cast<uint32_t>(nvec / tile + 1);
+    uniform = uniform && fan_in[t] == fan_in[t0];
+  }
+  s.ntasks = t1 - t0;
+  s.block_start[t1 - t0] = blocks;
+  if (uniform) return launch_batch_fixed<Op, 1>(s, fan_in[t0], blocks, st);
+  return launch_batch_nf<Op, 0>(s, blocks, st);
+}
+
+template <class Op>
+int run_batched(int b, const int* fan_in, const void* const* in, const float* w, void* const* outs,
+                const size_t* nelem, hipStream_t st, const float* divs = nullptr) {
+  std::vector<size_t> off(static_cast<size_t>(b) + 1, 0);
+  for (int t = 0; t < b; ++t) off[t + 1] = off[t] + static_cast<size_t>(fan_in[t]);
+  if (cross_task_overlap(b, fan_in, in, outs, nelem, Op::kBytes)) {
+    // A task reads or writes another task's output: keep the semantics of b
+    // separate calls by running the tasks one launch each, in order.
+    for (int t = 0; t < b; ++t) {
+      int rc = run<Op>(in + off[t], fan_in[t], w + off[t], outs[t], nelem[t], st, divs ? divs[t] : 1.0f);
+      if (rc != DLSIM_OK) return rc;
+    }
+    return DLSIM_OK;
+  }
+  const size_t tile = static_cast<size_t>(dlsim::kBlock) * kVpt;
+  auto batchable = [&](int t) {
+    if (nelem[t] == 0 || fan_in[t] > 16) return false;
+    if (nelem[t] * Op::kBytes > kMaxLaunchOutBytes) return false;
+    if (!aligned16(outs[t])) return false;
+    for (int i = 0; i < fan_in[t]; ++i)
+      if (!aligned16(in[off[t] + i])) return false;
+    return true;
+  };
+  // Tasks that cannot ride in a batch (large fan-in, misaligned, > 2 GiB) go
+  // alone (no task touches another's output, so the order is free).
+  std::vector<int> group;
+  for (int t = 0; t < b; ++t) {
+    if (batchable(t)) {
+      group.push_back(t);
+      continue;
+    }
+    if (nelem[t] == 0) continue;
+    int rc = run<Op>(in + off[t], fan_in[t], w + off[t], outs[t], nelem[t], st, divs ? divs[t] : 1.0f);
+    if (rc != DLSIM_OK) return rc;
+  }
+  // Pack the rest greedily into kernel-argument batches, in task order.
+  std::vector<const void*> ins;
+  std::vector<float> ws, dv;
+  std::vector<void*> os;
+  std::vector<size_t> ne, ioff;
+  std::vector<int> fi;
+  for (int t : group) {
+    ioff.push_back(ins.size());
+    for (int i = 0; i < fan_in[t]; ++i) {
+      ins.push_back(in[off[t] + i]);
+      ws.push_back(w[off[t] + i]);
+    }
+    os.push_back(outs[t]);
+    ne.push_back(nelem[t]);
+    fi.push_back(fan_in[t]);
+    dv.push_back(divs ? divs[t] : 1.0f);
+  }
+  const int g = static_cast<int>(group.size());
+  int t0 = 0;
+  while (t0 < g) {
+    int t1 = t0, ptrs = 0;
+    uint64_t blocks = 0;
+    while (t1 < g && t1 - t0 < dlsim::kBatchMaxTasks && ptrs + fi[t1] <= dlsim::kBatchMaxPtrs &&
+           blocks + ne[t1] / Op::E / tile + 1 < 0x7fffffffull) {
+      ptrs += fi[t1];
+      blocks += ne[t1] / Op::E / tile + 1;
+      ++t1;
+    }
+    hipError_t e = launch_batch<Op>(fi.data(), ioff.data(), ins.data(), ws.data(), dv.data(), os.data(),
+                                    ne.data(), t0, t1, st);
+    if (e != hipSuccess) return hip_fail(e, "batched kernel launch");
+    t0 = t1;
+  }
+  return DLSIM_OK;
+}
+
+// ---- descriptor-table batches ---------------------------------------------------
+struct TableLayout {
+  size_t tasks_off, map_off, ptrs_off, w_off, bytes;
+  uint32_t nblocks;
+};
+
+inline size_t round8(size_t x) { return (x + 7) / 8 * 8; }
+
+template <class Op>
+uint32_t task_blocks(size_t nelem) {
+  const size_t tile = static_cast<size_t>(dlsim::kBlock) * kVpt;
+  return static_cast<uint32_t>(nelem / Op::E / tile + 1);
+}
+
+template <class Op>
+bool table_layout(int b, const int* fan_in, const size_t* nelem, TableLayout* L) {
+  uint64_t blocks = 0, ptrs = 0;
+  for (int t = 0; t < b; ++t) {
+    blocks += task_blocks<Op>(nelem[t]);
+    ptrs += static_cast<uint64_t>(fan_in[t]);
+  }
+  if (blocks >= 0x7fffffffull) return false;
+  L->nblocks = static_cast<uint32_t>(blocks);
+  L->tasks_off = round8(sizeof(dlsim::BatchTableHeader));
+  L->map_off = round8(L->tasks_off + sizeof(dlsim::BatchTaskDesc) * static_cast<size_t>(b));
+  L->ptrs_off = round8(L->map_off + sizeof(uint32_t) * static_cast<size_t>(blocks));
+  L->w_off = round8(L->ptrs_off + sizeof(void*) * static_cast<size_t>(ptrs));
+  L->bytes = round8(L->w_off + sizeof(float) * static_cast<size_t>(ptrs));
+  return true;
+}
+
+template <class Op>
+int table_fill(int b, const int* fan_in, const void* const* in, const float* w, void* const* outs,
+               const size_t* nelem, void* h_table, size_t bytes) {
+  TableLayout L;
+  if (!table_layout<Op>(b, fan_in, nelem, &L)) return fail(DLSIM_E_ARG, "batch too large");
+  if (bytes < L.bytes) return fail(DLSIM_E_ARG, "table buffer too small (%zu < %zu)", bytes, L.bytes);
+  if (cross_task_overlap(b, fan_in, in, outs, nelem, Op::kBytes))
+    return fail(DLSIM_E_ARG,
+                "a task's output overlaps another task's input or output: one table launch runs all tasks "
+                "concurrently (use separate calls, or dlsim_wreduce_batched, which orders them)");
+  unsigned char* base = static_cast<unsigned char*>(h_table);
+  std::memset(base, 0, L.bytes);
+  auto* h = reinterpret_cast<dlsim::BatchTableHeader*>(base);
+  auto* tasks = reinterpret_cast<dlsim::BatchTaskDesc*>(base + L.tasks_off);
+  auto* map = reinterpret_cast<uint32_t*>(base + L.map_off);
+  auto* ptrs = reinterpret_cast<const void**>(base + L.ptrs_off);
+  auto* ws = reinterpret_cast<float*>(base + L.w_off);
+  h->ntasks = static_cast<uint32_t>(b);
+  h->nblocks = L.nblocks;
+  h->tasks_off = L.tasks_off;
+  h->map_off = L.map_off;
+  h->ptrs_off = L.ptrs_off;
+  h->w_off = L.w_off;
+  uint32_t blk = 0, off = 0;
+  bool uniform = true;
+  for (int t = 0; t < b; ++t) {
+    const size_t total = nelem[t] * Op::kBytes;
+    if (fan_in[t] > DLSIM_MAX_FUSED_INPUTS || total > kMaxLaunchOutBytes || !aligned16(outs[t]))
+      return fail(DLSIM_E_ARG, "task %d cannot be table-batched (fan-in <= %d, 16-B aligned, < 2 GiB)", t,
+                  DLSIM_MAX_FUSED_INPUTS);
+    const uint32_t nb = task_blocks<Op>(nelem[t]);
+    tasks[t].out = outs[t];
+    tasks[t].nvec = nelem[t] / Op::E;
+    tasks[t].nelem = nelem[t];
+    tasks[t].block_start = blk;
+    tasks[t].ptr_off = off;
+    tasks[t].fan_in = static_cast<uint32_t>(fan_in[t]);
+    for (uint32_t k = 0; k < nb; ++k) map[blk + k] = static_cast<uint32_t>(t);
+    for (int i = 0; i < fan_in[t]; ++i) {
+      if (!aligned16(in[off + i]))
+        return fail(DLSIM_E_ARG, "task %d input %d is not 16-byte aligned", t, i);
+      ptrs[off + i] = in[off + i];
+      ws[off + i] = w[off + i];
+    }
+    blk += nb;
+    off += static_cast<uint32_t>(fan_in[t]);
+    uniform = uniform && fan_in[t] == fan_in[0];
+  }
+  h->uniform_fan_in = uniform ? static_cast<uint32_t>(fan_in[0]) : 0u;
+  return DLSIM_OK;
+}
+
+template <class Op, int NF>
+hipError_t launch_table_nf(const void* d_table, uint32_t blocks, hipStream_t st) {
+  hipLaunchKernelGGL((dlsim::k_wreduce_batch_table<Op, NF, group_size<Op>(), kVpt, kNT, store_policy<Op>()>),
+                     dim3(blocks), dim3(dlsim::kBlock), 0, st, static_cast<const unsigned char*>(d_table));
+  return hipGetLastError();
+}
+
+template <class Op, int K>
+hipError_t launch_table_fixed(const void* d_table, int n, uint32_t blocks, hipStream_t st) {
+  if constexpr (K > max_fixed_fan_in<Op>()) {
+    return launch_table_nf<Op, 0>(d_table, blocks, st);
+  } else {
+    if (n == K) return launch_table_nf<Op, K>(d_table, blocks, st);
+    return launch_table_fixed<Op, K + 1>(d_table, n, blocks, st);
+  }
+}
+
+template <class Op>
+int table_launch(const void* h_table, const void* d_table, hipStream_t st) {
+  const auto* h = static_cast<const dlsim::BatchTableHeader*>(h_table);
+  if (h->ntasks == 0) return DLSIM_OK;
+  hipError_t e = h->uniform_fan_in ? launch_table_fixed<Op, 1>(d_table, static_cast<int>(h->uniform_fan_in),
+                                                               h->nblocks, st)
+                                   : launch_table_nf<Op, 0>(d_table, h->nblocks, st);
+  if (e != hipSuccess) return hip_fail(e, "table batch launch");
+  return DLSIM_OK;
+}
+
+
+// ---- chunk mean in PyTorch's CPU order (chunk_mean_kernels.hpp) --------------
+// First column that ATen's cascade_sum folds in row_sum (ilp) order, for an
+// [m, n] fp32 reduction over dim 0 at `threads` intra-op threads
+// (parallel_dim_reduction's column split, 32-column rounding; the 8-wide
+// vectorized_outer_sum blocks of 32 columns; scalar_outer_sum's groups of 4
+// under 8 columns). n == 1 is the inner reduction (all "ilp"/inner).
+inline size_t chunk_mean_ilp_begin(int m, size_t n, int threads) {
+  if (n <= 1) return 0;
+  size_t b = 0, e = n;
+  if (!(static_cast<unsigned long long>(m) * n < 32768ULL || threads <= 1)) {
+    const size_t tp = static_cast<size_t>(threads) < n ? static_cast<size_t>(threads) : n;
+    const size_t cs = (n + tp - 1) / tp;
+    for (size_t t = 0; t < tp; ++t) {
+      size_t tb = t * cs;
+      if (tb >= n) break;
+      size_t te = tb + cs < n ? tb + cs : n;
+      tb -= tb % 32;
+      if (te != n) te -= te % 32;
+      if (tb < te) {
+        b = tb;
+        e = te;
+      }
+    }
+  }
+  const size_t s1 = e - b;
+  return b + (s1 >= 8 ? s1 / 32 * 32 : s1 / 4 * 4);
+}
+
+// Chunk mean tiles: VPT 4, wave map, 8 rows per load group. Block and wave
+// maps, VPT 2/4 and 8/16 rows in flight measured within +-3% of each other
+// (profiles/r01_tune_chunk_mean_shapes.log); the wave map matches the fp32
+// reduce's shape.
+using CmDefault = dlsim::CmShape<4, true, 8>;
+
+template <class Op>
+int run_chunk_mean(int b, const int* fan_in, const void* const* in, void* const* outs, const size_t* nelem,
+                   int threads, hipStream_t st) {
+  constexpr size_t tile = static_cast<size_t>(dlsim::kBlock) * CmDefault::VPT;
+  std::vector<size_t> off(static_cast<size_t>(b) + 1, 0);
+  for (int t = 0; t < b; ++t) off[t + 1] = off[t] + static_cast<size_t>(fan_in[t]);
+  if (b > 1 && cross_task_overlap(b, fan_in, in, outs, nelem, Op::kBytes)) {
+    // tasks touch each other's outputs: one launch per task, in order
+    for (int t = 0; t < b; ++t) {
+      int rc = run_chunk_mean<Op>(1, fan_in + t, in + off[t], outs + t, nelem + t, threads, st);
+      if (rc != DLSIM_OK) return rc;
+    }
+    return DLSIM_OK;
+  }
+  auto task_flags = [&](int t) {
+    bool vec = aligned16(outs[t]);
+    for (int i = 0; i < fan_in[t] && vec; ++i) vec = aligned16(in[off[t] + i]);
+    uint8_t f = vec ? dlsim::kCmVec : 0;
+    if (nelem[t] == 1 && fan_in[t] >= 8) f |= dlsim::kCmInner;
+    return f;
+  };
+  auto task_blocks = [&](int t, size_t ib) { return ib / Op::E / tile + 1; };
+  dlsim::ChunkMeanSlots s;
+  std::memset(&s, 0, sizeof(s));
+  int nt = 0, np = 0;
+  size_t blocks = 0;
+  auto flush = [&]() -> int {
+    if (nt == 0) return DLSIM_OK;
+    s.ntasks = nt;
+    s.block_start[nt] = static_cast<uint32_t>(blocks);
+    hipLaunchKernelGGL((dlsim::k_chunk_mean_batch<Op, CmDefault>), dim3(static_cast<unsigned>(blocks)),
+                       dim3(dlsim::kBlock), 0, st, s);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "chunk mean batch launch");
+    std::memset(&s, 0, sizeof(s));
+    nt = np = 0;
+    blocks = 0;
+    return DLSIM_OK;
+  };
+  for (int t = 0; t < b; ++t) {
+    const size_t n = nelem[t];
+    if (n == 0) continue;
+    const int m = fan_in[t];
+    const size_t ib = chunk_mean_ilp_begin(m, n, threads);
+    const uint8_t flags = task_flags(t);
+    const size_t tb = task_blocks(t, ib);
+    if (m > dlsim::kCmMaxPtrs) {
+      // input pointers through a stream-ordered device array (any m)
+      void* d = nullptr;
+      const size_t bytes = static_cast<size_t>(m) * sizeof(void*);
+      hipError_t e = hipMallocAsync(&d, bytes, st);
+      if (e != hipSuccess) return hip_fail(e, "chunk mean pointer table alloc");
+      // pageable source: the copy is staged before the call returns
+      e = hipMemcpyAsync(d, in + off[t], bytes, hipMemcpyHostToDevice, st);
+      if (e == hipSuccess) {
+        hipLaunchKernelGGL((dlsim::k_chunk_mean_table<Op, CmDefault>), dim3(static_cast<unsigned>(tb)),
+                           dim3(dlsim::kBlock), 0, st, static_cast<const void* const*>(d), m, outs[t], n, ib,
+                           flags);
+        e = hipGetLastError();
+      }
+      hipError_t e2 = hipFreeAsync(d, st);
+      if (e != hipSuccess) return hip_fail(e, "chunk mean table launch");
+      if (e2 != hipSuccess) return hip_fail(e2, "chunk mean pointer table free");
+      continue;
+    }
+    if (nt == dlsim::kCmMaxTasks || np + m > dlsim::kCmMaxPtrs || blocks + tb > 0x7fffffffu) {
+      int rc = flush();
+      if (rc != DLSIM_OK) return rc;
+    }
+    s.block_start[nt] = static_cast<uint32_t>(blocks);
+    s.ptr_off[nt] = static_cast<uint16_t>(np);
+    s.m[nt] = static_cast<uint16_t>(m);
+    s.out[nt] = outs[t];
+    s.nelem[nt] = n;
+    s.ilp_begin[nt] = ib;
+    s.flags[nt] = flags;
+    for (int i = 0; i < m; ++i) s.p[np + i] = in[off[t] + i];
+    np += m;
+    blocks += tb;
+    ++nt;
+  }
+  return flush();
+}
+
+}  // namespace dlsim_host
+
+// ---- per-policy entry points, instantiated by the inst_*.hip units ----------------
+#define DLSIM_REDUCE_ENTRIES(X, Op)                                                                      \
+  X int dlsim_host::run<Op>(const void* const*, int, const float*, void*, size_t, hipStream_t, float);  \
+  X int dlsim_host::run_batched<Op>(int, const int*, const void* const*, const float*, void* const*,    \
+                                    const size_t*, hipStream_t, const float*);                          \
+  X bool dlsim_host::table_layout<Op>(int, const int*, const size_t*, dlsim_host::TableLayout*);        \
+  X int dlsim_host::table_fill<Op>(int, const int*, const void* const*, const float*, void* const*,     \
+                                   const size_t*, void*, size_t);                                       \
+  X int dlsim_host::table_launch<Op>(const void*, const void*, hipStream_t);
+#define DLSIM_MEAN_ENTRIES(X, Op)                                                                        \
+  X int dlsim_host::run<Op>(const void* const*, int, const float*, void*, size_t, hipStream_t, float);  \
+  X int dlsim_host::run_batched<Op>(int, const int*, const void* const*, const float*, void* const*,    \
+                                    const size_t*, hipStream_t, const float*);                          \
+  X int dlsim_host::run_chunk_mean<Op>(int, const int*, const void* const*, void* const*, const size_t*, \
+                                       int, hipStream_t);
+#define DLSIM_PROBE_ENTRIES(X, Op) \
+  X int dlsim_host::run<Op>(const void* const*, int, const float*, void*, size_t, hipStream_t, float);
+#define DLSIM_F64_ENTRIES(X, Op) \
+  X int dlsim_host::run<Op>(const void* const*, int, const double*, void*, size_t, hipStream_t, float);
+
+// every policy's entries, with X = `extern template` (declare) or `template` (define)
+#define DLSIM_ALL_ENTRIES(X)                  \
+  DLSIM_REDUCE_ENTRIES(X, dlsim::F32Exact)    \
+  DLSIM_REDUCE_ENTRIES(X, dlsim::F32Fast)     \
+  DLSIM_REDUCE_ENTRIES(X, dlsim::BF16Exact)   \
+  DLSIM_REDUCE_ENTRIES(X, dlsim::BF16Fast)    \
+  DLSIM_REDUCE_ENTRIES(X, dlsim::F16Exact)    \
+  DLSIM_REDUCE_ENTRIES(X, dlsim::F16Fast)     \
+  DLSIM_MEAN_ENTRIES(X, dlsim::F32Mean)       \
+  DLSIM_MEAN_ENTRIES(X, dlsim::BF16Mean)      \
+  DLSIM_MEAN_ENTRIES(X, dlsim::F16Mean)       \
+  DLSIM_PROBE_ENTRIES(X, dlsim::XorProbe<4>)  \
+  DLSIM_PROBE_ENTRIES(X, dlsim::XorProbe<2>)  \
+  DLSIM_F64_ENTRIES(X, dlsim::F64Exact)       \
+  DLSIM_F64_ENTRIES(X, dlsim::F64Fast)

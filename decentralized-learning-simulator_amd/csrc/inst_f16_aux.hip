@@ -1,0 +1,6 @@
+// inst_f16_aux.hip — instantiation unit: the kernels and host dispatch of these
+// element policies (dispatch.hpp); compiled in parallel with the others.
+#include "dispatch.hpp"
+
+DLSIM_REDUCE_ENTRIES(template, dlsim::F16Fast)
+DLSIM_MEAN_ENTRIES(template, dlsim::F16Mean)

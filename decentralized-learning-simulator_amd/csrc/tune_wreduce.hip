@@ -221,26 +221,13 @@ void launch_x(const Slots<128>& s, int n, void* out, size_t nvec, size_t, hipStr
 // loads, sc1 stores, same tiles) with the arithmetic replaced by a bitwise
 // XOR of the inputs. Its time is what the HBM allows for exactly this
 // read/write mix; the exact reduce is compared against it.
-struct XorProbe {
-  static constexpr int E = 4;
-  static constexpr int kBytes = 4;
-  static constexpr int kFmt = kFmtF32;
-  __device__ static float init(float) { return 0.0f; }
-  __device__ static float step(float acc, float, float x) {
-    return __uint_as_float(__float_as_uint(acc) ^ __float_as_uint(x));
-  }
-  __device__ static void step2(float& a0, float& a1, float w, float x0, float x1) {
-    a0 = step(a0, w, x0);
-    a1 = step(a1, w, x1);
-  }
-  __device__ static float finish(float a, float) { return a; }
-};
+using XorProbeF32 = XorProbe<4>;  // wreduce_kernels.hpp
 
 template <class Op, int NF>
 void launch_probe(const Slots<128>& s, int n, void* out, size_t nvec, size_t nelem, hipStream_t st, int) {
   if constexpr (Op::kBytes == 4) {
     const size_t full = nvec / ((size_t)kBlock * 4);
-    hipLaunchKernelGGL((k_wreduce_tiles<XorProbe, Slots<128>, NF, 8, 4, 1, 16, true>), dim3((unsigned)(full + 1)),
+    hipLaunchKernelGGL((k_wreduce_tiles<XorProbeF32, Slots<128>, NF, 8, 4, 1, 16, true>), dim3((unsigned)(full + 1)),
                        dim3(kBlock), 0, st, s, n, out, nvec, nelem);
   }
 }
@@ -505,7 +492,7 @@ int run(int n, size_t P, int reps, double peak_gbs) {
       cs.p[0] = ca[k % csets];
       cs.w[0] = 1.0f;
       cs.div = 1.0f;
-      launch_ts<CopyProbe, 1, 8, 4, 1, 16, true>(cs, 1, cb[k % csets], nv, nv * 4, st, 0);
+      launch_ts<XorProbeF32, 1, 8, 4, 1, 16, true>(cs, 1, cb[k % csets], nv, nv * 4, st, 0);
     };
     for (int k = 0; k < 10; ++k) launch_copy(k);
     CK(hipEventRecord(ev[0], st));

@@ -25,6 +25,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 // Multiply and add must stay separate roundings: hipcc defaults to
 // -ffp-contract=fast-honor-pragmas, which would fuse acc + w*x into v_fma_f32
 // and change ~55% of the results (hard part (a)).
@@ -189,6 +191,58 @@ struct F16Fast {
   __device__ static float finish(float a, float) { return f16_round(a); }
 };
 
+// fp64 (a double model, dlsim_wreduce_f64): `w * p1` keeps the Python float
+// exact as a double scalar and every product and sum is rounded to double
+// (PyTorch's CPU opmath for a double tensor), so acc, weights and elements are
+// doubles. T / W name the accumulator and weight types of a policy (float for
+// every other policy, see acc_t / wt_t below).
+struct F64Exact {
+  using T = double;
+  using W = double;
+  static constexpr int E = 2;
+  static constexpr int kBytes = 8;
+  static constexpr int kFmt = kFmtF32;
+  __device__ static double init(double x) { return x * 0.0; }
+  __device__ static double step(double acc, double w, double x) {
+    const double p = w * x;  // rounded: contraction is off
+    return acc + p;
+  }
+  __device__ static void step2(double& a0, double& a1, double w, double x0, double x1) {
+    a0 = step(a0, w, x0);
+    a1 = step(a1, w, x1);
+  }
+  __device__ static double finish(double a, float) { return a; }
+};
+
+struct F64Fast {
+  using T = double;
+  using W = double;
+  static constexpr int E = 2;
+  static constexpr int kBytes = 8;
+  static constexpr int kFmt = kFmtF32;
+  __device__ static double init(double x) { return x * 0.0; }
+  __device__ static double step(double acc, double w, double x) { return __builtin_fma(w, x, acc); }
+  __device__ static void step2(double& a0, double& a1, double w, double x0, double x1) {
+    a0 = step(a0, w, x0);
+    a1 = step(a1, w, x1);
+  }
+  __device__ static double finish(double a, float) { return a; }
+};
+
+// Accumulator and weight types of a policy: float unless it names T / W.
+template <class Op, class = void>
+struct OpTypes {
+  using T = float;
+  using W = float;
+};
+template <class Op>
+struct OpTypes<Op, std::void_t<typename Op::T>> {
+  using T = typename Op::T;
+  using W = typename Op::W;
+};
+template <class Op> using acc_t = typename OpTypes<Op>::T;
+template <class Op> using wt_t = typename OpTypes<Op>::W;
+
 // Mean of the inputs in input order (dlsim_mean): acc starts at +0 (the
 // reduction's identity), adds every input in order, then one division by n
 // (weights unused). bf16: the sum is accumulated in fp32, divided in fp32 and
@@ -237,8 +291,12 @@ struct F16Mean {
 
 // ---- 16-byte vector <-> E floats --------------------------------------------
 template <class Op>
-__device__ __forceinline__ void unpack(const u32x4& r, float (&x)[Op::E]) {
-  if constexpr (Op::kBytes == 4) {
+__device__ __forceinline__ void unpack(const u32x4& r, acc_t<Op> (&x)[Op::E]) {
+  if constexpr (Op::kBytes == 8) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+      x[e] = __builtin_bit_cast(double, static_cast<uint64_t>(r[2 * e]) | (static_cast<uint64_t>(r[2 * e + 1]) << 32));
+  } else if constexpr (Op::kBytes == 4) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) x[e] = __uint_as_float(r[e]);
   } else if constexpr (Op::kFmt == kFmtF16) {
@@ -258,9 +316,16 @@ __device__ __forceinline__ void unpack(const u32x4& r, float (&x)[Op::E]) {
 }
 
 template <class Op>
-__device__ __forceinline__ u32x4 pack(const float (&a)[Op::E], float div) {
+__device__ __forceinline__ u32x4 pack(const acc_t<Op> (&a)[Op::E], float div) {
   u32x4 r;
-  if constexpr (Op::kBytes == 4) {
+  if constexpr (Op::kBytes == 8) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const uint64_t u = __builtin_bit_cast(uint64_t, Op::finish(a[e], div));
+      r[2 * e] = static_cast<uint32_t>(u);
+      r[2 * e + 1] = static_cast<uint32_t>(u >> 32);
+    }
+  } else if constexpr (Op::kBytes == 4) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) r[e] = __float_as_uint(Op::finish(a[e], div));
   } else if constexpr (Op::kFmt == kFmtF16) {
@@ -284,8 +349,10 @@ __device__ __forceinline__ u32x4 pack(const float (&a)[Op::E], float div) {
 
 // ---- scalar element load/store (tail and misaligned paths) ------------------
 template <class Op>
-__device__ __forceinline__ float load_elem(const void* p, size_t j) {
-  if constexpr (Op::kBytes == 4) {
+__device__ __forceinline__ acc_t<Op> load_elem(const void* p, size_t j) {
+  if constexpr (Op::kBytes == 8) {
+    return static_cast<const double*>(p)[j];
+  } else if constexpr (Op::kBytes == 4) {
     return static_cast<const float*>(p)[j];
   } else if constexpr (Op::kFmt == kFmtF16) {
     return static_cast<float>(static_cast<const _Float16*>(p)[j]);
@@ -295,8 +362,10 @@ __device__ __forceinline__ float load_elem(const void* p, size_t j) {
 }
 
 template <class Op>
-__device__ __forceinline__ void store_elem(void* p, size_t j, float a, float div) {
-  if constexpr (Op::kBytes == 4) {
+__device__ __forceinline__ void store_elem(void* p, size_t j, acc_t<Op> a, float div) {
+  if constexpr (Op::kBytes == 8) {
+    static_cast<double*>(p)[j] = Op::finish(a, div);
+  } else if constexpr (Op::kBytes == 4) {
     static_cast<float*>(p)[j] = Op::finish(a, div);
   } else if constexpr (Op::kFmt == kFmtF16) {
     static_cast<_Float16*>(p)[j] = static_cast<_Float16>(Op::finish(a, div));
@@ -370,13 +439,13 @@ __device__ __forceinline__ OutRef make_out(void* out, size_t nvec) {
 // ---- kernel arguments -------------------------------------------------------
 // Input pointers and fp32 weights travel in the kernarg segment (read with
 // scalar loads, wave-uniform), NB slots; n <= NB inputs used.
-template <int NB>
+template <int NB, class W = float>
 struct Slots {
   const void* p[NB];
-  float w[NB];
+  W w[NB];
   float div;  // final divisor of the mean policies (1 for the weighted reduce)
   __device__ const void* ptr(int i) const { return p[i]; }
-  __device__ float wt(int i) const { return w[i]; }
+  __device__ W wt(int i) const { return w[i]; }
   __device__ float divisor() const { return div; }
 };
 
@@ -385,12 +454,13 @@ struct Slots {
 // stream (read with scalar loads like the kernargs), so every n is one pass
 // over the inputs: each output element is written once, after all n of its
 // terms are folded.
+template <class W = float>
 struct DevSlots {
   const void* const* p;
-  const float* w;
+  const W* w;
   float div;
   __device__ const void* ptr(int i) const { return p[i]; }
-  __device__ float wt(int i) const { return w[i]; }
+  __device__ W wt(int i) const { return w[i]; }
   __device__ float divisor() const { return div; }
 };
 
@@ -400,9 +470,9 @@ __device__ __forceinline__ void fold_scalar(const S& s, int n, void* out, size_t
   // Every load of a chunk of 8 inputs issues before its first use: one HBM
   // round trip per chunk, not one per input. The first input doubles as the
   // x0*0 seed (n >= 1).
-  float a = 0.0f;
+  acc_t<Op> a = 0;
   for (int i = 0; i < n; i += 8) {
-    float x[8];
+    acc_t<Op> x[8];
 #pragma unroll
     for (int g = 0; g < 8; ++g) x[g] = (i + g < n) ? load_elem<Op>(s.ptr(i + g), j) : 0.0f;
     if (i == 0) a = Op::init(x[0]);
@@ -447,10 +517,10 @@ __device__ __forceinline__ void load_tile(const void* src, size_t v0, size_t nve
 }
 
 template <class Op, int VPT>
-__device__ __forceinline__ void fold_tile(float (&a)[VPT][Op::E], float w, const u32x4 (&r)[VPT]) {
+__device__ __forceinline__ void fold_tile(acc_t<Op> (&a)[VPT][Op::E], wt_t<Op> w, const u32x4 (&r)[VPT]) {
 #pragma unroll
   for (int v = 0; v < VPT; ++v) {
-    float x[Op::E];
+    acc_t<Op> x[Op::E];
     unpack<Op>(r[v], x);
 #pragma unroll
     for (int e = 0; e < Op::E; e += 2) Op::step2(a[v][e], a[v][e + 1], w, x[e], x[e + 1]);
@@ -458,10 +528,10 @@ __device__ __forceinline__ void fold_tile(float (&a)[VPT][Op::E], float w, const
 }
 
 template <class Op, int VPT>
-__device__ __forceinline__ void init_tile(float (&a)[VPT][Op::E], const u32x4 (&r)[VPT], bool from_acc) {
+__device__ __forceinline__ void init_tile(acc_t<Op> (&a)[VPT][Op::E], const u32x4 (&r)[VPT], bool from_acc) {
 #pragma unroll
   for (int v = 0; v < VPT; ++v) {
-    float x[Op::E];
+    acc_t<Op> x[Op::E];
     unpack<Op>(r[v], x);
 #pragma unroll
     for (int e = 0; e < Op::E; ++e) a[v][e] = from_acc ? x[e] : Op::init(x[e]);
@@ -470,7 +540,7 @@ __device__ __forceinline__ void init_tile(float (&a)[VPT][Op::E], const u32x4 (&
 
 template <class Op, class S, int NF, int G, int VPT, int NT, bool CHECK, int STP, int VS = kBlock>
 __device__ __forceinline__ void reduce_tile(const S& s, int n, const OutRef& out, size_t v0, size_t nvec) {
-  float a[VPT][Op::E];
+  acc_t<Op> a[VPT][Op::E];
   if constexpr (NF > 0) {
     u32x4 r[NF][VPT];
 #pragma unroll
@@ -660,18 +730,25 @@ __global__ __launch_bounds__(kBlock) void k_wreduce_batch_table(const unsigned c
   reduce_tile<Op, TableArgs, NF, G, VPT, NT, false, STP>(a, n, o, (local - 1) * kTile + threadIdx.x, nvec);
 }
 
-// Copy probe: the streaming ceiling of the reduce's own access pattern.
-// With n = 1 the tiled kernel reads one stream and writes one (same grid,
-// lane map, nt loads and sc1 stores as the fp32 reduce): a bit-exact copy of
-// 16-byte vectors (dlsim_probe_copy), so a 1:1 read/write stream is timed
-// with exactly the machinery the reduce uses.
-struct CopyProbe {
-  static constexpr int E = 4;
-  static constexpr int kBytes = 4;
-  static constexpr int kFmt = kFmtF32;
-  __device__ static float init(float x) { return x; }
-  __device__ static float step(float acc, float, float) { return acc; }
-  __device__ static void step2(float&, float&, float, float, float) {}
+// Memory-only probe (dlsim_probe_pattern): the element policy of the reduce
+// with the weighted fold replaced by a bitwise XOR of the inputs' bits, run
+// through the same dispatch (kernel, launch shape, load and store policies).
+// Its time is what the memory system allows for exactly the reduce's
+// read/write mix; the reduce is timed against it. n = 1 is a
+// bit-exact copy.
+template <int BYTES>
+struct XorProbe {
+  static constexpr int E = 16 / BYTES;
+  static constexpr int kBytes = BYTES;
+  static constexpr int kFmt = BYTES == 4 ? kFmtF32 : kFmtBF16;
+  __device__ static float init(float) { return 0.0f; }
+  __device__ static float step(float acc, float, float x) {
+    return __uint_as_float(__float_as_uint(acc) ^ __float_as_uint(x));
+  }
+  __device__ static void step2(float& a0, float& a1, float w, float x0, float x1) {
+    a0 = step(a0, w, x0);
+    a1 = step(a1, w, x1);
+  }
   __device__ static float finish(float a, float) { return a; }
 };
 

@@ -18,6 +18,7 @@ LIB_PATH = os.path.join(LIB_DIR, "libdlsim_hip.so")
 DLSIM_F32 = 0
 DLSIM_BF16 = 1
 DLSIM_F16 = 2
+DLSIM_F64 = 3
 DLSIM_EXACT = 0
 DLSIM_FAST = 1
 MAX_FUSED_INPUTS = 128
@@ -26,6 +27,7 @@ MAX_FUSED_INPUTS = 128
 # against this list and the library's exports).
 EXPORTS = (
     "dlsim_wreduce",
+    "dlsim_wreduce_f64",
     "dlsim_wreduce_tensors",
     "dlsim_wreduce_batched",
     "dlsim_batch_table_bytes",
@@ -41,7 +43,7 @@ EXPORTS = (
     "dlsim_host_chunk_mean",
     "dlsim_host_pack",
     "dlsim_shard_range",
-    "dlsim_probe_copy",
+    "dlsim_probe_pattern",
     "dlsim_last_error",
     "dlsim_version",
 )
@@ -75,6 +77,8 @@ def load() -> ctypes.CDLL:
         lib.dlsim_wreduce.argtypes = [ctypes.POINTER(vp), i, ctypes.POINTER(ctypes.c_float), vp,
                                       sz, i, i, vp]
         lib.dlsim_wreduce.restype = i
+        lib.dlsim_wreduce_f64.argtypes = [ctypes.POINTER(vp), i, ctypes.POINTER(ctypes.c_double), vp, sz, i, vp]
+        lib.dlsim_wreduce_f64.restype = i
         lib.dlsim_wreduce_tensors.argtypes = [ctypes.POINTER(vp), i, i, ctypes.POINTER(sz),
                                               ctypes.POINTER(ctypes.c_float), ctypes.POINTER(vp),
                                               i, i, vp]
@@ -118,8 +122,8 @@ def load() -> ctypes.CDLL:
         lib.dlsim_host_pack.restype = i
         lib.dlsim_shard_range.argtypes = [sz, i, i, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)]
         lib.dlsim_shard_range.restype = i
-        lib.dlsim_probe_copy.argtypes = [vp, vp, sz, vp]
-        lib.dlsim_probe_copy.restype = i
+        lib.dlsim_probe_pattern.argtypes = [ctypes.POINTER(vp), i, vp, sz, i, vp]
+        lib.dlsim_probe_pattern.restype = i
         lib.dlsim_last_error.argtypes = []
         lib.dlsim_last_error.restype = ctypes.c_char_p
         lib.dlsim_version.argtypes = []
@@ -152,7 +156,23 @@ def fp32_weights(weights: Sequence[float]) -> np.ndarray:
     return np.asarray([float(w) for w in weights], dtype=np.float64).astype(np.float32)
 
 
-def dtype_code(torch_dtype) -> int:
+def f64_weights(weights: Sequence[float]) -> np.ndarray:
+    """Python floats as doubles: for a double tensor the reference's `w * p1`
+    keeps the weight exact (fedavg.py:25)."""
+    return np.asarray([float(w) for w in weights], dtype=np.float64)
+
+
+def weights_for_dtype(weights: Sequence[float], torch_dtype) -> np.ndarray:
+    """The weights as the reference's op sees them for this parameter dtype:
+    fp32-rounded for fp32/bf16/fp16 tensors, exact doubles for fp64."""
+    import torch
+    return f64_weights(weights) if torch_dtype == torch.float64 else fp32_weights(weights)
+
+
+def dtype_code(torch_dtype, single_task: bool = False) -> int:
+    """ABI dtype of a parameter dtype. fp64 has one entry point
+    (dlsim_wreduce_f64, single task); the batched, tensor-list, mean and host
+    entries take fp32/bf16/fp16 only."""
     import torch
     if torch_dtype == torch.float32:
         return DLSIM_F32
@@ -160,7 +180,12 @@ def dtype_code(torch_dtype) -> int:
         return DLSIM_BF16
     if torch_dtype == torch.float16:
         return DLSIM_F16
-    raise TypeError(f"aggregation supports float32, bfloat16 and float16 parameters, got {torch_dtype}")
+    if torch_dtype == torch.float64:
+        if single_task:
+            return DLSIM_F64
+        raise TypeError("float64 parameters are reduced one task at a time (dlsim_wreduce_f64); "
+                        "this entry point takes float32, bfloat16 and float16")
+    raise TypeError(f"aggregation supports float32, bfloat16, float16 and float64 parameters, got {torch_dtype}")
 
 
 def _stream_handle(device, stream) -> Optional[int]:
@@ -174,14 +199,14 @@ class ReducePlan:
     """One prepared `dlsim_wreduce` call: pointer and weight arrays built once,
     `launch()` is a single ctypes call (used by hot loops and bench.py)."""
 
-    def __init__(self, inputs, weights_f32: np.ndarray, out, mode: int = DLSIM_EXACT):
+    def __init__(self, inputs, weights_f32: np.ndarray, out, mode: int = DLSIM_EXACT, probe: bool = False):
         import torch
         n = len(inputs)
         if n < 1:
             raise IndexError("list index out of range")
         if len(weights_f32) != n:
             raise AssertionError("weights/models length mismatch")
-        dt = dtype_code(out.dtype)
+        dt = dtype_code(out.dtype, single_task=not probe)
         numel = out.numel()
         for t in list(inputs) + [out]:
             if not t.is_cuda:
@@ -194,20 +219,37 @@ class ReducePlan:
         self.n, self.numel, self.dtype, self.mode = n, numel, dt, mode
         self._keep = (list(inputs), out)  # keep storages alive while planned
         self._ptrs = (ctypes.c_void_p * n)(*[t.data_ptr() for t in inputs])
-        self._w = np.ascontiguousarray(weights_f32, dtype=np.float32)
-        self._wp = self._w.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+        if dt == DLSIM_F64:
+            # exact double weights (weights_for_dtype); fp32 arrays widen exactly
+            self._w = np.ascontiguousarray(weights_f32, dtype=np.float64)
+            self._wp = self._w.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+        else:
+            self._w = np.ascontiguousarray(weights_f32, dtype=np.float32)
+            self._wp = self._w.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
         self._out = ctypes.c_void_p(out.data_ptr())
         self._lib = load()
+        self.probe = probe
         torch.cuda.current_device()  # a GPU must be present
 
     def launch(self, stream=None) -> None:
+        if self.probe:
+            _check("dlsim_probe_pattern",
+                   self._lib.dlsim_probe_pattern(self._ptrs, self.n, self._out, self.numel, self.dtype,
+                                                 _stream_handle(self.device, stream)))
+            return
+        if self.dtype == DLSIM_F64:
+            _check("dlsim_wreduce_f64",
+                   self._lib.dlsim_wreduce_f64(self._ptrs, self.n, self._wp, self._out, self.numel, self.mode,
+                                               _stream_handle(self.device, stream)))
+            return
         rc = self._lib.dlsim_wreduce(self._ptrs, self.n, self._wp, self._out, self.numel,
                                      self.dtype, self.mode, _stream_handle(self.device, stream))
         _check("dlsim_wreduce", rc)
 
 
 def wreduce(inputs, weights_f32, out, mode: int = DLSIM_EXACT, stream=None):
-    """out = sum_i w_i * inputs[i] on the device (flat tensors), stream-ordered."""
+    """out = sum_i w_i * inputs[i] on the device (flat tensors), stream-ordered.
+    fp64 tensors take double weights (weights_for_dtype)."""
     ReducePlan(inputs, weights_f32, out, mode).launch(stream)
     return out
 
@@ -603,8 +645,8 @@ def host_pack(srcs, dst_offsets, dst, threads: Optional[int] = None):
     return dst
 
 
-def probe_copy(src, dst, stream=None) -> None:
-    lib = load()
-    nbytes = src.numel() * src.element_size()
-    _check("dlsim_probe_copy", lib.dlsim_probe_copy(src.data_ptr(), dst.data_ptr(), nbytes,
-                                                    _stream_handle(src.device, stream)))
+def probe_pattern(inputs, out, stream=None):
+    """dlsim_probe_pattern: the reduce's dispatch for these buffers (kernel,
+    launch shape, load/store policies) with the fold replaced by a bitwise
+    XOR — the memory-only ceiling of this exact access pattern."""
+    return ReducePlan(inputs, np.ones(len(inputs), np.float32), out, probe=True).launch(stream)

@@ -24,6 +24,7 @@ the reduced arena, keeping each original's requires_grad.
 from __future__ import annotations
 
 import copy
+import threading
 import time
 import weakref
 from collections import OrderedDict
@@ -71,7 +72,7 @@ class ParamLayout:
         self.totals: Dict[torch.dtype, int] = {}
         self._group_offsets: Dict[torch.dtype, List[int]] = {}
         for dt, idx in self.groups.items():
-            _native.dtype_code(dt)  # raises TypeError for unsupported dtypes
+            _native.dtype_code(dt, single_task=True)  # raises TypeError for unsupported dtypes
             off = 0
             offs = []
             for k in idx:
@@ -140,49 +141,72 @@ def row_stride(numel: int, elem_bytes: int) -> int:
 
 
 class _Staging:
-    """Reusable device/pinned buffers keyed by (device, dtype, n, numel)."""
+    """Reusable staging rows: ONE grow-only device buffer per (device, dtype)
+    and one grow-only pinned buffer per (device, dtype), carved into rows for
+    each call (`rows[i, :numel]`, rows 16-byte aligned at row_stride). Memory
+    is bounded by the largest request seen, not by the number of distinct
+    (fan-in, size) shapes: gossip and D-PSGD vary the fan-in per peer.
+
+    acquire() takes the key's lock and waits for the previous user's event
+    (its H2D copies and kernel may still be queued when it returns);
+    release() records the new event and drops the lock. Callers pair them
+    with try/finally, so a failing call cannot leave the rows reusable while
+    copies into them are still in flight, and two threads cannot pack into
+    the same rows at once."""
 
     def __init__(self):
         self.dev: Dict[Tuple, torch.Tensor] = {}
         self.host: Dict[Tuple, torch.Tensor] = {}
-        # last use of a (device rows, pinned rows) pair: the next call waits on
-        # it before overwriting either buffer (a previous call may have
-        # returned with its H2D copies and kernel still queued).
         self.last_use: Dict[Tuple, torch.cuda.Event] = {}
+        self._locks: Dict[Tuple, threading.Lock] = {}
+        self._locks_guard = threading.Lock()
 
-    def acquire(self, device, dt, n, numel, stream):
-        key = (str(device), dt, n, numel)
-        ev = self.last_use.get(key)
-        if ev is not None:
-            ev.synchronize()
-        return self.device_rows(device, dt, n, numel), self.pinned_rows(dt, n, numel)
+    @staticmethod
+    def _key(device, dt):
+        return (str(device), dt)
 
-    def release(self, device, dt, n, numel, stream):
+    def _lock(self, key) -> threading.Lock:
+        with self._locks_guard:
+            lk = self._locks.get(key)
+            if lk is None:
+                lk = self._locks[key] = threading.Lock()
+            return lk
+
+    @staticmethod
+    def _grow(pool: Dict[Tuple, torch.Tensor], key, need: int, make) -> torch.Tensor:
+        buf = pool.get(key)
+        if buf is None or buf.numel() < need:
+            pool.pop(key, None)  # drop the old one first (device memory returns to torch's cache)
+            buf = pool[key] = make(need)
+        return buf
+
+    def acquire(self, device, dt, n, numel, stream, pinned: bool = True):
+        """(device rows, pinned rows or None) as [n, numel] views."""
+        key = self._key(device, dt)
+        self._lock(key).acquire()
+        try:
+            ev = self.last_use.pop(key, None)
+            if ev is not None:
+                ev.synchronize()
+            stride = row_stride(numel, torch.empty((), dtype=dt).element_size())
+            need = max(1, n * stride)
+            flat = self._grow(self.dev, key, need, lambda k: torch.empty(k, dtype=dt, device=device))
+            rows = flat[:n * stride].view(n, stride)[:, :numel]
+            host = None
+            if pinned:
+                hflat = self._grow(self.host, key, need, lambda k: torch.empty(k, dtype=dt, pin_memory=True))
+                host = hflat[:n * stride].view(n, stride)[:, :numel]
+            return rows, host
+        except BaseException:
+            self._lock(key).release()
+            raise
+
+    def release(self, device, dt, stream):
+        key = self._key(device, dt)
         ev = torch.cuda.Event()
         ev.record(stream)
-        self.last_use[(str(device), dt, n, numel)] = ev
-
-    # Rows start 16-byte aligned (the vector kernel's requirement) at an HBM
-    # friendly stride (row_stride); callers use rows[i, :numel].
-    @staticmethod
-    def _padded(numel, dt):
-        return row_stride(numel, torch.empty((), dtype=dt).element_size())
-
-    def device_rows(self, device, dt, n, numel) -> torch.Tensor:
-        key = (str(device), dt, n, numel)
-        buf = self.dev.get(key)
-        if buf is None:
-            buf = torch.empty((n, self._padded(numel, dt)), dtype=dt, device=device)[:, :numel]
-            self.dev[key] = buf
-        return buf
-
-    def pinned_rows(self, dt, n, numel) -> torch.Tensor:
-        key = (dt, n, numel)
-        buf = self.host.get(key)
-        if buf is None:
-            buf = torch.empty((n, self._padded(numel, dt)), dtype=dt, pin_memory=True)[:, :numel]
-            self.host[key] = buf
-        return buf
+        self.last_use[key] = ev
+        self._lock(key).release()
 
     def clear(self):
         for ev in self.last_use.values():
@@ -266,21 +290,42 @@ def _host_pipeline(all_params, idx, layout, dt, dev, out, weights_f32, mode, str
     once `stream` is) or None (the result is in `out`, queued on `stream`)."""
     n = len(all_params)
     total = layout.totals[dt]
-    dev_rows, pinned = STAGING.acquire(dev, dt, n, total, stream)
     chunk = pipeline_chunk_elems(total, out.element_size())
     h2d, d2h = _side_streams(dev) if chunk else (None, None)
     host = torch.empty(total, dtype=dt, pin_memory=True) if want_host else None
-    _native.host_wreduce([[ps[k] for k in idx] for ps in all_params], weights_f32, pinned, dev_rows, out,
-                         host, mode, chunk, None, stream, h2d, d2h)
-    STAGING.release(dev, dt, n, total, stream)
+    dev_rows, pinned = STAGING.acquire(dev, dt, n, total, stream)
+    try:
+        _native.host_wreduce([[ps[k] for k in idx] for ps in all_params], weights_f32, pinned, dev_rows, out,
+                             host, mode, chunk, None, stream, h2d, d2h)
+    finally:
+        STAGING.release(dev, dt, stream)
     return host
 
 
+def _staged_reduce(all_params, idx, dt, dev, out, weights, mode, stream):
+    """Models whose parameters are neither one device arena nor host tensors
+    the native pipeline takes (another GPU; separate fp64 tensors): each
+    model's parameters are concatenated into a device staging row, then one
+    reduce over the rows."""
+    n = len(all_params)
+    dev_rows, _ = STAGING.acquire(dev, dt, n, out.numel(), stream, pinned=False)
+    try:
+        for i, ps in enumerate(all_params):
+            torch.cat([ps[k].detach().reshape(-1).to(dev) for k in idx], out=dev_rows[i])
+        _native.wreduce([dev_rows[i] for i in range(n)], weights, out, mode)
+    finally:
+        STAGING.release(dev, dt, stream)
+
+
 def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, mode: int,
-                             device=None, timing: Optional[dict] = None, host_out: bool = False
+                             device=None, timing: Optional[dict] = None, host_out: bool = False,
+                             weights_f64: Optional[np.ndarray] = None
                              ) -> Tuple[ParamLayout, Dict[torch.dtype, torch.Tensor], torch.device, bool]:
     """Reduce the parameters of `models` into one fresh arena per dtype.
 
+    weights_f32: the fp32-rounded weights (fp32/bf16/fp16 groups);
+    weights_f64: the exact double weights an fp64 group needs (fedavg.py:25
+    keeps the Python float exact for a double tensor); default: widened fp32.
     Returns (layout, arenas, device, on_host). With host_out, host models take
     the chunked pipeline and come back already in pinned host memory
     (on_host True, copies complete); otherwise the arenas are on the device."""
@@ -296,6 +341,8 @@ def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, m
     with torch.no_grad():
         for dt, idx in layout.groups.items():
             total = layout.totals[dt]
+            f64 = dt == torch.float64
+            w = (weights_f64 if weights_f64 is not None else weights_f32.astype(np.float64)) if f64 else weights_f32
             out = torch.empty(total, dtype=dt, device=dev)
             outs[dt] = out
             if total == 0:
@@ -307,7 +354,11 @@ def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, m
                 views = in_views[dt]
                 st.mark("layout")
                 if views is not None:
-                    _native.wreduce(views, weights_f32, out, mode)
+                    _native.wreduce(views, w, out, mode)
+                    st.mark("kernel")
+                    continue
+                if f64:  # one task through dlsim_wreduce_f64
+                    _staged_reduce(all_params, idx, dt, dev, out, w, mode, stream)
                     st.mark("kernel")
                     continue
                 # the ABI reads data pointers only: no detach() objects for
@@ -319,7 +370,7 @@ def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, m
                 _native.wreduce_tensors(rows, weights_f32, outs_k, mode)
                 st.mark("kernel")
                 continue
-            if not any(all_params[i][idx[0]].is_cuda for i in range(n)):
+            if not f64 and not any(all_params[i][idx[0]].is_cuda for i in range(n)):
                 # host models (the reference's case): chunked pack / H2D /
                 # reduce (/ D2H) pipeline
                 st.mark("layout")
@@ -328,13 +379,10 @@ def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, m
                     outs[dt] = h
                 st.mark("pipeline")
                 continue
-            # models on another GPU: gather onto this one, then reduce
-            dev_rows, _ = STAGING.acquire(dev, dt, n, total, stream)
+            # models on another GPU (or fp64 host models): gather onto this
+            # one, then reduce
             st.mark("layout")
-            for i, ps in enumerate(all_params):
-                torch.cat([ps[k].detach().reshape(-1).to(dev) for k in idx], out=dev_rows[i])
-            _native.wreduce([dev_rows[i] for i in range(n)], weights_f32, out, mode)
-            STAGING.release(dev, dt, n, total, stream)
+            _staged_reduce(all_params, idx, dt, dev, out, w, mode, stream)
             st.mark("kernel")
     if piped:
         left = {dt: a for dt, a in outs.items() if a.is_cuda}
@@ -509,7 +557,8 @@ def aggregate_modules(models: List[nn.Module], weights: Optional[Sequence[float]
     model0 = models[0]  # IndexError for an empty list, as the reference
     w32 = _native.fp32_weights(weights)
     host_out = to_host if to_host is not None else not any(p.is_cuda for p in module_params(model0))
-    layout, arenas, dev, on_host = reduce_modules_to_arenas(models, w32, mode, device, timing, host_out)
+    layout, arenas, dev, on_host = reduce_modules_to_arenas(models, w32, mode, device, timing, host_out,
+                                                            weights_f64=_native.f64_weights(weights))
     stream = torch.cuda.current_stream(dev)
     st = _Stages(timing, stream)
     if host_out and not on_host:

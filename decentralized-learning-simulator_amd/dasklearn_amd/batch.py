@@ -20,13 +20,14 @@ from . import _native
 from .arena import aggregate_modules, input_arenas, module_from_arenas
 
 
-def _resolve(models, weights):
-    # fedavg.py:14-17 rules, same exceptions
+def _resolve(models, weights) -> List[float]:
+    # fedavg.py:14-17 rules, same exceptions; the Python floats (each dtype
+    # group rounds them as the reference's op does: _native.weights_for_dtype)
     if not weights:
         weights = [float(1. / len(models)) for _ in range(len(models))]
     else:
         assert len(weights) == len(models)
-    return _native.fp32_weights(weights)
+    return [float(w) for w in weights]
 
 
 def aggregate_batch(tasks: Sequence[Tuple[List[nn.Module], Optional[Sequence[float]]]],
@@ -40,13 +41,13 @@ def aggregate_batch(tasks: Sequence[Tuple[List[nn.Module], Optional[Sequence[flo
     results: List[Optional[nn.Module]] = [None] * len(tasks)
     prepared, where = [], []
     for ti, (models, weights) in enumerate(tasks):
-        w32 = _resolve(models, weights)
+        ws = _resolve(models, weights)
         model0 = models[0]  # IndexError for an empty task, as the reference
         layout, _, views = input_arenas(models)
         if _device_views(views) is None:
             results[ti] = aggregate_modules(models, weights, mode)
             continue
-        prepared.append((model0, layout, views, w32))
+        prepared.append((model0, layout, views, ws))
         where.append(ti)
     for ti, out in zip(where, aggregate_arena_tasks(prepared, mode)):
         results[ti] = out
@@ -70,19 +71,25 @@ def _device_views(views) -> Optional[torch.device]:
 
 def aggregate_arena_tasks(prepared, mode: int = _native.DLSIM_EXACT) -> List[nn.Module]:
     """prepared: [(model0, layout of model0, {dtype: [flat arena per model]},
-    fp32 weights)] with every arena on one device -> one module per task
-    (deepcopy(model0) semantics, parameters views of a fresh output arena),
-    all tasks of a dtype and device in batched launches."""
+    weights as Python floats)] with every arena on one device -> one module
+    per task (deepcopy(model0) semantics, parameters views of a fresh output
+    arena), all tasks of a dtype and device in batched launches (fp64 groups:
+    one dlsim_wreduce_f64 per task)."""
     by_dtype = {}
     outs = []
-    for model0, layout, views, w32 in prepared:
+    for model0, layout, views, ws in prepared:
         o = {}
         for dt, vs in views.items():
             dev = vs[0].device
             out = torch.empty(layout.totals[dt], dtype=dt, device=dev)
             o[dt] = out
-            by_dtype.setdefault((dt, dev), []).append((vs, w32, out))
+            by_dtype.setdefault((dt, dev), []).append((vs, _native.weights_for_dtype(ws, dt), out))
         outs.append(o)
     for (dt, dev), group in by_dtype.items():
-        _native.wreduce_batched(group, mode, torch.cuda.current_stream(dev))
+        stream = torch.cuda.current_stream(dev)
+        if dt == torch.float64:
+            for vs, w, out in group:
+                _native.wreduce(vs, w, out, mode, stream)
+            continue
+        _native.wreduce_batched(group, mode, stream)
     return [module_from_arenas(model0, layout, o) for (model0, layout, _, _), o in zip(prepared, outs)]

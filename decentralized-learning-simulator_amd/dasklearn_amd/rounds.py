@@ -33,6 +33,10 @@ from .batch import _device_views, _resolve, aggregate_arena_tasks
 
 Task = Tuple[str, str, dict]  # (task_name, func_name, data with placeholders)
 
+# Host-trained models of a wave go to the device in groups of at most this
+# many bytes (RoundExecutor._upload_host_models).
+UPLOAD_GROUP_BYTES = 256 << 20
+
 
 def _same_signature(ps, sig) -> bool:
     if len(ps) != len(sig):
@@ -75,6 +79,8 @@ class RoundExecutor:
         self.results: Dict[str, list] = {}
         self.waves: List[List[str]] = []
         self._layouts: Dict[type, object] = {}  # model class -> a ParamLayout of it
+        self._stages: List[Optional[torch.Tensor]] = [None, None]  # pinned upload buffers
+        self._stage_events: List[Optional[torch.cuda.Event]] = [None, None]
 
     def _resolve(self, v):
         if _is_ref(v):
@@ -123,11 +129,27 @@ class RoundExecutor:
         cache[id(m)] = (m, layout, arenas)
         return layout, arenas
 
+    def _stage(self, k: int, nbytes: int) -> torch.Tensor:
+        """Pinned staging buffer k of 2 (grow-only, reused across waves), once
+        the H2D copy that last read it has completed."""
+        ev = self._stage_events[k]
+        if ev is not None:
+            ev.synchronize()
+        buf = self._stages[k]
+        if buf is None or buf.numel() < nbytes:
+            self._stages[k] = None  # back to torch's pinned cache before growing
+            buf = self._stages[k] = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+        return buf
+
     def _upload_host_models(self, models, cache: dict) -> None:
         """Every host model of a wave (the reference's CPU-trained models) to
-        one device buffer: the library's threads pack all their parameters
-        into one pinned buffer (dlsim_host_pack; one arena per model and
-        dtype at 256-B aligned offsets), then one H2D. Fills `cache` as
+        the device in bounded groups: the library's threads pack a group's
+        parameters into a persistent pinned buffer (dlsim_host_pack; one arena
+        per model and dtype at 256-B aligned offsets), then one H2D per group.
+        Groups hold at most UPLOAD_GROUP_BYTES (a larger model is a group of
+        its own) and alternate between two pinned buffers, so the pack of
+        group g+1 overlaps the copy of group g and pinned memory stays bounded
+        by two groups, however many models a wave has. Fills `cache` as
         _arena_of would (instead of one small H2D per parameter tensor)."""
         pending, seen = [], set()
         for m in models:
@@ -141,26 +163,42 @@ class RoundExecutor:
         if not pending:
             return
         dev = _target_device(pending[0][1].params, self.device)
-        srcs, offs, spans, off = [], [], [], 0
+        stream = torch.cuda.current_stream(dev)
+        groups, cur, cur_bytes = [], [], 0
         for m, layout in pending:
-            span = {}
-            for dt, idx in layout.groups.items():
-                esz = layout.params[idx[0]].element_size()
-                span[dt] = (off, layout.totals[dt], esz)
-                for k in idx:
-                    p = layout.params[k]
-                    srcs.append(p.detach() if p.is_contiguous() else p.detach().contiguous())
-                    offs.append(off)
-                    off += p.numel() * esz
-                off = (off + 255) // 256 * 256
-            spans.append(span)
-        stage = torch.empty(max(off, 1), dtype=torch.uint8, pin_memory=True)
-        _native.host_pack(srcs, offs, stage)
-        buf = torch.empty(max(off, 1), dtype=torch.uint8, device=dev)
-        buf.copy_(stage, non_blocking=True)  # torch keeps `stage` until the copy is done
-        for (m, layout), span in zip(pending, spans):
-            arenas = {dt: buf[o:o + n * esz].view(dt) for dt, (o, n, esz) in span.items()}
-            cache[id(m)] = (m, layout, arenas)
+            nb = sum((layout.totals[dt] * layout.params[idx[0]].element_size() + 255) // 256 * 256
+                     for dt, idx in layout.groups.items())
+            if cur and cur_bytes + nb > UPLOAD_GROUP_BYTES:
+                groups.append(cur)
+                cur, cur_bytes = [], 0
+            cur.append((m, layout))
+            cur_bytes += nb
+        groups.append(cur)
+        for g, group in enumerate(groups):
+            srcs, offs, spans, off = [], [], [], 0
+            for m, layout in group:
+                span = {}
+                for dt, idx in layout.groups.items():
+                    esz = layout.params[idx[0]].element_size()
+                    span[dt] = (off, layout.totals[dt], esz)
+                    for k in idx:
+                        p = layout.params[k]
+                        srcs.append(p.detach() if p.is_contiguous() else p.detach().contiguous())
+                        offs.append(off)
+                        off += p.numel() * esz
+                    off = (off + 255) // 256 * 256
+                spans.append(span)
+            size = max(off, 1)
+            stage = self._stage(g % 2, size)
+            _native.host_pack(srcs, offs, stage[:size])
+            buf = torch.empty(size, dtype=torch.uint8, device=dev)
+            buf.copy_(stage[:size], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            self._stage_events[g % 2] = ev
+            for (m, layout), span in zip(group, spans):
+                arenas = {dt: buf[o:o + n * esz].view(dt) for dt, (o, n, esz) in span.items()}
+                cache[id(m)] = (m, layout, arenas)
 
     def _aggregate_wave(self, aggs) -> List[nn.Module]:
         cache: dict = {}
@@ -169,10 +207,10 @@ class RoundExecutor:
         for name, _, data in aggs:
             d = self._resolve(data)
             models = d["models"]
-            w32 = _resolve(models, d.get("weights"))  # fedavg.py:14-17 rules and exceptions
-            resolved.append((models, w32))
+            ws = _resolve(models, d.get("weights"))  # fedavg.py:14-17 rules and exceptions
+            resolved.append((models, ws))
         self._upload_host_models([m for models, _ in resolved for m in models], cache)
-        for models, w32 in resolved:
+        for models, ws in resolved:
             ents = [self._arena_of(m, cache) for m in models]
             layout0 = ents[0][0]
             sig = layout0._signature
@@ -181,7 +219,7 @@ class RoundExecutor:
                 if lay._signature is not sig and lay._signature != sig:
                     layout0.check_compatible(models[i])  # raises the shape/dtype error
             views = {dt: [a[dt] for _, a in ents] for dt in layout0.groups}
-            prepared.append((models[0], layout0, views, w32))
+            prepared.append((models[0], layout0, views, ws))
         return aggregate_arena_tasks(prepared, self.mode)
 
     def run(self, tasks: Sequence[Task], seed: Optional[Dict[str, list]] = None) -> Dict[str, list]:

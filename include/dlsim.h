@@ -39,7 +39,8 @@ extern "C" {
 enum dlsim_dtype {
   DLSIM_F32 = 0,  /* IEEE binary32                                      */
   DLSIM_BF16 = 1, /* bfloat16 (upper 16 bits of binary32), RNE rounding  */
-  DLSIM_F16 = 2   /* IEEE binary16, RNE rounding                        */
+  DLSIM_F16 = 2,  /* IEEE binary16, RNE rounding                        */
+  DLSIM_F64 = 3   /* IEEE binary64: dlsim_wreduce_f64 only (double weights) */
 };
 
 enum dlsim_mode {
@@ -91,6 +92,19 @@ enum dlsim_mode {
 int dlsim_wreduce(const void* const* d_inputs, int n, const float* h_weights,
                   void* d_out, size_t n_elems, int dtype, int mode,
                   void* stream);
+
+/*
+ * dlsim_wreduce_f64 — dlsim_wreduce for fp64 (double) parameters.
+ *
+ * For a double model the reference's `w * p1` (fedavg.py:25) keeps the
+ * Python-float weight exact as a double scalar, so the weights here are
+ * doubles (no fp32 rounding), and every product and partial sum is rounded to
+ * double, in input order, without FMA (DLSIM_EXACT; DLSIM_FAST is an fma
+ * chain). Same buffer, aliasing, fan-in and stream rules as dlsim_wreduce.
+ * The other entry points take float weights and reject DLSIM_F64.
+ */
+int dlsim_wreduce_f64(const void* const* d_inputs, int n, const double* h_weights, void* d_out, size_t n_elems,
+                      int mode, void* stream);
 
 /*
  * dlsim_wreduce_tensors — the same reduce over T separate tensors per model,
@@ -324,12 +338,16 @@ int dlsim_shard_range(size_t n_elems, int world, int rank, size_t align_elems,
                       size_t* begin, size_t* end);
 
 /*
- * dlsim_probe_copy — bit-exact copy through the reduce's own tile kernel
- * (n = 1, same grid, lane map, nt loads and sc1 stores as the fp32 reduce of
- * that size): the 1:1 read/write streaming ceiling of the access pattern,
- * reported next to the reduce. bytes % 16 == 0, 16-B aligned, < 2 GiB.
+ * dlsim_probe_pattern — memory-only probe of dlsim_wreduce's access pattern:
+ * the same dispatch for these buffers (kernel, launch shape, fan-in form,
+ * load and store policies) with the weighted fold replaced by a bitwise XOR
+ * of the inputs (n = 1: a bit-exact copy). Its time is what the memory
+ * system allows for exactly the reduce's read/write mix; bench.py times the
+ * reduce against it. dtype DLSIM_F32, DLSIM_BF16 or DLSIM_F16 (16-bit types
+ * share one probe); same buffer and stream rules as dlsim_wreduce.
  */
-int dlsim_probe_copy(const void* d_src, void* d_dst, size_t bytes, void* stream);
+int dlsim_probe_pattern(const void* const* d_inputs, int n, void* d_out, size_t n_elems, int dtype,
+                        void* stream);
 
 /* Message for the last failing call on this thread ("" if none). */
 const char* dlsim_last_error(void);

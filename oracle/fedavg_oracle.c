@@ -98,6 +98,32 @@ int oracle_wreduce_f32(const float* const* in, int n, const float* w, float* out
 /* Same fold, element-major over a (n, p) row-major block: faster restatement
  * used for full-size checks (identical arithmetic, loop order swapped: every
  * element's terms are still added in input order). */
+/* fp64 (fedavg.py:20-25 on a double model): `w * p1` keeps the Python-float
+ * weight exact as a double scalar, and every product and partial sum is a
+ * double rounding (PyTorch's CPU opmath for double is double). */
+int oracle_wreduce_f64(const double* const* in, int n, const double* w, double* out, size_t p) {
+  if (n < 1 || !in || !w || !out) return -1;
+  for (size_t j = 0; j < p; ++j) {
+    double acc = in[0][j] * 0.0;
+    for (int i = 0; i < n; ++i) {
+      double prod = w[i] * in[i][j];
+      acc = acc + prod;
+    }
+    out[j] = acc;
+  }
+  return 0;
+}
+
+int oracle_wreduce_fast_f64(const double* const* in, int n, const double* w, double* out, size_t p) {
+  if (n < 1 || !in || !w || !out) return -1;
+  for (size_t j = 0; j < p; ++j) {
+    double acc = in[0][j] * 0.0;
+    for (int i = 0; i < n; ++i) acc = fma(w[i], in[i][j], acc);
+    out[j] = acc;
+  }
+  return 0;
+}
+
 int oracle_wreduce_f32_rows(const float* x, int n, const float* w, float* out, size_t p) {
   if (n < 1 || !x || !w || !out) return -1;
   for (size_t j = 0; j < p; ++j) out[j] = x[j] * 0.0f;

@@ -57,11 +57,25 @@ def _load():
         fn.restype = ctypes.c_int
     lib.oracle_chunk_mean_ilp_begin.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int]
     lib.oracle_chunk_mean_ilp_begin.restype = ctypes.c_size_t
+    for name in ("oracle_wreduce_f64", "oracle_wreduce_fast_f64"):
+        fn = getattr(lib, name)
+        fn.argtypes = [pp, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+        fn.restype = ctypes.c_int
     lib.oracle_wreduce_f32_rows.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                                             ctypes.c_void_p, ctypes.c_size_t]
     lib.oracle_wreduce_f32_rows.restype = ctypes.c_int
     _lib = lib
     return lib
+
+
+def reference_weights_f64(n: int, weights: Optional[Sequence[float]]) -> np.ndarray:
+    """fedavg.py:14-17 weight rules for a double model: the Python floats,
+    exact (a double tensor's `w * p1` keeps them as double scalars)."""
+    if not weights:
+        weights = [float(1.0 / n) for _ in range(n)]
+    else:
+        assert len(weights) == n
+    return np.asarray([float(w) for w in weights], dtype=np.float64)
 
 
 def reference_weights(n: int, weights: Optional[Sequence[float]]) -> np.ndarray:
@@ -88,18 +102,24 @@ def _as_rows(xs, np_dtype):
 def wreduce(xs, weights, dtype: str = "f32", mode: str = "exact") -> np.ndarray:
     """N-way weighted reduce of flat arrays, reference rounding order.
 
-    xs: sequence of N arrays — float32 for "f32", uint16 bit patterns for
-    "bf16" and "f16". weights: fp32 array-like of length N (already resolved).
-    Returns float32 (f32) or uint16 bit patterns (bf16, f16).
+    xs: sequence of N arrays — float32 for "f32", float64 for "f64", uint16
+    bit patterns for "bf16" and "f16". weights: array-like of length N,
+    already resolved: fp32 (reference_weights) for f32/bf16/f16, the exact
+    doubles (reference_weights_f64) for f64.
+    Returns float32 (f32), float64 (f64) or uint16 bit patterns (bf16, f16).
     """
     lib = _load()
     n = len(xs)
     if n < 1:
         raise IndexError("list index out of range")
-    w = np.ascontiguousarray(weights, dtype=np.float32)
+    w = np.ascontiguousarray(weights, dtype=np.float64 if dtype == "f64" else np.float32)
     if w.size != n:
         raise AssertionError("weights/models length mismatch")
-    if dtype == "f32":
+    if dtype == "f64":
+        rows, p = _as_rows(xs, np.float64)
+        out = np.empty(p, dtype=np.float64)
+        fn = lib.oracle_wreduce_f64 if mode == "exact" else lib.oracle_wreduce_fast_f64
+    elif dtype == "f32":
         rows, p = _as_rows(xs, np.float32)
         out = np.empty(p, dtype=np.float32)
         fn = lib.oracle_wreduce_f32 if mode == "exact" else lib.oracle_wreduce_fast_f32
@@ -227,6 +247,11 @@ def same_bits(a: np.ndarray, b: np.ndarray) -> bool:
     elif a.dtype == np.uint16:
         fa, fb = bf16_bits_to_f32(a), bf16_bits_to_f32(b)
         ia, ib = a, b
+    elif np.float64 in (a.dtype, b.dtype):
+        if a.dtype != b.dtype:
+            return False
+        fa, fb = a, b
+        ia, ib = a.view(np.uint64), b.view(np.uint64)
     else:
         fa, fb = a.astype(np.float32), b.astype(np.float32)
         ia, ib = fa.view(np.uint32), fb.view(np.uint32)

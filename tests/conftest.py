@@ -49,6 +49,16 @@ def load_golden(path):
     return d
 
 
+def golden_weights(g):
+    """The fixture's weights as the reference's op sees them: fp32-rounded for
+    f32/bf16/f16 models, the exact doubles for f64 models (fedavg.py:25)."""
+    from oracle import oracle as orc
+    meta = g["meta"]
+    if meta["dtype"] == "f64":
+        return orc.reference_weights_f64(meta["n"], g["weights_arg"])
+    return orc.reference_weights(meta["n"], g["weights_arg"])
+
+
 @pytest.fixture(scope="session")
 def goldens():
     return {os.path.basename(p)[:-4]: load_golden(p) for p in golden_paths()}

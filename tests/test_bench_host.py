@@ -1,0 +1,89 @@
+"""bench.py's host-side machinery (CPU): the timed window, rank launch and
+input-set rotation. The GPU leg itself runs on the box (bench.py, -m gpu)."""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import textwrap
+import time
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+
+class _ClockEvent:
+    def record(self):
+        self.t = time.perf_counter()
+
+    def elapsed_time(self, other):
+        return (other.t - self.t) * 1e3
+
+
+def test_barriers_are_outside_the_timed_window():
+    """A 0.3 s barrier on both sides of 5 x 2 ms launches: both clocks see
+    only the launches."""
+    calls = []
+
+    def barrier():
+        calls.append("barrier")
+        time.sleep(0.3)
+
+    def launch(k):
+        calls.append(k)
+        time.sleep(0.002)
+
+    ev_ms, wall_ms = bench.time_steps(launch, 5, lambda: calls.append("sync"), barrier, _ClockEvent)
+    assert 9.0 <= ev_ms < 100.0
+    assert 9.0 <= wall_ms < 100.0
+    assert calls[0] == "barrier" and calls[-1] == "barrier"
+    assert calls[1:-1] == ["sync", 0, 1, 2, 3, 4, "sync"]
+
+
+def test_input_sets_cover_the_infinity_cache():
+    # the north star (402.5 MB a step): 3 sets; its 8-rank slice (50.3 MB): 22
+    assert bench.n_sets(402_539_112) == 3
+    assert bench.n_sets(50_319_360) == 22
+    assert bench.n_sets(50_319_360) * 50_319_360 >= bench.MIN_SET_FOOTPRINT
+
+
+def test_strong_split_is_the_default_for_several_gpus():
+    a = bench.parse(["--gpus", "4"])
+    assert not a.weak
+    assert bench.parse(["--gpus", "4", "--weak"]).weak
+
+
+_RANK_SCRIPT = textwrap.dedent("""
+    import json, os, sys
+    import torch, torch.distributed as dist
+    dist.init_process_group("gloo")
+    r, w = dist.get_rank(), dist.get_world_size()
+    assert os.environ["MASTER_ADDR"] == "127.0.0.1" and int(os.environ["LOCAL_RANK"]) == r
+    t = torch.tensor([float(r + 1)])
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if "--fail" in sys.argv and r == 1:
+        sys.exit(3)
+    if r == 0:
+        print(json.dumps({"world": w, "max": t.item(), "argv": sys.argv[1:]}), flush=True)
+    dist.destroy_process_group()
+""")
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_spawn_ranks_runs_one_process_per_rank(tmp_path, capfd, n):
+    script = tmp_path / "rank.py"
+    script.write_text(_RANK_SCRIPT)
+    rc = bench.spawn_ranks(n, ["--gpus", str(n)], script=str(script))
+    assert rc == 0
+    line = json.loads(capfd.readouterr().out.strip().splitlines()[-1])
+    assert line == {"world": n, "max": float(n), "argv": ["--gpus", str(n)]}
+
+
+def test_spawn_ranks_reports_a_failing_rank(tmp_path):
+    script = tmp_path / "rank.py"
+    script.write_text(_RANK_SCRIPT)
+    assert bench.spawn_ranks(2, ["--fail"], script=str(script)) == 3

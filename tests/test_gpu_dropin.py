@@ -32,7 +32,7 @@ class Ragged(nn.Module):
 
 def modules_from_golden(g):
     meta = g["meta"]
-    dt = {"bf16": torch.bfloat16, "f16": torch.float16}.get(meta["dtype"], torch.float32)
+    dt = {"bf16": torch.bfloat16, "f16": torch.float16, "f64": torch.float64}.get(meta["dtype"], torch.float32)
     models = []
     for row in g["inputs"]:
         m = Ragged(meta["shapes"], dt)

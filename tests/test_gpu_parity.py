@@ -14,7 +14,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import golden_paths, load_golden
+from conftest import golden_paths, golden_weights, load_golden
 from oracle import oracle as orc
 
 pytestmark = pytest.mark.gpu
@@ -34,6 +34,8 @@ def to_dev(rows, dtype):
     if dtype in HALF:
         return [torch.from_numpy(np.ascontiguousarray(r).view(np.int16).copy()).view(HALF[dtype]).to(dev())
                 for r in rows]
+    if dtype == "f64":
+        return [torch.from_numpy(np.ascontiguousarray(r, dtype=np.float64)).to(dev()) for r in rows]
     return [torch.from_numpy(np.ascontiguousarray(r, dtype=np.float32)).to(dev()) for r in rows]
 
 
@@ -41,7 +43,7 @@ def from_dev(t):
     t = t.cpu()
     if t.dtype == torch.bfloat16:
         return t.view(torch.int16).numpy().view(np.uint16)
-    return t.numpy()  # float32, or float16 (compared as binary16)
+    return t.numpy()  # float32 / float64, or float16 (compared as binary16)
 
 
 def hip_reduce(rows, w, dtype, mode=_native.DLSIM_EXACT):
@@ -57,8 +59,7 @@ def hip_reduce(rows, w, dtype, mode=_native.DLSIM_EXACT):
 def test_flat_abi_matches_reference_golden(path):
     g = load_golden(path)
     meta = g["meta"]
-    w = orc.reference_weights(meta["n"], g["weights_arg"])
-    got = hip_reduce(list(g["inputs"]), w, meta["dtype"])
+    got = hip_reduce(list(g["inputs"]), golden_weights(g), meta["dtype"])
     assert orc.same_bits(got, g["expected"]), meta["case"]
 
 
@@ -75,6 +76,8 @@ def make_rows(n, p, seed, dtype):
         return orc.f32_to_bf16_bits(x)
     if dtype == "f16":
         return orc.f32_to_f16_bits(x)
+    if dtype == "f64":
+        return rng.standard_normal((n, p)) * 0.05
     return x
 
 
@@ -133,9 +136,12 @@ def test_empty_tensor_is_noop():
 
 
 def test_unsupported_dtype_raises():
-    x = torch.zeros(16, dtype=torch.float64, device=dev())
+    x = torch.zeros(16, dtype=torch.int32, device=dev())
     with pytest.raises(TypeError):
         _native.wreduce([x], orc.reference_weights(1, None), x)
+    d = torch.zeros(16, dtype=torch.float64, device=dev())
+    with pytest.raises(TypeError, match="one task at a time"):
+        _native.wreduce_batched([([d], orc.reference_weights(1, None), d)])
 
 
 # ---- tensor-list entry ----------------------------------------------------------
@@ -247,13 +253,14 @@ def test_cfg4_2way_125M_bf16_properties():
     assert orc.same_bits(from_dev(out[idx]), orc.wreduce(rows, w, "bf16"))
 
 
-@pytest.mark.parametrize("dtype,p", [("f32", 4_999_997), ("f32", 5_000_003),
+@pytest.mark.parametrize("dtype,p", [("f32", 1_999_999), ("f32", 2_000_003), ("f32", 4_999_997), ("f32", 5_000_003),
                                      ("bf16", 47_999_993), ("bf16", 48_000_007)])
 @pytest.mark.parametrize("n", [2, 8])
 def test_launch_shapes_either_side_of_the_size_switch(dtype, p, n):
     """The fixed fan-in kernels change launch shape by size (dlsim_abi.hip
-    fixed_shape: fp32 block/wave map at 5 M elements, bf16 VPT 1 sc1 / VPT 4 nt
-    at 48 M): both shapes bit-exact against the oracle over every element."""
+    fixed_shape: fp32 VPT 2 / VPT 4 block map at 2 M elements, block/wave map at
+    5 M, bf16 VPT 1 sc1 / VPT 4 nt at 48 M): every shape bit-exact against the
+    oracle over every element."""
     g = torch.Generator(device=dev()).manual_seed(p + n)
     tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
     xs = [(torch.randn(p, generator=g, device=dev()) * 0.05).to(tdt) for _ in range(n)]

@@ -47,11 +47,26 @@ def test_no_cpu_fallback_without_gpu():
 
 
 def test_unsupported_param_dtype_raises():
-    """float32, bfloat16 and float16 parameters run on the GPU; others raise."""
+    """float32, bfloat16, float16 and float64 parameters run on the GPU;
+    others (integer, complex) raise. fp64 is single-task only."""
     arena.ParamLayout(nn.Linear(3, 3).to(torch.float16))
-    m = nn.Linear(3, 3).to(torch.float64)
+    arena.ParamLayout(nn.Linear(3, 3).to(torch.float64))
+    m = nn.Linear(3, 3).to(torch.complex64)
     with pytest.raises(TypeError):
         arena.ParamLayout(m)
+    with pytest.raises(TypeError, match="one task at a time"):
+        _native.dtype_code(torch.float64)
+    assert _native.dtype_code(torch.float64, single_task=True) == _native.DLSIM_F64
+
+
+def test_weights_per_dtype_follow_the_reference_op():
+    """w * p1 (fedavg.py:25): an fp32/bf16/fp16 tensor rounds the Python float
+    to fp32; a double tensor keeps it exact."""
+    ws = [0.1, 1.0 / 3.0]
+    assert _native.weights_for_dtype(ws, torch.float32).dtype == np.float32
+    assert _native.weights_for_dtype(ws, torch.bfloat16)[1] == np.float32(1.0 / 3.0)
+    w64 = _native.weights_for_dtype(ws, torch.float64)
+    assert w64.dtype == np.float64 and w64[0] == 0.1 and w64[1] == 1.0 / 3.0
 
 
 def test_layout_groups_by_dtype_in_parameters_order():
