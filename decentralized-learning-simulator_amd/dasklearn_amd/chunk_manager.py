@@ -21,16 +21,67 @@ functions.py:142-146). That average is a second N-way reduce of the hot path
   tests/test_chunk_mean_order.py).
   As in the reference, `chunks[c]` is replaced in place by its mean and the
   result is copied into `model.state_dict()` (parameters and buffers).
+
+Scope of that parity claim: the order restated is ATen's CPU cascade_sum of
+torch 2.10 with AVX2/AVX512 dispatch (8-float vectors), the build the
+reference's chunk fixtures were generated with (their meta records
+torch_version and cpu_capability). The reference pins torch~=2.1.2
+(requirements.txt:1); a reference worker on another torch or ISA may order
+the sum differently, so `order_scope()` names such a process and the first
+reconstruction in it warns (ParityScopeWarning).
 """
 from __future__ import annotations
 
-from typing import List
+import warnings
+from typing import List, Optional
 
 import torch
 from torch import nn
 
 from . import _native
 from .arena import _side_streams, _target_device
+
+
+ORDER_PINNED_TORCH = "2.10"
+ORDER_PINNED_CPU_CAPABILITIES = ("AVX2", "AVX512")
+
+
+class ParityScopeWarning(UserWarning):
+    """The running process is outside the torch build / CPU dispatch the chunk
+    mean order was pinned against."""
+
+
+def order_scope(version: Optional[str] = None, capability: Optional[str] = None) -> Optional[str]:
+    """None when this process's torch and CPU dispatch are those the chunk
+    mean order is pinned to, else a message saying what differs."""
+    version = torch.__version__ if version is None else version
+    if capability is None:
+        try:
+            capability = torch.backends.cpu.get_cpu_capability()
+        except Exception:
+            capability = "unknown"
+    why = []
+    if ".".join(version.split("+")[0].split(".")[:2]) != ORDER_PINNED_TORCH:
+        why.append(f"torch {version} (order pinned against {ORDER_PINNED_TORCH})")
+    if capability not in ORDER_PINNED_CPU_CAPABILITIES:
+        why.append(f"CPU capability {capability} (pinned: {'/'.join(ORDER_PINNED_CPU_CAPABILITIES)})")
+    if not why:
+        return None
+    return ("chunk means follow ATen's cascade_sum order of the pinned build; this process runs "
+            + " and ".join(why) + ": the reference on this build may sum in another order")
+
+
+_SCOPE_CHECKED = False
+
+
+def _check_order_scope() -> None:
+    global _SCOPE_CHECKED
+    if _SCOPE_CHECKED:
+        return
+    _SCOPE_CHECKED = True
+    msg = order_scope()
+    if msg:
+        warnings.warn(msg, ParityScopeWarning, stacklevel=3)
 
 
 class ChunkManager:
@@ -63,6 +114,7 @@ class ChunkManager:
         through dlsim_host_chunk_mean (threaded pack into pinned staging,
         per-row H2D, per-index mean and D2H, overlapped). Each result lives
         where its first chunk lives."""
+        _check_order_scope()
         for cs in chunks:
             first = cs[0]
             for c in cs:

@@ -11,7 +11,9 @@ inputs and outputs as .npz data next to this script. Skips when
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_chunks.py
 
 Per case (np.load(..., allow_pickle=False)):
-    meta       JSON: case, num_chunks k, contributors per chunk index, shapes
+    meta       JSON: case, num_chunks k, contributors per chunk index, shapes,
+               torch_version / cpu_capability of the generating process (the
+               summation order of torch.mean is pinned to them)
     flat_<p>   flat state_dict of contributing model p (float32, cat order)
     chunks_<c> (m_c, L_c) chunk c of each contributor, in the order given to
                reconstruct_model
@@ -68,7 +70,11 @@ def main() -> int:
         expected = ChunkManager.get_flat_params(out).numpy().copy()
         case = f"chunks_k{k}_m{'-'.join(map(str, counts))}"
         meta = dict(case=case, num_chunks=k, counts=counts, shapes=shapes, torch_threads=4,
-                    source="seeded randn*0.05 models (stored)")
+                    source="seeded randn*0.05 models (stored)",
+                    # the order torch.mean follows is ATen's cascade_sum of THIS
+                    # torch build and CPU dispatch: parity is pinned to them
+                    torch_version=torch.__version__,
+                    cpu_capability=torch.backends.cpu.get_cpu_capability())
         arrays = dict(meta=np.array(json.dumps(meta)), expected=expected, **chunk_arrays)
         for p in range(mmax):
             arrays[f"flat_{p}"] = ChunkManager.get_flat_params(models[p]).numpy().copy()

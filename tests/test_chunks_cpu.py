@@ -110,3 +110,35 @@ def test_chunk_mean_oracle_bit_exact_vs_reference(path):
     got = np.concatenate([orc.chunk_mean(list(d[f"chunks_{c}"]), "f32", d["meta"]["torch_threads"])
                           for c in range(k)])
     assert orc.same_bits(got, d["expected"])
+
+
+@pytest.mark.parametrize("path", CHUNK_FIXTURES, ids=lambda p: os.path.basename(p)[:-4])
+def test_fixtures_record_the_build_their_order_is_pinned_to(path):
+    """Every chunk fixture says which torch build and CPU dispatch produced it,
+    and that is the scope ChunkManager.order_scope() accepts."""
+    from dasklearn_amd import chunk_manager as cm
+    meta = load(path)["meta"]
+    assert cm.order_scope(meta["torch_version"], meta["cpu_capability"]) is None
+    assert meta["torch_version"].startswith(cm.ORDER_PINNED_TORCH + ".")
+
+
+def test_order_scope_names_another_build():
+    from dasklearn_amd import chunk_manager as cm
+    assert cm.order_scope("2.10.0+rocm7.0", "AVX512") is None
+    assert cm.order_scope("2.10.1", "AVX2") is None
+    msg = cm.order_scope("2.1.2+cpu", "AVX2")
+    assert msg and "torch 2.1.2+cpu" in msg
+    msg = cm.order_scope("2.10.0", "DEFAULT")
+    assert msg and "CPU capability DEFAULT" in msg
+
+
+def test_reconstruction_warns_once_outside_the_pinned_build(monkeypatch):
+    from dasklearn_amd import chunk_manager as cm
+    monkeypatch.setattr(cm, "_SCOPE_CHECKED", False)
+    monkeypatch.setattr(cm.torch, "__version__", "2.1.2+cpu")
+    with pytest.warns(cm.ParityScopeWarning, match="2.1.2"):
+        cm._check_order_scope()
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        cm._check_order_scope()  # once per process
