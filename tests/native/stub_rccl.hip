@@ -1,0 +1,122 @@
+// stub_rccl.hip — TEST INFRASTRUCTURE: a stand-in for the five RCCL entry
+// points dlsim_wreduce_sharded binds (dlsim_rccl_bind dlopens this file), so
+// its gather path runs with W > 1 ranks on ONE GPU.
+//
+// A stub communicator names a world size W, this rank r, this rank's full
+// output buffer and the full output buffers the other W - 1 ranks would hold
+// (pre-filled by the test). ncclBroadcast(root) of an in-place slice copies
+// that slice from root's buffer (hipMemcpyAsync on the caller's stream) and
+// logs (root, byte offset, count), which is exactly what the real grouped
+// broadcasts deliver when every rank runs the call. Host code only.
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <vector>
+
+namespace {
+
+struct StubComm {
+  int world;
+  int rank;
+  char* own_out;
+  std::vector<char*> peer_out;
+  struct Call {
+    int root;
+    size_t offset_bytes;
+    size_t count;
+    int dtype;
+  };
+  std::vector<Call> calls;
+  int group_depth = 0;
+  int max_group_depth = 0;
+};
+
+size_t nccl_bytes(int dtype) {
+  switch (dtype) {
+    case 6:  // ncclFloat16
+    case 9:  // ncclBfloat16
+      return 2;
+    case 7:  // ncclFloat32
+      return 4;
+    case 8:  // ncclFloat64
+      return 8;
+    default:
+      return 0;
+  }
+}
+
+int g_depth = 0;
+
+}  // namespace
+
+extern "C" {
+
+int ncclGroupStart() {
+  ++g_depth;
+  return 0;
+}
+
+int ncclGroupEnd() {
+  if (g_depth <= 0) return 5;  // ncclInvalidUsage
+  --g_depth;
+  return 0;
+}
+
+int ncclCommCount(void* comm, int* count) {
+  if (!comm || !count) return 4;  // ncclInvalidArgument
+  *count = static_cast<StubComm*>(comm)->world;
+  return 0;
+}
+
+int ncclCommUserRank(void* comm, int* rank) {
+  if (!comm || !rank) return 4;
+  *rank = static_cast<StubComm*>(comm)->rank;
+  return 0;
+}
+
+const char* ncclGetErrorString(int) { return "stub RCCL error"; }
+
+int ncclBroadcast(const void* sendbuff, void* recvbuff, size_t count, int datatype, int root, void* comm,
+                  hipStream_t stream) {
+  StubComm* c = static_cast<StubComm*>(comm);
+  const size_t esz = nccl_bytes(datatype);
+  if (!c || esz == 0 || root < 0 || root >= c->world) return 4;
+  if (sendbuff != recvbuff) return 4;  // dlsim broadcasts in place
+  char* dst = static_cast<char*>(recvbuff);
+  if (dst < c->own_out) return 4;
+  const size_t off = static_cast<size_t>(dst - c->own_out);
+  c->calls.push_back({root, off, count, datatype});
+  if (g_depth > c->max_group_depth) c->max_group_depth = g_depth;
+  if (root == c->rank || count == 0) return 0;
+  const hipError_t e = hipMemcpyAsync(dst, c->peer_out[root] + off, count * esz, hipMemcpyDeviceToDevice, stream);
+  return e == hipSuccess ? 0 : 1;  // ncclUnhandledCudaError
+}
+
+// ---- test helpers ------------------------------------------------------------
+void* stub_comm_create(int world, int rank, void* own_out, void* const* peer_out) {
+  StubComm* c = new StubComm;
+  c->world = world;
+  c->rank = rank;
+  c->own_out = static_cast<char*>(own_out);
+  for (int q = 0; q < world; ++q) c->peer_out.push_back(static_cast<char*>(peer_out[q]));
+  return c;
+}
+
+void stub_comm_destroy(void* comm) { delete static_cast<StubComm*>(comm); }
+
+// Broadcast calls logged so far (at most max written); returns their number.
+int stub_comm_calls(void* comm, int* roots, size_t* offsets, size_t* counts, int max) {
+  StubComm* c = static_cast<StubComm*>(comm);
+  const int n = static_cast<int>(c->calls.size());
+  for (int k = 0; k < n && k < max; ++k) {
+    roots[k] = c->calls[k].root;
+    offsets[k] = c->calls[k].offset_bytes;
+    counts[k] = c->calls[k].count;
+  }
+  return n;
+}
+
+int stub_comm_max_group_depth(void* comm) { return static_cast<StubComm*>(comm)->max_group_depth; }
+
+}  // extern "C"

@@ -1,0 +1,130 @@
+"""dlsim_wreduce_sharded's gather path with W > 1 ranks on one GPU (GPU).
+
+The C ABI binds RCCL at run time (dlsim_rccl_bind). Here it binds a stub
+(tests/native/stub_rccl.hip, built by __graft_entry__.build()) whose
+communicator says "rank r of W" and whose in-place ncclBroadcast(root) copies
+root's slice out of a buffer the test pre-fills with what rank root would hold
+(its exact slice, NaN everywhere else). Every rank r of W in {2, 3, 8} then
+runs the real entry point: its local reduce lands at its own slice, the
+grouped broadcasts fill every other slice, and the assembled output must be
+bit-identical to dlsim_wreduce over the whole buffers. Ragged last slices and
+empty shards (more ranks than 64-element units) are included; the broadcast
+log shows each non-empty slice requested once, with its byte offset and count,
+inside one group.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+from dasklearn_amd import _native  # noqa: E402
+from test_gpu_parity import dev, from_dev, make_rows, to_dev  # noqa: E402
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+STUB = os.path.join(ROOT, "tests", "native", "_build", "libstub_rccl.so")
+
+
+@pytest.fixture(scope="module")
+def stub():
+    assert os.path.exists(STUB), "stub RCCL not built: run __graft_entry__.build()"
+    lib = ctypes.CDLL(STUB)
+    vp = ctypes.c_void_p
+    lib.stub_comm_create.argtypes = [ctypes.c_int, ctypes.c_int, vp, ctypes.POINTER(vp)]
+    lib.stub_comm_create.restype = vp
+    lib.stub_comm_destroy.argtypes = [vp]
+    lib.stub_comm_calls.argtypes = [vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_size_t),
+                                    ctypes.POINTER(ctypes.c_size_t), ctypes.c_int]
+    lib.stub_comm_calls.restype = ctypes.c_int
+    lib.stub_comm_max_group_depth.argtypes = [vp]
+    lib.stub_comm_max_group_depth.restype = ctypes.c_int
+    _native.rccl_bind(STUB)
+    yield lib
+    _native.rccl_bind()  # back to torch's RCCL for the other tests
+
+
+def _nan_like(t):
+    return torch.full_like(t, float("nan"))
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16"])
+@pytest.mark.parametrize("world,p", [(2, 64 * 37 * 2 + 13), (3, 64 * 41 * 3 + 50), (8, 64 * 29 * 8 + 63),
+                                     (8, 100), (3, 64)])
+def test_sharded_gather_assembles_the_whole_output(stub, world, p, dtype):
+    n = 5
+    rows = make_rows(n, p, world * 1000 + p, dtype)
+    w = orc.reference_weights(n, list(np.random.default_rng(world).dirichlet(np.ones(n))))
+    xs = to_dev(list(rows), dtype)
+    full = torch.empty_like(xs[0])
+    _native.wreduce(xs, w, full)
+    expected = from_dev(full)
+    assert orc.same_bits(expected, orc.wreduce(list(rows), w, dtype))
+    esz = xs[0].element_size()
+    bounds = [_native.shard_range(p, world, r, 64) for r in range(world)]
+    assert bounds[0][0] == 0 and bounds[-1][1] == p
+    assert all(bounds[q][1] == bounds[q + 1][0] for q in range(world - 1))
+    for r in range(world):
+        peers = []
+        for q, (b, e) in enumerate(bounds):
+            buf = _nan_like(full)
+            buf[b:e].copy_(full[b:e])  # what rank q holds after its own reduce
+            peers.append(buf)
+        out = _nan_like(full)
+        comm = stub.stub_comm_create(world, r, out.data_ptr(),
+                                     (ctypes.c_void_p * world)(*[t.data_ptr() for t in peers]))
+        try:
+            b, e = bounds[r]
+            _native.wreduce_sharded([x[b:e] for x in xs], w, out, comm, gather=True)
+            torch.cuda.synchronize()
+            assert orc.same_bits(from_dev(out), expected), f"rank {r} of {world}"
+            k = 64
+            roots = (ctypes.c_int * k)()
+            offs = (ctypes.c_size_t * k)()
+            cnts = (ctypes.c_size_t * k)()
+            m = stub.stub_comm_calls(comm, roots, offs, cnts, k)
+            want = [(q, bq * esz, eq - bq) for q, (bq, eq) in enumerate(bounds) if eq > bq]
+            assert [(roots[i], offs[i], cnts[i]) for i in range(m)] == want
+            assert stub.stub_comm_max_group_depth(comm) == 1  # one ncclGroupStart/End around them
+        finally:
+            stub.stub_comm_destroy(comm)
+
+
+def test_sharded_without_gather_writes_only_the_own_slice(stub):
+    world, p, n = 4, 64 * 10 * 4 + 7, 3
+    rows = make_rows(n, p, 5, "f32")
+    w = orc.reference_weights(n, None)
+    xs = to_dev(list(rows), "f32")
+    expected = orc.wreduce(list(rows), w, "f32")
+    peers = [_nan_like(xs[0]) for _ in range(world)]
+    for r in range(world):
+        b, e = _native.shard_range(p, world, r, 64)
+        out = _nan_like(xs[0])
+        comm = stub.stub_comm_create(world, r, out.data_ptr(),
+                                     (ctypes.c_void_p * world)(*[t.data_ptr() for t in peers]))
+        try:
+            _native.wreduce_sharded([x[b:e] for x in xs], w, out, comm, gather=False)
+            got = from_dev(out)
+            assert orc.same_bits(got[b:e], expected[b:e])
+            assert np.isnan(np.delete(got, np.arange(b, e))).all()
+            assert stub.stub_comm_calls(comm, None, None, None, 0) == 0
+        finally:
+            stub.stub_comm_destroy(comm)
+
+
+def test_sharded_rejects_a_slice_of_the_wrong_length(stub):
+    world, p = 2, 1000
+    x = torch.zeros(p, device=dev())
+    out = torch.empty(p, device=dev())
+    comm = stub.stub_comm_create(world, 1, out.data_ptr(), (ctypes.c_void_p * 2)(out.data_ptr(), out.data_ptr()))
+    try:
+        with pytest.raises(_native.DlsimError, match="slices have"):
+            _native.wreduce_sharded([x[:500]], orc.reference_weights(1, None), out, comm)
+    finally:
+        stub.stub_comm_destroy(comm)

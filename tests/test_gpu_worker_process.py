@@ -1,79 +1,59 @@
 """The reference's process model around the HIP aggregate (GPU).
 
-The broker hands tasks to worker processes over torch.multiprocessing queues
-with the file_system sharing strategy (dasklearn/worker.py:6,21-38,
-broker.py:142-143, 227-236): host models cross the process boundary through
-shared memory, the worker runs globals()[func_name](settings, data), and the
-result models travel back the same way. Here one spawned worker process runs
-that loop (tests/_worker_child.py) with the HIP task functions; the parent
-checks every result against the oracle bit for bit, and that a failing task
-comes back as ("error", task, None) and ends the worker, as in the reference."""
+dasklearn/broker.py imports the task functions at top level (broker.py:16),
+sets the file_system sharing strategy (broker.py:26) and starts its workers
+with multiprocessing.Process under the default start method — fork on Linux
+(broker.py:227-233); each worker runs worker.py:21-38's loop, host models
+crossing the process boundary through shared memory. With INTEGRATION.md's
+hook the top-level import is `from dasklearn_amd.functions import *`, so the
+package must import in the broker WITHOUT initialising the GPU, and a forked
+worker must run the HIP aggregate.
+
+tests/_broker_child.py is that broker, started here as a fresh interpreter
+(this pytest process has used the GPU, so it must not be the one that forks;
+and torch's shm-manager helper then belongs to the broker and leaves with it,
+not with pytest). Its worker runs the restated loop (tests/_worker_child.py):
+results are checked against the oracle bit for bit, buffers come from
+models[0], and a failing task comes back as ("error", task, None) and ends the
+worker, as in the reference. Both start methods are covered."""
 from __future__ import annotations
 
-import numpy as np
-import pytest
-import torch
-import torch.multiprocessing as mp
-from torch import nn
+import json
+import os
+import subprocess
+import sys
+import time
 
-from oracle import oracle as orc
+import pytest
 
 pytestmark = pytest.mark.gpu
 
-
-class Net(nn.Module):
-    """GNLeNet-sized convolutional model with GroupNorm-free BN buffers."""
-
-    def __init__(self, seed):
-        super().__init__()
-        g = torch.Generator().manual_seed(seed)
-        self.conv = nn.Conv2d(3, 32, 5)
-        self.bn = nn.BatchNorm2d(32)
-        self.fc = nn.Linear(576, 10)
-        with torch.no_grad():
-            for p in self.parameters():
-                p.copy_(torch.randn(p.shape, generator=g) * 0.05)
-            self.bn.running_mean.copy_(torch.randn(32, generator=g))
+HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def _flat(m):
-    return torch.cat([p.detach().reshape(-1) for p in m.parameters()]).numpy()
+def _wait_gone(pids, seconds):
+    import psutil
+    deadline = time.monotonic() + seconds
+    alive = list(pids)
+    while True:
+        alive = [p for p in alive if psutil.pid_exists(p) and psutil.Process(p).status() != psutil.STATUS_ZOMBIE]
+        if not alive or time.monotonic() > deadline:
+            return alive
+        time.sleep(0.1)
 
 
-def test_worker_process_round_trip():
-    torch.multiprocessing.set_sharing_strategy("file_system")
-    ctx = mp.get_context("spawn")
-    shared, results = ctx.Queue(), ctx.Queue()
-    from _worker_child import worker_main
-    proc = ctx.Process(target=worker_main, args=(shared, results, 0), daemon=True)
-    proc.start()
-    try:
-        models = [Net(s) for s in range(6)]
-        w = [0.1, 0.3, 0.2, 0.15, 0.05, 0.2]
-        shared.put(("agg_0", "aggregate", {"models": models[:4], "round": 1, "peer": 0}))
-        shared.put(("agg_1", "aggregate", {"models": models, "round": 1, "peer": 1, "weights": w}))
-        shared.put(("agg_bad", "aggregate", {"models": models[:3], "round": 1, "peer": 2, "weights": w}))
-        got = {}
-        for _ in range(3):
-            name, res, info = results.get(timeout=90)
-            got[name] = (res, info)
-        # aggregate tasks: [model] on the host, bit-identical to the oracle,
-        # buffers from models[0] (fedavg.py:20)
-        for name, ms, weights in (("agg_0", models[:4], None), ("agg_1", models, w)):
-            res, info = got[name]
-            assert isinstance(res, list) and len(res) == 1 and info["worker"] == 0
-            out = res[0]
-            assert all(not p.is_cuda for p in out.parameters())
-            exp = orc.wreduce([_flat(m) for m in ms], orc.reference_weights(len(ms), weights), "f32")
-            assert orc.same_bits(_flat(out), exp), name
-            assert torch.equal(out.bn.running_mean, ms[0].bn.running_mean)
-        # a weight-count mismatch fails the task: ("error", task, None), worker exits
-        assert got["error"][0] == "agg_bad" and got["error"][1] is None
-        proc.join(timeout=30)
-        assert not proc.is_alive()
-    finally:
-        if proc.is_alive():
-            shared.put(None)
-            proc.join(timeout=10)
-        if proc.is_alive():
-            proc.kill()
+@pytest.mark.parametrize("method", ["fork", "spawn"])
+def test_broker_worker_round_trip(method):
+    r = subprocess.run([sys.executable, os.path.join(HERE, "_broker_child.py"), method], capture_output=True,
+                       text=True, timeout=240)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert lines, r.stdout[-2000:] + r.stderr[-3000:]
+    out = json.loads(lines[-1])
+    assert out["start_method"] == method
+    assert out["gpu_initialised_before_fork"] is False  # importing the hook does not touch the GPU
+    assert out["checks"] == {"agg_0": True, "agg_1": True, "agg_2": True, "error_protocol": True}, out
+    assert out["worker_exitcode"] == 0 and out["ok"] and r.returncode == 0, out
+    # torch's helpers (the file_system strategy's shm manager) leave with their
+    # last client; none may outlive the broker for long
+    left = _wait_gone([h["pid"] for h in out["helpers"]], 15)
+    assert not left, f"helper processes still alive: {out['helpers']}"
