@@ -533,6 +533,20 @@ def chunk_mean_ilp_begin(m: int, n: int, threads: int) -> int:
     return int(load().dlsim_chunk_mean_ilp_begin(m, n, threads))
 
 
+def wreduce_tensors_raw(in_ptrs: Sequence[int], n: int, numels: Sequence[int], weights_f32, out_ptrs: Sequence[int],
+                       dtype: int, mode: int, stream_handle) -> None:
+    """dlsim_wreduce_tensors on pointers the caller has already validated
+    (the arena path: every tensor checked against models[0]'s layout, on the
+    output's device, contiguous): no per-tensor Python checks.
+    in_ptrs model-major (tensor k of model i at i * t + k)."""
+    t = len(numels)
+    w = np.ascontiguousarray(weights_f32, dtype=np.float32)
+    rc = load().dlsim_wreduce_tensors((ctypes.c_void_p * len(in_ptrs))(*in_ptrs), n, t,
+                                      (ctypes.c_size_t * t)(*numels), w.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                                      (ctypes.c_void_p * t)(*out_ptrs), dtype, mode, stream_handle)
+    _check("dlsim_wreduce_tensors", rc)
+
+
 def wreduce_tensors(inputs_by_model, weights_f32, outs, mode: int = DLSIM_EXACT, stream=None):
     """Tensor-list form: inputs_by_model[i][k] is tensor k of model i."""
     lib = load()
@@ -567,6 +581,25 @@ def wreduce_tensors(inputs_by_model, weights_f32, outs, mode: int = DLSIM_EXACT,
                                    optrs, dt, mode, _stream_handle(dev, stream) if t else None)
     _check("dlsim_wreduce_tensors", rc)
     return outs
+
+
+def host_wreduce_raw(src_ptrs: Sequence[int], n: int, numels: Sequence[int], weights_f32, staging, rows, out,
+                     host_out, dtype: int, mode: int, chunk_elems: int, threads: int, stream_handle,
+                     h2d_stream=None, d2h_stream=None) -> None:
+    """dlsim_host_wreduce on host pointers the caller has already validated
+    (the arena path: contiguous host tensors of models[0]'s layout), with
+    staging / rows / out / host_out checked here once."""
+    if staging.stride(0) != rows.stride(0) or staging.is_cuda or not rows.is_cuda or not out.is_cuda:
+        raise ValueError("staging/rows: a pinned host and a device [n, >= total] buffer with equal strides")
+    t = len(numels)
+    w = np.ascontiguousarray(weights_f32, dtype=np.float32)
+    rc = load().dlsim_host_wreduce(
+        n, t, (ctypes.c_void_p * len(src_ptrs))(*src_ptrs), (ctypes.c_size_t * t)(*numels),
+        w.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), staging.data_ptr(), rows.data_ptr(), staging.stride(0),
+        out.data_ptr(), None if host_out is None else host_out.data_ptr(), dtype, mode, chunk_elems, threads,
+        stream_handle, None if h2d_stream is None else h2d_stream.cuda_stream,
+        None if d2h_stream is None else d2h_stream.cuda_stream)
+    _check("dlsim_host_wreduce", rc)
 
 
 def host_wreduce(inputs_by_model, weights_f32, staging, rows, out, host_out=None, mode: int = DLSIM_EXACT,

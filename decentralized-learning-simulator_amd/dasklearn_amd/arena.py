@@ -41,29 +41,30 @@ def module_params(module: nn.Module) -> List[nn.Parameter]:
     """list(module.parameters()) without torch's generator stack: the modules
     in named_modules() pre-order (each once), then each module's _parameters
     in order, skipping None and parameters already seen (by identity) — the
-    same list, ~3x faster on the per-task path."""
+    same list, several times faster on the per-task path."""
     out: List[nn.Parameter] = []
-    seen_p, seen_m = set(), set()
-    stack = [module]
-    while stack:
-        m = stack.pop()
-        if id(m) in seen_m:
-            continue
-        seen_m.add(id(m))
+    seen = set()  # ids of modules and parameters visited
+
+    def visit(m):
         for p in m._parameters.values():
-            if p is not None and id(p) not in seen_p:
-                seen_p.add(id(p))
+            if p is not None and id(p) not in seen:
+                seen.add(id(p))
                 out.append(p)
-        kids = [c for c in m._modules.values() if c is not None]
-        stack.extend(reversed(kids))
+        for c in m._modules.values():
+            if c is not None and id(c) not in seen:
+                seen.add(id(c))
+                visit(c)
+
+    seen.add(id(module))
+    visit(module)
     return out
 
 
 class ParamLayout:
     """parameters() of a module grouped by dtype, with flat offsets."""
 
-    def __init__(self, module: nn.Module):
-        self.params: List[nn.Parameter] = module_params(module)
+    def __init__(self, module: nn.Module, params: Optional[List[nn.Parameter]] = None):
+        self.params: List[nn.Parameter] = module_params(module) if params is None else params
         self.shapes = [tuple(p.shape) for p in self.params]
         self.groups: "OrderedDict[torch.dtype, List[int]]" = OrderedDict()
         for k, p in enumerate(self.params):
@@ -94,15 +95,26 @@ class ParamLayout:
         other.params = params
         return other
 
+    def matches(self, ps: Sequence[torch.Tensor]) -> bool:
+        """ps has this layout's signature (count, shapes, dtypes)."""
+        if len(ps) != len(self._signature):
+            return False
+        for a, (shape, dt) in zip(ps, self._signature):
+            if a.dtype is not dt or a.shape != shape:
+                return False
+        return True
+
     def check_compatible(self, module: nn.Module) -> List[nn.Parameter]:
         ps = module_params(module)
         # The reference zips parameters() (fedavg.py:24) and silently truncates
-        # on a mismatch; equal shapes are what it assumes, so insist on them.
-        if len(ps) != len(self.params):
-            raise ValueError("models have different numbers of parameters")
-        for k, (a, (shape, dt)) in enumerate(zip(ps, self._signature)):
-            if a.dtype is not dt or a.shape != shape:
-                raise ValueError(f"parameter {k}: shape/dtype differs from models[0]")
+        # on a mismatch; equal shapes are what it assumes, so insist on them
+        # (INTEGRATION.md §3 lists this deviation).
+        if not self.matches(ps):
+            if len(ps) != len(self.params):
+                raise ValueError("models have different numbers of parameters")
+            for k, (a, (shape, dt)) in enumerate(zip(ps, self._signature)):
+                if a.dtype is not dt or a.shape != shape:
+                    raise ValueError(f"parameter {k}: shape/dtype differs from models[0]")
         return ps
 
     def arena_view(self, params: Sequence[torch.Tensor], dt: torch.dtype) -> Optional[torch.Tensor]:
@@ -112,16 +124,35 @@ class ParamLayout:
         first = params[idx[0]]
         base = first.data_ptr()
         esz = first.element_size()
-        if [params[k].data_ptr() - base for k in idx] != [o * esz for o in self._group_offsets[dt]]:
-            return None
-        # one storage (adjacent separate allocations are not an arena) and
-        # contiguous tensors (a transposed view could start at the right place)
-        storage = first.untyped_storage().data_ptr()
-        if any(params[k].untyped_storage().data_ptr() != storage or not params[k].is_contiguous()
-               for k in idx):
-            return None
+        # every tensor contiguous (a transposed view could start at the right
+        # place) and at its offset in the layout
+        for k, o in zip(idx, self._group_offsets[dt]):
+            q = params[k]
+            if q.data_ptr() - base != o * esz or not q.is_contiguous():
+                return None
+        # ...inside the first tensor's storage: adjacent separate allocations
+        # are not an arena (one storage check instead of one per tensor)
         total = self.totals[dt]
+        if first.untyped_storage().nbytes() < (first.storage_offset() + total) * esz:
+            return None
         return torch.as_strided(first.detach(), (total,), (1,), first.storage_offset())
+
+
+# One ParamLayout per model class, reused for every model of that class whose
+# parameter signature matches (a new layout replaces it otherwise): the
+# per-task path then builds no layout for the models of a simulation.
+_CLASS_LAYOUTS: Dict[type, ParamLayout] = {}
+
+
+def layout_of(module: nn.Module, params: Optional[List[nn.Parameter]] = None) -> ParamLayout:
+    """ParamLayout over `module`'s parameters, from the per-class cache."""
+    ps = module_params(module) if params is None else params
+    known = _CLASS_LAYOUTS.get(type(module))
+    if known is not None and known.matches(ps):
+        return known.rebind(ps)
+    layout = ParamLayout(module, ps)
+    _CLASS_LAYOUTS[type(module)] = layout
+    return layout
 
 
 def row_stride(numel: int, elem_bytes: int) -> int:
@@ -276,6 +307,14 @@ def pipeline_chunk_elems(total: int, esz: int) -> int:
     return 0 if k == 1 else -(-total // k)
 
 
+# Host results below this many bytes come back into pageable memory (the
+# runtime stages the copy): a fresh page-locked block costs far more than the
+# staged copy of a small model (hipHostMalloc ~0.2 ms against ~0.05 ms for a
+# GNLeNet result, scripts/probe_result_alloc.py), and a result the caller
+# keeps would hold the pinned block for its lifetime.
+PAGEABLE_RESULT_BYTES = 4 << 20
+
+
 def _host_pipeline(all_params, idx, layout, dt, dev, out, weights_f32, mode, stream, want_host):
     """Host models -> device reduce (-> host result) in one dlsim_host_wreduce
     call: the parameters are packed into pinned staging rows by the library's
@@ -290,13 +329,27 @@ def _host_pipeline(all_params, idx, layout, dt, dev, out, weights_f32, mode, str
     once `stream` is) or None (the result is in `out`, queued on `stream`)."""
     n = len(all_params)
     total = layout.totals[dt]
-    chunk = pipeline_chunk_elems(total, out.element_size())
+    esz = out.element_size()
+    chunk = pipeline_chunk_elems(total, esz)
     h2d, d2h = _side_streams(dev) if chunk else (None, None)
-    host = torch.empty(total, dtype=dt, pin_memory=True) if want_host else None
+    host = None
+    if want_host:
+        host = torch.empty(total, dtype=dt, pin_memory=total * esz >= PAGEABLE_RESULT_BYTES)
+    # the layout checked every tensor's shape and dtype against models[0];
+    # the library reads data pointers, so only non-contiguous ones are copied
+    keep, ptrs = [], []
+    for ps in all_params:
+        for k in idx:
+            q = ps[k]
+            if not q.is_contiguous():
+                q = q.contiguous()
+                keep.append(q)
+            ptrs.append(q.data_ptr())
     dev_rows, pinned = STAGING.acquire(dev, dt, n, total, stream)
     try:
-        _native.host_wreduce([[ps[k] for k in idx] for ps in all_params], weights_f32, pinned, dev_rows, out,
-                             host, mode, chunk, None, stream, h2d, d2h)
+        _native.host_wreduce_raw(ptrs, n, layout.split_sizes[dt], weights_f32, pinned, dev_rows, out, host,
+                                 _native.dtype_code(dt), mode, chunk, torch.get_num_threads(), stream.cuda_stream,
+                                 h2d, d2h)
     finally:
         STAGING.release(dev, dt, stream)
     return host
@@ -318,18 +371,22 @@ def _staged_reduce(all_params, idx, dt, dev, out, weights, mode, stream):
 
 
 def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, mode: int,
-                             device=None, timing: Optional[dict] = None, host_out: bool = False,
+                             device=None, timing: Optional[dict] = None, host_out: Optional[bool] = False,
                              weights_f64: Optional[np.ndarray] = None
-                             ) -> Tuple[ParamLayout, Dict[torch.dtype, torch.Tensor], torch.device, bool]:
+                             ) -> Tuple[ParamLayout, Dict[torch.dtype, torch.Tensor], torch.device, bool, bool]:
     """Reduce the parameters of `models` into one fresh arena per dtype.
 
     weights_f32: the fp32-rounded weights (fp32/bf16/fp16 groups);
     weights_f64: the exact double weights an fp64 group needs (fedavg.py:25
     keeps the Python float exact for a double tensor); default: widened fp32.
-    Returns (layout, arenas, device, on_host). With host_out, host models take
-    the chunked pipeline and come back already in pinned host memory
-    (on_host True, copies complete); otherwise the arenas are on the device."""
+    host_out None: as the reference's output, iff models[0]'s parameters are on
+    the host. Returns (layout, arenas, device, on_host, host_out). With
+    host_out, host models take the chunked pipeline and come back already in
+    host memory (on_host True, copies complete); otherwise the arenas are on
+    the device."""
     layout, all_params, in_views = input_arenas(models)
+    if host_out is None:
+        host_out = not any(p.is_cuda for p in layout.params)
     dev = _target_device(all_params[0], device)
     n = len(models)
     outs: Dict[torch.dtype, torch.Tensor] = {}
@@ -349,7 +406,8 @@ def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, m
                 if piped:
                     outs[dt] = torch.empty(0, dtype=dt)
                 continue
-            on_dev = all(all_params[i][idx[0]].device == dev for i in range(n))
+            dix = dev.index
+            on_dev = all(all_params[i][idx[0]].get_device() == dix for i in range(n))
             if on_dev:
                 views = in_views[dt]
                 st.mark("layout")
@@ -361,13 +419,21 @@ def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, m
                     _staged_reduce(all_params, idx, dt, dev, out, w, mode, stream)
                     st.mark("kernel")
                     continue
-                # the ABI reads data pointers only: no detach() objects for
-                # contiguous parameters
-                rows = [[ps[k] if ps[k].is_contiguous() else ps[k].detach().contiguous() for k in idx]
-                        for ps in all_params]
-                outs_k = [out[layout.offsets[k]:layout.offsets[k] + layout.params[k].numel()]
-                          for k in idx]
-                _native.wreduce_tensors(rows, weights_f32, outs_k, mode)
+                # separate device tensors, read in place: the layout checked
+                # shapes and dtypes, so only pointers go to the library (no
+                # detach() objects, no output slices)
+                keep, ptrs = [], []
+                for ps in all_params:
+                    for k in idx:
+                        q = ps[k]
+                        if not q.is_contiguous():
+                            q = q.detach().contiguous()
+                            keep.append(q)
+                        ptrs.append(q.data_ptr())
+                base, esz = out.data_ptr(), out.element_size()
+                _native.wreduce_tensors_raw(ptrs, n, layout.split_sizes[dt], weights_f32,
+                                            [base + layout.offsets[k] * esz for k in idx],
+                                            _native.dtype_code(dt), mode, stream.cuda_stream)
                 st.mark("kernel")
                 continue
             if not f64 and not any(all_params[i][idx[0]].is_cuda for i in range(n)):
@@ -391,7 +457,7 @@ def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, m
             st.mark("d2h")
         else:
             stream.synchronize()
-    return layout, outs, dev, piped
+    return layout, outs, dev, piped, host_out
 
 
 def arenas_to_host(arenas: Dict[torch.dtype, torch.Tensor], stream) -> Dict[torch.dtype, torch.Tensor]:
@@ -409,30 +475,55 @@ def arenas_to_host(arenas: Dict[torch.dtype, torch.Tensor], stream) -> Dict[torc
 
 
 # Atomic attribute types a module clone may share (deepcopy returns them as is).
-_ATOMIC = (type(None), bool, int, float, complex, str, bytes, torch.dtype, torch.device, torch.layout,
-           torch.memory_format)
+_ATOMIC = frozenset((type(None), bool, int, float, complex, str, bytes, torch.dtype, torch.device, torch.layout,
+                     torch.memory_format))
+
+_PLAIN_CLASSES: Dict[type, bool] = {}
 
 
 def _plain_module_class(cls) -> bool:
     """Classes whose copy.deepcopy is nn.Module's default reduce/getstate/
     setstate round trip, which _clone_module restates without the generic
-    __reduce_ex__ machinery."""
-    return (cls.__reduce_ex__ is object.__reduce_ex__ and cls.__reduce__ is object.__reduce__
-            and getattr(cls, "__deepcopy__", None) is None and cls.__getstate__ is nn.Module.__getstate__)
+    __reduce_ex__ machinery (cached per class)."""
+    ok = _PLAIN_CLASSES.get(cls)
+    if ok is None:
+        ok = _PLAIN_CLASSES[cls] = (cls.__reduce_ex__ is object.__reduce_ex__ and cls.__reduce__ is object.__reduce__
+                                    and getattr(cls, "__deepcopy__", None) is None
+                                    and cls.__getstate__ is nn.Module.__getstate__
+                                    and cls.__setstate__ is nn.Module.__setstate__)
+    return ok
+
+
+# Attributes nn.Module.__setstate__ adds when an (old) state lacks them; with
+# all of them present it is exactly __dict__.update(state).
+_SETSTATE_KEYS = frozenset(("_forward_pre_hooks", "_forward_pre_hooks_with_kwargs", "_forward_hooks_with_kwargs",
+                            "_forward_hooks_always_called", "_state_dict_hooks", "_state_dict_pre_hooks",
+                            "_load_state_dict_pre_hooks", "_load_state_dict_post_hooks",
+                            "_non_persistent_buffers_set", "_is_full_backward_hook", "_backward_pre_hooks"))
+
+
+def _all_atomic(v) -> bool:
+    for x in v:
+        if type(x) not in _ATOMIC:
+            return False
+    return True
 
 
 def _clone_module(m: nn.Module, memo: dict) -> nn.Module:
-    """copy.deepcopy(m, memo) for a module tree, ~5x faster for plain modules.
+    """copy.deepcopy(m, memo) for a module tree, several times faster for plain
+    modules.
 
     deepcopy of an nn.Module is: state = Module.__getstate__() (the __dict__
     minus _compiled_call_impl), deep-copied with the shared memo, then
     cls.__new__(cls).__setstate__(state). That is what this does, taking
     parameters from the memo (the arena views module_from_arenas installs),
-    recursing into `_modules` directly, and sharing atomic values and fresh
-    empty hook containers without a generic round trip. Anything else (buffers,
-    non-empty containers, custom attributes) goes through copy.deepcopy with
-    the same memo; classes with their own reduce/deepcopy/getstate take
-    copy.deepcopy whole."""
+    recursing into `_modules` directly, and keeping what deepcopy would return
+    unchanged without a round trip: atomic values and tuples of atomic values
+    (deepcopy returns those very objects), lists of atomic values (a shallow
+    copy, entered in the memo like deepcopy does) and fresh empty hook
+    containers. Anything else (buffers, non-empty containers, custom
+    attributes) goes through copy.deepcopy with the same memo; classes with
+    their own reduce/deepcopy/getstate take copy.deepcopy whole."""
     got = memo.get(id(m))
     if got is not None:
         return got
@@ -441,23 +532,34 @@ def _clone_module(m: nn.Module, memo: dict) -> nn.Module:
         return copy.deepcopy(m, memo)
     new = cls.__new__(cls)
     memo[id(m)] = new
-    state = {}
-    for k, v in m.__dict__.items():
-        if k == "_compiled_call_impl":
-            continue
+    d = m.__dict__
+    state = d.copy()
+    for k, v in d.items():
         tv = type(v)
+        if tv in _ATOMIC:
+            continue
         if k == "_modules":
             state[k] = tv((name, None if c is None else _clone_module(c, memo)) for name, c in v.items())
         elif k == "_parameters":
             state[k] = tv((name, None if q is None else (memo[id(q)] if id(q) in memo else copy.deepcopy(q, memo)))
                           for name, q in v.items())
-        elif tv in _ATOMIC:
-            state[k] = v
+        elif k == "_compiled_call_impl":
+            del state[k]
+        elif tv is tuple and _all_atomic(v):
+            continue
         elif (tv is dict or tv is OrderedDict or tv is set) and not v:
             state[k] = tv()
+        elif tv is list and _all_atomic(v):
+            c = memo.get(id(v))
+            if c is None:
+                c = memo[id(v)] = list(v)
+            state[k] = c
         else:
             state[k] = copy.deepcopy(v, memo)
-    new.__setstate__(state)
+    if _SETSTATE_KEYS.issubset(state):
+        new.__dict__.update(state)  # what Module.__setstate__ does with a complete state
+    else:
+        new.__setstate__(state)
     return new
 
 
@@ -521,7 +623,7 @@ def input_arenas(models: Sequence[nn.Module]):
     not an arena (separate storages, host memory, ...). Registered arenas
     (module_from_arenas outputs) skip the layout and contiguity checks."""
     reg0 = registered_arenas(models[0])
-    layout = reg0[0] if reg0 is not None else ParamLayout(models[0])
+    layout = reg0[0] if reg0 is not None else layout_of(models[0])
     all_params, views = [], {dt: [] for dt in layout.groups}
     for i, m in enumerate(models):
         reg = reg0 if i == 0 else registered_arenas(m)
@@ -556,9 +658,8 @@ def aggregate_modules(models: List[nn.Module], weights: Optional[Sequence[float]
         assert len(weights) == len(models)
     model0 = models[0]  # IndexError for an empty list, as the reference
     w32 = _native.fp32_weights(weights)
-    host_out = to_host if to_host is not None else not any(p.is_cuda for p in module_params(model0))
-    layout, arenas, dev, on_host = reduce_modules_to_arenas(models, w32, mode, device, timing, host_out,
-                                                            weights_f64=_native.f64_weights(weights))
+    layout, arenas, dev, on_host, host_out = reduce_modules_to_arenas(models, w32, mode, device, timing, to_host,
+                                                                      weights_f64=_native.f64_weights(weights))
     stream = torch.cuda.current_stream(dev)
     st = _Stages(timing, stream)
     if host_out and not on_host:

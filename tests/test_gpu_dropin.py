@@ -188,8 +188,11 @@ def test_device_resident_option_keeps_result_on_gpu():
     assert orc.same_bits(flat_of(res[0]), g["expected"])
 
 
-def test_host_result_is_pinned_and_stage_timing_works():
-    from dasklearn_amd import _native
+def test_host_result_placement_and_stage_timing_works():
+    """Host models -> host result: a small result comes back in pageable
+    memory (arena.PAGEABLE_RESULT_BYTES), a large one in page-locked memory;
+    both exact."""
+    from dasklearn_amd import _native, arena
     from dasklearn_amd.arena import aggregate_modules
     g = load_golden(os.path.join(GOLDEN, "cfg1_gnlenet_f32_n2_none.npz"))
     models = modules_from_golden(g)
@@ -197,8 +200,18 @@ def test_host_result_is_pinned_and_stage_timing_works():
     out = aggregate_modules(models, None, _native.DLSIM_EXACT, timing=stages)
     assert set(stages) >= {"layout", "pipeline", "module"}  # the D2H is part of the pipeline
     p0 = next(out.parameters())
-    assert not p0.is_cuda and p0.is_pinned()
+    assert not p0.is_cuda and not p0.is_pinned()  # 341 KB < PAGEABLE_RESULT_BYTES
     assert orc.same_bits(flat_of(out), g["expected"])
+    torch.manual_seed(9)
+    big = [Ragged([(arena.PAGEABLE_RESULT_BYTES // 4 + 1000,), (77,)]) for _ in range(3)]
+    with torch.no_grad():
+        for m in big:
+            for q in m.parameters():
+                q.normal_()
+    out = aggregate_modules(big, [0.2, 0.3, 0.5], _native.DLSIM_EXACT)
+    assert next(out.parameters()).is_pinned()
+    exp = orc.wreduce([flat_of(m) for m in big], orc.reference_weights(3, [0.2, 0.3, 0.5]), "f32")
+    assert orc.same_bits(flat_of(out), exp)
 
 
 def test_wire_decode_to_device_feeds_aggregate_without_packing():

@@ -286,3 +286,14 @@ def test_module_params_matches_parameters():
     for m in (Odd(), nn.Sequential(nn.Linear(2, 2), nn.Linear(2, 2)), nn.Linear(1, 1), nn.Module()):
         got, ref = module_params(m), list(m.parameters())
         assert len(got) == len(ref) and all(a is b for a, b in zip(got, ref))
+
+
+def test_clone_skips_setstate_only_when_it_is_a_plain_update():
+    """arena._clone_module replaces nn.Module.__setstate__ by __dict__.update
+    when the state has every attribute __setstate__ would add: the key list
+    must be exactly the one of this torch's __setstate__."""
+    import inspect
+    import re
+    src = inspect.getsource(nn.Module.__setstate__)
+    keys = set(re.findall(r'"(_\w+)" not in self\.__dict__', src))
+    assert keys == set(arena._SETSTATE_KEYS)
