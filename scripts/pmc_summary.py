@@ -23,6 +23,11 @@ import os
 import statistics
 
 KERNEL_RE = "k_wreduce"
+PROBE_RE = "XorProbe"  # bench.py's pattern probe runs the same kernel template: not the reduce
+
+
+def is_reduce(name: str) -> bool:
+    return KERNEL_RE in name and PROBE_RE not in name
 
 
 def rows(dirpath, suffix):
@@ -37,7 +42,7 @@ def counter_avg(dirpath, counter):
     vals = []
     for r in rows(dirpath, "counter_collection.csv"):
         name = r.get("Kernel_Name", "")
-        if KERNEL_RE in name and r.get("Counter_Name") == counter:
+        if is_reduce(name) and r.get("Counter_Name") == counter:
             vals.append(float(r["Counter_Value"]))
     if not vals:
         return None, 0
@@ -49,7 +54,7 @@ def counter_avg(dirpath, counter):
 def trace_avg_ns(dirpath):
     durs = []
     for r in rows(dirpath, "kernel_trace.csv"):
-        if KERNEL_RE in r.get("Kernel_Name", ""):
+        if is_reduce(r.get("Kernel_Name", "")):
             durs.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     if not durs:
         return None, 0
