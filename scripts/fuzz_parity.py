@@ -1,9 +1,13 @@
 """Randomised parity soak (GPU): every entry point against the oracle on random
 shapes, dtypes, alignments, weights and special values, for a time budget.
 
-  reduce      dlsim_wreduce (flat; exact bit-for-bit, FAST against its own oracle)
+  reduce      dlsim_wreduce / dlsim_wreduce_f64 (flat; exact bit-for-bit, FAST
+              against its own oracle; any fan-in; sometimes in place, the
+              output being one of the inputs)
   tensors     dlsim_wreduce_tensors (one model split into random tensors)
-  batched     dlsim_wreduce_batched (random tasks, mixed fan-in and sizes)
+  batched     dlsim_wreduce_batched (random tasks, mixed fan-in and sizes; some
+              tasks read earlier tasks' outputs or overwrite their inputs, which
+              must give the results of the calls made in task order)
   chunk_mean  dlsim_chunk_mean_batched (random m, n, threads) vs PyTorch's CPU order
   modules     FedAvg.aggregate on random module trees (mixed fp32/bf16/fp16
               parameters, buffers, host or device) vs the oracle per dtype group
@@ -36,10 +40,17 @@ import torch  # noqa: E402
 from dasklearn_amd import _native  # noqa: E402
 from oracle import oracle as orc  # noqa: E402
 
-DT = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16}
+DT = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16, "f64": torch.float64}
 
 
 def rand_values(rng, n, p, dtype):
+    if dtype == "f64":
+        x = rng.standard_normal((n, p)) * np.exp(rng.uniform(-20, 20))
+        if rng.random() < 0.3 and p > 0:
+            k = max(1, p // 50)
+            specials = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 5e-324, -1e-310, 1.7e308, 0.1, 1e-300])
+            x[rng.integers(0, n, size=k), rng.integers(0, p, size=k)] = rng.choice(specials, size=k)
+        return x
     scale = np.exp(rng.uniform(-6, 6)) if dtype == "f32" else np.exp(rng.uniform(-4, 4))
     x = (rng.standard_normal((n, p)) * scale).astype(np.float32)
     if rng.random() < 0.3 and p > 0:  # sprinkle special values
@@ -59,7 +70,7 @@ def rand_values(rng, n, p, dtype):
 def to_dev(rows, dtype, offset):
     out = []
     for r in rows:
-        h = torch.from_numpy(np.ascontiguousarray(r).view(np.int16).copy()).view(DT[dtype]) if dtype != "f32" \
+        h = torch.from_numpy(np.ascontiguousarray(r).view(np.int16).copy()).view(DT[dtype]) if dtype in ("bf16", "f16") \
             else torch.from_numpy(np.ascontiguousarray(r).copy())
         buf = torch.empty(h.numel() + offset, dtype=h.dtype, device="cuda")
         buf[offset:].copy_(h)
@@ -102,15 +113,18 @@ def first_diff(got, exp, rows, w):
                 inputs=[hex(int(c)) for c in col[:8]], weights=[float(x) for x in np.asarray(w)[:8]])
 
 
-def rand_weights(rng, n):
+def rand_weights(rng, n, dtype="f32"):
+    """Random weights as the reference's op sees them for this dtype (fp32-
+    rounded; exact doubles for f64)."""
     kind = rng.integers(0, 4)
-    if kind == 0:
-        return orc.reference_weights(n, None)
+    raw = None
     if kind == 1:
-        return orc.reference_weights(n, list(rng.dirichlet(np.ones(n))))
-    if kind == 2:
-        return orc.reference_weights(n, list(rng.standard_normal(n)))  # negative weights
-    return orc.reference_weights(n, list(rng.choice([0.0, 1.0, 1e-39, -2.5, 0.5], size=n)))
+        raw = [float(v) for v in rng.dirichlet(np.ones(n))]
+    elif kind == 2:
+        raw = [float(v) for v in rng.standard_normal(n)]  # negative weights
+    elif kind == 3:
+        raw = [float(v) for v in rng.choice([0.0, 1.0, 1e-39, -2.5, 0.5, 0.1], size=n)]
+    return orc.reference_weights_f64(n, raw) if dtype == "f64" else orc.reference_weights(n, raw)
 
 
 def rand_module(rng, seed):
@@ -120,7 +134,7 @@ def rand_module(rng, seed):
     from torch import nn
     g = torch.Generator().manual_seed(int(seed))
     n_leaf = int(rng.integers(1, 6))
-    dts = [DT[str(d)] for d in rng.choice(["f32", "f32", "bf16", "f16"], size=n_leaf)]
+    dts = [DT[str(d)] for d in rng.choice(["f32", "f32", "bf16", "f16", "f64"], size=n_leaf)]
     shapes = [tuple(int(v) for v in rng.integers(1, 40, size=int(rng.integers(1, 4)))) for _ in range(n_leaf)]
 
     class Leaf(nn.Module):
@@ -153,10 +167,12 @@ def main():
         if time.time() > t_note:  # progress (long runs must keep writing)
             print(json.dumps({"progress": counts, "failures": len(fails)}), file=sys.stderr, flush=True)
             t_note = time.time() + 20
-        dtype = rng.choice(["f32", "bf16", "f16"])
+        dtype = str(rng.choice(["f32", "bf16", "f16", "f64"]))
         which = rng.choice(["reduce", "tensors", "batched", "chunk_mean", "modules", "reconstruct",
                             "host_reduce", "host_chunk"],
                            p=[0.25, 0.1, 0.1, 0.2, 0.1, 0.1, 0.1, 0.05])
+        if dtype == "f64" and which != "reduce":  # fp64 is the single-task entry (dlsim_wreduce_f64)
+            dtype = "f32"
         try:
             if which == "reduce":
                 n = int(rng.choice([1, 2, 3, 5, 8, 9, 14, 15, 16, 17, 33, 128, 129, 200]))
@@ -164,17 +180,19 @@ def main():
                 rows = rand_values(rng, n, p, dtype)
                 off = int(rng.choice([0, 0, 0, 1]))
                 xs = to_dev(rows, dtype, off)
-                w = rand_weights(rng, n)
-                # FAST folds n > 128 in passes that round the partial sum to the
-                # element type between passes (tolerance-only there)
-                fast = n <= 128 and rng.random() < 0.2
-                out = to_dev([np.zeros(p, dtype=np.float32 if dtype == "f32" else np.uint16)], dtype,
-                             int(rng.choice([0, 0, 1])))[0]
+                w = rand_weights(rng, n, dtype)
+                fast = rng.random() < 0.2  # one pass for every n: one final rounding
+                in_place = rng.random() < 0.15
+                if in_place:
+                    out = xs[int(rng.integers(0, n))]
+                else:
+                    zero = np.zeros(p, dtype={"f32": np.float32, "f64": np.float64}.get(dtype, np.uint16))
+                    out = to_dev([zero], dtype, int(rng.choice([0, 0, 1])))[0]
                 _native.wreduce(xs, w, out, _native.DLSIM_FAST if fast else _native.DLSIM_EXACT)
                 exp = orc.wreduce(list(rows), w, dtype, "fast" if fast else "exact")
                 ok = orc.same_bits(bits(out), exp)
                 counts["reduce_fast" if fast else "reduce"] += 1
-                case = dict(kind="reduce", dtype=dtype, n=n, p=p, off=off, fast=bool(fast))
+                case = dict(kind="reduce", dtype=dtype, n=n, p=p, off=off, fast=bool(fast), in_place=bool(in_place))
                 if not ok:
                     case["diff"] = first_diff(bits(out), exp, rows, w)
             elif which == "tensors":
@@ -194,17 +212,37 @@ def main():
                 case = dict(kind="tensors", dtype=dtype, n=n, sizes=len(sizes))
             elif which == "batched":
                 tasks, exps = [], []
+                chain = rng.random() < 0.3
+                p_chain = int(rng.choice([1, 5, 100, 4097]))
                 for _ in range(int(rng.integers(1, 60))):
                     n = int(rng.choice([1, 2, 3, 7, 8, 16, 17, 40]))
-                    p = int(rng.choice([1, 5, 100, 4097, 85_354]))
+                    p = p_chain if chain else int(rng.choice([1, 5, 100, 4097, 85_354]))
                     rows = rand_values(rng, n, p, dtype)
                     xs = to_dev(rows, dtype, int(rng.choice([0, 0, 0, 1])))
+                    rows = list(rows)
                     w = rand_weights(rng, n)
                     out = torch.empty(p, dtype=DT[dtype], device="cuda")
+                    if chain and tasks and rng.random() < 0.5:
+                        # read an earlier task's output (its result, in task order)
+                        j = int(rng.integers(0, len(tasks)))
+                        i = int(rng.integers(0, n))
+                        xs[i], rows[i] = tasks[j][2], exps[j][0]
+                    if chain and tasks and rng.random() < 0.2:
+                        # overwrite an input of an earlier task (after it was read);
+                        # never one of this task's own inputs or an earlier output
+                        j = int(rng.integers(0, len(tasks)))
+                        cand = tasks[j][0][0]
+                        if all(cand is not x for x in xs) and all(cand is not t[2] for t in tasks):
+                            out = cand
                     tasks.append((xs, w, out))
-                    exps.append((orc.wreduce(list(rows), w, dtype), rows, n, p))
+                    exps.append((orc.wreduce(rows, w, dtype), rows, n, p))
                 _native.wreduce_batched(tasks)
-                oks = [orc.same_bits(bits(t[2]), e[0]) for t, e in zip(tasks, exps)]
+                # a buffer written by a later task holds that task's result
+                final = {}
+                for t, e in zip(tasks, exps):
+                    final[id(t[2])] = (t[2], e[0])
+                oks = [orc.same_bits(bits(t[2]), e[0]) if final[id(t[2])][1] is e[0] else True
+                       for t, e in zip(tasks, exps)]
                 ok = all(oks)
                 counts["batched"] += 1
                 case = dict(kind="batched", dtype=dtype, tasks=len(tasks))
@@ -220,11 +258,12 @@ def main():
                 on_dev = bool(rng.random() < 0.5)
                 if on_dev:
                     models = [m.to("cuda") for m in models]
-                weights = None if rng.random() < 0.4 else [float(v) for v in rand_weights(rng, n)]
+                weights = None if rng.random() < 0.4 else [float(v) for v in rng.standard_normal(n)]
                 out = FedAvg.aggregate(models, weights)
-                w = orc.reference_weights(n, weights)
                 ok = all(p.is_cuda == on_dev for p in out.parameters())
-                for dt, code in ((torch.float32, "f32"), (torch.bfloat16, "bf16"), (torch.float16, "f16")):
+                for dt, code in ((torch.float32, "f32"), (torch.bfloat16, "bf16"), (torch.float16, "f16"),
+                                 (torch.float64, "f64")):
+                    w = orc.reference_weights_f64(n, weights) if code == "f64" else orc.reference_weights(n, weights)
                     rows = []
                     for m in models:
                         ps = [p.detach().reshape(-1).cpu() for p in m.parameters() if p.dtype == dt]
