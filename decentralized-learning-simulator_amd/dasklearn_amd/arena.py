@@ -35,13 +35,19 @@ import torch
 from torch import nn
 
 from . import _native
+from . import _pyhost  # csrc/pyhost.cpp (built with the library by __graft_entry__.build())
 
 
 def module_params(module: nn.Module) -> List[nn.Parameter]:
-    """list(module.parameters()) without torch's generator stack: the modules
-    in named_modules() pre-order (each once), then each module's _parameters
-    in order, skipping None and parameters already seen (by identity) — the
-    same list, several times faster on the per-task path."""
+    """list(module.parameters()): the modules in named_modules() pre-order
+    (each once), then each module's _parameters in order, skipping None and
+    parameters already seen (by identity) — walked in C (csrc/pyhost.cpp),
+    the per-task path visits every parameter of every model."""
+    return _pyhost.module_params(module)
+
+
+def module_params_py(module: nn.Module) -> List[nn.Parameter]:
+    """The same list in Python (tests compare the two)."""
     out: List[nn.Parameter] = []
     seen = set()  # ids of modules and parameters visited
 
@@ -82,7 +88,7 @@ class ParamLayout:
                 off += self.params[k].numel()
             self.totals[dt] = off
             self._group_offsets[dt] = offs
-        self._signature = [(p.shape, p.dtype) for p in self.params]
+        self._signature = tuple((p.shape, p.dtype) for p in self.params)
         # per dtype group: element counts and shapes for splitting an arena
         self.split_sizes = {dt: [self.params[k].numel() for k in idx] for dt, idx in self.groups.items()}
         self.split_shapes = {dt: [None if self.params[k].dim() == 1 else self.params[k].shape for k in idx]
@@ -96,13 +102,8 @@ class ParamLayout:
         return other
 
     def matches(self, ps: Sequence[torch.Tensor]) -> bool:
-        """ps has this layout's signature (count, shapes, dtypes)."""
-        if len(ps) != len(self._signature):
-            return False
-        for a, (shape, dt) in zip(ps, self._signature):
-            if a.dtype is not dt or a.shape != shape:
-                return False
-        return True
+        """ps has this layout's signature (count, shapes, dtypes); in C."""
+        return _pyhost.matches(ps, self._signature)
 
     def check_compatible(self, module: nn.Module) -> List[nn.Parameter]:
         ps = module_params(module)
@@ -337,14 +338,7 @@ def _host_pipeline(all_params, idx, layout, dt, dev, out, weights_f32, mode, str
         host = torch.empty(total, dtype=dt, pin_memory=total * esz >= PAGEABLE_RESULT_BYTES)
     # the layout checked every tensor's shape and dtype against models[0];
     # the library reads data pointers, so only non-contiguous ones are copied
-    keep, ptrs = [], []
-    for ps in all_params:
-        for k in idx:
-            q = ps[k]
-            if not q.is_contiguous():
-                q = q.contiguous()
-                keep.append(q)
-            ptrs.append(q.data_ptr())
+    keep, ptrs = _data_ptrs(all_params, idx)
     dev_rows, pinned = STAGING.acquire(dev, dt, n, total, stream)
     try:
         _native.host_wreduce_raw(ptrs, n, layout.split_sizes[dt], weights_f32, pinned, dev_rows, out, host,
@@ -353,6 +347,24 @@ def _host_pipeline(all_params, idx, layout, dt, dev, out, weights_f32, mode, str
     finally:
         STAGING.release(dev, dt, stream)
     return host
+
+
+def _data_ptrs(all_params, idx):
+    """(keep-alive list, data pointers of tensor k of every model for k in
+    idx, model-major). Non-contiguous tensors are copied (and kept alive until
+    the stream-ordered work that reads them is queued)."""
+    ptrs = _pyhost.data_ptrs(all_params, idx)
+    if ptrs is not None:
+        return [], ptrs
+    keep, ptrs = [], []
+    for ps in all_params:
+        for k in idx:
+            q = ps[k]
+            if not q.is_contiguous():
+                q = q.detach().contiguous()
+                keep.append(q)
+            ptrs.append(q.data_ptr())
+    return keep, ptrs
 
 
 def _staged_reduce(all_params, idx, dt, dev, out, weights, mode, stream):
@@ -422,14 +434,7 @@ def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, m
                 # separate device tensors, read in place: the layout checked
                 # shapes and dtypes, so only pointers go to the library (no
                 # detach() objects, no output slices)
-                keep, ptrs = [], []
-                for ps in all_params:
-                    for k in idx:
-                        q = ps[k]
-                        if not q.is_contiguous():
-                            q = q.detach().contiguous()
-                            keep.append(q)
-                        ptrs.append(q.data_ptr())
+                keep, ptrs = _data_ptrs(all_params, idx)
                 base, esz = out.data_ptr(), out.element_size()
                 _native.wreduce_tensors_raw(ptrs, n, layout.split_sizes[dt], weights_f32,
                                             [base + layout.offsets[k] * esz for k in idx],

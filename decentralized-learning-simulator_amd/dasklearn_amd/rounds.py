@@ -28,7 +28,7 @@ import torch
 from torch import nn
 
 from . import _native
-from .arena import ParamLayout, _target_device, module_params, registered_arenas
+from .arena import ParamLayout, _target_device, layout_of, module_params, registered_arenas
 from .batch import _device_views, _resolve, aggregate_arena_tasks
 
 Task = Tuple[str, str, dict]  # (task_name, func_name, data with placeholders)
@@ -36,15 +36,6 @@ Task = Tuple[str, str, dict]  # (task_name, func_name, data with placeholders)
 # Host-trained models of a wave go to the device in groups of at most this
 # many bytes (RoundExecutor._upload_host_models).
 UPLOAD_GROUP_BYTES = 256 << 20
-
-
-def _same_signature(ps, sig) -> bool:
-    if len(ps) != len(sig):
-        return False
-    for p, (shape, dt) in zip(ps, sig):
-        if p.dtype is not dt or p.shape != shape:
-            return False
-    return True
 
 
 def _is_ref(v) -> bool:
@@ -78,7 +69,6 @@ class RoundExecutor:
         self.mode = mode
         self.results: Dict[str, list] = {}
         self.waves: List[List[str]] = []
-        self._layouts: Dict[type, object] = {}  # model class -> a ParamLayout of it
         self._stages: List[Optional[torch.Tensor]] = [None, None]  # pinned upload buffers
         self._stage_events: List[Optional[torch.cuda.Event]] = [None, None]
 
@@ -93,14 +83,8 @@ class RoundExecutor:
 
     def _layout_for(self, m: nn.Module) -> ParamLayout:
         """m's ParamLayout; a model of a class seen before reuses that layout
-        when the parameter signature matches (no per-model ParamLayout build)."""
-        known = self._layouts.get(type(m))
-        ps = module_params(m)
-        if known is not None and _same_signature(ps, known._signature):
-            return known.rebind(ps)
-        layout = ParamLayout(m)
-        self._layouts[type(m)] = layout
-        return layout
+        when the parameter signature matches (arena.layout_of)."""
+        return layout_of(m)
 
     def _arena_of(self, m: nn.Module, cache: dict):
         """(layout over m's parameters, {dtype: flat device arena}) for one

@@ -130,6 +130,9 @@ def main():
     ap.add_argument("--host", action="store_true", help="train returns host models (CPU training)")
     ap.add_argument("--profile", default=None, help="cProfile the batched run into this file")
     ap.add_argument("--profile-seq", default=None, help="cProfile the sequential run into this file")
+    ap.add_argument("--reps", type=int, default=3,
+                    help="repetitions of each way, interleaved; the line reports the median and the best "
+                         "(Python's collector runs at times set by the objects the whole run keeps alive)")
     a = ap.parse_args()
     from dasklearn_amd.functions import aggregate
     from dasklearn_amd.rounds import RoundExecutor
@@ -152,45 +155,71 @@ def main():
     RoundExecutor({"train": tr}, Settings(), device=dev).run(wt, seed={"init": [init_x]})
     sequential(wt, aggregate, init_x, sync, tr)
 
-    ex = RoundExecutor({"train": tr}, Settings(), device=dev, timing=True)
-    if a.profile:
-        import cProfile
-        import pstats
-        prof = cProfile.Profile()
-        prof.enable()
-        ex.run(tasks, seed={"init": [init_x]})
-        prof.disable()
-        with open(a.profile, "w") as f:
-            pstats.Stats(prof, stream=f).sort_stats("tottime").print_stats(45)
-    else:
-        ex.run(tasks, seed={"init": [init_x]})
-    bt, bn = ex.stats["aggregate"], ex.stats["aggregate_tasks"]
-    if a.profile_seq:
-        import cProfile
-        import pstats
-        prof = cProfile.Profile()
-        prof.enable()
-        st, sn = sequential(tasks, aggregate, init_x, sync, tr)
-        prof.disable()
-        with open(a.profile_seq, "w") as f:
-            pstats.Stats(prof, stream=f).sort_stats("tottime").print_stats(45)
-    else:
-        st, sn = sequential(tasks, aggregate, init_x, sync, tr)
+    def run_batched(profile=None):
+        ex = RoundExecutor({"train": tr}, Settings(), device=dev, timing=True)
+        if profile:
+            import cProfile
+            import pstats
+            prof = cProfile.Profile()
+            prof.enable()
+            ex.run(tasks, seed={"init": [init_x]})
+            prof.disable()
+            with open(profile, "w") as f:
+                pstats.Stats(prof, stream=f).sort_stats("tottime").print_stats(45)
+        else:
+            ex.run(tasks, seed={"init": [init_x]})
+        return ex.stats["aggregate"], ex.stats["aggregate_tasks"]
+
+    def run_sequential(profile=None):
+        if profile:
+            import cProfile
+            import pstats
+            prof = cProfile.Profile()
+            prof.enable()
+            r = sequential(tasks, aggregate, init_x, sync, tr)
+            prof.disable()
+            with open(profile, "w") as f:
+                pstats.Stats(prof, stream=f).sort_stats("tottime").print_stats(45)
+            return r
+        return sequential(tasks, aggregate, init_x, sync, tr)
 
     def cpu_agg(settings, d):
         return [fedavg_torch.aggregate_modules(d["models"], d.get("weights"))]
 
-    torch.set_num_threads(4)
     ctasks, _ = dag(a.peers, a.cpu_rounds)
-    ct, cn = sequential(ctasks, cpu_agg, init_h, lambda: None)
 
-    def line(kind, t, n):
-        return {"kind": kind + ("_host_models" if a.host and not kind.startswith("cpu") else ""), "peers": a.peers, "fan_in": fan, "tasks": n, "params": p,
-                "ms_per_round": round(t / n * a.peers * 1e3, 3), "us_per_task": round(t / n * 1e6, 1),
-                "GBps_algorithmic": round(task_bytes * n / t / 1e9, 2)}
+    def run_cpu():
+        prev = torch.get_num_threads()
+        torch.set_num_threads(4)
+        try:
+            return sequential(ctasks, cpu_agg, init_h, lambda: None)
+        finally:
+            torch.set_num_threads(prev)
 
-    for l in (line("batched", bt, bn), line("sequential", st, sn), line("cpu_ref_4threads", ct, cn)):
-        print(json.dumps(l), flush=True)
+    import gc
+    import statistics
+    if a.profile:  # profiled passes are not timed
+        run_batched(a.profile)
+    if a.profile_seq:
+        run_sequential(a.profile_seq)
+    samples = {"batched": [], "sequential": [], "cpu_ref_4threads": []}
+    for _ in range(max(1, a.reps)):
+        for kind, fn in (("batched", run_batched), ("sequential", run_sequential), ("cpu_ref_4threads", run_cpu)):
+            gc.collect()
+            t, n = fn()
+            samples[kind].append(t / n)
+
+    def line(kind):
+        per = statistics.median(samples[kind])
+        return {"kind": kind + ("_host_models" if a.host and not kind.startswith("cpu") else ""), "peers": a.peers,
+                "fan_in": fan, "reps": len(samples[kind]), "params": p,
+                "ms_per_round": round(per * a.peers * 1e3, 3), "us_per_task": round(per * 1e6, 1),
+                "us_per_task_best": round(min(samples[kind]) * 1e6, 1),
+                "us_per_task_all": [round(x * 1e6, 1) for x in samples[kind]],
+                "GBps_algorithmic": round(task_bytes / per / 1e9, 2)}
+
+    for kind in samples:
+        print(json.dumps(line(kind)), flush=True)
 
 
 if __name__ == "__main__":

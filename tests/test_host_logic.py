@@ -284,6 +284,8 @@ def test_module_params_matches_parameters():
             self.shared_again = self.seq  # shared submodule
 
     for m in (Odd(), nn.Sequential(nn.Linear(2, 2), nn.Linear(2, 2)), nn.Linear(1, 1), nn.Module()):
+        from dasklearn_amd.arena import module_params_py
+        assert [id(q) for q in module_params_py(m)] == [id(q) for q in m.parameters()]
         got, ref = module_params(m), list(m.parameters())
         assert len(got) == len(ref) and all(a is b for a, b in zip(got, ref))
 
@@ -297,3 +299,23 @@ def test_clone_skips_setstate_only_when_it_is_a_plain_update():
     src = inspect.getsource(nn.Module.__setstate__)
     keys = set(re.findall(r'"(_\w+)" not in self\.__dict__', src))
     assert keys == set(arena._SETSTATE_KEYS)
+
+
+def test_pyhost_signature_and_pointer_helpers():
+    """csrc/pyhost.cpp: matches() compares count, shapes and dtypes;
+    data_ptrs() returns model-major pointers, or None when a tensor is not
+    contiguous (the caller then copies it)."""
+    from dasklearn_amd import _pyhost
+    m = nn.Sequential(nn.Linear(3, 4), nn.Linear(4, 2))
+    lay = arena.ParamLayout(m)
+    ps = arena.module_params(m)
+    assert _pyhost.matches(ps, lay._signature)
+    assert not _pyhost.matches(ps[:-1], lay._signature)
+    other = nn.Sequential(nn.Linear(3, 4), nn.Linear(4, 3))
+    assert not _pyhost.matches(arena.module_params(other), lay._signature)
+    assert not _pyhost.matches(arena.module_params(m.double()), lay._signature)
+    rows = [ps, ps]
+    assert _pyhost.data_ptrs(rows, [0, 2]) == [ps[0].data_ptr(), ps[2].data_ptr()] * 2
+    t = [torch.zeros(4, 3).t(), torch.zeros(2)]
+    assert _pyhost.data_ptrs([t], [1]) == [t[1].data_ptr()]
+    assert _pyhost.data_ptrs([t], [0, 1]) is None
