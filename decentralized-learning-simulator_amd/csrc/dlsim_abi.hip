@@ -142,18 +142,23 @@ struct StreamLinks {
 };
 
 // Pack `job` on `threads` host threads (the caller's included) and call
-// on_unit(u) for u = 0, 1, ... as each unit completes, in order, on this
-// thread. Below ~1 MiB of input the helpers stay asleep: their wake-up costs
-// more than they save.
+// on_units(u, v) on this thread for each run [u, v) of units that completed,
+// in order (u = 0 first; a run is every unit already packed when the
+// dispatcher looks, so a fast pack hands over long runs the caller can copy
+// with one DMA each). Below ~1 MiB of input the helpers stay asleep: their
+// wake-up costs more than they save.
 template <class F>
-void pack_and_dispatch(dlsim::PackJob& job, int threads, size_t in_bytes, F&& on_unit) {
+void pack_and_dispatch(dlsim::PackJob& job, int threads, size_t in_bytes, F&& on_units) {
   const int helpers = in_bytes < (size_t{1} << 20) ? 0 : std::min(std::max(threads, 1), 64) - 1;
   dlsim::PackPool& pool = dlsim::PackPool::get();
   std::lock_guard<std::mutex> lk(pool.call_mutex());
   if (helpers > 0) pool.start(&job, helpers);
   for (size_t u = 0; u < job.units;) {
     if (job.unit_done(u)) {
-      on_unit(u++);
+      size_t v = u + 1;
+      while (v < job.units && job.unit_done(v)) ++v;
+      on_units(u, v);
+      u = v;
     } else if (!job.run_one()) {
       std::this_thread::yield();
     }
@@ -476,17 +481,9 @@ int dlsim_host_wreduce(int n, int t, const void* const* h_srcs, const size_t* nu
   ln.link(st, h2d, "order H2D after stream");
   if (h_out) ln.link(st, d2h, "order D2H after stream");
   std::vector<const void*> ins(static_cast<size_t>(n));
-  pack_and_dispatch(job, threads, total * esz * n, [&](size_t u) {
-    if (ln.rc != DLSIM_OK) return;
-    const size_t c = u / n, i = u % n;
+  // Once every model's share of chunk c is on the device: reduce it, D2H it.
+  auto finish_chunk = [&](size_t c) {
     const size_t c0 = c * chunk, c1 = std::min(total, c0 + chunk);
-    const size_t o = i * row_bytes + c0 * esz;
-    hipError_t e = hipMemcpyAsync(rows + o, stage + o, (c1 - c0) * esz, hipMemcpyHostToDevice, h2d);
-    if (e != hipSuccess) {
-      ln.rc = hip_fail(e, "staging H2D");
-      return;
-    }
-    if (i + 1 < static_cast<size_t>(n)) return;
     ln.link(h2d, st, "order reduce after H2D");
     if (ln.rc != DLSIM_OK) return;
     for (int r = 0; r < n; ++r) ins[r] = rows + r * row_bytes + c0 * esz;
@@ -494,9 +491,28 @@ int dlsim_host_wreduce(int n, int t, const void* const* h_srcs, const size_t* nu
     if (ln.rc != DLSIM_OK || !h_out) return;
     ln.link(st, d2h, "order D2H after reduce");
     if (ln.rc != DLSIM_OK) return;
-    e = hipMemcpyAsync(static_cast<char*>(h_out) + c0 * esz, out + c0 * esz, (c1 - c0) * esz,
-                       hipMemcpyDeviceToHost, d2h);
+    const hipError_t e = hipMemcpyAsync(static_cast<char*>(h_out) + c0 * esz, out + c0 * esz, (c1 - c0) * esz,
+                                        hipMemcpyDeviceToHost, d2h);
     if (e != hipSuccess) ln.rc = hip_fail(e, "result D2H");
+  };
+  pack_and_dispatch(job, threads, total * esz * n, [&](size_t u0, size_t u1) {
+    for (size_t u = u0; u < u1 && ln.rc == DLSIM_OK;) {
+      const size_t c = u / n, i = u % n;
+      const size_t c0 = c * chunk, c1 = std::min(total, c0 + chunk);
+      // units of one chunk in the run: rows [i, j) of chunk c. With one chunk
+      // they are consecutive whole rows, one DMA (latency, not bandwidth,
+      // bounds small models: one copy per model was 7 DMAs for a GNLeNet task)
+      const size_t j = n_chunks == 1 ? std::min(static_cast<size_t>(n), i + (u1 - u)) : i + 1;
+      const size_t o = i * row_bytes + c0 * esz;
+      const size_t bytes = (j - i - 1) * row_bytes + (c1 - c0) * esz;
+      const hipError_t e = hipMemcpyAsync(rows + o, stage + o, bytes, hipMemcpyHostToDevice, h2d);
+      if (e != hipSuccess) {
+        ln.rc = hip_fail(e, "staging H2D");
+        return;
+      }
+      u += j - i;
+      if (j == static_cast<size_t>(n)) finish_chunk(c);
+    }
   });
   if (h_out) ln.link(d2h, st, "order stream after D2H");
   return ln.rc;
@@ -560,17 +576,11 @@ int dlsim_host_chunk_mean(int b, const int* fan_in, const void* const* h_inputs,
   if (h_outs) ln.link(st, d2h, "order D2H after stream");
   std::vector<const void*> ins;
   size_t task_first = 0;  // first row of the current task
-  pack_and_dispatch(job, threads, need * esz, [&](size_t r) {
+  // Row r is on the device: if it completes its task, that task's mean and D2H.
+  auto row_done = [&](size_t r) {
     if (ln.rc != DLSIM_OK) return;
     const int t = static_cast<int>(row_task[r]);
     const size_t n = n_elems[t];
-    if (n > 0) {
-      hipError_t e = hipMemcpyAsync(ds + row_off[r] * esz, hs + row_off[r] * esz, n * esz, hipMemcpyHostToDevice, h2d);
-      if (e != hipSuccess) {
-        ln.rc = hip_fail(e, "staging H2D");
-        return;
-      }
-    }
     if (r + 1 - task_first < static_cast<size_t>(fan_in[t])) return;
     const size_t first = task_first;
     task_first = r + 1;
@@ -589,6 +599,20 @@ int dlsim_host_chunk_mean(int b, const int* fan_in, const void* const* h_inputs,
     if (ln.rc != DLSIM_OK) return;
     hipError_t e = hipMemcpyAsync(h_outs[t], out, n * esz, hipMemcpyDeviceToHost, d2h);
     if (e != hipSuccess) ln.rc = hip_fail(e, "result D2H");
+  };
+  pack_and_dispatch(job, threads, need * esz, [&](size_t r0, size_t r1) {
+    if (ln.rc != DLSIM_OK) return;
+    // the run's rows lie back to back in staging (256-B aligned offsets, the
+    // gaps are copied too): one DMA for all of them
+    const size_t b = row_off[r0] * esz, e1 = (row_off[r1 - 1] + n_elems[row_task[r1 - 1]]) * esz;
+    if (e1 > b) {
+      const hipError_t e = hipMemcpyAsync(ds + b, hs + b, e1 - b, hipMemcpyHostToDevice, h2d);
+      if (e != hipSuccess) {
+        ln.rc = hip_fail(e, "staging H2D");
+        return;
+      }
+    }
+    for (size_t r = r0; r < r1; ++r) row_done(r);
   });
   if (h_outs) ln.link(d2h, st, "order stream after D2H");
   return ln.rc;
@@ -610,7 +634,7 @@ int dlsim_host_pack(int t, const void* const* h_srcs, const size_t* nbytes, cons
     total += nbytes[j];
   }
   job.seal(1);
-  pack_and_dispatch(job, threads, total, [](size_t) {});
+  pack_and_dispatch(job, threads, total, [](size_t, size_t) {});
   return DLSIM_OK;
 }
 
