@@ -6,7 +6,7 @@
 // parameter lists, checked against models[0]'s layout, and their data
 // pointers. For the reference's default model (GNLeNet, 14 tensors, fan-in 7)
 // that is ~100 tensor visits per task, which in Python cost more than the
-// kernel. These three helpers do the visits in C:
+// kernel. These helpers do the visits in C:
 //
 //   module_params(module)          == list(module.parameters()): modules in
 //                                      named_modules() pre-order, each once,
@@ -17,6 +17,8 @@
 //                                      signature [(torch.Size, dtype), ...]
 //   data_ptrs(rows, idx)           [rows[i][k].data_ptr() for i, k], or None
 //                                      if one of them is not contiguous
+//   clone_module(module, memo)     arena._clone_module_py: copy.deepcopy of
+//                                      models[0] with parameters from the memo
 //
 // Built by __graft_entry__.build() as dasklearn_amd/_pyhost*.so.
 #define PY_SSIZE_T_CLEAN
@@ -187,10 +189,253 @@ PyObject* py_data_ptrs(PyObject*, PyObject* args) {
   return out;
 }
 
+// ---- module clone (arena._clone_module restated; see its docstring) --------
+//
+// copy.deepcopy(models[0]) with the parameters taken from the memo: for the
+// reference's GNLeNet (16 modules, ~20 attributes each) this walk is the
+// largest host cost of one aggregate task. The Python version in arena.py is
+// the specification; tests/test_host_logic.py compares the two.
+struct CloneCtx {
+  PyObject* plain_cache = nullptr;    // {cls: kind}
+  PyObject* plain_fn = nullptr;       // cls -> kind 0/1/2 (fills plain_cache)
+  PyObject* atomic = nullptr;         // frozenset of atomic types
+  PyObject* setstate_keys = nullptr;  // frozenset of attribute names
+  PyObject* deepcopy = nullptr;       // copy.deepcopy
+  PyObject* odict = nullptr;          // collections.OrderedDict
+} g_clone;
+
+PyObject* s_modules_key = nullptr;
+PyObject* s_params_key = nullptr;
+PyObject* s_compiled_key = nullptr;
+PyObject* s_new = nullptr;
+PyObject* s_setstate = nullptr;
+
+bool key_is(PyObject* k, PyObject* s) {
+  return k == s || (PyUnicode_CheckExact(k) && PyUnicode_Compare(k, s) == 0);
+}
+
+int is_atomic(PyObject* v) { return PySet_Contains(g_clone.atomic, reinterpret_cast<PyObject*>(Py_TYPE(v))); }
+
+int all_atomic(PyObject* seq) {  // tuple or list
+  const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+  PyObject** items = PySequence_Fast_ITEMS(seq);
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    const int a = is_atomic(items[i]);
+    if (a != 1) return a;
+  }
+  return 1;
+}
+
+PyObject* deepcopy(PyObject* v, PyObject* memo) { return PyObject_CallFunctionObjArgs(g_clone.deepcopy, v, memo, nullptr); }
+
+// new reference to memo[id(v)] or nullptr (no error) / nullptr (error set)
+PyObject* memo_get(PyObject* memo, PyObject* v) {
+  PyObject* key = PyLong_FromVoidPtr(v);
+  if (!key) return nullptr;
+  PyObject* got = PyDict_GetItemWithError(memo, key);
+  Py_DECREF(key);
+  Py_XINCREF(got);
+  return got;
+}
+
+int memo_set(PyObject* memo, PyObject* v, PyObject* value) {
+  PyObject* key = PyLong_FromVoidPtr(v);
+  if (!key) return -1;
+  const int rc = PyDict_SetItem(memo, key, value);
+  Py_DECREF(key);
+  return rc;
+}
+
+PyObject* clone(PyObject* m, PyObject* memo, int depth);
+
+// the mapping `src` (dict or OrderedDict of name -> value) with each value
+// passed through `f` (None kept), as an object of src's type
+template <class F>
+PyObject* map_values(PyObject* src, F&& f) {
+  PyObject* d = PyDict_New();
+  if (!d) return nullptr;
+  Py_ssize_t pos = 0;
+  PyObject *name, *v;
+  while (PyDict_Next(src, &pos, &name, &v)) {
+    PyObject* nv = v == Py_None ? (Py_INCREF(Py_None), Py_None) : f(v);
+    if (!nv || PyDict_SetItem(d, name, nv) < 0) {
+      Py_XDECREF(nv);
+      Py_DECREF(d);
+      return nullptr;
+    }
+    Py_DECREF(nv);
+  }
+  if (PyDict_CheckExact(src)) return d;
+  PyObject* r = PyObject_CallOneArg(reinterpret_cast<PyObject*>(Py_TYPE(src)), d);
+  Py_DECREF(d);
+  return r;
+}
+
+// state[k] for one attribute v of a plain module; returns a new reference,
+// Py_None-borrowed sentinel `keep` (leave state[k] as is) or nullptr (error)
+PyObject* const kKeep = reinterpret_cast<PyObject*>(1);
+
+PyObject* clone_attr(PyObject* k, PyObject* v, PyObject* memo, int depth) {
+  const int at = is_atomic(v);
+  if (at < 0) return nullptr;
+  if (at) return kKeep;
+  if (key_is(k, s_modules_key) && PyDict_Check(v))
+    return map_values(v, [&](PyObject* c) { return clone(c, memo, depth + 1); });
+  if (key_is(k, s_params_key) && PyDict_Check(v))
+    return map_values(v, [&](PyObject* q) -> PyObject* {
+      PyObject* got = memo_get(memo, q);
+      if (got || PyErr_Occurred()) return got;
+      return deepcopy(q, memo);
+    });
+  if (PyTuple_CheckExact(v)) {
+    const int a = all_atomic(v);
+    if (a < 0) return nullptr;
+    if (a) return kKeep;
+  } else if (PyDict_CheckExact(v) || Py_IS_TYPE(v, reinterpret_cast<PyTypeObject*>(g_clone.odict)) ||
+             PySet_CheckExact(v)) {
+    const Py_ssize_t len = PyObject_Length(v);
+    if (len < 0) return nullptr;
+    if (len == 0) return PyObject_CallNoArgs(reinterpret_cast<PyObject*>(Py_TYPE(v)));
+  } else if (PyList_CheckExact(v)) {
+    const int a = all_atomic(v);
+    if (a < 0) return nullptr;
+    if (a) {
+      PyObject* got = memo_get(memo, v);
+      if (got || PyErr_Occurred()) return got;
+      PyObject* c = PyList_GetSlice(v, 0, PyList_GET_SIZE(v));
+      if (!c || memo_set(memo, v, c) < 0) {
+        Py_XDECREF(c);
+        return nullptr;
+      }
+      return c;
+    }
+  }
+  return deepcopy(v, memo);
+}
+
+// arena._plain_module_class: 0 deepcopy, 1 Module's setstate, 2 own setstate
+int plain_class(PyObject* cls) {
+  PyObject* kind = PyDict_GetItemWithError(g_clone.plain_cache, cls);
+  if (kind) return static_cast<int>(PyLong_AsLong(kind));
+  if (PyErr_Occurred()) return -1;
+  PyObject* r = PyObject_CallOneArg(g_clone.plain_fn, cls);
+  if (!r) return -1;
+  const long t = PyLong_AsLong(r);
+  Py_DECREF(r);
+  return static_cast<int>(t);
+}
+
+PyObject* clone(PyObject* m, PyObject* memo, int depth) {
+  if (depth > 10000) {
+    PyErr_SetString(PyExc_RecursionError, "module tree too deep");
+    return nullptr;
+  }
+  PyObject* got = memo_get(memo, m);
+  if (got || PyErr_Occurred()) return got;
+  PyObject* cls = reinterpret_cast<PyObject*>(Py_TYPE(m));
+  const int plain = plain_class(cls);
+  if (plain < 0) return nullptr;
+  if (!plain) return deepcopy(m, memo);
+  PyObject* newobj = PyObject_CallMethodOneArg(cls, s_new, cls);
+  if (!newobj) return nullptr;
+  PyObject* state = nullptr;
+  PyObject* d = nullptr;
+  int ok = -1;
+  do {
+    if (memo_set(memo, m, newobj) < 0) break;
+    d = PyObject_GenericGetDict(m, nullptr);
+    if (!d) break;
+    state = PyDict_Copy(d);
+    if (!state) break;
+    Py_ssize_t pos = 0;
+    PyObject *k, *v;
+    ok = 0;
+    while (ok == 0 && PyDict_Next(d, &pos, &k, &v)) {
+      if (key_is(k, s_compiled_key)) {
+        ok = PyDict_DelItem(state, k);
+        continue;
+      }
+      PyObject* nv = clone_attr(k, v, memo, depth);
+      if (!nv) ok = -1;
+      else if (nv != kKeep) {
+        ok = PyDict_SetItem(state, k, nv);
+        Py_DECREF(nv);
+      }
+    }
+    if (ok < 0) break;
+    // Module.__setstate__ is __dict__.update(state) when the state already has
+    // every attribute it would add; a class's own __setstate__ is called
+    int complete = plain == 1;
+    if (complete) {
+      PyObject* it = PyObject_GetIter(g_clone.setstate_keys);
+      if (!it) {
+        ok = -1;
+        break;
+      }
+      PyObject* key;
+      while (complete == 1 && (key = PyIter_Next(it))) {
+        complete = PyDict_Contains(state, key);
+        Py_DECREF(key);
+      }
+      Py_DECREF(it);
+    }
+    if (complete < 0 || PyErr_Occurred()) {
+      ok = -1;
+      break;
+    }
+    if (complete) {
+      PyObject* nd = PyObject_GenericGetDict(newobj, nullptr);
+      ok = nd ? PyDict_Update(nd, state) : -1;
+      Py_XDECREF(nd);
+    } else {
+      PyObject* r = PyObject_CallMethodOneArg(newobj, s_setstate, state);
+      ok = r ? 0 : -1;
+      Py_XDECREF(r);
+    }
+  } while (false);
+  Py_XDECREF(d);
+  Py_XDECREF(state);
+  if (ok < 0) {
+    Py_DECREF(newobj);
+    return nullptr;
+  }
+  return newobj;
+}
+
+PyObject* py_clone_init(PyObject*, PyObject* args) {
+  CloneCtx c;
+  if (!PyArg_ParseTuple(args, "O!OO!O!OO", &PyDict_Type, &c.plain_cache, &c.plain_fn, &PyFrozenSet_Type, &c.atomic,
+                        &PyFrozenSet_Type, &c.setstate_keys, &c.deepcopy, &c.odict))
+    return nullptr;
+  if (!PyType_Check(c.odict)) {
+    PyErr_SetString(PyExc_TypeError, "odict must be a type");
+    return nullptr;
+  }
+  for (PyObject* o : {c.plain_cache, c.plain_fn, c.atomic, c.setstate_keys, c.deepcopy, c.odict}) Py_INCREF(o);
+  for (PyObject* o : {g_clone.plain_cache, g_clone.plain_fn, g_clone.atomic, g_clone.setstate_keys, g_clone.deepcopy,
+                      g_clone.odict})
+    Py_XDECREF(o);
+  g_clone = c;
+  Py_RETURN_NONE;
+}
+
+PyObject* py_clone_module(PyObject*, PyObject* args) {
+  PyObject *m, *memo;
+  if (!PyArg_ParseTuple(args, "OO!", &m, &PyDict_Type, &memo)) return nullptr;
+  if (!g_clone.atomic) {
+    PyErr_SetString(PyExc_RuntimeError, "clone_init was not called");
+    return nullptr;
+  }
+  return clone(m, memo, 0);
+}
+
 PyMethodDef kMethods[] = {
     {"module_params", py_module_params, METH_O, "list(module.parameters()), in C"},
     {"matches", py_matches, METH_VARARGS, "params match a [(shape, dtype)] signature"},
     {"data_ptrs", py_data_ptrs, METH_VARARGS, "data pointers of rows[i][k] for k in idx, None if not contiguous"},
+    {"clone_init", py_clone_init, METH_VARARGS,
+     "clone_init(plain_cache, plain_fn, atomic_types, setstate_keys, deepcopy, OrderedDict)"},
+    {"clone_module", py_clone_module, METH_VARARGS, "clone_module(module, memo): arena._clone_module in C"},
     {nullptr, nullptr, 0, nullptr}};
 
 PyModuleDef kModule = {PyModuleDef_HEAD_INIT, "_pyhost", "CPython helpers of the per-task module path", -1,
@@ -205,6 +450,13 @@ PyMODINIT_FUNC PyInit__pyhost(void) {
   s_dtype = PyUnicode_InternFromString("dtype");
   s_data_ptr = PyUnicode_InternFromString("data_ptr");
   s_is_contiguous = PyUnicode_InternFromString("is_contiguous");
-  if (!s_parameters || !s_modules || !s_shape || !s_dtype || !s_data_ptr || !s_is_contiguous) return nullptr;
+  s_modules_key = s_modules;
+  s_params_key = s_parameters;
+  s_compiled_key = PyUnicode_InternFromString("_compiled_call_impl");
+  s_new = PyUnicode_InternFromString("__new__");
+  s_setstate = PyUnicode_InternFromString("__setstate__");
+  if (!s_parameters || !s_modules || !s_shape || !s_dtype || !s_data_ptr || !s_is_contiguous || !s_compiled_key ||
+      !s_new || !s_setstate)
+    return nullptr;
   return PyModule_Create(&kModule);
 }

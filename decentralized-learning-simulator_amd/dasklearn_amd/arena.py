@@ -483,20 +483,23 @@ def arenas_to_host(arenas: Dict[torch.dtype, torch.Tensor], stream) -> Dict[torc
 _ATOMIC = frozenset((type(None), bool, int, float, complex, str, bytes, torch.dtype, torch.device, torch.layout,
                      torch.memory_format))
 
-_PLAIN_CLASSES: Dict[type, bool] = {}
+_PLAIN_CLASSES: Dict[type, int] = {}
 
 
-def _plain_module_class(cls) -> bool:
-    """Classes whose copy.deepcopy is nn.Module's default reduce/getstate/
-    setstate round trip, which _clone_module restates without the generic
-    __reduce_ex__ machinery (cached per class)."""
-    ok = _PLAIN_CLASSES.get(cls)
-    if ok is None:
-        ok = _PLAIN_CLASSES[cls] = (cls.__reduce_ex__ is object.__reduce_ex__ and cls.__reduce__ is object.__reduce__
-                                    and getattr(cls, "__deepcopy__", None) is None
-                                    and cls.__getstate__ is nn.Module.__getstate__
-                                    and cls.__setstate__ is nn.Module.__setstate__)
-    return ok
+def _plain_module_class(cls) -> int:
+    """How copy.deepcopy copies an instance of module class `cls`, which
+    _clone_module restates without the generic __reduce_ex__ machinery
+    (cached per class):
+      0 — its own reduce/deepcopy/getstate: copy.deepcopy itself;
+      1 — nn.Module's default reduce/getstate/setstate round trip;
+      2 — the same with the class's own __setstate__ (e.g. _ConvNd's), which
+          the clone calls with the copied state, as copy.deepcopy does."""
+    kind = _PLAIN_CLASSES.get(cls)
+    if kind is None:
+        default = (cls.__reduce_ex__ is object.__reduce_ex__ and cls.__reduce__ is object.__reduce__
+                   and getattr(cls, "__deepcopy__", None) is None and cls.__getstate__ is nn.Module.__getstate__)
+        kind = _PLAIN_CLASSES[cls] = 0 if not default else (1 if cls.__setstate__ is nn.Module.__setstate__ else 2)
+    return kind
 
 
 # Attributes nn.Module.__setstate__ adds when an (old) state lacks them; with
@@ -514,9 +517,10 @@ def _all_atomic(v) -> bool:
     return True
 
 
-def _clone_module(m: nn.Module, memo: dict) -> nn.Module:
+def _clone_module_py(m: nn.Module, memo: dict) -> nn.Module:
     """copy.deepcopy(m, memo) for a module tree, several times faster for plain
-    modules.
+    modules. The product path runs the same walk in C (`_clone_module`,
+    csrc/pyhost.cpp); this is its specification, and tests compare the two.
 
     deepcopy of an nn.Module is: state = Module.__getstate__() (the __dict__
     minus _compiled_call_impl), deep-copied with the shared memo, then
@@ -533,7 +537,8 @@ def _clone_module(m: nn.Module, memo: dict) -> nn.Module:
     if got is not None:
         return got
     cls = type(m)
-    if not _plain_module_class(cls):
+    kind = _plain_module_class(cls)
+    if not kind:
         return copy.deepcopy(m, memo)
     new = cls.__new__(cls)
     memo[id(m)] = new
@@ -544,7 +549,7 @@ def _clone_module(m: nn.Module, memo: dict) -> nn.Module:
         if tv in _ATOMIC:
             continue
         if k == "_modules":
-            state[k] = tv((name, None if c is None else _clone_module(c, memo)) for name, c in v.items())
+            state[k] = tv((name, None if c is None else _clone_module_py(c, memo)) for name, c in v.items())
         elif k == "_parameters":
             state[k] = tv((name, None if q is None else (memo[id(q)] if id(q) in memo else copy.deepcopy(q, memo)))
                           for name, q in v.items())
@@ -561,11 +566,18 @@ def _clone_module(m: nn.Module, memo: dict) -> nn.Module:
             state[k] = c
         else:
             state[k] = copy.deepcopy(v, memo)
-    if _SETSTATE_KEYS.issubset(state):
+    if kind == 1 and _SETSTATE_KEYS.issubset(state):
         new.__dict__.update(state)  # what Module.__setstate__ does with a complete state
     else:
         new.__setstate__(state)
     return new
+
+
+_pyhost.clone_init(_PLAIN_CLASSES, _plain_module_class, _ATOMIC, _SETSTATE_KEYS, copy.deepcopy, OrderedDict)
+_clone_module = _pyhost.clone_module
+
+
+_make_param = torch.Tensor._make_subclass
 
 
 class _ArenaEntry:
@@ -611,7 +623,9 @@ def module_from_arenas(model0: nn.Module, layout: ParamLayout,
         parts = torch.split(arenas[dt], layout.split_sizes[dt])  # one call for the group
         for k, part, shape in zip(idx, parts, layout.split_shapes[dt]):
             p = layout.params[k]
-            q = nn.Parameter(part if shape is None else part.view(shape), requires_grad=p.requires_grad)
+            # nn.Parameter(t, requires_grad) for a plain tensor, without its
+            # Python __new__ frame
+            q = _make_param(nn.Parameter, part if shape is None else part.view(shape), p.requires_grad)
             memo[id(p)] = q
             new_params[k] = q
     out = _clone_module(model0, memo)

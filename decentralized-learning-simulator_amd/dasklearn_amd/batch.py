@@ -11,7 +11,7 @@ FedAvg.aggregate on each task.
 """
 from __future__ import annotations
 
-from typing import List, Optional, Sequence, Tuple
+from typing import Callable, List, Optional, Sequence, Tuple
 
 import torch
 from torch import nn
@@ -69,12 +69,20 @@ def _device_views(views) -> Optional[torch.device]:
     return dev
 
 
-def aggregate_arena_tasks(prepared, mode: int = _native.DLSIM_EXACT) -> List[nn.Module]:
+def aggregate_arena_tasks(prepared, mode: int = _native.DLSIM_EXACT,
+                          on_launched: Optional[Callable[[], None]] = None) -> List[nn.Module]:
     """prepared: [(model0, layout of model0, {dtype: [flat arena per model]},
     weights as Python floats)] with every arena on one device -> one module
     per task (deepcopy(model0) semantics, parameters views of a fresh output
     arena), all tasks of a dtype and device in batched launches (fp64 groups:
-    one dlsim_wreduce_f64 per task)."""
+    one dlsim_wreduce_f64 per task).
+
+    on_launched: called once every launch is queued, before the output
+    modules are built; the list `prepared` is consumed while they are (each
+    entry set to None once its module exists). A caller that drops its own
+    references to the input modules there lets them go as the outputs are
+    made: the arenas stay alive through the launch views, and the stream
+    orders any reuse of their memory after the kernels."""
     by_dtype = {}
     outs = []
     for model0, layout, views, ws in prepared:
@@ -92,4 +100,12 @@ def aggregate_arena_tasks(prepared, mode: int = _native.DLSIM_EXACT) -> List[nn.
                 _native.wreduce(vs, w, out, mode, stream)
             continue
         _native.wreduce_batched(group, mode, stream)
-    return [module_from_arenas(model0, layout, o) for (model0, layout, _, _), o in zip(prepared, outs)]
+    by_dtype.clear()
+    if on_launched is not None:
+        on_launched()
+    mods = []
+    for i, o in enumerate(outs):
+        model0, layout, _, _ = prepared[i]
+        prepared[i] = None
+        mods.append(module_from_arenas(model0, layout, o))
+    return mods

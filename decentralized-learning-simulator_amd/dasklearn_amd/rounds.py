@@ -57,11 +57,16 @@ def _refs(v, out):
 class RoundExecutor:
 
     def __init__(self, funcs: Dict[str, Callable], settings, device=None,
-                 mode: int = _native.DLSIM_EXACT, timing: bool = False):
+                 mode: int = _native.DLSIM_EXACT, timing: bool = False, keep_all: bool = False):
         """timing: accumulate wall seconds per kind of wave work in
         `self.stats` ("aggregate", "other"); the stream is synchronised after
-        every batched aggregate so its kernels count (measurement only)."""
+        every batched aggregate so its kernels count (measurement only).
+        keep_all: keep every task's result; by default a result is dropped
+        once every task that reads it has run, as the broker clears a
+        completed task's data (broker.py:221), so memory is bounded by the
+        DAG's frontier, not by the number of rounds."""
         self.timing = timing
+        self.keep_all = keep_all
         self.stats: Dict[str, float] = {"aggregate": 0.0, "other": 0.0, "aggregate_tasks": 0}
         self.funcs = dict(funcs)
         self.settings = settings
@@ -184,7 +189,11 @@ class RoundExecutor:
                 arenas = {dt: buf[o:o + n * esz].view(dt) for dt, (o, n, esz) in span.items()}
                 cache[id(m)] = (m, layout, arenas)
 
-    def _aggregate_wave(self, aggs) -> List[nn.Module]:
+    def _aggregate_wave(self, aggs, on_launched=None) -> List[nn.Module]:
+        """One batched aggregate per dtype over the wave's tasks. on_launched:
+        see batch.aggregate_arena_tasks (the executor releases the results
+        no later task reads there, so the input modules are freed while the
+        output modules are built)."""
         cache: dict = {}
         prepared = []
         resolved = []
@@ -204,15 +213,23 @@ class RoundExecutor:
                     layout0.check_compatible(models[i])  # raises the shape/dtype error
             views = {dt: [a[dt] for _, a in ents] for dt in layout0.groups}
             prepared.append((models[0], layout0, views, ws))
-        return aggregate_arena_tasks(prepared, self.mode)
+        resolved.clear()
+        cache.clear()
+        return aggregate_arena_tasks(prepared, self.mode, on_launched)
 
     def run(self, tasks: Sequence[Task], seed: Optional[Dict[str, list]] = None) -> Dict[str, list]:
         """Execute `tasks`; `seed` pre-populates results (e.g. initial models).
-        Returns {task_name: result list}."""
+        Returns {task_name: result list}: every result (keep_all), else the
+        results no task of `tasks` reads (the DAG's sinks, e.g. the last
+        round's aggregates) and the seeds none of them reads."""
         if seed:
             self.results.update(seed)
         pending = list(tasks)
         names = {t[0] for t in pending}
+        readers: Dict[str, int] = {}
+        for t in pending:
+            for r in set(_refs(t[2], [])):
+                readers[r] = readers.get(r, 0) + 1
         while pending:
             ready = [t for t in pending
                      if all(r in self.results for r in _refs(t[2], []))]
@@ -221,6 +238,18 @@ class RoundExecutor:
                                   if r not in self.results and r not in names})
                 raise RuntimeError(f"unresolvable task inputs: {missing[:5]}")
             aggs = [t for t in ready if t[1] == "aggregate"]
+            dying: List[str] = []  # results no task after this wave reads
+            if not self.keep_all:
+                for t in ready:
+                    for r in set(_refs(t[2], [])):
+                        readers[r] -= 1
+                        if readers[r] == 0:
+                            dying.append(r)
+
+            def release():
+                for r in dying:
+                    self.results.pop(r, None)
+                dying.clear()
             t0 = time.perf_counter()
             for name, func, data in ready:
                 if func == "aggregate":
@@ -232,7 +261,7 @@ class RoundExecutor:
                 torch.cuda.synchronize()
             t1 = time.perf_counter()
             if aggs:
-                outs = self._aggregate_wave(aggs)
+                outs = self._aggregate_wave(aggs, release)
                 for (name, _, _), out in zip(aggs, outs):
                     self.results[name] = [out]
                 if self.timing:
@@ -244,5 +273,6 @@ class RoundExecutor:
                 self.stats["aggregate_tasks"] += len(aggs)
             done = {t[0] for t in ready}
             self.waves.append(sorted(done))
+            release()
             pending = [t for t in pending if t[0] not in done]
         return self.results

@@ -16,7 +16,7 @@ host model instead (the reference's CPU training, model_trainer.py:129), so
 every aggregate reads host models: the executor uploads each wave's models
 once, the sequential worker loop stages them per task.
 
-    python scripts/bench_rounds.py [--peers 100] [--rounds 4] [--host]
+    python scripts/bench_rounds.py [--peers 100] [--rounds 4] [--host] [--model gnlenet|flat]
 """
 from __future__ import annotations
 
@@ -44,6 +44,29 @@ class Shaped(nn.Module):
     def __init__(self, shapes):
         super().__init__()
         self.ps = nn.ParameterList([nn.Parameter(torch.randn(*s) * 0.05) for s in shapes])
+
+
+class GNLeNetTree(nn.Module):
+    """The module tree of the reference's default model (GNLeNet,
+    dasklearn/models/cifar10.py:103-136, on models/Model.py's attributes):
+    16 modules, 14 parameters in GNLENET's order. The per-task host cost of
+    both the reference (deepcopy of models[0]) and this package (its clone)
+    grows with the module count, so the round is timed on this tree."""
+
+    def __init__(self):
+        super().__init__()
+        self.model_change = self._param_count_ot = self._param_count_total = None
+        self.accumulated_changes = self.shared_parameters_counter = self.gradient = None
+        self.input_channel, self.output, self.model_input, self.classifier_input = 3, 10, (24, 24), 576
+        self.features = nn.Sequential(
+            nn.Conv2d(3, 32, 5, 1, 2), nn.MaxPool2d(3, 2), nn.GroupNorm(2, 32), nn.ReLU(True),
+            nn.Conv2d(32, 32, 5, 1, 2), nn.GroupNorm(2, 32), nn.MaxPool2d(3, 2), nn.ReLU(True),
+            nn.Conv2d(32, 64, 5, 1, 2), nn.GroupNorm(2, 64), nn.MaxPool2d(3, 2), nn.ReLU(True))
+        self.classifier = nn.Sequential(nn.Linear(576, 10))
+
+
+def make_model(kind):
+    return GNLeNetTree() if kind == "gnlenet" else Shaped(GNLENET)
 
 
 class Settings:
@@ -103,22 +126,75 @@ def resolve(results, v):
     return v
 
 
+class GCMeter:
+    """Python's cyclic collector inside the timed regions (gc.callbacks): its
+    pauses are charged to whatever code allocates when a threshold trips, and
+    their length grows with every container object the process keeps alive,
+    so the lines report them beside the per-task time."""
+
+    def __init__(self):
+        self.active = False
+        self.seconds = 0.0
+        self.collections = [0, 0, 0]
+        self._t0 = None
+
+    def __call__(self, phase, info):
+        if phase == "start":
+            self._t0 = time.perf_counter()
+        elif self._t0 is not None:
+            if self.active:
+                self.seconds += time.perf_counter() - self._t0
+                self.collections[info["generation"]] += 1
+            self._t0 = None
+
+    def reset(self):
+        self.seconds, self.collections = 0.0, [0, 0, 0]
+
+
+GC = GCMeter()
+
+
+def _reads(v, out):
+    if isinstance(v, tuple) and len(v) == 2 and isinstance(v[0], str):
+        out.add(v[0])
+    elif isinstance(v, list):
+        for x in v:
+            _reads(x, out)
+    return out
+
+
 def sequential(tasks, agg_fn, init, sync, train_fn=None):
-    """The worker's one-task-at-a-time loop; only aggregate calls are timed."""
+    """The worker's one-task-at-a-time loop; only aggregate calls are timed.
+    A result is dropped once every task reading it has run (the broker
+    clears a completed task's data, broker.py:221), so the process holds the
+    DAG's frontier, like the reference's broker and workers, not every model
+    of the run."""
     train_fn = train_fn or train
     results = {"init": [init]}
+    reads = [_reads(list(data.values()), set()) for _, _, data in tasks]
+    left = {}
+    for rs in reads:
+        for r in rs:
+            left[r] = left.get(r, 0) + 1
     t_agg, n_agg = 0.0, 0
-    for name, f, data in tasks:
+    for (name, f, data), rs in zip(tasks, reads):
         d = {k: resolve(results, v) for k, v in data.items()}
         if f == "aggregate":
             sync()
+            GC.active = True
             t0 = time.perf_counter()
             results[name] = agg_fn(Settings(), d)
             sync()
             t_agg += time.perf_counter() - t0
+            GC.active = False
             n_agg += 1
         else:
             results[name] = train_fn(Settings(), d)
+        del d
+        for r in rs:
+            left[r] -= 1
+            if left[r] == 0:
+                del results[r]
     return t_agg, n_agg
 
 
@@ -128,6 +204,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--cpu-rounds", type=int, default=2)
     ap.add_argument("--host", action="store_true", help="train returns host models (CPU training)")
+    ap.add_argument("--model", choices=("gnlenet", "flat"), default="gnlenet",
+                    help="gnlenet: the reference's module tree; flat: the same 14 tensors in one ParameterList")
     ap.add_argument("--profile", default=None, help="cProfile the batched run into this file")
     ap.add_argument("--profile-seq", default=None, help="cProfile the sequential run into this file")
     ap.add_argument("--reps", type=int, default=3,
@@ -140,7 +218,8 @@ def main():
 
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
-    init_h = Shaped(GNLENET)
+    init_h = make_model(a.model)
+    assert [tuple(q.shape) for q in init_h.parameters()] == GNLENET
     init_d = copy.deepcopy(init_h).to(dev)
     tasks, fan = dag(a.peers, a.rounds)
     p = sum(int(torch.Size(s).numel()) for s in GNLENET)
@@ -157,6 +236,15 @@ def main():
 
     def run_batched(profile=None):
         ex = RoundExecutor({"train": tr}, Settings(), device=dev, timing=True)
+        wave = ex._aggregate_wave
+
+        def metered(aggs, *rest):  # the executor times the wave plus a sync
+            GC.active = True
+            try:
+                return wave(aggs, *rest)
+            finally:
+                GC.active = False
+        ex._aggregate_wave = metered
         if profile:
             import cProfile
             import pstats
@@ -203,20 +291,30 @@ def main():
     if a.profile_seq:
         run_sequential(a.profile_seq)
     samples = {"batched": [], "sequential": [], "cpu_ref_4threads": []}
+    gc_s = {k: [] for k in samples}
+    gc_n = {k: [0, 0, 0] for k in samples}
+    gc.callbacks.append(GC)
     for _ in range(max(1, a.reps)):
         for kind, fn in (("batched", run_batched), ("sequential", run_sequential), ("cpu_ref_4threads", run_cpu)):
             gc.collect()
+            GC.reset()
             t, n = fn()
             samples[kind].append(t / n)
+            gc_s[kind].append(GC.seconds / n)
+            gc_n[kind] = [x + y for x, y in zip(gc_n[kind], GC.collections)]
+    gc.callbacks.remove(GC)
 
     def line(kind):
         per = statistics.median(samples[kind])
-        return {"kind": kind + ("_host_models" if a.host and not kind.startswith("cpu") else ""), "peers": a.peers,
+        return {"kind": kind + ("_host_models" if a.host and not kind.startswith("cpu") else ""), "model": a.model,
+                "peers": a.peers,
                 "fan_in": fan, "reps": len(samples[kind]), "params": p,
                 "ms_per_round": round(per * a.peers * 1e3, 3), "us_per_task": round(per * 1e6, 1),
                 "us_per_task_best": round(min(samples[kind]) * 1e6, 1),
                 "us_per_task_all": [round(x * 1e6, 1) for x in samples[kind]],
-                "GBps_algorithmic": round(task_bytes / per / 1e9, 2)}
+                "GBps_algorithmic": round(task_bytes / per / 1e9, 2),
+                "gc_us_per_task": round(statistics.median(gc_s[kind]) * 1e6, 1),
+                "gc_collections_by_generation": gc_n[kind]}
 
     for kind in samples:
         print(json.dumps(line(kind)), flush=True)

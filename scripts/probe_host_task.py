@@ -1,7 +1,7 @@
 """Probe: one aggregate task of host models (the reference worker's case) on
 the native pipeline, by pack threads and host-result memory.
 
-7 x GNLeNet (14 tensors, 85,354 fp32; fan-in 7 = the reference's 100-peer
+7 x GNLeNet (the reference's 16-module tree, 14 tensors, 85,354 fp32; fan-in 7 = the reference's 100-peer
 D-PSGD default) and 8 x ResNet-18 (62 tensors, 11,181,642 fp32), host tensors
 in, host result out: `_native.host_wreduce` (dlsim_host_wreduce) alone with
 1/2/4/8/16 pack threads and a pageable or page-locked result, then the whole
@@ -23,7 +23,7 @@ for p in (ROOT, os.path.join(ROOT, "scripts"), os.path.join(ROOT, "decentralized
 import torch  # noqa: E402
 
 from bench import resnet18_shapes  # noqa: E402
-from bench_rounds import GNLENET, Shaped  # noqa: E402
+from bench_rounds import GNLeNetTree, Shaped  # noqa: E402
 from dasklearn_amd import _native, arena  # noqa: E402
 from dasklearn_amd.gradient_aggregation.fedavg import FedAvg  # noqa: E402
 
@@ -44,9 +44,9 @@ def med(f, reps):
 
 def main():
     dev = torch.device("cuda", 0)
-    for name, shapes, n, reps in (("gnlenet", GNLENET, 7, 300), ("resnet18", resnet18_shapes(), 8, 30)):
+    for name, n, reps in (("gnlenet", 7, 300), ("resnet18", 8, 30)):
         torch.manual_seed(0)
-        models = [Shaped(shapes) for _ in range(n)]
+        models = [GNLeNetTree() if name == "gnlenet" else Shaped(resnet18_shapes()) for _ in range(n)]
         by_model = [[p.detach() for p in m.parameters()] for m in models]
         total = sum(t.numel() for t in by_model[0])
         stride = arena.row_stride(total, 4)

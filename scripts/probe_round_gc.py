@@ -30,11 +30,11 @@ def run(peers, nrounds, pause_gc):
     orig = ex._aggregate_wave
     t_up = [0.0]
 
-    def wave(aggs):
+    def wave(aggs, *rest):
         if pause_gc:
             gc.disable()
         try:
-            return orig(aggs)
+            return orig(aggs, *rest)
         finally:
             if pause_gc:
                 gc.enable()

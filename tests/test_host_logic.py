@@ -172,6 +172,108 @@ def test_fast_clone_matches_deepcopy(make):
     assert arena.registered_arenas(out) is not None
 
 
+class _GNLeNetTree(nn.Module):
+    """The module tree of the reference's default model
+    (dasklearn/models/cifar10.py:103-136): 16 modules, 14 parameters, plain
+    attributes including a tuple."""
+
+    def __init__(self):
+        super().__init__()
+        self.model_change = None
+        self.gradient = None
+        self.input_channel, self.output, self.model_input, self.classifier_input = 3, 10, (24, 24), 576
+        self.features = nn.Sequential(
+            nn.Conv2d(3, 32, 5, 1, 2), nn.MaxPool2d(3, 2), nn.GroupNorm(2, 32), nn.ReLU(True),
+            nn.Conv2d(32, 32, 5, 1, 2), nn.GroupNorm(2, 32), nn.MaxPool2d(3, 2), nn.ReLU(True),
+            nn.Conv2d(32, 64, 5, 1, 2), nn.GroupNorm(2, 64), nn.MaxPool2d(3, 2), nn.ReLU(True))
+        self.classifier = nn.Sequential(nn.Linear(576, 10))
+
+
+class _OldState(nn.Linear):
+    """A module whose state lacks attributes Module.__setstate__ adds (an old
+    pickle): the clone must take the __setstate__ route."""
+
+    def __init__(self):
+        super().__init__(2, 2)
+        del self._forward_hooks_always_called
+
+
+def _deep_equal(v, w):
+    if type(v) is not type(w):
+        return False
+    if isinstance(v, torch.Tensor):
+        return torch.equal(v, w)
+    if isinstance(v, (list, tuple)):
+        return len(v) == len(w) and all(_deep_equal(x, y) for x, y in zip(v, w))
+    if isinstance(v, dict):
+        return list(v.keys()) == list(w.keys()) and all(_deep_equal(v[k], w[k]) for k in v)
+    return v == w
+
+
+def _compare_clones(a, b, m):
+    """Two clones of m: same classes, attribute names, attribute values
+    (tensors by value), the same sharing among themselves as m has, and no
+    mutable object shared with m except what deepcopy shares (atomic values,
+    tuples of them)."""
+    ma, mb = dict(a.named_modules(remove_duplicate=False)), dict(b.named_modules(remove_duplicate=False))
+    assert ma.keys() == mb.keys()
+    for name, x in ma.items():
+        y = mb[name]
+        assert type(x) is type(y)
+        assert x.__dict__.keys() == y.__dict__.keys(), name
+        for k, v in x.__dict__.items():
+            w = y.__dict__[k]
+            assert type(v) is type(w), (name, k)
+            if k not in ("_modules", "_parameters"):
+                assert _deep_equal(v, w), (name, k)
+            orig = dict(m.named_modules(remove_duplicate=False))[name].__dict__.get(k)  # __setstate__ may add k
+            if isinstance(v, (list, dict, set)) or isinstance(v, torch.Tensor):
+                assert (v is orig) == (w is orig), (name, k)
+
+
+@pytest.mark.parametrize("make", [lambda: _GNLeNetTree(), lambda: _Tied(), lambda: _OldState(),
+                                  lambda: nn.Sequential(_CustomCopy(3, 2), nn.BatchNorm1d(2)),
+                                  lambda: nn.ModuleDict({"a": nn.Linear(2, 2), "b": nn.ParameterList(
+                                      [nn.Parameter(torch.ones(3)), nn.Parameter(torch.zeros(2, 2))])})])
+def test_c_clone_matches_python_clone(make):
+    """arena._clone_module (csrc/pyhost.cpp) against its Python specification
+    arena._clone_module_py, with the same parameter memo."""
+    m = make()
+    m.extra = {"k": [1, 2]}
+    m.ints = [3, 4]
+    m.mixed = [torch.ones(1), 2]
+
+    def memo():
+        return {id(p): nn.Parameter(p.detach().clone(), requires_grad=p.requires_grad) for p in m.parameters()}
+
+    ma, mb = memo(), memo()
+    torch.manual_seed(1)  # _CustomCopy's __deepcopy__ draws a fresh Linear
+    a = arena._clone_module(m, ma)
+    torch.manual_seed(1)
+    b = arena._clone_module_py(m, mb)
+    _compare_clones(a, b, m)
+    assert a.ints == m.ints and a.ints is not m.ints
+    assert a.mixed is not m.mixed and a.mixed[0] is not m.mixed[0]
+    for p, q in zip(a.parameters(), b.parameters()):
+        assert torch.equal(p, q) and p.requires_grad == q.requires_grad
+    if all(arena._plain_module_class(type(x)) for x in m.modules()):  # else deepcopy makes the parameters
+        assert [id(p) for p in a.parameters()] == [id(ma[id(p)]) for p in m.parameters()]
+    assert ma[id(m)] is a and mb[id(m)] is b
+    again = arena._clone_module(m, ma)  # a module already in the memo
+    assert again is a
+
+
+def test_c_clone_propagates_errors():
+    class Bad:
+        def __deepcopy__(self, memo):
+            raise RuntimeError("no copy")
+
+    m = nn.Linear(2, 2)
+    m.bad = Bad()
+    with pytest.raises(RuntimeError, match="no copy"):
+        arena._clone_module(m, {})
+
+
 def test_fast_clone_respects_custom_deepcopy():
     m = nn.Sequential(_CustomCopy(3, 2))
     lay = arena.ParamLayout(m)
