@@ -19,12 +19,19 @@
 //                                      if one of them is not contiguous
 //   clone_module(module, memo)     arena._clone_module_py: copy.deepcopy of
 //                                      models[0] with parameters from the memo
+//   checked_params(module, sig)    module_params + matches in one call
+//   flat_run(params, idx, offs)    the dtype group already is one flat run
+//   wreduce_rows(...)              the data pointers of a task's parameter
+//                                      tensors straight into one
+//                                      dlsim_wreduce_tensors call
 //
 // Built by __graft_entry__.build() as dasklearn_amd/_pyhost*.so.
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
 
+#include <cstdint>
 #include <unordered_set>
+#include <vector>
 
 namespace {
 
@@ -189,6 +196,202 @@ PyObject* py_data_ptrs(PyObject*, PyObject* args) {
   return out;
 }
 
+// checked_params(module, signature) -> module_params(module) if it matches the
+// signature, else None
+PyObject* py_checked_params(PyObject*, PyObject* args) {
+  PyObject *module, *sig;
+  if (!PyArg_ParseTuple(args, "OO", &module, &sig)) return nullptr;
+  PyObject* ps = py_module_params(nullptr, module);
+  if (!ps) return nullptr;
+  PyObject* pair = PyTuple_Pack(2, ps, sig);
+  PyObject* ok = pair ? py_matches(nullptr, pair) : nullptr;
+  Py_XDECREF(pair);
+  if (!ok) {
+    Py_DECREF(ps);
+    return nullptr;
+  }
+  const bool m = ok == Py_True;
+  Py_DECREF(ok);
+  if (m) return ps;
+  Py_DECREF(ps);
+  Py_RETURN_NONE;
+}
+
+// flat_run(params, idx, byte_offsets) -> True iff every params[idx[j]] is
+// contiguous and starts byte_offsets[j] bytes after params[idx[0]]
+PyObject* py_flat_run(PyObject*, PyObject* args) {
+  PyObject *params, *idx, *offs;
+  if (!PyArg_ParseTuple(args, "OOO", &params, &idx, &offs)) return nullptr;
+  PyObject* ps = PySequence_Fast(params, "params must be a sequence");
+  if (!ps) return nullptr;
+  PyObject* ks = PySequence_Fast(idx, "idx must be a sequence");
+  PyObject* os = ks ? PySequence_Fast(offs, "byte_offsets must be a sequence") : nullptr;
+  int result = -1;
+  do {
+    if (!os) break;
+    const Py_ssize_t t = PySequence_Fast_GET_SIZE(ks);
+    if (PySequence_Fast_GET_SIZE(os) != t) {
+      PyErr_SetString(PyExc_ValueError, "idx and byte_offsets differ in length");
+      break;
+    }
+    uintptr_t base = 0;
+    result = 1;
+    for (Py_ssize_t j = 0; result == 1 && j < t; ++j) {
+      PyObject* q = PyObject_GetItem(ps, PySequence_Fast_GET_ITEM(ks, j));
+      if (!q) {
+        result = -1;
+        break;
+      }
+      PyObject* ptr = PyObject_CallMethodNoArgs(q, s_data_ptr);
+      const uintptr_t p = ptr ? reinterpret_cast<uintptr_t>(PyLong_AsVoidPtr(ptr)) : 0;
+      Py_XDECREF(ptr);
+      if (!ptr || PyErr_Occurred()) {
+        Py_DECREF(q);
+        result = -1;
+        break;
+      }
+      if (j == 0) base = p;
+      const size_t off = PyLong_AsSize_t(PySequence_Fast_GET_ITEM(os, j));
+      if (PyErr_Occurred()) {
+        Py_DECREF(q);
+        result = -1;
+        break;
+      }
+      if (p - base != off) {
+        Py_DECREF(q);
+        result = 0;
+        break;
+      }
+      PyObject* c = PyObject_CallMethodNoArgs(q, s_is_contiguous);
+      Py_DECREF(q);
+      result = c ? PyObject_IsTrue(c) : -1;
+      Py_XDECREF(c);
+    }
+  } while (false);
+  Py_XDECREF(os);
+  Py_XDECREF(ks);
+  Py_DECREF(ps);
+  if (result < 0) return nullptr;
+  return PyBool_FromLong(result);
+}
+
+// ---- one device task's reduce: pointers collected and the library called ----
+//
+// dlsim_wreduce_tensors (include/dlsim.h) bound by address from _native.py, so
+// a task whose models keep their parameters in separate device tensors makes
+// one call from Python: the data pointers of rows[i][k] for k in idx go
+// straight into the C arrays (no list of ints, no ctypes marshalling).
+using WreduceTensorsFn = int (*)(const void* const*, int, int, const size_t*, const float*, void* const*, int, int,
+                                 void*);
+WreduceTensorsFn g_wreduce_tensors = nullptr;
+
+PyObject* py_bind_wreduce_tensors(PyObject*, PyObject* addr) {
+  void* p = PyLong_AsVoidPtr(addr);
+  if (!p && PyErr_Occurred()) return nullptr;
+  g_wreduce_tensors = reinterpret_cast<WreduceTensorsFn>(p);
+  Py_RETURN_NONE;
+}
+
+// wreduce_rows(rows, idx, numels, weights_f32, out_base, out_offsets, dtype,
+//              mode, stream) -> rc, or None (nothing launched) if a tensor is
+// not contiguous. rows[i][idx[j]] is tensor j of model i; numels[j] its
+// element count; out_offsets[j] its byte offset from out_base; weights_f32
+// a C-contiguous buffer of len(rows) floats.
+PyObject* py_wreduce_rows(PyObject*, PyObject* args) {
+  PyObject *rows, *idx, *numels, *weights, *offsets;
+  unsigned long long out_base, stream;
+  int dtype, mode;
+  if (!PyArg_ParseTuple(args, "OOOOKOiiK", &rows, &idx, &numels, &weights, &out_base, &offsets, &dtype, &mode,
+                        &stream))
+    return nullptr;
+  if (!g_wreduce_tensors) {
+    PyErr_SetString(PyExc_RuntimeError, "bind_wreduce_tensors was not called");
+    return nullptr;
+  }
+  PyObject* rs = PySequence_Fast(rows, "rows must be a sequence");
+  if (!rs) return nullptr;
+  PyObject* ks = PySequence_Fast(idx, "idx must be a sequence");
+  PyObject* ns = ks ? PySequence_Fast(numels, "numels must be a sequence") : nullptr;
+  PyObject* os = ns ? PySequence_Fast(offsets, "out_offsets must be a sequence") : nullptr;
+  PyObject* result = nullptr;
+  Py_buffer wb{};
+  bool have_wb = false;
+  do {
+    if (!os) break;
+    const Py_ssize_t n = PySequence_Fast_GET_SIZE(rs), t = PySequence_Fast_GET_SIZE(ks);
+    if (PySequence_Fast_GET_SIZE(ns) != t || PySequence_Fast_GET_SIZE(os) != t) {
+      PyErr_SetString(PyExc_ValueError, "idx, numels and out_offsets differ in length");
+      break;
+    }
+    if (PyObject_GetBuffer(weights, &wb, PyBUF_C_CONTIGUOUS) < 0) break;
+    have_wb = true;
+    if (wb.len != static_cast<Py_ssize_t>(n * sizeof(float))) {
+      PyErr_SetString(PyExc_ValueError, "weights_f32 must hold one float per model");
+      break;
+    }
+    std::vector<const void*> ins(static_cast<size_t>(n * t));
+    std::vector<size_t> ne(static_cast<size_t>(t));
+    std::vector<void*> outs(static_cast<size_t>(t));
+    bool ok = true, contiguous = true;
+    for (Py_ssize_t j = 0; ok && j < t; ++j) {
+      ne[j] = PyLong_AsSize_t(PySequence_Fast_GET_ITEM(ns, j));
+      const size_t off = PyLong_AsSize_t(PySequence_Fast_GET_ITEM(os, j));
+      if (PyErr_Occurred()) ok = false;
+      outs[j] = reinterpret_cast<void*>(static_cast<uintptr_t>(out_base + off));
+    }
+    for (Py_ssize_t i = 0; ok && contiguous && i < n; ++i) {
+      PyObject* row = PySequence_Fast_GET_ITEM(rs, i);
+      for (Py_ssize_t j = 0; j < t; ++j) {
+        PyObject* tt = PyObject_GetItem(row, PySequence_Fast_GET_ITEM(ks, j));
+        if (!tt) {
+          ok = false;
+          break;
+        }
+        PyObject* c = PyObject_CallMethodNoArgs(tt, s_is_contiguous);
+        const int isc = c ? PyObject_IsTrue(c) : -1;
+        Py_XDECREF(c);
+        if (isc != 1) {
+          Py_DECREF(tt);
+          if (isc < 0) ok = false;
+          contiguous = false;
+          break;
+        }
+        PyObject* ptr = PyObject_CallMethodNoArgs(tt, s_data_ptr);
+        Py_DECREF(tt);
+        if (!ptr) {
+          ok = false;
+          break;
+        }
+        ins[static_cast<size_t>(i * t + j)] = PyLong_AsVoidPtr(ptr);
+        Py_DECREF(ptr);
+        if (PyErr_Occurred()) {
+          ok = false;
+          break;
+        }
+      }
+    }
+    if (!ok) break;
+    if (!contiguous) {
+      Py_INCREF(Py_None);
+      result = Py_None;
+      break;
+    }
+    int rc;
+    const float* w = static_cast<const float*>(wb.buf);
+    Py_BEGIN_ALLOW_THREADS
+    rc = g_wreduce_tensors(ins.data(), static_cast<int>(n), static_cast<int>(t), ne.data(), w, outs.data(), dtype,
+                           mode, reinterpret_cast<void*>(static_cast<uintptr_t>(stream)));
+    Py_END_ALLOW_THREADS
+    result = PyLong_FromLong(rc);
+  } while (false);
+  if (have_wb) PyBuffer_Release(&wb);
+  Py_XDECREF(os);
+  Py_XDECREF(ns);
+  Py_XDECREF(ks);
+  Py_DECREF(rs);
+  return result;
+}
+
 // ---- module clone (arena._clone_module restated; see its docstring) --------
 //
 // copy.deepcopy(models[0]) with the parameters taken from the memo: for the
@@ -295,7 +498,18 @@ PyObject* clone_attr(PyObject* k, PyObject* v, PyObject* memo, int depth) {
              PySet_CheckExact(v)) {
     const Py_ssize_t len = PyObject_Length(v);
     if (len < 0) return nullptr;
-    if (len == 0) return PyObject_CallNoArgs(reinterpret_cast<PyObject*>(Py_TYPE(v)));
+    if (len == 0) {
+      PyObject* e = PyObject_CallNoArgs(reinterpret_cast<PyObject*>(Py_TYPE(v)));
+      // An empty OrderedDict (the hook registries, 11 per module) holds
+      // nothing a cycle could pass through; like the empty plain dicts
+      // CPython creates untracked, it is re-tracked by the dict insert path
+      // (MAINTAIN_TRACKING) the moment a trackable object is put in it. Left
+      // tracked, the clones of a 16-module tree add ~180 objects to every
+      // collection the process runs.
+      if (e && Py_IS_TYPE(e, reinterpret_cast<PyTypeObject*>(g_clone.odict)) && PyObject_GC_IsTracked(e))
+        PyObject_GC_UnTrack(e);
+      return e;
+    }
   } else if (PyList_CheckExact(v)) {
     const int a = all_atomic(v);
     if (a < 0) return nullptr;
@@ -436,6 +650,11 @@ PyMethodDef kMethods[] = {
     {"clone_init", py_clone_init, METH_VARARGS,
      "clone_init(plain_cache, plain_fn, atomic_types, setstate_keys, deepcopy, OrderedDict)"},
     {"clone_module", py_clone_module, METH_VARARGS, "clone_module(module, memo): arena._clone_module in C"},
+    {"bind_wreduce_tensors", py_bind_wreduce_tensors, METH_O, "bind dlsim_wreduce_tensors by address"},
+    {"checked_params", py_checked_params, METH_VARARGS, "module_params(module) if it matches signature, else None"},
+    {"flat_run", py_flat_run, METH_VARARGS, "params[idx] contiguous at byte_offsets from params[idx[0]]"},
+    {"wreduce_rows", py_wreduce_rows, METH_VARARGS,
+     "wreduce_rows(rows, idx, numels, weights_f32, out_base, out_offsets, dtype, mode, stream) -> rc or None"},
     {nullptr, nullptr, 0, nullptr}};
 
 PyModuleDef kModule = {PyModuleDef_HEAD_INIT, "_pyhost", "CPython helpers of the per-task module path", -1,

@@ -66,6 +66,14 @@ def module_params_py(module: nn.Module) -> List[nn.Parameter]:
     return out
 
 
+def _contiguous_strides(shape) -> Tuple[int, ...]:
+    strides, acc = [], 1
+    for d in reversed(tuple(shape)):
+        strides.append(acc)
+        acc *= max(int(d), 1)
+    return tuple(reversed(strides))
+
+
 class ParamLayout:
     """parameters() of a module grouped by dtype, with flat offsets."""
 
@@ -89,10 +97,24 @@ class ParamLayout:
             self.totals[dt] = off
             self._group_offsets[dt] = offs
         self._signature = tuple((p.shape, p.dtype) for p in self.params)
+        # per dtype group: each tensor's byte offset in the arena
+        self.byte_offsets = {dt: tuple(o * self.params[idx[0]].element_size() for o in self._group_offsets[dt])
+                             for dt, idx in self.groups.items()}
         # per dtype group: element counts and shapes for splitting an arena
         self.split_sizes = {dt: [self.params[k].numel() for k in idx] for dt, idx in self.groups.items()}
         self.split_shapes = {dt: [None if self.params[k].dim() == 1 else self.params[k].shape for k in idx]
                              for dt, idx in self.groups.items()}
+        # per dtype group: (shape, contiguous strides, element offset) of each
+        # tensor's view into an arena (one as_strided per parameter)
+        self.view_specs = {dt: [(tuple(self.params[k].shape), _contiguous_strides(self.params[k].shape), o)
+                                for k, o in zip(idx, self._group_offsets[dt])]
+                           for dt, idx in self.groups.items()}
+        # per parameter, in parameters() order: (dtype, byte offset in its
+        # dtype's arena, shape) -- what a registered arena's views must match
+        self.param_slots = [None] * len(self.params)
+        for dt, idx in self.groups.items():
+            for k, bo in zip(idx, self.byte_offsets[dt]):
+                self.param_slots[k] = (dt, bo, self.params[k].shape)
 
     def rebind(self, params: List[nn.Parameter]) -> "ParamLayout":
         """The same layout over another module's parameters (same signature,
@@ -106,6 +128,9 @@ class ParamLayout:
         return _pyhost.matches(ps, self._signature)
 
     def check_compatible(self, module: nn.Module) -> List[nn.Parameter]:
+        ps = _pyhost.checked_params(module, self._signature)  # walk + signature check in C
+        if ps is not None:
+            return ps
         ps = module_params(module)
         # The reference zips parameters() (fedavg.py:24) and silently truncates
         # on a mismatch; equal shapes are what it assumes, so insist on them
@@ -122,15 +147,12 @@ class ParamLayout:
         """If the dtype group of `params` already is one contiguous flat buffer
         (in layout order), return a flat view of it, else None."""
         idx = self.groups[dt]
-        first = params[idx[0]]
-        base = first.data_ptr()
-        esz = first.element_size()
         # every tensor contiguous (a transposed view could start at the right
-        # place) and at its offset in the layout
-        for k, o in zip(idx, self._group_offsets[dt]):
-            q = params[k]
-            if q.data_ptr() - base != o * esz or not q.is_contiguous():
-                return None
+        # place) and at its offset in the layout (checked in C)
+        if not _pyhost.flat_run(params, idx, self.byte_offsets[dt]):
+            return None
+        first = params[idx[0]]
+        esz = first.element_size()
         # ...inside the first tensor's storage: adjacent separate allocations
         # are not an arena (one storage check instead of one per tensor)
         total = self.totals[dt]
@@ -389,8 +411,9 @@ def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, m
     """Reduce the parameters of `models` into one fresh arena per dtype.
 
     weights_f32: the fp32-rounded weights (fp32/bf16/fp16 groups);
-    weights_f64: the exact double weights an fp64 group needs (fedavg.py:25
-    keeps the Python float exact for a double tensor); default: widened fp32.
+    weights_f64: the Python-float weights, kept exact as doubles for an fp64
+    group (fedavg.py:25 keeps the Python float exact for a double tensor);
+    default: widened fp32.
     host_out None: as the reference's output, iff models[0]'s parameters are on
     the host. Returns (layout, arenas, device, on_host, host_out). With
     host_out, host models take the chunked pipeline and come back already in
@@ -411,7 +434,8 @@ def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, m
         for dt, idx in layout.groups.items():
             total = layout.totals[dt]
             f64 = dt == torch.float64
-            w = (weights_f64 if weights_f64 is not None else weights_f32.astype(np.float64)) if f64 else weights_f32
+            w = (_native.f64_weights(weights_f64) if weights_f64 is not None else weights_f32.astype(np.float64)) \
+                if f64 else weights_f32
             out = torch.empty(total, dtype=dt, device=dev)
             outs[dt] = out
             if total == 0:
@@ -432,13 +456,16 @@ def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, m
                     st.mark("kernel")
                     continue
                 # separate device tensors, read in place: the layout checked
-                # shapes and dtypes, so only pointers go to the library (no
-                # detach() objects, no output slices)
-                keep, ptrs = _data_ptrs(all_params, idx)
-                base, esz = out.data_ptr(), out.element_size()
-                _native.wreduce_tensors_raw(ptrs, n, layout.split_sizes[dt], weights_f32,
-                                            [base + layout.offsets[k] * esz for k in idx],
-                                            _native.dtype_code(dt), mode, stream.cuda_stream)
+                # shapes and dtypes, so only pointers go to the library, read
+                # in C (no detach() objects, no output slices)
+                if not _native.wreduce_rows(all_params, idx, layout.split_sizes[dt], weights_f32, out.data_ptr(),
+                                            layout.byte_offsets[dt], _native.dtype_code(dt), mode,
+                                            stream.cuda_stream):
+                    keep, ptrs = _data_ptrs(all_params, idx)  # copies the non-contiguous ones
+                    base = out.data_ptr()
+                    _native.wreduce_tensors_raw(ptrs, n, layout.split_sizes[dt], weights_f32,
+                                                [base + o for o in layout.byte_offsets[dt]],
+                                                _native.dtype_code(dt), mode, stream.cuda_stream)
                 st.mark("kernel")
                 continue
             if not f64 and not any(all_params[i][idx[0]].is_cuda for i in range(n)):
@@ -581,16 +608,35 @@ _make_param = torch.Tensor._make_subclass
 
 
 class _ArenaEntry:
-    __slots__ = ("layout", "arenas", "ptrs")
+    __slots__ = ("layout", "arenas", "bases")
 
-    def __init__(self, layout, arenas, ptrs):
-        self.layout, self.arenas, self.ptrs = layout, arenas, ptrs
+    def __init__(self, layout, arenas, bases):
+        self.layout, self.arenas, self.bases = layout, arenas, bases
 
 
 # Modules whose parameters this package installed as views of flat arenas
 # (module_from_arenas): their layout and arenas, so later aggregates skip the
 # layout/contiguity checks. Weak keys: an entry lives as long as its module.
-_ARENAS: "weakref.WeakKeyDictionary[nn.Module, _ArenaEntry]" = weakref.WeakKeyDictionary()
+_ARENAS: Dict[int, Tuple["weakref.ref", _ArenaEntry]] = {}  # id(module) -> (weak ref, entry)
+
+
+def _arena_entry(module) -> Optional[_ArenaEntry]:
+    """The entry of `module` (one dict lookup by id; the weak reference
+    proves the id still belongs to it)."""
+    e = _ARENAS.get(id(module))
+    if e is None or e[0]() is not module:
+        return None
+    return e[1]
+
+
+def _register_arenas(module: nn.Module, entry: _ArenaEntry) -> None:
+    key = id(module)
+
+    def gone(ref, key=key):  # runs when the module is freed, before its id can be reused
+        cur = _ARENAS.get(key)
+        if cur is not None and cur[0] is ref:
+            del _ARENAS[key]
+    _ARENAS[key] = (weakref.ref(module, gone), entry)
 
 
 def registered_arenas(module: nn.Module, params: Optional[List[nn.Parameter]] = None):
@@ -598,17 +644,15 @@ def registered_arenas(module: nn.Module, params: Optional[List[nn.Parameter]] = 
     built by module_from_arenas and its parameters still are those views
     (same count, shapes and addresses: a parameter re-assigned or re-pointed
     since, e.g. `p.data = t`, invalidates the entry); else None."""
-    try:
-        e = _ARENAS.get(module)
-    except TypeError:
-        return None
+    e = _arena_entry(module)
     if e is None:
         return None
     ps = module_params(module) if params is None else params
-    if len(ps) != len(e.ptrs):
+    slots, bases = e.layout.param_slots, e.bases
+    if len(ps) != len(slots):
         return None
-    for q, (ptr, shape) in zip(ps, e.ptrs):
-        if q.data_ptr() != ptr or q.shape != shape:
+    for q, (dt, bo, shape) in zip(ps, slots):
+        if q.data_ptr() != bases[dt] + bo or q.shape != shape:
             return None
     return e.layout.rebind(ps), e.arenas
 
@@ -618,21 +662,21 @@ def module_from_arenas(model0: nn.Module, layout: ParamLayout,
     """`copy.deepcopy(model0)` whose parameters are views of `arenas`
     (registered, so a later aggregate reads the arenas without checks)."""
     memo = {}
-    new_params = [None] * len(layout.params)
+    params = layout.params
     for dt, idx in layout.groups.items():
-        parts = torch.split(arenas[dt], layout.split_sizes[dt])  # one call for the group
-        for k, part, shape in zip(idx, parts, layout.split_shapes[dt]):
-            p = layout.params[k]
-            # nn.Parameter(t, requires_grad) for a plain tensor, without its
+        a = arenas[dt]
+        base = a.storage_offset()
+        view = a.as_strided
+        for k, (shape, strides, off) in zip(idx, layout.view_specs[dt]):
+            p = params[k]
+            # nn.Parameter(view, requires_grad) for a plain tensor, without its
             # Python __new__ frame
-            q = _make_param(nn.Parameter, part if shape is None else part.view(shape), p.requires_grad)
-            memo[id(p)] = q
-            new_params[k] = q
+            memo[id(p)] = _make_param(nn.Parameter, view(shape, strides, base + off), p.requires_grad)
     out = _clone_module(model0, memo)
     # The clone maps every parameter of model0 to its view one to one and keeps
-    # the module/parameter order, so parameters() of `out` is new_params.
-    _ARENAS[out] = _ArenaEntry(layout.rebind([]), dict(arenas),
-                               tuple((q.data_ptr(), q.shape) for q in new_params))
+    # the module/parameter order, so parameters() of `out` are those views.
+    _register_arenas(out, _ArenaEntry(layout.rebind([]), dict(arenas),
+                                      {dt: a.data_ptr() for dt, a in arenas.items()}))
     return out
 
 
@@ -678,7 +722,9 @@ def aggregate_modules(models: List[nn.Module], weights: Optional[Sequence[float]
     model0 = models[0]  # IndexError for an empty list, as the reference
     w32 = _native.fp32_weights(weights)
     layout, arenas, dev, on_host, host_out = reduce_modules_to_arenas(models, w32, mode, device, timing, to_host,
-                                                                      weights_f64=_native.f64_weights(weights))
+                                                                      weights_f64=weights)
+    if timing is None and not (host_out and not on_host):
+        return module_from_arenas(model0, layout, arenas)
     stream = torch.cuda.current_stream(dev)
     st = _Stages(timing, stream)
     if host_out and not on_host:

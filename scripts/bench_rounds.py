@@ -314,6 +314,8 @@ def main():
                 "us_per_task_all": [round(x * 1e6, 1) for x in samples[kind]],
                 "GBps_algorithmic": round(task_bytes / per / 1e9, 2),
                 "gc_us_per_task": round(statistics.median(gc_s[kind]) * 1e6, 1),
+                "us_per_task_excl_gc": round(statistics.median([t - g for t, g in zip(samples[kind], gc_s[kind])])
+                                             * 1e6, 1),
                 "gc_collections_by_generation": gc_n[kind]}
 
     for kind in samples:

@@ -421,3 +421,87 @@ def test_pyhost_signature_and_pointer_helpers():
     t = [torch.zeros(4, 3).t(), torch.zeros(2)]
     assert _pyhost.data_ptrs([t], [1]) == [t[1].data_ptr()]
     assert _pyhost.data_ptrs([t], [0, 1]) is None
+
+
+def test_arena_registry_follows_module_lifetime():
+    """Registered arenas are keyed by id(module) with a weak reference: the
+    entry goes when the module does, and a new object at a reused id is not
+    mistaken for the old one."""
+    import gc
+    m = nn.Sequential(nn.Linear(4, 3))
+    lay = arena.ParamLayout(m)
+    out = arena.module_from_arenas(m, lay, {torch.float32: torch.zeros(lay.totals[torch.float32])})
+    key = id(out)
+    assert key in arena._ARENAS and arena.registered_arenas(out) is not None
+    del out
+    gc.collect()
+    assert key not in arena._ARENAS
+    import weakref
+    other = nn.Sequential(nn.Linear(4, 3))
+    arena._ARENAS[id(other)] = (weakref.ref(m), None)  # a slot whose weak ref names another module
+    assert arena._arena_entry(other) is None
+    del arena._ARENAS[id(other)]
+
+
+def test_wreduce_rows_validates_without_launching():
+    """_native.wreduce_rows (csrc/pyhost.cpp): argument checks, and a
+    non-contiguous tensor returns False before anything reaches the library.
+    Zero tensors call the library, which returns before any HIP call."""
+    rows = [[torch.zeros(4, 3), torch.zeros(3)], [torch.zeros(4, 3).t(), torch.zeros(3)]]
+    w = _native.fp32_weights([0.5, 0.5])
+    assert _native.wreduce_rows(rows, [0, 1], [12, 3], w, 0, [0, 48], _native.DLSIM_F32, 0, 0) is False
+    assert _native.wreduce_rows(rows, [], [], w, 0, [], _native.DLSIM_F32, 0, 0) is True
+    with pytest.raises(ValueError, match="one float per model"):
+        _native.wreduce_rows(rows, [1], [3], _native.fp32_weights([1.0]), 0, [0], _native.DLSIM_F32, 0, 0)
+    with pytest.raises(ValueError, match="differ in length"):
+        _native.wreduce_rows(rows, [1], [3, 4], w, 0, [0], _native.DLSIM_F32, 0, 0)
+
+
+def test_pyhost_checked_params_and_flat_run():
+    """checked_params = module_params + matches in one call (None on a
+    mismatch); flat_run = the tensors of a dtype group are contiguous and at
+    their byte offsets from the group's first tensor."""
+    from dasklearn_amd import _pyhost
+    m = nn.Sequential(nn.Linear(3, 4), nn.Linear(4, 2))
+    lay = arena.ParamLayout(m)
+    ps = _pyhost.checked_params(m, lay._signature)
+    assert ps is not None and all(a is b for a, b in zip(ps, m.parameters()))
+    assert _pyhost.checked_params(nn.Sequential(nn.Linear(3, 4), nn.Linear(4, 3)), lay._signature) is None
+    dt = torch.float32
+    idx = lay.groups[dt]
+    assert not _pyhost.flat_run(ps, idx, lay.byte_offsets[dt])  # separate storages
+    out = arena.module_from_arenas(m, lay, {dt: torch.zeros(lay.totals[dt])})
+    qs = arena.module_params(out)
+    assert _pyhost.flat_run(qs, idx, lay.byte_offsets[dt])
+    assert lay.arena_view(qs, dt) is not None and lay.arena_view(ps, dt) is None
+    flat = torch.zeros(lay.totals[dt])
+    t = [flat[0:12].view(4, 3).t(), flat[12:16], flat[16:24].view(2, 4), flat[24:26]]  # right place, transposed
+    assert not _pyhost.flat_run(t, idx, lay.byte_offsets[dt])
+    with pytest.raises(ValueError, match="differ in length"):
+        _pyhost.flat_run(qs, idx, lay.byte_offsets[dt][:-1])
+
+
+def test_clone_leaves_empty_hook_registries_untracked_until_used():
+    """The C clone hands out its fresh empty OrderedDicts untracked by the
+    cyclic collector; inserting a hook re-tracks the registry (CPython's dict
+    insert path), so a cycle through a hook is still collected."""
+    import gc
+    import weakref
+    m = nn.Sequential(nn.Linear(2, 2))
+    lay = arena.ParamLayout(m)
+    out = arena.module_from_arenas(m, lay, {torch.float32: torch.zeros(lay.totals[torch.float32])})
+    assert not gc.is_tracked(out._forward_hooks) and not gc.is_tracked(out[0]._forward_pre_hooks)
+    assert gc.is_tracked(m._forward_hooks)  # the original is untouched
+
+    class Hook:
+        def __call__(self, mod, inp, o):
+            return None
+
+    h = Hook()
+    h.cycle = out  # hook -> module -> registry -> hook
+    out.register_forward_hook(h)
+    assert gc.is_tracked(out._forward_hooks)
+    r = weakref.ref(out)
+    del out, h
+    gc.collect()
+    assert r() is None  # the cycle was found
