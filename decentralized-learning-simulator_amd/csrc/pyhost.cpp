@@ -20,14 +20,21 @@
 //   clone_module(module, memo)     arena._clone_module_py: copy.deepcopy of
 //                                      models[0] with parameters from the memo
 //   checked_params(module, sig)    module_params + matches in one call
-//   flat_run(params, idx, offs)    the dtype group already is one flat run
+//   flat_run(params, idx, offs, n) the dtype group already is one flat arena
 //   wreduce_rows(...)              the data pointers of a task's parameter
 //                                      tensors straight into one
 //                                      dlsim_wreduce_tensors call
 //
+// Tensor fields (shape, dtype, contiguity, device, data pointer) are read from
+// the at::Tensor itself (libtorch headers; the extension links torch's
+// libraries), not through Python attribute calls.
+//
 // Built by __graft_entry__.build() as dasklearn_amd/_pyhost*.so.
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
+
+#include <torch/csrc/Dtype.h>
+#include <torch/csrc/autograd/python_variable.h>
 
 #include <cstdint>
 #include <unordered_set>
@@ -37,10 +44,6 @@ namespace {
 
 PyObject* s_parameters = nullptr;
 PyObject* s_modules = nullptr;
-PyObject* s_shape = nullptr;
-PyObject* s_dtype = nullptr;
-PyObject* s_data_ptr = nullptr;
-PyObject* s_is_contiguous = nullptr;
 
 int visit(PyObject* m, PyObject* out, std::unordered_set<PyObject*>& seen, int depth) {
   if (depth > 10000) {
@@ -100,98 +103,161 @@ PyObject* py_module_params(PyObject*, PyObject* module) {
   return out;
 }
 
+// ---- tensor fields read in C++ ---------------------------------------------
+//
+// THPVariable_Unpack gives the at::Tensor behind a torch.Tensor/nn.Parameter
+// object, so shape, dtype, contiguity, device and data pointer are field reads
+// instead of Python attribute and method calls (about 100 tensors per task).
+
+// The tensor behind `o`, or nullptr (TypeError set) for anything else.
+const at::Tensor* tensor_of(PyObject* o) {
+  if (!THPVariable_Check(o)) {
+    PyErr_Format(PyExc_TypeError, "expected a tensor, got %.200s", Py_TYPE(o)->tp_name);
+    return nullptr;
+  }
+  return &THPVariable_Unpack(o);
+}
+
+// A layout signature ((torch.Size, torch.dtype), ...) as C++ values, cached by
+// the identity of the tuple (ParamLayout.rebind shares it across tasks). The
+// cache holds a reference to each key, so a cached address cannot be reused
+// by another object while its entry exists.
+struct Sig {
+  std::vector<std::vector<int64_t>> shapes;
+  std::vector<at::ScalarType> dtypes;
+};
+constexpr size_t kSigCache = 16;
+std::vector<std::pair<PyObject*, Sig>> g_sigs;
+
+const Sig* sig_of(PyObject* sig) {
+  for (auto& e : g_sigs)
+    if (e.first == sig) return &e.second;
+  PyObject* ss = PySequence_Fast(sig, "signature must be a sequence");
+  if (!ss) return nullptr;
+  Sig s;
+  bool ok = true;
+  for (Py_ssize_t k = 0; ok && k < PySequence_Fast_GET_SIZE(ss); ++k) {
+    PyObject* entry = PySequence_Fast_GET_ITEM(ss, k);
+    if (!PyTuple_Check(entry) || PyTuple_GET_SIZE(entry) != 2 || !THPDtype_Check(PyTuple_GET_ITEM(entry, 1))) {
+      PyErr_SetString(PyExc_TypeError, "signature entries are (shape, dtype)");
+      ok = false;
+      break;
+    }
+    PyObject* sh = PySequence_Fast(PyTuple_GET_ITEM(entry, 0), "shape must be a sequence");
+    if (!sh) {
+      ok = false;
+      break;
+    }
+    std::vector<int64_t> dims;
+    for (Py_ssize_t d = 0; d < PySequence_Fast_GET_SIZE(sh); ++d)
+      dims.push_back(PyLong_AsLongLong(PySequence_Fast_GET_ITEM(sh, d)));
+    Py_DECREF(sh);
+    if (PyErr_Occurred()) {
+      ok = false;
+      break;
+    }
+    s.shapes.push_back(std::move(dims));
+    s.dtypes.push_back(reinterpret_cast<THPDtype*>(PyTuple_GET_ITEM(entry, 1))->scalar_type);
+  }
+  Py_DECREF(ss);
+  if (!ok) return nullptr;
+  if (g_sigs.size() == kSigCache) {
+    Py_DECREF(g_sigs.front().first);
+    g_sigs.erase(g_sigs.begin());
+  }
+  Py_INCREF(sig);
+  g_sigs.emplace_back(sig, std::move(s));
+  return &g_sigs.back().second;
+}
+
+// 1 if the tensors in `ps` (a PySequence_Fast) have the signature's count,
+// shapes and dtypes, 0 if not, -1 on error
+int matches_sig(PyObject* ps, const Sig& s) {
+  const Py_ssize_t n = PySequence_Fast_GET_SIZE(ps);
+  if (static_cast<size_t>(n) != s.shapes.size()) return 0;
+  for (Py_ssize_t k = 0; k < n; ++k) {
+    const at::Tensor* t = tensor_of(PySequence_Fast_GET_ITEM(ps, k));
+    if (!t) return -1;
+    if (t->scalar_type() != s.dtypes[k] || !t->sizes().equals(s.shapes[k])) return 0;
+  }
+  return 1;
+}
+
 PyObject* py_matches(PyObject*, PyObject* args) {
   PyObject *params, *sig;
   if (!PyArg_ParseTuple(args, "OO", &params, &sig)) return nullptr;
+  const Sig* s = sig_of(sig);
+  if (!s) return nullptr;
   PyObject* ps = PySequence_Fast(params, "params must be a sequence");
   if (!ps) return nullptr;
-  PyObject* ss = PySequence_Fast(sig, "signature must be a sequence");
-  if (!ss) {
-    Py_DECREF(ps);
-    return nullptr;
-  }
-  const Py_ssize_t n = PySequence_Fast_GET_SIZE(ps);
-  int ok = n == PySequence_Fast_GET_SIZE(ss);
-  for (Py_ssize_t k = 0; ok && k < n; ++k) {
-    PyObject* p = PySequence_Fast_GET_ITEM(ps, k);
-    PyObject* entry = PySequence_Fast_GET_ITEM(ss, k);  // (shape, dtype)
-    if (!PyTuple_Check(entry) || PyTuple_GET_SIZE(entry) != 2) {
-      PyErr_SetString(PyExc_TypeError, "signature entries are (shape, dtype)");
-      ok = -1;
-      break;
-    }
-    PyObject* dt = PyObject_GetAttr(p, s_dtype);
-    if (!dt) {
-      ok = -1;
-      break;
-    }
-    ok = dt == PyTuple_GET_ITEM(entry, 1);
-    Py_DECREF(dt);
-    if (!ok) break;
-    PyObject* sh = PyObject_GetAttr(p, s_shape);
-    if (!sh) {
-      ok = -1;
-      break;
-    }
-    ok = PyObject_RichCompareBool(sh, PyTuple_GET_ITEM(entry, 0), Py_EQ);
-    Py_DECREF(sh);
-  }
+  const int ok = matches_sig(ps, *s);
   Py_DECREF(ps);
-  Py_DECREF(ss);
   if (ok < 0) return nullptr;
   return PyBool_FromLong(ok);
+}
+
+// rows[i][idx[j]] for every i, j (model-major) as tensors; false (error set)
+// if an item is missing or not a tensor
+bool row_tensors(PyObject* rows, PyObject* idx, std::vector<const at::Tensor*>& out, Py_ssize_t* n_out,
+                 Py_ssize_t* t_out) {
+  PyObject* rs = PySequence_Fast(rows, "rows must be a sequence");
+  if (!rs) return false;
+  PyObject* ks = PySequence_Fast(idx, "idx must be a sequence");
+  if (!ks) {
+    Py_DECREF(rs);
+    return false;
+  }
+  const Py_ssize_t n = PySequence_Fast_GET_SIZE(rs), t = PySequence_Fast_GET_SIZE(ks);
+  out.resize(static_cast<size_t>(n * t));
+  bool ok = true;
+  for (Py_ssize_t i = 0; ok && i < n; ++i) {
+    PyObject* row = PySequence_Fast(PySequence_Fast_GET_ITEM(rs, i), "each row must be a sequence");
+    if (!row) {
+      ok = false;
+      break;
+    }
+    const Py_ssize_t len = PySequence_Fast_GET_SIZE(row);
+    for (Py_ssize_t j = 0; j < t; ++j) {
+      const Py_ssize_t k = PyLong_AsSsize_t(PySequence_Fast_GET_ITEM(ks, j));
+      if (k < 0 || k >= len) {
+        if (!PyErr_Occurred()) PyErr_SetString(PyExc_IndexError, "parameter index out of range");
+        ok = false;
+        break;
+      }
+      // the rows (and so the tensors) outlive this call: borrowed pointers
+      const at::Tensor* tt = tensor_of(PySequence_Fast_GET_ITEM(row, k));
+      if (!tt) {
+        ok = false;
+        break;
+      }
+      out[static_cast<size_t>(i * t + j)] = tt;
+    }
+    Py_DECREF(row);
+  }
+  Py_DECREF(ks);
+  Py_DECREF(rs);
+  *n_out = n;
+  *t_out = t;
+  return ok;
 }
 
 PyObject* py_data_ptrs(PyObject*, PyObject* args) {
   PyObject *rows, *idx;
   if (!PyArg_ParseTuple(args, "OO", &rows, &idx)) return nullptr;
-  PyObject* rs = PySequence_Fast(rows, "rows must be a sequence");
-  if (!rs) return nullptr;
-  PyObject* ks = PySequence_Fast(idx, "idx must be a sequence");
-  if (!ks) {
-    Py_DECREF(rs);
-    return nullptr;
-  }
-  const Py_ssize_t nr = PySequence_Fast_GET_SIZE(rs), nk = PySequence_Fast_GET_SIZE(ks);
-  PyObject* out = PyList_New(nr * nk);
-  bool contiguous = true;
-  for (Py_ssize_t i = 0; out && contiguous && i < nr; ++i) {
-    PyObject* row = PySequence_Fast_GET_ITEM(rs, i);
-    for (Py_ssize_t j = 0; j < nk; ++j) {
-      PyObject* t = PyObject_GetItem(row, PySequence_Fast_GET_ITEM(ks, j));
-      if (!t) {
-        Py_CLEAR(out);
-        break;
-      }
-      PyObject* c = PyObject_CallMethodNoArgs(t, s_is_contiguous);
-      if (!c) {
-        Py_DECREF(t);
-        Py_CLEAR(out);
-        break;
-      }
-      const int isc = PyObject_IsTrue(c);
-      Py_DECREF(c);
-      if (isc != 1) {
-        Py_DECREF(t);
-        if (isc < 0) Py_CLEAR(out);
-        contiguous = false;
-        break;
-      }
-      PyObject* ptr = PyObject_CallMethodNoArgs(t, s_data_ptr);
-      Py_DECREF(t);
-      if (!ptr) {
-        Py_CLEAR(out);
-        break;
-      }
-      PyList_SET_ITEM(out, i * nk + j, ptr);  // steals the reference
-    }
-  }
-  Py_DECREF(rs);
-  Py_DECREF(ks);
+  std::vector<const at::Tensor*> ts;
+  Py_ssize_t n, t;
+  if (!row_tensors(rows, idx, ts, &n, &t)) return nullptr;
+  for (const at::Tensor* x : ts)
+    if (!x->is_contiguous()) Py_RETURN_NONE;
+  PyObject* out = PyList_New(static_cast<Py_ssize_t>(ts.size()));
   if (!out) return nullptr;
-  if (!contiguous) {
-    Py_DECREF(out);
-    Py_RETURN_NONE;
+  for (size_t q = 0; q < ts.size(); ++q) {
+    PyObject* p = PyLong_FromVoidPtr(const_cast<void*>(ts[q]->const_data_ptr()));
+    if (!p) {
+      Py_DECREF(out);
+      return nullptr;
+    }
+    PyList_SET_ITEM(out, static_cast<Py_ssize_t>(q), p);
   }
   return out;
 }
@@ -201,78 +267,61 @@ PyObject* py_data_ptrs(PyObject*, PyObject* args) {
 PyObject* py_checked_params(PyObject*, PyObject* args) {
   PyObject *module, *sig;
   if (!PyArg_ParseTuple(args, "OO", &module, &sig)) return nullptr;
+  const Sig* s = sig_of(sig);
+  if (!s) return nullptr;
   PyObject* ps = py_module_params(nullptr, module);
   if (!ps) return nullptr;
-  PyObject* pair = PyTuple_Pack(2, ps, sig);
-  PyObject* ok = pair ? py_matches(nullptr, pair) : nullptr;
-  Py_XDECREF(pair);
-  if (!ok) {
-    Py_DECREF(ps);
-    return nullptr;
-  }
-  const bool m = ok == Py_True;
-  Py_DECREF(ok);
-  if (m) return ps;
+  const int ok = matches_sig(ps, *s);  // a list is its own PySequence_Fast
+  if (ok == 1) return ps;
   Py_DECREF(ps);
+  if (ok < 0) return nullptr;
   Py_RETURN_NONE;
 }
 
-// flat_run(params, idx, byte_offsets) -> True iff every params[idx[j]] is
-// contiguous and starts byte_offsets[j] bytes after params[idx[0]]
+// flat_run(params, idx, byte_offsets, total_elems) -> True iff the dtype group
+// params[idx] already is one flat arena: every tensor contiguous and
+// byte_offsets[j] bytes after params[idx[0]], and total_elems elements from
+// the first one still inside its storage (adjacent separate allocations are
+// not an arena)
 PyObject* py_flat_run(PyObject*, PyObject* args) {
   PyObject *params, *idx, *offs;
-  if (!PyArg_ParseTuple(args, "OOO", &params, &idx, &offs)) return nullptr;
-  PyObject* ps = PySequence_Fast(params, "params must be a sequence");
-  if (!ps) return nullptr;
-  PyObject* ks = PySequence_Fast(idx, "idx must be a sequence");
-  PyObject* os = ks ? PySequence_Fast(offs, "byte_offsets must be a sequence") : nullptr;
-  int result = -1;
-  do {
-    if (!os) break;
-    const Py_ssize_t t = PySequence_Fast_GET_SIZE(ks);
-    if (PySequence_Fast_GET_SIZE(os) != t) {
-      PyErr_SetString(PyExc_ValueError, "idx and byte_offsets differ in length");
-      break;
-    }
-    uintptr_t base = 0;
-    result = 1;
-    for (Py_ssize_t j = 0; result == 1 && j < t; ++j) {
-      PyObject* q = PyObject_GetItem(ps, PySequence_Fast_GET_ITEM(ks, j));
-      if (!q) {
-        result = -1;
-        break;
-      }
-      PyObject* ptr = PyObject_CallMethodNoArgs(q, s_data_ptr);
-      const uintptr_t p = ptr ? reinterpret_cast<uintptr_t>(PyLong_AsVoidPtr(ptr)) : 0;
-      Py_XDECREF(ptr);
-      if (!ptr || PyErr_Occurred()) {
-        Py_DECREF(q);
-        result = -1;
-        break;
-      }
-      if (j == 0) base = p;
+  unsigned long long total;
+  if (!PyArg_ParseTuple(args, "OOOK", &params, &idx, &offs, &total)) return nullptr;
+  PyObject* row = PyTuple_Pack(1, params);
+  if (!row) return nullptr;
+  std::vector<const at::Tensor*> ts;
+  Py_ssize_t n, t;
+  const bool got = row_tensors(row, idx, ts, &n, &t);
+  Py_DECREF(row);
+  if (!got) return nullptr;
+  PyObject* os = PySequence_Fast(offs, "byte_offsets must be a sequence");
+  if (!os) return nullptr;
+  if (PySequence_Fast_GET_SIZE(os) != t) {
+    Py_DECREF(os);
+    PyErr_SetString(PyExc_ValueError, "idx and byte_offsets differ in length");
+    return nullptr;
+  }
+  bool flat = t > 0;
+  try {
+    const auto base = reinterpret_cast<uintptr_t>(flat ? ts[0]->const_data_ptr() : nullptr);
+    for (Py_ssize_t j = 0; flat && j < t; ++j) {
       const size_t off = PyLong_AsSize_t(PySequence_Fast_GET_ITEM(os, j));
       if (PyErr_Occurred()) {
-        Py_DECREF(q);
-        result = -1;
-        break;
+        Py_DECREF(os);
+        return nullptr;
       }
-      if (p - base != off) {
-        Py_DECREF(q);
-        result = 0;
-        break;
-      }
-      PyObject* c = PyObject_CallMethodNoArgs(q, s_is_contiguous);
-      Py_DECREF(q);
-      result = c ? PyObject_IsTrue(c) : -1;
-      Py_XDECREF(c);
+      flat = reinterpret_cast<uintptr_t>(ts[j]->const_data_ptr()) - base == off && ts[j]->is_contiguous();
     }
-  } while (false);
-  Py_XDECREF(os);
-  Py_XDECREF(ks);
-  Py_DECREF(ps);
-  if (result < 0) return nullptr;
-  return PyBool_FromLong(result);
+    if (flat) {
+      const at::Tensor& first = *ts[0];
+      flat = first.has_storage() &&
+             first.storage().nbytes() >= (static_cast<size_t>(first.storage_offset()) + total) * first.element_size();
+    }
+  } catch (const std::exception&) {  // tensors without a plain storage (sparse, nested, ...)
+    flat = false;
+  }
+  Py_DECREF(os);
+  return PyBool_FromLong(flat);
 }
 
 // ---- one device task's reduce: pointers collected and the library called ----
@@ -293,32 +342,31 @@ PyObject* py_bind_wreduce_tensors(PyObject*, PyObject* addr) {
 }
 
 // wreduce_rows(rows, idx, numels, weights_f32, out_base, out_offsets, dtype,
-//              mode, stream) -> rc, or None (nothing launched) if a tensor is
-// not contiguous. rows[i][idx[j]] is tensor j of model i; numels[j] its
-// element count; out_offsets[j] its byte offset from out_base; weights_f32
-// a C-contiguous buffer of len(rows) floats.
+//              mode, stream, device) -> rc, or None (nothing launched) if a
+// tensor is not contiguous or not on CUDA device `device`. rows[i][idx[j]] is
+// tensor j of model i; numels[j] its element count; out_offsets[j] its byte
+// offset from out_base; weights_f32 a C-contiguous buffer of len(rows) floats.
 PyObject* py_wreduce_rows(PyObject*, PyObject* args) {
   PyObject *rows, *idx, *numels, *weights, *offsets;
   unsigned long long out_base, stream;
-  int dtype, mode;
-  if (!PyArg_ParseTuple(args, "OOOOKOiiK", &rows, &idx, &numels, &weights, &out_base, &offsets, &dtype, &mode,
-                        &stream))
+  int dtype, mode, device;
+  if (!PyArg_ParseTuple(args, "OOOOKOiiKi", &rows, &idx, &numels, &weights, &out_base, &offsets, &dtype, &mode,
+                        &stream, &device))
     return nullptr;
   if (!g_wreduce_tensors) {
     PyErr_SetString(PyExc_RuntimeError, "bind_wreduce_tensors was not called");
     return nullptr;
   }
-  PyObject* rs = PySequence_Fast(rows, "rows must be a sequence");
-  if (!rs) return nullptr;
-  PyObject* ks = PySequence_Fast(idx, "idx must be a sequence");
-  PyObject* ns = ks ? PySequence_Fast(numels, "numels must be a sequence") : nullptr;
+  std::vector<const at::Tensor*> ts;
+  Py_ssize_t n, t;
+  if (!row_tensors(rows, idx, ts, &n, &t)) return nullptr;
+  PyObject* ns = PySequence_Fast(numels, "numels must be a sequence");
   PyObject* os = ns ? PySequence_Fast(offsets, "out_offsets must be a sequence") : nullptr;
   PyObject* result = nullptr;
   Py_buffer wb{};
   bool have_wb = false;
   do {
     if (!os) break;
-    const Py_ssize_t n = PySequence_Fast_GET_SIZE(rs), t = PySequence_Fast_GET_SIZE(ks);
     if (PySequence_Fast_GET_SIZE(ns) != t || PySequence_Fast_GET_SIZE(os) != t) {
       PyErr_SetString(PyExc_ValueError, "idx, numels and out_offsets differ in length");
       break;
@@ -329,49 +377,22 @@ PyObject* py_wreduce_rows(PyObject*, PyObject* args) {
       PyErr_SetString(PyExc_ValueError, "weights_f32 must hold one float per model");
       break;
     }
-    std::vector<const void*> ins(static_cast<size_t>(n * t));
+    std::vector<const void*> ins(ts.size());
     std::vector<size_t> ne(static_cast<size_t>(t));
     std::vector<void*> outs(static_cast<size_t>(t));
-    bool ok = true, contiguous = true;
-    for (Py_ssize_t j = 0; ok && j < t; ++j) {
+    for (Py_ssize_t j = 0; j < t; ++j) {
       ne[j] = PyLong_AsSize_t(PySequence_Fast_GET_ITEM(ns, j));
-      const size_t off = PyLong_AsSize_t(PySequence_Fast_GET_ITEM(os, j));
-      if (PyErr_Occurred()) ok = false;
-      outs[j] = reinterpret_cast<void*>(static_cast<uintptr_t>(out_base + off));
+      outs[j] = reinterpret_cast<void*>(
+          static_cast<uintptr_t>(out_base + PyLong_AsSize_t(PySequence_Fast_GET_ITEM(os, j))));
     }
-    for (Py_ssize_t i = 0; ok && contiguous && i < n; ++i) {
-      PyObject* row = PySequence_Fast_GET_ITEM(rs, i);
-      for (Py_ssize_t j = 0; j < t; ++j) {
-        PyObject* tt = PyObject_GetItem(row, PySequence_Fast_GET_ITEM(ks, j));
-        if (!tt) {
-          ok = false;
-          break;
-        }
-        PyObject* c = PyObject_CallMethodNoArgs(tt, s_is_contiguous);
-        const int isc = c ? PyObject_IsTrue(c) : -1;
-        Py_XDECREF(c);
-        if (isc != 1) {
-          Py_DECREF(tt);
-          if (isc < 0) ok = false;
-          contiguous = false;
-          break;
-        }
-        PyObject* ptr = PyObject_CallMethodNoArgs(tt, s_data_ptr);
-        Py_DECREF(tt);
-        if (!ptr) {
-          ok = false;
-          break;
-        }
-        ins[static_cast<size_t>(i * t + j)] = PyLong_AsVoidPtr(ptr);
-        Py_DECREF(ptr);
-        if (PyErr_Occurred()) {
-          ok = false;
-          break;
-        }
-      }
+    if (PyErr_Occurred()) break;
+    bool here = true;
+    for (size_t q = 0; here && q < ts.size(); ++q) {
+      const at::Tensor& x = *ts[q];
+      here = x.is_cuda() && x.get_device() == device && x.is_contiguous();
+      ins[q] = x.const_data_ptr();
     }
-    if (!ok) break;
-    if (!contiguous) {
+    if (!here) {
       Py_INCREF(Py_None);
       result = Py_None;
       break;
@@ -387,8 +408,6 @@ PyObject* py_wreduce_rows(PyObject*, PyObject* args) {
   if (have_wb) PyBuffer_Release(&wb);
   Py_XDECREF(os);
   Py_XDECREF(ns);
-  Py_XDECREF(ks);
-  Py_DECREF(rs);
   return result;
 }
 
@@ -652,9 +671,9 @@ PyMethodDef kMethods[] = {
     {"clone_module", py_clone_module, METH_VARARGS, "clone_module(module, memo): arena._clone_module in C"},
     {"bind_wreduce_tensors", py_bind_wreduce_tensors, METH_O, "bind dlsim_wreduce_tensors by address"},
     {"checked_params", py_checked_params, METH_VARARGS, "module_params(module) if it matches signature, else None"},
-    {"flat_run", py_flat_run, METH_VARARGS, "params[idx] contiguous at byte_offsets from params[idx[0]]"},
+    {"flat_run", py_flat_run, METH_VARARGS, "flat_run(params, idx, byte_offsets, total): the group is one arena"},
     {"wreduce_rows", py_wreduce_rows, METH_VARARGS,
-     "wreduce_rows(rows, idx, numels, weights_f32, out_base, out_offsets, dtype, mode, stream) -> rc or None"},
+     "wreduce_rows(rows, idx, numels, weights_f32, out_base, out_offsets, dtype, mode, stream, device) -> rc or None"},
     {nullptr, nullptr, 0, nullptr}};
 
 PyModuleDef kModule = {PyModuleDef_HEAD_INIT, "_pyhost", "CPython helpers of the per-task module path", -1,
@@ -665,17 +684,12 @@ PyModuleDef kModule = {PyModuleDef_HEAD_INIT, "_pyhost", "CPython helpers of the
 PyMODINIT_FUNC PyInit__pyhost(void) {
   s_parameters = PyUnicode_InternFromString("_parameters");
   s_modules = PyUnicode_InternFromString("_modules");
-  s_shape = PyUnicode_InternFromString("shape");
-  s_dtype = PyUnicode_InternFromString("dtype");
-  s_data_ptr = PyUnicode_InternFromString("data_ptr");
-  s_is_contiguous = PyUnicode_InternFromString("is_contiguous");
   s_modules_key = s_modules;
   s_params_key = s_parameters;
   s_compiled_key = PyUnicode_InternFromString("_compiled_call_impl");
   s_new = PyUnicode_InternFromString("__new__");
   s_setstate = PyUnicode_InternFromString("__setstate__");
-  if (!s_parameters || !s_modules || !s_shape || !s_dtype || !s_data_ptr || !s_is_contiguous || !s_compiled_key ||
-      !s_new || !s_setstate)
+  if (!s_parameters || !s_modules || !s_compiled_key || !s_new || !s_setstate)
     return nullptr;
   return PyModule_Create(&kModule);
 }

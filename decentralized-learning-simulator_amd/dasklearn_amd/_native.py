@@ -551,20 +551,21 @@ _ROWS_BOUND = False
 
 
 def wreduce_rows(rows, idx: Sequence[int], numels: Sequence[int], weights_f32: np.ndarray, out_base: int,
-                 out_offsets: Sequence[int], dtype: int, mode: int, stream_handle: int) -> bool:
+                 out_offsets: Sequence[int], dtype: int, mode: int, stream_handle: int, device: int = 0) -> bool:
     """dlsim_wreduce_tensors over tensor k of every model (k in idx;
     rows[i][k] is a tensor of model i), called from C (csrc/pyhost.cpp) with
-    the data pointers read there: the caller has checked shapes, dtypes and
-    devices (the layout). Output tensor j is at out_base + out_offsets[j]
-    bytes. Returns False, having launched nothing, when a tensor is not
-    contiguous (the caller then copies it)."""
+    the data pointers read from the tensors there: the caller has checked
+    shapes and dtypes (the layout). Output tensor j is at out_base +
+    out_offsets[j] bytes. Returns False, having launched nothing, when a
+    tensor is not contiguous or not on CUDA device `device` (the caller then
+    stages it)."""
     global _ROWS_BOUND
     from . import _pyhost
     if not _ROWS_BOUND:
         _pyhost.bind_wreduce_tensors(ctypes.cast(load().dlsim_wreduce_tensors, ctypes.c_void_p).value)
         _ROWS_BOUND = True
     rc = _pyhost.wreduce_rows(rows, idx, numels, weights_f32, out_base, out_offsets, dtype, mode,
-                              stream_handle or 0)
+                              stream_handle or 0, device)
     if rc is None:
         return False
     _check("dlsim_wreduce_tensors", rc)

@@ -147,17 +147,14 @@ class ParamLayout:
         """If the dtype group of `params` already is one contiguous flat buffer
         (in layout order), return a flat view of it, else None."""
         idx = self.groups[dt]
+        total = self.totals[dt]
         # every tensor contiguous (a transposed view could start at the right
-        # place) and at its offset in the layout (checked in C)
-        if not _pyhost.flat_run(params, idx, self.byte_offsets[dt]):
+        # place) and at its offset in the layout, and the whole run inside the
+        # first tensor's storage: adjacent separate allocations are not an
+        # arena (read from the tensors in C++, csrc/pyhost.cpp)
+        if not _pyhost.flat_run(params, idx, self.byte_offsets[dt], total):
             return None
         first = params[idx[0]]
-        esz = first.element_size()
-        # ...inside the first tensor's storage: adjacent separate allocations
-        # are not an arena (one storage check instead of one per tensor)
-        total = self.totals[dt]
-        if first.untyped_storage().nbytes() < (first.storage_offset() + total) * esz:
-            return None
         return torch.as_strided(first.detach(), (total,), (1,), first.storage_offset())
 
 
@@ -460,12 +457,10 @@ def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, m
                 # in C (no detach() objects, no output slices)
                 if not _native.wreduce_rows(all_params, idx, layout.split_sizes[dt], weights_f32, out.data_ptr(),
                                             layout.byte_offsets[dt], _native.dtype_code(dt), mode,
-                                            stream.cuda_stream):
-                    keep, ptrs = _data_ptrs(all_params, idx)  # copies the non-contiguous ones
-                    base = out.data_ptr()
-                    _native.wreduce_tensors_raw(ptrs, n, layout.split_sizes[dt], weights_f32,
-                                                [base + o for o in layout.byte_offsets[dt]],
-                                                _native.dtype_code(dt), mode, stream.cuda_stream)
+                                            stream.cuda_stream, dix):
+                    # a tensor is not contiguous, or (in a model whose first
+                    # tensor is here) on another device: stage them all
+                    _staged_reduce(all_params, idx, dt, dev, out, w, mode, stream)
                 st.mark("kernel")
                 continue
             if not f64 and not any(all_params[i][idx[0]].is_cuda for i in range(n)):

@@ -112,9 +112,16 @@ class RoundExecutor:
             arenas = {dt: vs[0] for dt, vs in views.items()}
         else:
             dev = _target_device(params[0], self.device)
+            arenas = {}
             with torch.no_grad():
-                arenas = {dt: torch.cat([params[0][k].detach().reshape(-1).to(dev, non_blocking=True) for k in idx])
-                          for dt, idx in layout.groups.items()}
+                for dt, idx in layout.groups.items():
+                    ts = [params[0][k] for k in idx]
+                    if all(t.device == dev for t in ts):
+                        # one C++ call (torch's flatten, as DDP buckets use)
+                        # instead of a reshape per tensor and a cat
+                        arenas[dt] = torch._C._nn.flatten_dense_tensors(ts)
+                    else:
+                        arenas[dt] = torch.cat([t.detach().reshape(-1).to(dev, non_blocking=True) for t in ts])
         cache[id(m)] = (m, layout, arenas)
         return layout, arenas
 

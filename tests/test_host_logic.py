@@ -449,7 +449,7 @@ def test_wreduce_rows_validates_without_launching():
     Zero tensors call the library, which returns before any HIP call."""
     rows = [[torch.zeros(4, 3), torch.zeros(3)], [torch.zeros(4, 3).t(), torch.zeros(3)]]
     w = _native.fp32_weights([0.5, 0.5])
-    assert _native.wreduce_rows(rows, [0, 1], [12, 3], w, 0, [0, 48], _native.DLSIM_F32, 0, 0) is False
+    assert _native.wreduce_rows(rows, [0, 1], [12, 3], w, 0, [0, 48], _native.DLSIM_F32, 0, 0) is False  # host
     assert _native.wreduce_rows(rows, [], [], w, 0, [], _native.DLSIM_F32, 0, 0) is True
     with pytest.raises(ValueError, match="one float per model"):
         _native.wreduce_rows(rows, [1], [3], _native.fp32_weights([1.0]), 0, [0], _native.DLSIM_F32, 0, 0)
@@ -469,16 +469,20 @@ def test_pyhost_checked_params_and_flat_run():
     assert _pyhost.checked_params(nn.Sequential(nn.Linear(3, 4), nn.Linear(4, 3)), lay._signature) is None
     dt = torch.float32
     idx = lay.groups[dt]
-    assert not _pyhost.flat_run(ps, idx, lay.byte_offsets[dt])  # separate storages
+    total = lay.totals[dt]
+    assert not _pyhost.flat_run(ps, idx, lay.byte_offsets[dt], total)  # separate storages
     out = arena.module_from_arenas(m, lay, {dt: torch.zeros(lay.totals[dt])})
     qs = arena.module_params(out)
-    assert _pyhost.flat_run(qs, idx, lay.byte_offsets[dt])
+    assert _pyhost.flat_run(qs, idx, lay.byte_offsets[dt], total)
+    assert not _pyhost.flat_run(qs, idx, lay.byte_offsets[dt], total + 1)  # past the storage
     assert lay.arena_view(qs, dt) is not None and lay.arena_view(ps, dt) is None
     flat = torch.zeros(lay.totals[dt])
     t = [flat[0:12].view(4, 3).t(), flat[12:16], flat[16:24].view(2, 4), flat[24:26]]  # right place, transposed
-    assert not _pyhost.flat_run(t, idx, lay.byte_offsets[dt])
+    assert not _pyhost.flat_run(t, idx, lay.byte_offsets[dt], total)
     with pytest.raises(ValueError, match="differ in length"):
-        _pyhost.flat_run(qs, idx, lay.byte_offsets[dt][:-1])
+        _pyhost.flat_run(qs, idx, lay.byte_offsets[dt][:-1], total)
+    with pytest.raises(TypeError, match="expected a tensor"):
+        _pyhost.flat_run([1, 2, 3, 4], idx, lay.byte_offsets[dt], total)
 
 
 def test_clone_leaves_empty_hook_registries_untracked_until_used():
