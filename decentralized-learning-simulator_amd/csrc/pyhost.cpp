@@ -20,6 +20,8 @@
 //   clone_module(module, memo)     arena._clone_module_py: copy.deepcopy of
 //                                      models[0] with parameters from the memo
 //   checked_params(module, sig)    module_params + matches in one call
+//   fill_param_views(...)          the output module's Parameters as views of
+//                                      the reduced arena, into the clone's memo
 //   flat_run(params, idx, offs, n) the dtype group already is one flat arena
 //   wreduce_rows(...)              the data pointers of a task's parameter
 //                                      tensors straight into one
@@ -322,6 +324,111 @@ PyObject* py_flat_run(PyObject*, PyObject* args) {
   }
   Py_DECREF(os);
   return PyBool_FromLong(flat);
+}
+
+// ---- the output module's parameters: views of the reduced arena --------------
+//
+int memo_set(PyObject* memo, PyObject* v, PyObject* value);  // memo[id(v)] = value (below)
+//
+// A layout's view specs [(shape, strides, element offset), ...] as C++
+// values, cached by the identity of the list like signatures above.
+struct ViewSpecs {
+  std::vector<std::vector<int64_t>> shapes, strides;
+  std::vector<int64_t> offsets;
+};
+std::vector<std::pair<PyObject*, ViewSpecs>> g_specs;
+
+bool int_seq(PyObject* o, std::vector<int64_t>& out) {
+  PyObject* f = PySequence_Fast(o, "expected a sequence of ints");
+  if (!f) return false;
+  for (Py_ssize_t d = 0; d < PySequence_Fast_GET_SIZE(f); ++d)
+    out.push_back(PyLong_AsLongLong(PySequence_Fast_GET_ITEM(f, d)));
+  Py_DECREF(f);
+  return !PyErr_Occurred();
+}
+
+const ViewSpecs* specs_of(PyObject* specs) {
+  for (auto& e : g_specs)
+    if (e.first == specs) return &e.second;
+  PyObject* ss = PySequence_Fast(specs, "view specs must be a sequence");
+  if (!ss) return nullptr;
+  ViewSpecs v;
+  bool ok = true;
+  for (Py_ssize_t k = 0; ok && k < PySequence_Fast_GET_SIZE(ss); ++k) {
+    PyObject* e = PySequence_Fast_GET_ITEM(ss, k);
+    if (!PyTuple_Check(e) || PyTuple_GET_SIZE(e) != 3) {
+      PyErr_SetString(PyExc_TypeError, "view specs are (shape, strides, offset)");
+      ok = false;
+      break;
+    }
+    v.shapes.emplace_back();
+    v.strides.emplace_back();
+    ok = int_seq(PyTuple_GET_ITEM(e, 0), v.shapes.back()) && int_seq(PyTuple_GET_ITEM(e, 1), v.strides.back());
+    if (ok) {
+      v.offsets.push_back(PyLong_AsLongLong(PyTuple_GET_ITEM(e, 2)));
+      ok = !PyErr_Occurred();
+    }
+  }
+  Py_DECREF(ss);
+  if (!ok) return nullptr;
+  if (g_specs.size() == kSigCache) {
+    Py_DECREF(g_specs.front().first);
+    g_specs.erase(g_specs.begin());
+  }
+  Py_INCREF(specs);
+  g_specs.emplace_back(specs, std::move(v));
+  return &g_specs.back().second;
+}
+
+// fill_param_views(memo, arena, specs, params, idx): for each j, memo[id(p)]
+// = nn.Parameter(arena.as_strided(*specs[j]) + offset, p.requires_grad) with
+// p = params[idx[j]] -- what torch.Tensor._make_subclass(nn.Parameter, view,
+// requires_grad) builds (detach, metadata changes allowed, requires_grad set,
+// wrapped as the Parameter class), without a Python call per parameter.
+PyObject* py_fill_param_views(PyObject*, PyObject* args) {
+  PyObject *memo, *arena, *specs, *params, *idx;
+  if (!PyArg_ParseTuple(args, "O!OOOO", &PyDict_Type, &memo, &arena, &specs, &params, &idx)) return nullptr;
+  const at::Tensor* a = tensor_of(arena);
+  if (!a) return nullptr;
+  const ViewSpecs* v = specs_of(specs);
+  if (!v) return nullptr;
+  PyObject* row = PyTuple_Pack(1, params);
+  if (!row) return nullptr;
+  std::vector<const at::Tensor*> ps;
+  Py_ssize_t n, t;
+  const bool got = row_tensors(row, idx, ps, &n, &t);
+  if (!got) {
+    Py_DECREF(row);
+    return nullptr;
+  }
+  if (static_cast<size_t>(t) != v->offsets.size()) {
+    Py_DECREF(row);
+    PyErr_SetString(PyExc_ValueError, "idx and view specs differ in length");
+    return nullptr;
+  }
+  PyObject* rs = PySequence_Fast(params, "params must be a sequence");
+  PyObject* ks = rs ? PySequence_Fast(idx, "idx must be a sequence") : nullptr;
+  bool ok = ks != nullptr;
+  try {
+    const int64_t base = a->storage_offset();
+    for (Py_ssize_t j = 0; ok && j < t; ++j) {
+      at::Tensor data = a->as_strided(v->shapes[j], v->strides[j], base + v->offsets[j]).detach();
+      data.unsafeGetTensorImpl()->set_allow_tensor_metadata_change(true);
+      data.set_requires_grad(ps[j]->requires_grad());
+      PyObject* q = THPVariable_Wrap(data, reinterpret_cast<PyTypeObject*>(ParameterClass));
+      PyObject* p = q ? PySequence_Fast_GET_ITEM(rs, PyLong_AsSsize_t(PySequence_Fast_GET_ITEM(ks, j))) : nullptr;
+      ok = q && p && memo_set(memo, p, q) == 0;
+      Py_XDECREF(q);
+    }
+  } catch (const std::exception& e) {
+    PyErr_SetString(PyExc_RuntimeError, e.what());
+    ok = false;
+  }
+  Py_XDECREF(ks);
+  Py_XDECREF(rs);
+  Py_DECREF(row);
+  if (!ok) return nullptr;
+  Py_RETURN_NONE;
 }
 
 // ---- one device task's reduce: pointers collected and the library called ----
@@ -670,6 +777,8 @@ PyMethodDef kMethods[] = {
      "clone_init(plain_cache, plain_fn, atomic_types, setstate_keys, deepcopy, OrderedDict)"},
     {"clone_module", py_clone_module, METH_VARARGS, "clone_module(module, memo): arena._clone_module in C"},
     {"bind_wreduce_tensors", py_bind_wreduce_tensors, METH_O, "bind dlsim_wreduce_tensors by address"},
+    {"fill_param_views", py_fill_param_views, METH_VARARGS,
+     "fill_param_views(memo, arena, specs, params, idx): memo[id(p)] = Parameter view of the arena"},
     {"checked_params", py_checked_params, METH_VARARGS, "module_params(module) if it matches signature, else None"},
     {"flat_run", py_flat_run, METH_VARARGS, "flat_run(params, idx, byte_offsets, total): the group is one arena"},
     {"wreduce_rows", py_wreduce_rows, METH_VARARGS,

@@ -659,20 +659,23 @@ def module_from_arenas(model0: nn.Module, layout: ParamLayout,
     memo = {}
     params = layout.params
     for dt, idx in layout.groups.items():
-        a = arenas[dt]
-        base = a.storage_offset()
-        view = a.as_strided
-        for k, (shape, strides, off) in zip(idx, layout.view_specs[dt]):
-            p = params[k]
-            # nn.Parameter(view, requires_grad) for a plain tensor, without its
-            # Python __new__ frame
-            memo[id(p)] = _make_param(nn.Parameter, view(shape, strides, base + off), p.requires_grad)
+        # memo[id(p)] = nn.Parameter(view of the arena, p.requires_grad) for
+        # every p of the group, built in C++ (_param_views_py restates it)
+        _pyhost.fill_param_views(memo, arenas[dt], layout.view_specs[dt], params, idx)
     out = _clone_module(model0, memo)
     # The clone maps every parameter of model0 to its view one to one and keeps
     # the module/parameter order, so parameters() of `out` are those views.
     _register_arenas(out, _ArenaEntry(layout.rebind([]), dict(arenas),
                                       {dt: a.data_ptr() for dt, a in arenas.items()}))
     return out
+
+
+def _param_views_py(memo: dict, arena: torch.Tensor, specs, params, idx) -> None:
+    """Specification of csrc/pyhost.cpp fill_param_views (tests compare them)."""
+    base = arena.storage_offset()
+    for k, (shape, strides, off) in zip(idx, specs):
+        p = params[k]
+        memo[id(p)] = _make_param(nn.Parameter, arena.as_strided(shape, strides, base + off), p.requires_grad)
 
 
 def input_arenas(models: Sequence[nn.Module]):

@@ -509,3 +509,39 @@ def test_clone_leaves_empty_hook_registries_untracked_until_used():
     del out, h
     gc.collect()
     assert r() is None  # the cycle was found
+
+
+@pytest.mark.parametrize("offset", [0, 64])
+def test_param_views_match_make_subclass(offset):
+    """fill_param_views (C++) builds what torch.Tensor._make_subclass(
+    nn.Parameter, arena.as_strided(...), requires_grad) does: Parameters that
+    are views of the arena at the layout's offsets, with models[0]'s
+    requires_grad, sharing the arena's storage (also at a storage offset)."""
+    from dasklearn_amd import _pyhost
+
+    class M(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = nn.Linear(3, 4)
+            self.s = nn.Parameter(torch.tensor(2.0))  # 0-dim
+            self.e = nn.Parameter(torch.zeros(0, 3))  # empty
+            self.c = nn.Conv2d(2, 3, 3)
+
+    m = M()
+    m.a.bias.requires_grad_(False)
+    lay = arena.ParamLayout(m)
+    dt = torch.float32
+    buf = torch.arange(offset + lay.totals[dt], dtype=dt)
+    a = buf[offset:]
+    idx = lay.groups[dt]
+    got, exp = {}, {}
+    _pyhost.fill_param_views(got, a, lay.view_specs[dt], lay.params, idx)
+    arena._param_views_py(exp, a, lay.view_specs[dt], lay.params, idx)
+    assert got.keys() == exp.keys() == {id(lay.params[k]) for k in idx}
+    for key in exp:
+        g, e = got[key], exp[key]
+        assert type(g) is nn.Parameter and g.requires_grad == e.requires_grad
+        assert g.shape == e.shape and g.stride() == e.stride() and g.data_ptr() == e.data_ptr()
+        assert torch.equal(g, e) and g.untyped_storage().data_ptr() == buf.untyped_storage().data_ptr()
+    a.add_(1)  # the views see the arena
+    assert all(torch.equal(got[k], exp[k]) for k in exp)
