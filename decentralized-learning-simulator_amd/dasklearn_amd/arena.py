@@ -175,6 +175,16 @@ def layout_of(module: nn.Module, params: Optional[List[nn.Parameter]] = None) ->
     return layout
 
 
+_ELEM_SIZE: Dict[torch.dtype, int] = {}
+
+
+def _elem_size(dt: torch.dtype) -> int:
+    esz = _ELEM_SIZE.get(dt)
+    if esz is None:
+        esz = _ELEM_SIZE[dt] = torch.empty((), dtype=dt).element_size()
+    return esz
+
+
 def row_stride(numel: int, elem_bytes: int) -> int:
     """Elements between consecutive model rows of a staging arena: `numel`
     rounded up to 256 B (every row 16-byte aligned for the vector kernel),
@@ -208,13 +218,18 @@ class _Staging:
     def __init__(self):
         self.dev: Dict[Tuple, torch.Tensor] = {}
         self.host: Dict[Tuple, torch.Tensor] = {}
-        self.last_use: Dict[Tuple, torch.cuda.Event] = {}
+        self.last_use: Dict[Tuple, torch.cuda.Event] = {}  # pending: the last user's work
+        self._events: Dict[Tuple, torch.cuda.Event] = {}    # one reusable event per key
+        self._views: Dict[Tuple, Tuple] = {}                # last (n, numel, bufs, rows, host) per key
         self._locks: Dict[Tuple, threading.Lock] = {}
         self._locks_guard = threading.Lock()
 
     @staticmethod
     def _key(device, dt):
-        return (str(device), dt)
+        if isinstance(device, torch.device):
+            return (device.type, device.index, dt)
+        d = torch.device(device)
+        return (d.type, d.index, dt)
 
     def _lock(self, key) -> threading.Lock:
         with self._locks_guard:
@@ -239,30 +254,39 @@ class _Staging:
             ev = self.last_use.pop(key, None)
             if ev is not None:
                 ev.synchronize()
-            stride = row_stride(numel, torch.empty((), dtype=dt).element_size())
+            stride = row_stride(numel, _elem_size(dt))
             need = max(1, n * stride)
             flat = self._grow(self.dev, key, need, lambda k: torch.empty(k, dtype=dt, device=device))
+            hflat = self._grow(self.host, key, need, lambda k: torch.empty(k, dtype=dt, pin_memory=True)) \
+                if pinned else None
+            last = self._views.get(key)
+            if last is not None and last[0] == n and last[1] == numel and last[2] is flat and last[3] is hflat:
+                return last[4], last[5]  # the same rows as the previous call
             rows = flat[:n * stride].view(n, stride)[:, :numel]
-            host = None
-            if pinned:
-                hflat = self._grow(self.host, key, need, lambda k: torch.empty(k, dtype=dt, pin_memory=True))
-                host = hflat[:n * stride].view(n, stride)[:, :numel]
+            host = hflat[:n * stride].view(n, stride)[:, :numel] if pinned else None
+            self._views[key] = (n, numel, flat, hflat, rows, host)
             return rows, host
         except BaseException:
             self._lock(key).release()
             raise
 
-    def release(self, device, dt, stream):
+    def release(self, device, dt, stream, synced: bool = False):
+        """synced: the caller has synchronised `stream` after its last use of
+        the rows, so the next user need not wait (no event)."""
         key = self._key(device, dt)
-        ev = torch.cuda.Event()
-        ev.record(stream)
-        self.last_use[key] = ev
+        if not synced:
+            ev = self._events.get(key)
+            if ev is None:
+                ev = self._events[key] = torch.cuda.Event()
+            ev.record(stream)  # re-recording moves the event to this call's work
+            self.last_use[key] = ev
         self._lock(key).release()
 
     def clear(self):
         for ev in self.last_use.values():
             ev.synchronize()
         self.last_use.clear()
+        self._views.clear()
         self.dev.clear()
         self.host.clear()
 
@@ -359,12 +383,18 @@ def _host_pipeline(all_params, idx, layout, dt, dev, out, weights_f32, mode, str
     # the library reads data pointers, so only non-contiguous ones are copied
     keep, ptrs = _data_ptrs(all_params, idx)
     dev_rows, pinned = STAGING.acquire(dev, dt, n, total, stream)
+    synced = False
     try:
         _native.host_wreduce_raw(ptrs, n, layout.split_sizes[dt], weights_f32, pinned, dev_rows, out, host,
                                  _native.dtype_code(dt), mode, chunk, torch.get_num_threads(), stream.cuda_stream,
                                  h2d, d2h)
+        if want_host:
+            # the host result is complete once `stream` is, and the caller
+            # waits for it anyway: wait here, and hand the rows back free
+            stream.synchronize()
+            synced = True
     finally:
-        STAGING.release(dev, dt, stream)
+        STAGING.release(dev, dt, stream, synced)
     return host
 
 

@@ -87,6 +87,35 @@ def main():
              "module_from_arenas": med(lambda: arena.module_from_arenas(models[0], layout, arenas)),
              "layout_of": med(lambda: arena.layout_of(models[0]))}
         print(json.dumps(r), flush=True)
+
+        # host models (the reference worker's case): the same task with every
+        # model on the host and the result back on the host
+        hmodels = [copy.deepcopy(m).cpu() for m in models]
+        hparams = {"models": hmodels, "round": 1, "peer": 0}
+        hlayout, hall, _ = arena.input_arenas(hmodels)
+        hidx = hlayout.groups[dt]
+        total = hlayout.totals[dt]
+
+        def pipeline():
+            arena._host_pipeline(hall, hidx, hlayout, dt, dev, out, w32, _native.DLSIM_EXACT, stream, True)
+
+        def stage_cycle():
+            arena.STAGING.acquire(dev, dt, 7, total, stream)
+            arena.STAGING.release(dev, dt, stream)
+
+        host_arena = {dt: torch.empty(total)}
+        h = {"model": kind + "_host",
+             "task_total_sync": med(lambda: functions.aggregate(Settings(), hparams), sync=True),
+             "input_arenas": med(lambda: arena.input_arenas(hmodels)),
+             "host_pipeline_plus_sync": med(pipeline, sync=True),
+             "staging_acquire_release": med(stage_cycle),
+             "host_result_alloc_pageable": med(lambda: torch.empty(total)),
+             "module_from_arenas": med(lambda: arena.module_from_arenas(hmodels[0], hlayout, host_arena))}
+        st = {}
+        for _ in range(200):
+            arena.aggregate_modules(hmodels, None, _native.DLSIM_EXACT, timing=st)
+        h["stages_us_mean"] = {k: round(v / 200 * 1e6, 1) for k, v in st.items()}
+        print(json.dumps(h), flush=True)
     gc.enable()
 
 
