@@ -95,9 +95,26 @@ hipError_t launch_shape(const S& s, int n, void* out, size_t nelem, hipStream_t 
   return hipGetLastError();
 }
 
+// Launch shape of the grouped (runtime fan-in, n > max_fixed_fan_in) kernel
+// by the same size classes (sweep: profiles/r02_tune_grouped/, n = 17 and 100
+// at 11.2 M and at the 8-rank slice, 1.4 M):
+//   4/8-byte  < 8 MB per stream : VPT 1, wave map,  sc1 (0.837 against 0.791
+//                                 at n = 100, 0.646 against 0.595 at n = 17)
+//   4/8-byte  larger            : VPT 4, block map, sc1 (0.801 against 0.791
+//                                 at n = 100 -- the memory-only probe's 0.802)
+//   2-byte                      : VPT 4, nt stores, block map (not re-swept)
+template <class Op, int C> constexpr Shape grouped_shape() {
+  if constexpr (Op::kBytes >= 4) {
+    if constexpr (C == 0) return Shape{1, kStore, true};
+    else return Shape{4, kStore, false};
+  } else {
+    return Shape{kVpt, store_policy<Op>(), wave_map<Op>()};
+  }
+}
+
 template <class Op, class S, int NF, int C>
 hipError_t launch_class(const S& s, int n, void* out, size_t nelem, hipStream_t st) {
-  constexpr Shape k = fixed_shape<Op, C>();
+  constexpr Shape k = NF > 0 ? fixed_shape<Op, C>() : grouped_shape<Op, C>();
   return launch_shape<Op, S, NF, k.vpt, k.store, k.wave>(s, n, out, nelem, st);
 }
 
@@ -109,8 +126,11 @@ hipError_t launch_tiles(const S& s, int n, void* out, size_t nelem, hipStream_t 
       case 1: return launch_class<Op, S, NF, 1>(s, n, out, nelem, st);
       default: return launch_class<Op, S, NF, 2>(s, n, out, nelem, st);
     }
+  } else if constexpr (Op::kBytes >= 4) {
+    return size_class<Op>(nelem) == 0 ? launch_class<Op, S, 0, 0>(s, n, out, nelem, st)
+                                      : launch_class<Op, S, 0, 2>(s, n, out, nelem, st);
   } else {
-    return launch_shape<Op, S, 0, kVpt, store_policy<Op>(), wave_map<Op>()>(s, n, out, nelem, st);
+    return launch_class<Op, S, 0, 2>(s, n, out, nelem, st);
   }
 }
 

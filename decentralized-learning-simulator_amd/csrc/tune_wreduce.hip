@@ -352,6 +352,15 @@ std::vector<Variant> variants(int n) {
       {"T_G8_V4", launch_t<Op, 0, 8, 4, true>, 0},
       {"T_G8_V4_sc1", launch_ts<Op, 0, 8, 4, 1, 16>, 0},
       {"T_G8_V4_sc1_wave", launch_ts<Op, 0, 8, 4, 1, 16, true>, 0},
+      // grouped (runtime fan-in) shapes beyond the shipped VPT 4 (round 2)
+      {"T_G8_V2_sc1_blk", launch_ts<Op, 0, 8, 2, 1, 16, false>, 0},
+      {"T_G8_V2_sc1_wave", launch_ts<Op, 0, 8, 2, 1, 16, true>, 0},
+      {"T_G8_V1_sc1_wave", launch_ts<Op, 0, 8, 1, 1, 16, true>, 0},
+      {"T_G4_V4_sc1_wave", launch_ts<Op, 0, 4, 4, 1, 16, true>, 0},
+      {"T_G4_V2_sc1_wave", launch_ts<Op, 0, 4, 2, 1, 16, true>, 0},
+      {"T_G16_V2_sc1_wave", launch_ts<Op, 0, 16, 2, 1, 16, true>, 0},
+      {"T_G16_V1_sc1_wave", launch_ts<Op, 0, 16, 1, 1, 16, true>, 0},
+      {"T_G8_V4_nt_wave", launch_ts<Op, 0, 8, 4, 1, kStNT, true>, 0},
       {"T_xorprobe", launch_probe<Op, 0>, 0},
   };
   add_nf<Op, 2>(vs, n);

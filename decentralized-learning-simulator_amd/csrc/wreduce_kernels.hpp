@@ -743,7 +743,12 @@ struct XorProbe {
   static constexpr int kFmt = BYTES == 4 ? kFmtF32 : kFmtBF16;
   __device__ static float init(float) { return 0.0f; }
   __device__ static float step(float acc, float, float x) {
-    return __uint_as_float(__float_as_uint(acc) ^ __float_as_uint(x));
+    float r = __uint_as_float(__float_as_uint(acc) ^ __float_as_uint(x));
+    // XOR is associative: without this pin the compiler may re-associate the
+    // chain and schedule the loads unlike the reduce's strictly ordered fold
+    // (seen as a probe slower than the reduce for the grouped VPT 1 shape)
+    asm volatile("" : "+v"(r));
+    return r;
   }
   __device__ static void step2(float& a0, float& a1, float w, float x0, float x1) {
     a0 = step(a0, w, x0);

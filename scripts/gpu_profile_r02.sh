@@ -3,7 +3,7 @@
 # driver's multi-GPU run), plus cfg3/cfg4/cfg5: a kernel trace with --stats,
 # then FETCH_SIZE and WRITE_SIZE in separate --pmc passes (no trace domains),
 # summarised per config by scripts/pmc_summary.py (gfx950 FETCH_SIZE x2).
-# usage: bash scripts/gpu_profile_r02.sh <outdir>
+# usage: bash scripts/gpu_profile_r02.sh <outdir> ["name:config:slice ..."]
 set -u
 export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -28,6 +28,13 @@ print((n + 1) * (e - b) * bench.ELEM_BYTES[dt])")
   python3 scripts/pmc_summary.py --trace $O/trace_$NAME --fetch $O/fetch_$NAME --write $O/write_$NAME \
     --config $KEY --mode exact --bytes-per-launch $BYTES --out $O/r02_pmc_traffic.json > /dev/null || return 1
 }
-run ns north_star 1 && run ns_s2 north_star 2 && run ns_s4 north_star 4 && run ns_s8 north_star 8 \
-  && run cfg4 cfg4 1 && run cfg5 cfg5 1 && run cfg3 cfg3 1 || exit 1
+if [ $# -ge 2 ]; then  # a chosen list: "name:config:slice ..."
+  for spec in $2; do
+    IFS=: read -r NAME C S <<< "$spec"
+    run $NAME $C $S || exit 1
+  done
+else
+  run ns north_star 1 && run ns_s2 north_star 2 && run ns_s4 north_star 4 && run ns_s8 north_star 8 \
+    && run cfg4 cfg4 1 && run cfg5 cfg5 1 && run cfg3 cfg3 1 || exit 1
+fi
 step done

@@ -272,6 +272,30 @@ def test_launch_shapes_either_side_of_the_size_switch(dtype, p, n):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("dtype,p", [("f32", 1_999_999), ("f32", 2_000_003), ("f32", 4_999_997),
+                                     ("f64", 999_999), ("f64", 1_000_003)])
+@pytest.mark.parametrize("n", [17, 130])
+def test_grouped_launch_shapes_either_side_of_the_size_switch(dtype, p, n):
+    """The grouped (runtime fan-in) kernel changes shape at 8 MB per stream
+    (dispatch.hpp grouped_shape: VPT 1 wave map below, VPT 4 block map
+    above), with its pointers as kernel arguments (n = 17) or in the device
+    table (n = 130): bit-exact against the oracle over every element."""
+    g = torch.Generator(device=dev()).manual_seed(p + n)
+    tdt = torch.float64 if dtype == "f64" else torch.float32
+    xs = [(torch.randn(p, generator=g, device=dev(), dtype=tdt) * 0.05) for _ in range(n)]
+    ws = list(np.random.default_rng(n).dirichlet(np.ones(n)))
+    out = torch.empty_like(xs[0])
+    if dtype == "f64":
+        w = orc.reference_weights_f64(n, ws)
+        _native.wreduce(xs, w, out)
+    else:
+        w = orc.reference_weights(n, ws)
+        _native.wreduce(xs, w, out)
+    assert orc.same_bits(from_dev(out), orc.wreduce([from_dev(x) for x in xs], w, dtype))
+    del xs, out
+    torch.cuda.empty_cache()
+
+
 def test_one_hot_weights_select_input_at_full_size():
     """Linearity/selection property at the north-star size: weights e_k return
     model k exactly (x0*0 + ... + 1*xk + ... sums exact zeros)."""
