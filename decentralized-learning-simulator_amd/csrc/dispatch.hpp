@@ -96,20 +96,20 @@ hipError_t launch_shape(const S& s, int n, void* out, size_t nelem, hipStream_t 
 }
 
 // Launch shape of the grouped (runtime fan-in, n > max_fixed_fan_in) kernel
-// by the same size classes (sweep: profiles/r02_tune_grouped/, n = 17 and 100
-// at 11.2 M and at the 8-rank slice, 1.4 M):
+// by the same size classes (sweeps: profiles/r02_tune_grouped/, fp32 n = 17
+// and 100 at 11.2 M and at the 8-rank slice, 1.4 M; bf16 n = 17 and 12):
 //   4/8-byte  < 8 MB per stream : VPT 1, wave map,  sc1 (0.837 against 0.791
 //                                 at n = 100, 0.646 against 0.595 at n = 17)
 //   4/8-byte  larger            : VPT 4, block map, sc1 (0.801 against 0.791
 //                                 at n = 100 -- the memory-only probe's 0.802)
-//   2-byte                      : VPT 4, nt stores, block map (not re-swept)
+//   2-byte    < 96 MB per stream: VPT 1, wave map,  sc1 (bf16 n = 17: 0.724
+//                                 against 0.691 at 11.2 M, 0.400 against 0.309
+//                                 at 1.4 M)
+//   2-byte    larger            : VPT 4, block map, nt (0.771 at n = 12, 62.5 M)
 template <class Op, int C> constexpr Shape grouped_shape() {
-  if constexpr (Op::kBytes >= 4) {
-    if constexpr (C == 0) return Shape{1, kStore, true};
-    else return Shape{4, kStore, false};
-  } else {
-    return Shape{kVpt, store_policy<Op>(), wave_map<Op>()};
-  }
+  if constexpr (C == 0) return Shape{1, kStore, true};
+  else if constexpr (Op::kBytes >= 4) return Shape{4, kStore, false};
+  else return Shape{4, dlsim::kStNT, false};
 }
 
 template <class Op, class S, int NF, int C>
@@ -126,11 +126,9 @@ hipError_t launch_tiles(const S& s, int n, void* out, size_t nelem, hipStream_t 
       case 1: return launch_class<Op, S, NF, 1>(s, n, out, nelem, st);
       default: return launch_class<Op, S, NF, 2>(s, n, out, nelem, st);
     }
-  } else if constexpr (Op::kBytes >= 4) {
+  } else {
     return size_class<Op>(nelem) == 0 ? launch_class<Op, S, 0, 0>(s, n, out, nelem, st)
                                       : launch_class<Op, S, 0, 2>(s, n, out, nelem, st);
-  } else {
-    return launch_class<Op, S, 0, 2>(s, n, out, nelem, st);
   }
 }
 

@@ -361,6 +361,12 @@ std::vector<Variant> variants(int n) {
       {"T_G16_V2_sc1_wave", launch_ts<Op, 0, 16, 2, 1, 16, true>, 0},
       {"T_G16_V1_sc1_wave", launch_ts<Op, 0, 16, 1, 1, 16, true>, 0},
       {"T_G8_V4_nt_wave", launch_ts<Op, 0, 8, 4, 1, kStNT, true>, 0},
+      // 2-byte elements group 4 inputs; the shipped grouped shape is G4 V4 nt block
+      {"T_G4_V4_nt_blk", launch_ts<Op, 0, 4, 4, 1, kStNT, false>, 0},
+      {"T_G4_V2_nt_blk", launch_ts<Op, 0, 4, 2, 1, kStNT, false>, 0},
+      {"T_G4_V1_sc1_wave", launch_ts<Op, 0, 4, 1, 1, 16, true>, 0},
+      {"T_G4_V1_nt_wave", launch_ts<Op, 0, 4, 1, 1, kStNT, true>, 0},
+      {"T_G4_V2_sc1_blk", launch_ts<Op, 0, 4, 2, 1, 16, false>, 0},
       {"T_xorprobe", launch_probe<Op, 0>, 0},
   };
   add_nf<Op, 2>(vs, n);

@@ -273,7 +273,8 @@ def test_launch_shapes_either_side_of_the_size_switch(dtype, p, n):
 
 
 @pytest.mark.parametrize("dtype,p", [("f32", 1_999_999), ("f32", 2_000_003), ("f32", 4_999_997),
-                                     ("f64", 999_999), ("f64", 1_000_003)])
+                                     ("f64", 999_999), ("f64", 1_000_003),
+                                     ("bf16", 47_999_993), ("bf16", 48_000_007)])
 @pytest.mark.parametrize("n", [17, 130])
 def test_grouped_launch_shapes_either_side_of_the_size_switch(dtype, p, n):
     """The grouped (runtime fan-in) kernel changes shape at 8 MB per stream
@@ -283,6 +284,8 @@ def test_grouped_launch_shapes_either_side_of_the_size_switch(dtype, p, n):
     g = torch.Generator(device=dev()).manual_seed(p + n)
     tdt = torch.float64 if dtype == "f64" else torch.float32
     xs = [(torch.randn(p, generator=g, device=dev(), dtype=tdt) * 0.05) for _ in range(n)]
+    if dtype == "bf16":
+        xs = [x.to(torch.bfloat16) for x in xs]
     ws = list(np.random.default_rng(n).dirichlet(np.ones(n)))
     out = torch.empty_like(xs[0])
     if dtype == "f64":
@@ -291,7 +294,11 @@ def test_grouped_launch_shapes_either_side_of_the_size_switch(dtype, p, n):
     else:
         w = orc.reference_weights(n, ws)
         _native.wreduce(xs, w, out)
-    assert orc.same_bits(from_dev(out), orc.wreduce([from_dev(x) for x in xs], w, dtype))
+    if dtype == "bf16":  # elements are independent: a strided sample and the ragged end
+        idx = torch.cat([torch.arange(0, p, 997, device=dev()), torch.arange(p - 1000, p, device=dev())])
+        assert orc.same_bits(from_dev(out[idx]), orc.wreduce([from_dev(x[idx]) for x in xs], w, dtype))
+    else:
+        assert orc.same_bits(from_dev(out), orc.wreduce([from_dev(x) for x in xs], w, dtype))
     del xs, out
     torch.cuda.empty_cache()
 
