@@ -32,6 +32,17 @@ int hip_fail(hipError_t e, const char* what);
 // are used only while they fit in 256 VGPRs (two waves per SIMD): past that
 // the measured rate drops by up to 20% (profiles/r01_sweep_fanin_*.jsonl).
 constexpr int kVpt = 4;
+// Vectors per lane of the batched kernels (kernel-argument and table batches),
+// by the largest task of the launch: VPT 1 when every task is under 1 MB per
+// stream (100 GNLeNet tasks per launch: 0.787 against 0.759 at VPT 4), else
+// VPT 4 (8 tasks of 1 M fp32: 0.797 against 0.778) (profiles/r02_batch_vpt/).
+constexpr size_t kBatchSmallBytes = size_t{1} << 20;
+template <class Op>
+int batch_vpt(const size_t* nelem, int t0, int t1) {
+  size_t mx = 0;
+  for (int t = t0; t < t1; ++t) mx = nelem[t] > mx ? nelem[t] : mx;
+  return mx * Op::kBytes < kBatchSmallBytes ? 1 : 4;
+}
 constexpr bool kNT = true;
 // Output stores are buffer_store_dwordx4 with sc1 (write-through): no dirty
 // output lines are left in L2 for the kernel-boundary writeback, which was
@@ -271,20 +282,20 @@ inline bool cross_task_overlap(int nt, const int* fan_in, const void* const* in,
 }
 
 // ---- batched launches ---------------------------------------------------------
-template <class Op, int NF>
+template <class Op, int NF, int VPT>
 hipError_t launch_batch_nf(const dlsim::BatchSlots& s, unsigned blocks, hipStream_t st) {
-  hipLaunchKernelGGL((dlsim::k_wreduce_batch<Op, NF, group_size<Op>(), kVpt, kNT, store_policy<Op>()>), dim3(blocks),
+  hipLaunchKernelGGL((dlsim::k_wreduce_batch<Op, NF, group_size<Op>(), VPT, kNT, store_policy<Op>()>), dim3(blocks),
                      dim3(dlsim::kBlock), 0, st, s);
   return hipGetLastError();
 }
 
-template <class Op, int K>
+template <class Op, int K, int VPT>
 hipError_t launch_batch_fixed(const dlsim::BatchSlots& s, int n, unsigned blocks, hipStream_t st) {
   if constexpr (K > max_fixed_fan_in<Op>()) {
-    return launch_batch_nf<Op, 0>(s, blocks, st);
+    return launch_batch_nf<Op, 0, VPT>(s, blocks, st);
   } else {
-    if (n == K) return launch_batch_nf<Op, K>(s, blocks, st);
-    return launch_batch_fixed<Op, K + 1>(s, n, blocks, st);
+    if (n == K) return launch_batch_nf<Op, K, VPT>(s, blocks, st);
+    return launch_batch_fixed<Op, K + 1, VPT>(s, n, blocks, st);
   }
 }
 
@@ -296,7 +307,8 @@ hipError_t launch_batch(const int* fan_in, const size_t* in_off, const void* con
                         hipStream_t st) {
   dlsim::BatchSlots s;
   std::memset(&s, 0, sizeof(s));
-  const size_t tile = static_cast<size_t>(dlsim::kBlock) * kVpt;
+  const int vpt = batch_vpt<Op>(nelem, t0, t1);
+  const size_t tile = static_cast<size_t>(dlsim::kBlock) * vpt;
   uint32_t blocks = 0;
   int ptrs = 0;
   bool uniform = true;
@@ -320,8 +332,12 @@ hipError_t launch_batch(const int* fan_in, const size_t* in_off, const void* con
   }
   s.ntasks = t1 - t0;
   s.block_start[t1 - t0] = blocks;
-  if (uniform) return launch_batch_fixed<Op, 1>(s, fan_in[t0], blocks, st);
-  return launch_batch_nf<Op, 0>(s, blocks, st);
+  if (vpt == 1) {
+    if (uniform) return launch_batch_fixed<Op, 1, 1>(s, fan_in[t0], blocks, st);
+    return launch_batch_nf<Op, 0, 1>(s, blocks, st);
+  }
+  if (uniform) return launch_batch_fixed<Op, 1, 4>(s, fan_in[t0], blocks, st);
+  return launch_batch_nf<Op, 0, 4>(s, blocks, st);
 }
 
 template <class Op>
@@ -338,7 +354,6 @@ int run_batched(int b, const int* fan_in, const void* const* in, const float* w,
     }
     return DLSIM_OK;
   }
-  const size_t tile = static_cast<size_t>(dlsim::kBlock) * kVpt;
   auto batchable = [&](int t) {
     if (nelem[t] == 0 || fan_in[t] > 16) return false;
     if (nelem[t] * Op::kBytes > kMaxLaunchOutBytes) return false;
@@ -377,14 +392,15 @@ int run_batched(int b, const int* fan_in, const void* const* in, const float* w,
     dv.push_back(divs ? divs[t] : 1.0f);
   }
   const int g = static_cast<int>(group.size());
+  const size_t tile1 = dlsim::kBlock;  // the most blocks a task can need (VPT 1)
   int t0 = 0;
   while (t0 < g) {
     int t1 = t0, ptrs = 0;
     uint64_t blocks = 0;
     while (t1 < g && t1 - t0 < dlsim::kBatchMaxTasks && ptrs + fi[t1] <= dlsim::kBatchMaxPtrs &&
-           blocks + ne[t1] / Op::E / tile + 1 < 0x7fffffffull) {
+           blocks + ne[t1] / Op::E / tile1 + 1 < 0x7fffffffull) {
       ptrs += fi[t1];
-      blocks += ne[t1] / Op::E / tile + 1;
+      blocks += ne[t1] / Op::E / tile1 + 1;
       ++t1;
     }
     hipError_t e = launch_batch<Op>(fi.data(), ioff.data(), ins.data(), ws.data(), dv.data(), os.data(),
@@ -399,21 +415,23 @@ int run_batched(int b, const int* fan_in, const void* const* in, const float* w,
 struct TableLayout {
   size_t tasks_off, map_off, ptrs_off, w_off, bytes;
   uint32_t nblocks;
+  int vpt;  // batch_vpt of the tasks, kept in the header
 };
 
 inline size_t round8(size_t x) { return (x + 7) / 8 * 8; }
 
 template <class Op>
-uint32_t task_blocks(size_t nelem) {
-  const size_t tile = static_cast<size_t>(dlsim::kBlock) * kVpt;
+uint32_t task_blocks(size_t nelem, int vpt) {
+  const size_t tile = static_cast<size_t>(dlsim::kBlock) * vpt;
   return static_cast<uint32_t>(nelem / Op::E / tile + 1);
 }
 
 template <class Op>
 bool table_layout(int b, const int* fan_in, const size_t* nelem, TableLayout* L) {
   uint64_t blocks = 0, ptrs = 0;
+  L->vpt = batch_vpt<Op>(nelem, 0, b);
   for (int t = 0; t < b; ++t) {
-    blocks += task_blocks<Op>(nelem[t]);
+    blocks += task_blocks<Op>(nelem[t], L->vpt);
     ptrs += static_cast<uint64_t>(fan_in[t]);
   }
   if (blocks >= 0x7fffffffull) return false;
@@ -445,6 +463,7 @@ int table_fill(int b, const int* fan_in, const void* const* in, const float* w, 
   auto* ws = reinterpret_cast<float*>(base + L.w_off);
   h->ntasks = static_cast<uint32_t>(b);
   h->nblocks = L.nblocks;
+  h->vpt = static_cast<uint32_t>(L.vpt);
   h->tasks_off = L.tasks_off;
   h->map_off = L.map_off;
   h->ptrs_off = L.ptrs_off;
@@ -456,7 +475,7 @@ int table_fill(int b, const int* fan_in, const void* const* in, const float* w, 
     if (fan_in[t] > DLSIM_MAX_FUSED_INPUTS || total > kMaxLaunchOutBytes || !aligned16(outs[t]))
       return fail(DLSIM_E_ARG, "task %d cannot be table-batched (fan-in <= %d, 16-B aligned, < 2 GiB)", t,
                   DLSIM_MAX_FUSED_INPUTS);
-    const uint32_t nb = task_blocks<Op>(nelem[t]);
+    const uint32_t nb = task_blocks<Op>(nelem[t], L.vpt);
     tasks[t].out = outs[t];
     tasks[t].nvec = nelem[t] / Op::E;
     tasks[t].nelem = nelem[t];
@@ -478,20 +497,20 @@ int table_fill(int b, const int* fan_in, const void* const* in, const float* w, 
   return DLSIM_OK;
 }
 
-template <class Op, int NF>
+template <class Op, int NF, int VPT>
 hipError_t launch_table_nf(const void* d_table, uint32_t blocks, hipStream_t st) {
-  hipLaunchKernelGGL((dlsim::k_wreduce_batch_table<Op, NF, group_size<Op>(), kVpt, kNT, store_policy<Op>()>),
+  hipLaunchKernelGGL((dlsim::k_wreduce_batch_table<Op, NF, group_size<Op>(), VPT, kNT, store_policy<Op>()>),
                      dim3(blocks), dim3(dlsim::kBlock), 0, st, static_cast<const unsigned char*>(d_table));
   return hipGetLastError();
 }
 
-template <class Op, int K>
+template <class Op, int K, int VPT>
 hipError_t launch_table_fixed(const void* d_table, int n, uint32_t blocks, hipStream_t st) {
   if constexpr (K > max_fixed_fan_in<Op>()) {
-    return launch_table_nf<Op, 0>(d_table, blocks, st);
+    return launch_table_nf<Op, 0, VPT>(d_table, blocks, st);
   } else {
-    if (n == K) return launch_table_nf<Op, K>(d_table, blocks, st);
-    return launch_table_fixed<Op, K + 1>(d_table, n, blocks, st);
+    if (n == K) return launch_table_nf<Op, K, VPT>(d_table, blocks, st);
+    return launch_table_fixed<Op, K + 1, VPT>(d_table, n, blocks, st);
   }
 }
 
@@ -499,9 +518,14 @@ template <class Op>
 int table_launch(const void* h_table, const void* d_table, hipStream_t st) {
   const auto* h = static_cast<const dlsim::BatchTableHeader*>(h_table);
   if (h->ntasks == 0) return DLSIM_OK;
-  hipError_t e = h->uniform_fan_in ? launch_table_fixed<Op, 1>(d_table, static_cast<int>(h->uniform_fan_in),
-                                                               h->nblocks, st)
-                                   : launch_table_nf<Op, 0>(d_table, h->nblocks, st);
+  if (h->vpt != 1 && h->vpt != 4)
+    return fail(DLSIM_E_ARG, "not a table written by dlsim_batch_table_fill (vectors per lane %u)", h->vpt);
+  const int n = static_cast<int>(h->uniform_fan_in);
+  hipError_t e;
+  if (h->vpt == 1)
+    e = n ? launch_table_fixed<Op, 1, 1>(d_table, n, h->nblocks, st) : launch_table_nf<Op, 0, 1>(d_table, h->nblocks, st);
+  else
+    e = n ? launch_table_fixed<Op, 1, 4>(d_table, n, h->nblocks, st) : launch_table_nf<Op, 0, 4>(d_table, h->nblocks, st);
   if (e != hipSuccess) return hip_fail(e, "table batch launch");
   return DLSIM_OK;
 }

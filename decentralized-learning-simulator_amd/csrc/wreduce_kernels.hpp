@@ -681,7 +681,7 @@ struct BatchTableHeader {
   uint32_t ntasks;
   uint32_t nblocks;
   uint32_t uniform_fan_in;  // fan-in shared by every task, or 0
-  uint32_t reserved;
+  uint32_t vpt;             // vectors per lane the block map was laid out for (1 or 4)
   uint64_t tasks_off;       // byte offsets from the table base
   uint64_t map_off;
   uint64_t ptrs_off;

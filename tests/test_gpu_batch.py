@@ -63,6 +63,26 @@ def test_mixed_fan_in_and_sizes(dtype):
     check(tasks, dtype)
 
 
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("sizes", [[262_143, 1000, 77], [262_144 * 2 // 2 + 1, 1000, 77], [600_001, 3]])
+def test_batch_vectors_per_lane_either_side_of_1_mb(dtype, sizes):
+    """A batch launch lays its tiles out for VPT 1 when every task is under
+    1 MB per stream, else VPT 4 (dispatch.hpp batch_vpt): both layouts, in
+    the kernel-argument batch and the descriptor table, bit-exact."""
+    esz = 2 if dtype == "bf16" else 4
+    sizes = [p * 4 // esz if p > 100_000 else p for p in sizes]  # the same byte sizes in bf16
+    rng = np.random.default_rng(sum(sizes))
+    tasks = [make_task(rng, 4, p, dtype) for p in sizes]
+    check(tasks, dtype)
+    for t in tasks:
+        t[3].zero_()
+    _native.BatchPlan([(t[0], t[2], t[3]) for t in tasks]).launch()
+    for ins, host, w, out in tasks:
+        got = out.cpu()
+        got = got.view(torch.int16).numpy().view(np.uint16) if dtype == "bf16" else got.numpy()
+        assert orc.same_bits(got, orc.wreduce(host, w, dtype))
+
+
 def test_batch_split_by_limits_and_solo_tasks():
     rng = np.random.default_rng(3)
     tasks = [make_task(rng, 8, 1000 + 37 * k, "f32") for k in range(40)]  # > 32 tasks, 320 ptrs
