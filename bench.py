@@ -262,6 +262,32 @@ def pattern_ceiling(wl, k_steps: int, sync, new_event, achieved_gbps: float):
             "kernel": "dlsim_probe_pattern: same dispatch and shapes, XOR fold (memory only)"}
 
 
+def launch_floor(n, dtype, w32, mode, dev, k_steps: int, sync, new_event, step_us: float, bytes_per_step: int):
+    """Per-launch floor of back-to-back launches on one stream: the same
+    entry point and fan-in with one 256-element tile per input, timed like the
+    steps. What remains of a step after this floor is the time the bytes
+    take; at the 8-rank slices the floor is a large part of the step
+    (MI355X_MICROARCH.md, price table row 'boundary': 1.7-1.9 us between
+    streaming kernels). Diagnostic only: `value` is the full step time."""
+    from dasklearn_amd import _native
+    tdt = TORCH_DTYPE[dtype]
+    x = torch.randn((n, 256), device=dev).to(tdt)
+    out = torch.empty(256, dtype=tdt, device=dev)
+    plan = _native.ReducePlan([x[i] for i in range(n)], w32, out, mode)
+    stream = torch.cuda.current_stream(dev)
+    for _ in range(10):
+        plan.launch(stream)
+    ev_ms, _ = time_steps(lambda k: plan.launch(stream), k_steps, sync, lambda: None, new_event)
+    floor_us = ev_ms * 1e3 / k_steps
+    body_us = step_us - floor_us
+    res = {"us_per_launch": round(floor_us, 3),
+           "note": f"{k_steps} back-to-back launches of the same entry point, n={n}, 256 elements per input; "
+                   "step time minus this floor = the time the step's bytes take"}
+    if body_us > 0:
+        res["bytes_frac_of_peak_excl_floor"] = round(bytes_per_step / (body_us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4)
+    return res
+
+
 def pmc_traffic(config: str, mode: str, split: int):
     """Per-launch HBM bytes for this config (and strong split) from the
     committed PMC summaries (profiles/*pmc*.json, scripts/pmc_summary.py over
@@ -439,6 +465,8 @@ def run_rank(args, rank: int, world: int, local: int):
         traffic, traffic_src = (pmc_traffic(args.config, args.mode, split) if B == 1
                                 else (None, "no committed PMC summary for batched launches"))
         probe = pattern_ceiling(wl, K, sync, new_event, achieved) if B == 1 else None
+        floor = launch_floor(n, dtype, w32, mode, dev, K, sync, new_event, ev_ms / K * 1e3,
+                             wl.bytes_per_step) if B == 1 else None
         scaling = "weak" if args.weak and world > 1 else "strong"
         workload = args.config + ": " + desc
         if B > 1:
@@ -479,6 +507,7 @@ def run_rank(args, rank: int, world: int, local: int):
                          "kernel": wl.kernel, "kernel_avg_us": round(ev_ms / K * 1e3, 3),
                          "timing": "rank 0: HIP events around the K timed launches on the launch stream"},
             "pattern_ceiling": probe,
+            "launch_floor": floor,
         }
         if single:
             result["single_gpu_reference"] = single

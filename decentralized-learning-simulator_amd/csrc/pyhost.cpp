@@ -47,12 +47,64 @@ namespace {
 PyObject* s_parameters = nullptr;
 PyObject* s_modules = nullptr;
 
-int visit(PyObject* m, PyObject* out, std::unordered_set<PyObject*>& seen, int depth) {
+// Identity set of the objects a walk has visited: open addressing over a
+// power-of-two table (a std::unordered_set allocated a node per insert, ~30
+// per GNLeNet model and per task).
+class PtrSet {
+ public:
+  explicit PtrSet(size_t cap = 128) : slots_(cap, nullptr) {}
+  // true if p was not in the set (and is now)
+  bool insert(PyObject* p) {
+    if (2 * (count_ + 1) > slots_.size()) grow();
+    if (!place(slots_, p)) return false;
+    ++count_;
+    return true;
+  }
+
+ private:
+  static bool place(std::vector<PyObject*>& t, PyObject* p) {
+    const size_t mask = t.size() - 1;
+    size_t h = (static_cast<size_t>(reinterpret_cast<uintptr_t>(p)) >> 4) * 0x9E3779B97F4A7C15ull;
+    for (size_t i = (h >> 20) & mask;; i = (i + 1) & mask) {
+      if (t[i] == p) return false;
+      if (!t[i]) {
+        t[i] = p;
+        return true;
+      }
+    }
+  }
+  void grow() {
+    std::vector<PyObject*> t(slots_.size() * 2, nullptr);
+    for (PyObject* p : slots_)
+      if (p) place(t, p);
+    slots_.swap(t);
+  }
+  std::vector<PyObject*> slots_;
+  size_t count_ = 0;
+};
+
+// m.<name> as a new reference: the instance dict first (where nn.Module keeps
+// _parameters and _modules; one dict lookup instead of the attribute protocol
+// of a class with __getattr__), the full attribute lookup otherwise
+PyObject* module_attr(PyObject* m, PyObject* name) {
+  PyObject** dp = _PyObject_GetDictPtr(m);
+  if (dp && *dp) {
+    PyObject* v = PyDict_GetItemWithError(*dp, name);
+    if (v) {
+      Py_INCREF(v);
+      return v;
+    }
+    if (PyErr_Occurred()) return nullptr;
+  }
+  return PyObject_GetAttr(m, name);
+}
+
+int visit(PyObject* m, PyObject* out, PtrSet& seen, int depth) {
   if (depth > 10000) {
     PyErr_SetString(PyExc_RecursionError, "module tree too deep");
     return -1;
   }
-  PyObject* params = PyObject_GetAttr(m, s_parameters);
+  PyObject* params = module_attr(m, s_parameters);
   if (!params) return -1;
   if (!PyDict_Check(params)) {
     Py_DECREF(params);
@@ -62,14 +114,14 @@ int visit(PyObject* m, PyObject* out, std::unordered_set<PyObject*>& seen, int d
   Py_ssize_t pos = 0;
   PyObject *key, *val;
   while (PyDict_Next(params, &pos, &key, &val)) {
-    if (val == Py_None || !seen.insert(val).second) continue;
+    if (val == Py_None || !seen.insert(val)) continue;
     if (PyList_Append(out, val) < 0) {
       Py_DECREF(params);
       return -1;
     }
   }
   Py_DECREF(params);
-  PyObject* mods = PyObject_GetAttr(m, s_modules);
+  PyObject* mods = module_attr(m, s_modules);
   if (!mods) return -1;
   if (!PyDict_Check(mods)) {
     Py_DECREF(mods);
@@ -80,7 +132,7 @@ int visit(PyObject* m, PyObject* out, std::unordered_set<PyObject*>& seen, int d
   // _modules may not change while we walk it (no Python code runs between
   // PyDict_Next calls except attribute lookups on plain instance dicts)
   while (PyDict_Next(mods, &pos, &key, &val)) {
-    if (val == Py_None || !seen.insert(val).second) continue;
+    if (val == Py_None || !seen.insert(val)) continue;
     Py_INCREF(val);
     const int rc = visit(val, out, seen, depth + 1);
     Py_DECREF(val);
@@ -96,7 +148,7 @@ int visit(PyObject* m, PyObject* out, std::unordered_set<PyObject*>& seen, int d
 PyObject* py_module_params(PyObject*, PyObject* module) {
   PyObject* out = PyList_New(0);
   if (!out) return nullptr;
-  std::unordered_set<PyObject*> seen;
+  PtrSet seen;
   seen.insert(module);
   if (visit(module, out, seen, 0) < 0) {
     Py_DECREF(out);
@@ -412,8 +464,15 @@ PyObject* py_fill_param_views(PyObject*, PyObject* args) {
   try {
     const int64_t base = a->storage_offset();
     for (Py_ssize_t j = 0; ok && j < t; ++j) {
-      at::Tensor data = a->as_strided(v->shapes[j], v->strides[j], base + v->offsets[j]).detach();
-      data.unsafeGetTensorImpl()->set_allow_tensor_metadata_change(true);
+      // the detached view built directly (what as_strided(...).detach()
+      // yields, minus two dispatcher round trips): a TensorImpl on the
+      // arena's storage with its key set and dtype, then this parameter's
+      // sizes, strides and offset. Its own version counter, like the
+      // reference's separately allocated deepcopy parameters.
+      c10::intrusive_ptr<c10::TensorImpl> impl =
+          a->unsafeGetTensorImpl()->shallow_copy_and_detach(c10::VariableVersion(0), true);
+      impl->set_sizes_and_strides(v->shapes[j], v->strides[j], base + v->offsets[j]);
+      at::Tensor data(std::move(impl));
       data.set_requires_grad(ps[j]->requires_grad());
       PyObject* q = THPVariable_Wrap(data, reinterpret_cast<PyTypeObject*>(ParameterClass));
       PyObject* p = q ? PySequence_Fast_GET_ITEM(rs, PyLong_AsSsize_t(PySequence_Fast_GET_ITEM(ks, j))) : nullptr;

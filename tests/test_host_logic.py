@@ -545,3 +545,18 @@ def test_param_views_match_make_subclass(offset):
         assert torch.equal(g, e) and g.untyped_storage().data_ptr() == buf.untyped_storage().data_ptr()
     a.add_(1)  # the views see the arena
     assert all(torch.equal(got[k], exp[k]) for k in exp)
+    # leaves like the reference's deepcopy parameters: no autograd base, no
+    # grad_fn, a version counter of their own, usable in autograd and in place
+    for key in exp:
+        g = got[key]
+        assert g.is_leaf and g.grad_fn is None and g._base is None and not g._is_view()
+        assert g._version == 0
+    w = got[id(m.a.weight)]
+    v0 = got[id(m.c.weight)]._version
+    with torch.no_grad():
+        w.mul_(2)
+    assert w._version == 1 and got[id(m.c.weight)]._version == v0
+    loss = (got[id(m.a.weight)] * 3).sum()
+    loss.backward()
+    assert torch.equal(w.grad, torch.full_like(w, 3.0))
+    assert got[id(m.a.bias)].grad is None and not got[id(m.a.bias)].requires_grad
