@@ -262,29 +262,53 @@ def pattern_ceiling(wl, k_steps: int, sync, new_event, achieved_gbps: float):
             "kernel": "dlsim_probe_pattern: same dispatch and shapes, XOR fold (memory only)"}
 
 
-def launch_floor(n, dtype, w32, mode, dev, k_steps: int, sync, new_event, step_us: float, bytes_per_step: int):
-    """Per-launch floor of back-to-back launches on one stream: the same
-    entry point and fan-in with one 256-element tile per input, timed like the
-    steps. What remains of a step after this floor is the time the bytes
-    take; at the 8-rank slices the floor is a large part of the step
-    (MI355X_MICROARCH.md, price table row 'boundary': 1.7-1.9 us between
-    streaming kernels). Diagnostic only: `value` is the full step time."""
+def launch_floor(wl, n, dtype, w32, mode, dev, k_steps: int, sync, new_event, step_us: float):
+    """GPU-side per-launch floor of back-to-back launches on one stream: the
+    same entry point with one 256-element tile per input (fan-in min(n, 8)). A host
+    launch through ctypes takes a few µs, about as long as such a kernel, so
+    the K tiny launches are queued behind a backlog of the step's own
+    launches (enough GPU time to cover the host's enqueue of all of them):
+    the events around them then see the GPU run them back to back. What
+    remains of a step after this floor is what its bytes take; at the 8-rank
+    slices the floor is a large part of a ~10 µs step (MI355X_MICROARCH.md,
+    price table row 'boundary': 1.7-1.9 µs between streaming kernels).
+    Diagnostic only: `value` is the full step time."""
     from dasklearn_amd import _native
     tdt = TORCH_DTYPE[dtype]
-    x = torch.randn((n, 256), device=dev).to(tdt)
+    # at most 8 inputs: with more, one 256-element tile is a chain of
+    # dependent load groups in a single block (latency, not launch cost)
+    nf = min(n, 8)
+    x = torch.randn((nf, 256), device=dev).to(tdt)
     out = torch.empty(256, dtype=tdt, device=dev)
-    plan = _native.ReducePlan([x[i] for i in range(n)], w32, out, mode)
-    stream = torch.cuda.current_stream(dev)
+    plan = _native.ReducePlan([x[i] for i in range(nf)], w32[:nf], out, mode)
+    stream = wl.stream
     for _ in range(10):
         plan.launch(stream)
-    ev_ms, _ = time_steps(lambda k: plan.launch(stream), k_steps, sync, lambda: None, new_event)
-    floor_us = ev_ms * 1e3 / k_steps
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(k_steps):
+        plan.launch(stream)
+    host_us = (time.perf_counter() - t0) * 1e6 / k_steps
+    sync()
+    # GPU time of the backlog >= 2x the host time to enqueue it and the K launches
+    backlog = min(4000, math.ceil(2.0 * k_steps * host_us / max(step_us - 2.0 * host_us, 0.5)) + 10)
+    e0, e1 = new_event(), new_event()
+    for k in range(backlog):
+        wl.launch(k)
+    e0.record()
+    for _ in range(k_steps):
+        plan.launch(stream)
+    e1.record()
+    sync()
+    floor_us = e0.elapsed_time(e1) * 1e3 / k_steps
+    res = {"us_per_launch": round(floor_us, 3), "host_enqueue_us_per_launch": round(host_us, 3),
+           "backlog_launches": backlog,
+           "note": f"{k_steps} back-to-back launches of the same entry point (n={nf}, 256 elements per input) "
+                   f"queued behind {backlog} launches of the step; HIP events on the launch stream"}
     body_us = step_us - floor_us
-    res = {"us_per_launch": round(floor_us, 3),
-           "note": f"{k_steps} back-to-back launches of the same entry point, n={n}, 256 elements per input; "
-                   "step time minus this floor = the time the step's bytes take"}
     if body_us > 0:
-        res["bytes_frac_of_peak_excl_floor"] = round(bytes_per_step / (body_us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4)
+        res["step_minus_floor_us"] = round(body_us, 3)
+        res["bytes_frac_of_peak_excl_floor"] = round(wl.bytes_per_step / (body_us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4)
     return res
 
 
@@ -465,8 +489,8 @@ def run_rank(args, rank: int, world: int, local: int):
         traffic, traffic_src = (pmc_traffic(args.config, args.mode, split) if B == 1
                                 else (None, "no committed PMC summary for batched launches"))
         probe = pattern_ceiling(wl, K, sync, new_event, achieved) if B == 1 else None
-        floor = launch_floor(n, dtype, w32, mode, dev, K, sync, new_event, ev_ms / K * 1e3,
-                             wl.bytes_per_step) if B == 1 else None
+        floor = launch_floor(wl, n, dtype, w32, mode, dev, K, sync, new_event, ev_ms / K * 1e3) \
+            if B == 1 else None
         scaling = "weak" if args.weak and world > 1 else "strong"
         workload = args.config + ": " + desc
         if B > 1:
