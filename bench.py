@@ -264,7 +264,8 @@ def pattern_ceiling(wl, k_steps: int, sync, new_event, achieved_gbps: float):
 
 def launch_floor(wl, n, dtype, w32, mode, dev, k_steps: int, sync, new_event, step_us: float):
     """GPU-side per-launch floor of back-to-back launches on one stream: the
-    same entry point with one 256-element tile per input (fan-in min(n, 8)). A host
+    step's dispatch (as dlsim_probe_pattern) with one 256-element tile per
+    input (fan-in min(n, 8)). A host
     launch through ctypes takes a few µs, about as long as such a kernel, so
     the K tiny launches are queued behind a backlog of the step's own
     launches (enough GPU time to cover the host's enqueue of all of them):
@@ -280,7 +281,10 @@ def launch_floor(wl, n, dtype, w32, mode, dev, k_steps: int, sync, new_event, st
     nf = min(n, 8)
     x = torch.randn((nf, 256), device=dev).to(tdt)
     out = torch.empty(256, dtype=tdt, device=dev)
-    plan = _native.ReducePlan([x[i] for i in range(nf)], w32[:nf], out, mode)
+    # the memory-only probe's entry (same dispatch, XOR fold): its kernel name
+    # differs from the reduce's, so rocprof's per-kernel averages of the step
+    # stay clean of these tiny launches
+    plan = _native.ReducePlan([x[i] for i in range(nf)], w32[:nf], out, mode, probe=True)
     stream = wl.stream
     for _ in range(10):
         plan.launch(stream)
@@ -303,7 +307,7 @@ def launch_floor(wl, n, dtype, w32, mode, dev, k_steps: int, sync, new_event, st
     floor_us = e0.elapsed_time(e1) * 1e3 / k_steps
     res = {"us_per_launch": round(floor_us, 3), "host_enqueue_us_per_launch": round(host_us, 3),
            "backlog_launches": backlog,
-           "note": f"{k_steps} back-to-back launches of the same entry point (n={nf}, 256 elements per input) "
+           "note": f"{k_steps} back-to-back launches of dlsim_probe_pattern (the step's dispatch; n={nf}, 256 elements per input) "
                    f"queued behind {backlog} launches of the step; HIP events on the launch stream"}
     body_us = step_us - floor_us
     if body_us > 0:

@@ -684,7 +684,14 @@ PyObject* clone_attr(PyObject* k, PyObject* v, PyObject* memo, int depth) {
     const Py_ssize_t len = PyObject_Length(v);
     if (len < 0) return nullptr;
     if (len == 0) {
-      PyObject* e = PyObject_CallNoArgs(reinterpret_cast<PyObject*>(Py_TYPE(v)));
+      // exact types through their C constructors (PyODict_New skips the
+      // type call and OrderedDict.__init__: 11 hook registries per module)
+      PyObject* e = Py_IS_TYPE(v, reinterpret_cast<PyTypeObject*>(g_clone.odict)) &&
+                            g_clone.odict == reinterpret_cast<PyObject*>(&PyODict_Type)
+                        ? PyODict_New()
+                    : PyDict_CheckExact(v) ? PyDict_New()
+                    : PySet_CheckExact(v)  ? PySet_New(nullptr)
+                                           : PyObject_CallNoArgs(reinterpret_cast<PyObject*>(Py_TYPE(v)));
       // An empty OrderedDict (the hook registries, 11 per module) holds
       // nothing a cycle could pass through; like the empty plain dicts
       // CPython creates untracked, it is re-tracked by the dict insert path

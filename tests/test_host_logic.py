@@ -511,6 +511,33 @@ def test_clone_leaves_empty_hook_registries_untracked_until_used():
     assert r() is None  # the cycle was found
 
 
+def test_clone_fresh_containers_are_distinct_working_objects():
+    """The clone makes its empty OrderedDict / dict / set attributes through
+    the C constructors (PyODict_New, PyDict_New, PySet_New): each is a fresh
+    object of the exact type, one per module and attribute, and works as a
+    hook registry (hooks run and are removed)."""
+    from collections import OrderedDict
+    m = nn.Sequential(nn.Linear(3, 3), nn.ReLU())
+    lay = arena.ParamLayout(m)
+    a = torch.cat([q.detach().reshape(-1) for q in lay.params])  # m's own values
+    out = arena.module_from_arenas(m, lay, {torch.float32: a})
+    seen = set()
+    for src, dst in zip(m.modules(), out.modules()):
+        for k, v in src.__dict__.items():
+            if type(v) in (OrderedDict, dict, set) and not v and k not in ("_parameters", "_modules"):
+                w = dst.__dict__[k]
+                assert type(w) is type(v) and not w and w is not v and id(w) not in seen, k
+                seen.add(id(w))
+    x = torch.ones(1, 3)
+    h = out.register_forward_hook(lambda mod, i, o: o * 2)
+    p = out[0].register_forward_pre_hook(lambda mod, i: (i[0] * 3,))
+    assert torch.equal(out(x), m(x * 3) * 2)
+    assert not m._forward_hooks and not m[0]._forward_pre_hooks  # the original is untouched
+    h.remove()
+    p.remove()
+    assert torch.equal(out(x), m(x)) and not out._forward_hooks
+
+
 @pytest.mark.parametrize("offset", [0, 64])
 def test_param_views_match_make_subclass(offset):
     """fill_param_views (C++) builds what torch.Tensor._make_subclass(
