@@ -547,7 +547,7 @@ def run_rank(args, rank: int, world: int, local: int):
             result["cpu_baseline"] = cpu_baseline(args.config, n, p, dtype, weights, args.cpu_seconds)
         else:
             result["cpu_baseline"] = None
-        print(json.dumps(result), flush=True)
+        print(json.dumps(result), file=_RESULT_OUT or sys.stdout, flush=True)
     if world > 1:
         dist.destroy_process_group()
     return 0
@@ -641,7 +641,22 @@ def main(argv=None):
     if world != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         return 2
+    _stdout_for_result_only()
     return run_rank(args, rank, world, local)
+
+
+_RESULT_OUT = None
+
+
+def _stdout_for_result_only():
+    """Keep this process's stdout for the one JSON line: libraries that write
+    to file descriptor 1 themselves (gloo's "[Gloo] Rank r is connected ..."
+    at rendezvous, RCCL warnings) go to stderr instead, so a multi-rank run
+    still prints exactly one parseable line."""
+    global _RESULT_OUT
+    sys.stdout.flush()
+    _RESULT_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
 
 
 if __name__ == "__main__":

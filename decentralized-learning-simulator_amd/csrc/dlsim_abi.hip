@@ -446,8 +446,12 @@ int dlsim_host_wreduce(int n, int t, const void* const* h_srcs, const size_t* nu
   const size_t chunk = chunk_elems == 0 || chunk_elems >= total ? total : (chunk_elems + 1023) / 1024 * 1024;
   const size_t n_chunks = (total + chunk - 1) / chunk;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  hipStream_t h2d = h2d_stream ? static_cast<hipStream_t>(h2d_stream) : st;
-  hipStream_t d2h = d2h_stream ? static_cast<hipStream_t>(d2h_stream) : st;
+  // One chunk has nothing to overlap (its H2D, reduce and D2H are serial):
+  // everything on `stream`, without the cross-stream event waits, whose
+  // signalling latency a small task would pay several times.
+  const bool side = n_chunks > 1;
+  hipStream_t h2d = side && h2d_stream ? static_cast<hipStream_t>(h2d_stream) : st;
+  hipStream_t d2h = side && d2h_stream ? static_cast<hipStream_t>(d2h_stream) : st;
   char* stage = static_cast<char*>(h_staging);
   char* rows = static_cast<char*>(d_rows);
   char* out = static_cast<char*>(d_out);
@@ -552,8 +556,9 @@ int dlsim_host_chunk_mean(int b, const int* fan_in, const void* const* h_inputs,
     }
   }
   hipStream_t st = static_cast<hipStream_t>(stream);
-  hipStream_t h2d = h2d_stream ? static_cast<hipStream_t>(h2d_stream) : st;
-  hipStream_t d2h = d2h_stream ? static_cast<hipStream_t>(d2h_stream) : st;
+  // one task: nothing to overlap, everything on `stream` (see dlsim_host_wreduce)
+  hipStream_t h2d = b > 1 && h2d_stream ? static_cast<hipStream_t>(h2d_stream) : st;
+  hipStream_t d2h = b > 1 && d2h_stream ? static_cast<hipStream_t>(d2h_stream) : st;
   char* hs = static_cast<char*>(h_staging);
   char* ds = static_cast<char*>(d_staging);
 

@@ -274,7 +274,9 @@ int dlsim_wreduce_sharded(const void* const* d_slices, size_t slice_elems, int n
  *   threads            host threads packing the staging rows (the caller's
  *                      own thread included; <= 1: the caller's thread only)
  *   stream             the reduce; h2d_stream / d2h_stream the copies (may be
- *                      `stream` itself or NULL = `stream`)
+ *                      `stream` itself or NULL = `stream`; with one chunk
+ *                      the copies go on `stream`, as there is nothing to
+ *                      overlap)
  * Model i's share of chunk c is packed (memcpy, several threads) into its
  * staging row and copied H2D on h2d_stream as soon as it is packed; once
  * every model's share of chunk c is on the device, the chunk is reduced on
@@ -306,8 +308,9 @@ int dlsim_host_wreduce(int n, int t, const void* const* h_srcs, const size_t* nu
  * Rows are packed on `threads` host threads; each row goes H2D as soon as it
  * is packed, each task's mean runs on `stream` once its rows are on the
  * device (in PyTorch's CPU order at cpu_threads, as dlsim_chunk_mean_batched),
- * and its result goes back on d2h_stream. Returns after packing and
- * queueing; `stream` is ordered after everything.
+ * and its result goes back on d2h_stream (with b == 1 every copy goes on
+ * `stream`). Returns after packing and queueing; `stream` is ordered after
+ * everything.
  */
 int dlsim_host_chunk_mean(int b, const int* fan_in, const void* const* h_inputs, const size_t* n_elems,
                           void* h_staging, void* d_staging, size_t staging_elems, void* const* d_outs,

@@ -87,3 +87,24 @@ def test_spawn_ranks_reports_a_failing_rank(tmp_path):
     script = tmp_path / "rank.py"
     script.write_text(_RANK_SCRIPT)
     assert bench.spawn_ranks(2, ["--fail"], script=str(script)) == 3
+
+
+def test_rank_stdout_carries_only_the_result_line(tmp_path):
+    """After _stdout_for_result_only, whatever a library writes to fd 1 (gloo
+    prints its rendezvous to stdout) lands on stderr; the result line alone
+    reaches stdout."""
+    import subprocess
+    script = tmp_path / "child.py"
+    script.write_text(textwrap.dedent(f"""
+        import os, sys, json
+        sys.path.insert(0, {ROOT!r})
+        import bench
+        bench._stdout_for_result_only()
+        os.write(1, b"[Gloo] Rank 0 is connected to 1 peer ranks\\n")
+        print("a stray print")
+        print(json.dumps({{"value": 1}}), file=bench._RESULT_OUT, flush=True)
+    """))
+    r = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.splitlines() == ['{"value": 1}']
+    assert "[Gloo] Rank 0" in r.stderr and "a stray print" in r.stderr
