@@ -69,13 +69,29 @@ def _device_views(views) -> Optional[torch.device]:
     return dev
 
 
+def _rows_device(rows, layout, dt) -> torch.device:
+    """The CUDA device of model 0's first tensor of group dt (wreduce_rows
+    checks every other tensor against it)."""
+    t = rows[0][layout.groups[dt][0]]
+    if not t.is_cuda:
+        raise ValueError("rows input: tensors must be on a CUDA device")
+    return t.device
+
+
 def aggregate_arena_tasks(prepared, mode: int = _native.DLSIM_EXACT,
                           on_launched: Optional[Callable[[], None]] = None) -> List[nn.Module]:
     """prepared: [(model0, layout of model0, {dtype: [flat arena per model]},
-    weights as Python floats)] with every arena on one device -> one module
-    per task (deepcopy(model0) semantics, parameters views of a fresh output
-    arena), all tasks of a dtype and device in batched launches (fp64 groups:
-    one dlsim_wreduce_f64 per task).
+    weights as Python floats[, rows])] with every arena on one device -> one
+    module per task (deepcopy(model0) semantics, parameters views of a fresh
+    output arena), all tasks of a dtype and device in batched launches (fp64
+    groups: one dlsim_wreduce_f64 per task).
+
+    rows (optional): every model's parameter list. A dtype group whose arena
+    list holds None (a model that keeps its parameters in separate device
+    tensors, e.g. a device train task's deepcopy) is read from those tensors
+    in place: one dlsim_wreduce_tensors per task, pointers collected in C
+    (the single-task path's wreduce_rows), instead of copying each such model
+    into an arena first.
 
     on_launched: called once every launch is queued, before the output
     modules are built; the list `prepared` is consumed while they are (each
@@ -85,9 +101,29 @@ def aggregate_arena_tasks(prepared, mode: int = _native.DLSIM_EXACT,
     orders any reuse of their memory after the kernels."""
     by_dtype = {}
     outs = []
-    for model0, layout, views, ws in prepared:
+    for entry in prepared:
+        model0, layout, views, ws = entry[:4]
         o = {}
         for dt, vs in views.items():
+            if any(v is None for v in vs):
+                rows = entry[4]
+                dev = _rows_device(rows, layout, dt)
+                out = torch.empty(layout.totals[dt], dtype=dt, device=dev)
+                o[dt] = out
+                stream = torch.cuda.current_stream(dev)
+                w = _native.weights_for_dtype(ws, dt)
+                idx = layout.groups[dt]
+                if not _native.wreduce_rows(rows, idx, layout.split_sizes[dt], w, out.data_ptr(),
+                                            layout.byte_offsets[dt], _native.dtype_code(dt), mode,
+                                            stream.cuda_stream, dev.index):
+                    # a model's tensors are elsewhere (its arena was copied
+                    # here): flatten the in-place ones too, one reduce
+                    with torch.no_grad():
+                        flat = [v if v is not None else
+                                torch._C._nn.flatten_dense_tensors([rows[i][k] for k in idx]).to(dev)
+                                for i, v in enumerate(vs)]
+                    _native.wreduce(flat, w, out, mode, stream)
+                continue
             dev = vs[0].device
             out = torch.empty(layout.totals[dt], dtype=dt, device=dev)
             o[dt] = out
@@ -105,7 +141,7 @@ def aggregate_arena_tasks(prepared, mode: int = _native.DLSIM_EXACT,
         on_launched()
     mods = []
     for i, o in enumerate(outs):
-        model0, layout, _, _ = prepared[i]
+        model0, layout = prepared[i][:2]
         prepared[i] = None
         mods.append(module_from_arenas(model0, layout, o))
     return mods

@@ -11,10 +11,12 @@ whose inputs are ready runs in the wave; the aggregate tasks of a wave go to
 `aggregate_batch` together (descriptor-table launches), other tasks (train,
 test, ...) are called through the function table like the worker does.
 
-Models that reach an aggregate are resolved once per wave to one flat device
-arena each: aggregate outputs are registered arenas (read in place), other
-device arenas are read in place, anything else is copied once into a fresh
-arena (one concatenation, no module built). So an aggregate -> train ->
+Models that reach an aggregate are resolved once per wave: aggregate outputs
+are registered arenas (read in place), other device arenas are read in place,
+models that keep their parameters in separate contiguous tensors on the
+device (a device train task's deepcopy) are read in place tensor by tensor,
+anything else (host models, other devices) is copied once into a fresh arena
+(one concatenation, no module built). So an aggregate -> train ->
 aggregate chain never crosses PCIe when the train function works on the
 device. Results are bit-identical to running the same tasks one by one with
 FedAvg.aggregate.
@@ -116,7 +118,12 @@ class RoundExecutor:
             with torch.no_grad():
                 for dt, idx in layout.groups.items():
                     ts = [params[0][k] for k in idx]
-                    if all(t.device == dev for t in ts):
+                    if dt != torch.float64 and all(t.device == dev and t.is_contiguous() for t in ts):
+                        # separate tensors on the target device (a device
+                        # train task's deepcopy): read in place by the wave's
+                        # reduce (None = "use the parameter tensors"), no copy
+                        arenas[dt] = None
+                    elif all(t.device == dev for t in ts):
                         # one C++ call (torch's flatten, as DDP buckets use)
                         # instead of a reshape per tensor and a cat
                         arenas[dt] = torch._C._nn.flatten_dense_tensors(ts)
@@ -219,7 +226,7 @@ class RoundExecutor:
                 if lay._signature is not sig and lay._signature != sig:
                     layout0.check_compatible(models[i])  # raises the shape/dtype error
             views = {dt: [a[dt] for _, a in ents] for dt in layout0.groups}
-            prepared.append((models[0], layout0, views, ws))
+            prepared.append((models[0], layout0, views, ws, [lay.params for lay, _ in ents]))
         resolved.clear()
         cache.clear()
         return aggregate_arena_tasks(prepared, self.mode, on_launched)

@@ -16,7 +16,7 @@ host model instead (the reference's CPU training, model_trainer.py:129), so
 every aggregate reads host models: the executor uploads each wave's models
 once, the sequential worker loop stages them per task.
 
-    python scripts/bench_rounds.py [--peers 100] [--rounds 4] [--host] [--model gnlenet|flat]
+    python scripts/bench_rounds.py [--peers 100] [--rounds 4] [--host] [--model gnlenet|flat|resnet18]
 """
 from __future__ import annotations
 
@@ -65,8 +65,19 @@ class GNLeNetTree(nn.Module):
         self.classifier = nn.Sequential(nn.Linear(576, 10))
 
 
+def resnet18_shapes():
+    from bench import resnet18_shapes as shapes
+    return shapes()
+
+
+def model_shapes(kind):
+    return resnet18_shapes() if kind == "resnet18" else GNLENET
+
+
 def make_model(kind):
-    return GNLeNetTree() if kind == "gnlenet" else Shaped(GNLENET)
+    if kind == "gnlenet":
+        return GNLeNetTree()
+    return Shaped(model_shapes(kind))
 
 
 class Settings:
@@ -204,8 +215,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--cpu-rounds", type=int, default=2)
     ap.add_argument("--host", action="store_true", help="train returns host models (CPU training)")
-    ap.add_argument("--model", choices=("gnlenet", "flat"), default="gnlenet",
-                    help="gnlenet: the reference's module tree; flat: the same 14 tensors in one ParameterList")
+    ap.add_argument("--model", choices=("gnlenet", "flat", "resnet18"), default="gnlenet",
+                    help="gnlenet: the reference's module tree; flat: the same 14 tensors in one ParameterList; "
+                         "resnet18: the north star's 62 ResNet-18 parameter tensors in one ParameterList")
     ap.add_argument("--profile", default=None, help="cProfile the batched run into this file")
     ap.add_argument("--profile-seq", default=None, help="cProfile the sequential run into this file")
     ap.add_argument("--reps", type=int, default=3,
@@ -219,10 +231,11 @@ def main():
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     init_h = make_model(a.model)
-    assert [tuple(q.shape) for q in init_h.parameters()] == GNLENET
+    shapes = model_shapes(a.model)
+    assert [tuple(q.shape) for q in init_h.parameters()] == [tuple(s) for s in shapes]
     init_d = copy.deepcopy(init_h).to(dev)
     tasks, fan = dag(a.peers, a.rounds)
-    p = sum(int(torch.Size(s).numel()) for s in GNLENET)
+    p = sum(int(torch.Size(s).numel()) for s in shapes)
     task_bytes = (fan + 1) * p * 4
     sync = torch.cuda.synchronize
 

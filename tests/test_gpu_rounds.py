@@ -95,3 +95,76 @@ def test_round_executor_host_trained_models(mixed):
                 x, y = torch.cat(ga), torch.cat(gb)
                 assert torch.equal(x.view(torch.int16) if x.element_size() == 2 else x.view(torch.int32),
                                    y.view(torch.int16) if y.element_size() == 2 else y.view(torch.int32)), (p, dt)
+
+
+class F64Shaped(torch.nn.Module):
+    """GNLeNet shapes in fp32 with two fp64 tensors (an fp64 dtype group)."""
+
+    def __init__(self):
+        super().__init__()
+        self.ps = torch.nn.ParameterList([torch.nn.Parameter(
+            (torch.randn(*s) * 0.05).to(torch.float64 if i in (1, 12) else torch.float32))
+            for i, s in enumerate(GNLENET)])
+
+
+def host_math_train(settings, params):
+    """device_agnostic_train with the update computed on the host and copied
+    back, so device and host replays train to the same bits (a bf16 add_ of
+    an fp32 tensor need not round alike on the CPU and the GPU)."""
+    model = params["model"]
+    out = copy.deepcopy(model)
+    g = torch.Generator().manual_seed(1000 * params["round"] + params["peer"])
+    with torch.no_grad():
+        for p in out.parameters():
+            p.copy_((p.detach().cpu() + torch.randn(p.shape, generator=g) * 0.01).to(p.device))
+    return [out]
+
+
+@pytest.mark.parametrize("make", [MixedShaped, F64Shaped])
+def test_round_executor_reads_device_trained_tensors_in_place(make):
+    """Device-trained models (deepcopies: separate parameter tensors) are read
+    in place tensor by tensor (no flatten copy), also in tasks that mix them
+    with registered arena outputs (round 2 reads its own round-1 aggregate)
+    and next to an fp64 group (flattened): bit-identical to the oracle replay
+    on host models."""
+    from dasklearn_amd import arena
+    torch.manual_seed(29)
+    init_h = make()
+    init_d = copy.deepcopy(init_h).cuda()
+    n = 5
+    tasks = []
+    for r in (1, 2):
+        for p in range(n):
+            src = ("init", 0) if r == 1 else (f"agg_{p}_{r - 1}", 0)
+            tasks.append((f"train_{p}_{r}", "train", {"model": src, "round": r, "peer": p}))
+        for p in range(n):
+            models = [(f"train_{(p + d) % n}_{r}", 0) for d in (1, 2)] + [(f"train_{p}_{r}", 0)]
+            if r == 2:
+                models.append((f"agg_{p}_1", 0))  # a registered arena next to deepcopies
+            tasks.append((f"agg_{p}_{r}", "aggregate", {"models": models, "round": r, "peer": p,
+                                                       "weights": [0.1, 0.2, 0.3, 0.4][:len(models)]}))
+    flattened = []
+    orig = torch._C._nn.flatten_dense_tensors
+
+    def spy(ts):
+        flattened.append(ts[0].dtype)
+        return orig(ts)
+    torch._C._nn.flatten_dense_tensors = spy
+    try:
+        ex = RoundExecutor({"train": host_math_train}, Settings())
+        got = ex.run(tasks, seed={"init": [init_d]})
+    finally:
+        torch._C._nn.flatten_dense_tensors = orig
+    assert all(dt == torch.float64 for dt in flattened)  # only the fp64 group is copied
+    exp = replay(tasks, {"aggregate": oracle_aggregate, "train": host_math_train}, init_h)
+    for p in range(n):
+        for r in (1, 2):
+            a, b = got.get(f"agg_{p}_{r}"), exp[f"agg_{p}_{r}"][0]
+            if a is None:
+                continue  # dropped after its last reader
+            a = a[0]
+            for x, y in zip(arena.module_params(a), arena.module_params(b)):
+                assert x.is_cuda and x.dtype == y.dtype
+                xs, ys = x.detach().cpu().reshape(-1), y.detach().reshape(-1)
+                iv = {8: torch.int64, 4: torch.int32, 2: torch.int16}[xs.element_size()]
+                assert torch.equal(xs.view(iv), ys.view(iv)), (p, r, x.dtype)
