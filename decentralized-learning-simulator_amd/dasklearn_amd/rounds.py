@@ -59,16 +59,21 @@ def _refs(v, out):
 class RoundExecutor:
 
     def __init__(self, funcs: Dict[str, Callable], settings, device=None,
-                 mode: int = _native.DLSIM_EXACT, timing: bool = False, keep_all: bool = False):
+                 mode: int = _native.DLSIM_EXACT, timing: bool = False, keep_all: bool = False,
+                 tensors_in_place: bool = True):
         """timing: accumulate wall seconds per kind of wave work in
         `self.stats` ("aggregate", "other"); the stream is synchronised after
         every batched aggregate so its kernels count (measurement only).
         keep_all: keep every task's result; by default a result is dropped
         once every task that reads it has run, as the broker clears a
         completed task's data (broker.py:221), so memory is bounded by the
-        DAG's frontier, not by the number of rounds."""
+        DAG's frontier, not by the number of rounds.
+        tensors_in_place: read models whose parameters are separate device
+        tensors where they are (False: copy each into an arena first, the
+        session-1 behaviour, kept for comparison)."""
         self.timing = timing
         self.keep_all = keep_all
+        self.tensors_in_place = tensors_in_place
         self.stats: Dict[str, float] = {"aggregate": 0.0, "other": 0.0, "aggregate_tasks": 0}
         self.funcs = dict(funcs)
         self.settings = settings
@@ -118,7 +123,8 @@ class RoundExecutor:
             with torch.no_grad():
                 for dt, idx in layout.groups.items():
                     ts = [params[0][k] for k in idx]
-                    if dt != torch.float64 and all(t.device == dev and t.is_contiguous() for t in ts):
+                    if self.tensors_in_place and dt != torch.float64 and \
+                            all(t.device == dev and t.is_contiguous() for t in ts):
                         # separate tensors on the target device (a device
                         # train task's deepcopy): read in place by the wave's
                         # reduce (None = "use the parameter tensors"), no copy
