@@ -316,6 +316,33 @@ def launch_floor(wl, n, dtype, w32, mode, dev, k_steps: int, sync, new_event, st
     return res
 
 
+def two_streams(wl, k_steps: int, sync, dev):
+    """The same K steps with consecutive steps on two streams (independent
+    aggregates: distinct inputs and outputs), so one launch's ramp overlaps
+    the previous one's drain instead of waiting behind the launch boundary.
+    A D-PSGD or gossip round has many such independent aggregates in flight
+    (the reference runs them in parallel worker processes, broker.py:137-149).
+    Diagnostic only: `value` is one aggregate after another on one stream."""
+    a = wl.stream
+    b = torch.cuda.Stream(dev)
+    for k in range(10):
+        wl.plans[k % wl.sets].launch(a if k % 2 == 0 else b)
+    sync()
+    e0, e1, eb = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+    e0.record(a)
+    b.wait_event(e0)
+    for k in range(k_steps):
+        wl.plans[k % wl.sets].launch(a if k % 2 == 0 else b)
+    eb.record(b)
+    a.wait_event(eb)
+    e1.record(a)
+    sync()
+    us = e0.elapsed_time(e1) * 1e3 / k_steps
+    gbps = wl.bytes_per_step / (us * 1e-6) / 1e9
+    return {"us_per_step": round(us, 3), "GBps": round(gbps, 1), "frac": round(gbps / HBM_PEAK_GBPS, 4),
+            "note": "steps alternate between two streams (independent aggregates in flight); not in value"}
+
+
 def pmc_traffic(config: str, mode: str, split: int):
     """Per-launch HBM bytes for this config (and strong split) from the
     committed PMC summaries (profiles/*pmc*.json, scripts/pmc_summary.py over
@@ -495,6 +522,7 @@ def run_rank(args, rank: int, world: int, local: int):
         probe = pattern_ceiling(wl, K, sync, new_event, achieved) if B == 1 else None
         floor = launch_floor(wl, n, dtype, w32, mode, dev, K, sync, new_event, ev_ms / K * 1e3) \
             if B == 1 else None
+        overlap = two_streams(wl, K, sync, dev) if B == 1 else None
         scaling = "weak" if args.weak and world > 1 else "strong"
         workload = args.config + ": " + desc
         if B > 1:
@@ -536,6 +564,7 @@ def run_rank(args, rank: int, world: int, local: int):
                          "timing": "rank 0: HIP events around the K timed launches on the launch stream"},
             "pattern_ceiling": probe,
             "launch_floor": floor,
+            "two_streams": overlap,
         }
         if single:
             result["single_gpu_reference"] = single
