@@ -69,9 +69,26 @@ def _device_views(views) -> Optional[torch.device]:
     return dev
 
 
-def _rows_device(rows, layout, dt) -> torch.device:
-    """The CUDA device of model 0's first tensor of group dt (wreduce_rows
-    checks every other tensor against it)."""
+def _row_on(params, view, idx, sizes, dev):
+    """Model i's tensors of a dtype group as the rows path reads them: its
+    parameters when they are on `dev` (read in place; a registered arena's
+    parameters are views of it), else the pieces of its flat view (an arena
+    uploaded or copied to `dev`, e.g. a host model of the wave)."""
+    if view is None or params[idx[0]].device == dev:
+        return params
+    row = [None] * len(params)
+    for k, piece in zip(idx, view.split(sizes)):
+        row[k] = piece
+    return row
+
+
+def _rows_device(vs, rows, layout, dt) -> torch.device:
+    """The task's device: that of its flat views, or (none) of the first
+    model read in place (its tensors are on the target device by
+    construction, RoundExecutor._arena_of)."""
+    for v in vs:
+        if v is not None:
+            return v.device
     t = rows[0][layout.groups[dt][0]]
     if not t.is_cuda:
         raise ValueError("rows input: tensors must be on a CUDA device")
@@ -107,12 +124,13 @@ def aggregate_arena_tasks(prepared, mode: int = _native.DLSIM_EXACT,
         for dt, vs in views.items():
             if any(v is None for v in vs):
                 rows = entry[4]
-                dev = _rows_device(rows, layout, dt)
+                dev = _rows_device(vs, rows, layout, dt)
                 out = torch.empty(layout.totals[dt], dtype=dt, device=dev)
                 o[dt] = out
                 stream = torch.cuda.current_stream(dev)
                 w = _native.weights_for_dtype(ws, dt)
                 idx = layout.groups[dt]
+                rows = [_row_on(rows[i], v, idx, layout.split_sizes[dt], dev) for i, v in enumerate(vs)]
                 if not _native.wreduce_rows(rows, idx, layout.split_sizes[dt], w, out.data_ptr(),
                                             layout.byte_offsets[dt], _native.dtype_code(dt), mode,
                                             stream.cuda_stream, dev.index):

@@ -120,6 +120,10 @@ def host_math_train(settings, params):
     return [out]
 
 
+def to_host(settings, params):
+    return [copy.deepcopy(params["model"]).cpu()]
+
+
 @pytest.mark.parametrize("make", [MixedShaped, F64Shaped])
 def test_round_executor_reads_device_trained_tensors_in_place(make):
     """Device-trained models (deepcopies: separate parameter tensors) are read
@@ -132,7 +136,7 @@ def test_round_executor_reads_device_trained_tensors_in_place(make):
     init_h = make()
     init_d = copy.deepcopy(init_h).cuda()
     n = 5
-    tasks = []
+    tasks = [("host_init", "to_host", {"model": ("init", 0)})]
     for r in (1, 2):
         for p in range(n):
             src = ("init", 0) if r == 1 else (f"agg_{p}_{r - 1}", 0)
@@ -141,6 +145,8 @@ def test_round_executor_reads_device_trained_tensors_in_place(make):
             models = [(f"train_{(p + d) % n}_{r}", 0) for d in (1, 2)] + [(f"train_{p}_{r}", 0)]
             if r == 2:
                 models.append((f"agg_{p}_1", 0))  # a registered arena next to deepcopies
+                if p == 0:  # a host model first (uploaded arena) next to in-place tensors
+                    models = [("host_init", 0)] + models[:3]
             tasks.append((f"agg_{p}_{r}", "aggregate", {"models": models, "round": r, "peer": p,
                                                        "weights": [0.1, 0.2, 0.3, 0.4][:len(models)]}))
     flattened = []
@@ -151,12 +157,12 @@ def test_round_executor_reads_device_trained_tensors_in_place(make):
         return orig(ts)
     torch._C._nn.flatten_dense_tensors = spy
     try:
-        ex = RoundExecutor({"train": host_math_train}, Settings())
+        ex = RoundExecutor({"train": host_math_train, "to_host": to_host}, Settings())
         got = ex.run(tasks, seed={"init": [init_d]})
     finally:
         torch._C._nn.flatten_dense_tensors = orig
     assert all(dt == torch.float64 for dt in flattened)  # only the fp64 group is copied
-    exp = replay(tasks, {"aggregate": oracle_aggregate, "train": host_math_train}, init_h)
+    exp = replay(tasks, {"aggregate": oracle_aggregate, "train": host_math_train, "to_host": to_host}, init_h)
     for p in range(n):
         for r in (1, 2):
             a, b = got.get(f"agg_{p}_{r}"), exp[f"agg_{p}_{r}"][0]
