@@ -189,10 +189,17 @@ def dtype_code(torch_dtype, single_task: bool = False) -> int:
 
 
 def _stream_handle(device, stream) -> Optional[int]:
+    """The hipStream_t of `stream`, or of `device`'s current stream (read raw:
+    no torch.cuda.Stream object is built, this runs once per launch)."""
     import torch
-    if stream is None:
-        stream = torch.cuda.current_stream(device)
-    return stream.cuda_stream
+    if stream is not None:
+        return stream.cuda_stream
+    if device is None:
+        return torch.cuda.current_stream().cuda_stream
+    idx = device.index if isinstance(device, torch.device) else int(device)
+    if idx is None:
+        idx = torch.cuda.current_device()
+    return torch._C._cuda_getCurrentRawStream(idx)
 
 
 class ReducePlan:

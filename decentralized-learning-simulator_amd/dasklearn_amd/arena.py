@@ -118,9 +118,13 @@ class ParamLayout:
 
     def rebind(self, params: List[nn.Parameter]) -> "ParamLayout":
         """The same layout over another module's parameters (same signature,
-        which the caller guarantees): no recomputation."""
-        other = copy.copy(self)
-        other.params = params
+        which the caller guarantees): no recomputation. A shallow copy of the
+        attribute dict (what copy.copy does, without its reduce protocol:
+        this runs several times per task)."""
+        other = ParamLayout.__new__(ParamLayout)
+        d = self.__dict__.copy()
+        d["params"] = params
+        other.__dict__ = d
         return other
 
     def matches(self, ps: Sequence[torch.Tensor]) -> bool:
@@ -453,6 +457,7 @@ def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, m
     n = len(models)
     outs: Dict[torch.dtype, torch.Tensor] = {}
     stream = torch.cuda.current_stream(dev)
+    raw_stream = stream.cuda_stream
     st = _Stages(timing, stream)
     host_models = all(not all_params[i][idx[0]].is_cuda
                       for idx in layout.groups.values() for i in range(n))
@@ -487,7 +492,7 @@ def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, m
                 # in C (no detach() objects, no output slices)
                 if not _native.wreduce_rows(all_params, idx, layout.split_sizes[dt], weights_f32, out.data_ptr(),
                                             layout.byte_offsets[dt], _native.dtype_code(dt), mode,
-                                            stream.cuda_stream, dix):
+                                            raw_stream, dix):
                     # a tensor is not contiguous, or (in a model whose first
                     # tensor is here) on another device: stage them all
                     _staged_reduce(all_params, idx, dt, dev, out, w, mode, stream)
