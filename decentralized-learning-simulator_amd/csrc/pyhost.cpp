@@ -26,6 +26,8 @@
 //   wreduce_rows(...)              the data pointers of a task's parameter
 //                                      tensors straight into one
 //                                      dlsim_wreduce_tensors call
+//   wreduce_rows_multi(...)        the same for many tasks, one
+//                                      dlsim_wreduce_batched call
 //
 // Tensor fields (shape, dtype, contiguity, device, data pointer) are read from
 // the at::Tensor itself (libtorch headers; the extension links torch's
@@ -577,6 +579,120 @@ PyObject* py_wreduce_rows(PyObject*, PyObject* args) {
   return result;
 }
 
+// ---- many device tasks' reduces in one library call ------------------------
+//
+// RoundExecutor's wave (dasklearn_amd/batch.py): every task whose models keep
+// their parameters in separate device tensors becomes one sub-task per
+// tensor, all of them through one dlsim_wreduce_batched call (its
+// kernel-argument batches), instead of one wreduce_rows call per task.
+using WreduceBatchedFn = int (*)(int, const int*, const void* const*, const float*, void* const*, const size_t*, int,
+                                 int, void*);
+WreduceBatchedFn g_wreduce_batched = nullptr;
+
+PyObject* py_bind_wreduce_batched(PyObject*, PyObject* addr) {
+  void* p = PyLong_AsVoidPtr(addr);
+  if (!p && PyErr_Occurred()) return nullptr;
+  g_wreduce_batched = reinterpret_cast<WreduceBatchedFn>(p);
+  Py_RETURN_NONE;
+}
+
+// wreduce_rows_multi(tasks, dtype, mode, stream, device) -> rc, or None
+// (nothing launched) if a tensor is not contiguous or not on CUDA device
+// `device`. tasks: [(rows, idx, numels, weights_f32, out_base, out_offsets)],
+// each as wreduce_rows takes them. Sub-tasks of zero elements are skipped.
+PyObject* py_wreduce_rows_multi(PyObject*, PyObject* args) {
+  PyObject* tasks;
+  unsigned long long stream;
+  int dtype, mode, device;
+  if (!PyArg_ParseTuple(args, "OiiKi", &tasks, &dtype, &mode, &stream, &device)) return nullptr;
+  if (!g_wreduce_batched) {
+    PyErr_SetString(PyExc_RuntimeError, "bind_wreduce_batched was not called");
+    return nullptr;
+  }
+  PyObject* tl = PySequence_Fast(tasks, "tasks must be a sequence");
+  if (!tl) return nullptr;
+  std::vector<int> fan;
+  std::vector<const void*> ins;
+  std::vector<float> ws;
+  std::vector<void*> outs;
+  std::vector<size_t> ne;
+  bool ok = true, here = true;
+  std::vector<const at::Tensor*> ts;
+  for (Py_ssize_t q = 0; ok && here && q < PySequence_Fast_GET_SIZE(tl); ++q) {
+    PyObject *rows, *idx, *numels, *weights, *offsets;
+    unsigned long long out_base;
+    if (!PyArg_ParseTuple(PySequence_Fast_GET_ITEM(tl, q), "OOOOKO", &rows, &idx, &numels, &weights, &out_base,
+                          &offsets)) {
+      ok = false;
+      break;
+    }
+    Py_ssize_t n, t;
+    if (!row_tensors(rows, idx, ts, &n, &t)) {
+      ok = false;
+      break;
+    }
+    PyObject* ns = PySequence_Fast(numels, "numels must be a sequence");
+    PyObject* os = ns ? PySequence_Fast(offsets, "out_offsets must be a sequence") : nullptr;
+    Py_buffer wb{};
+    bool have_wb = false;
+    do {
+      if (!os) {
+        ok = false;
+        break;
+      }
+      if (PySequence_Fast_GET_SIZE(ns) != t || PySequence_Fast_GET_SIZE(os) != t) {
+        PyErr_SetString(PyExc_ValueError, "idx, numels and out_offsets differ in length");
+        ok = false;
+        break;
+      }
+      if (PyObject_GetBuffer(weights, &wb, PyBUF_C_CONTIGUOUS) < 0) {
+        ok = false;
+        break;
+      }
+      have_wb = true;
+      if (wb.len != static_cast<Py_ssize_t>(n * sizeof(float))) {
+        PyErr_SetString(PyExc_ValueError, "weights_f32 must hold one float per model");
+        ok = false;
+        break;
+      }
+      const float* w = static_cast<const float*>(wb.buf);
+      for (Py_ssize_t j = 0; here && j < t; ++j) {
+        const size_t e = PyLong_AsSize_t(PySequence_Fast_GET_ITEM(ns, j));
+        const size_t o = PyLong_AsSize_t(PySequence_Fast_GET_ITEM(os, j));
+        if (PyErr_Occurred()) {
+          ok = false;
+          break;
+        }
+        for (Py_ssize_t i = 0; i < n; ++i) {
+          const at::Tensor& x = *ts[static_cast<size_t>(i * t + j)];
+          here = here && x.is_cuda() && x.get_device() == device && x.is_contiguous();
+        }
+        if (!here || e == 0) continue;
+        fan.push_back(static_cast<int>(n));
+        for (Py_ssize_t i = 0; i < n; ++i) {
+          ins.push_back(ts[static_cast<size_t>(i * t + j)]->const_data_ptr());
+          ws.push_back(w[i]);
+        }
+        outs.push_back(reinterpret_cast<void*>(static_cast<uintptr_t>(out_base + o)));
+        ne.push_back(e);
+      }
+    } while (false);
+    if (have_wb) PyBuffer_Release(&wb);
+    Py_XDECREF(os);
+    Py_XDECREF(ns);
+  }
+  Py_DECREF(tl);
+  if (!ok) return nullptr;
+  if (!here) Py_RETURN_NONE;
+  if (fan.empty()) return PyLong_FromLong(0);
+  int rc;
+  Py_BEGIN_ALLOW_THREADS
+  rc = g_wreduce_batched(static_cast<int>(fan.size()), fan.data(), ins.data(), ws.data(), outs.data(), ne.data(),
+                         dtype, mode, reinterpret_cast<void*>(static_cast<uintptr_t>(stream)));
+  Py_END_ALLOW_THREADS
+  return PyLong_FromLong(rc);
+}
+
 // ---- module clone (arena._clone_module restated; see its docstring) --------
 //
 // copy.deepcopy(models[0]) with the parameters taken from the memo: for the
@@ -843,6 +959,9 @@ PyMethodDef kMethods[] = {
      "clone_init(plain_cache, plain_fn, atomic_types, setstate_keys, deepcopy, OrderedDict)"},
     {"clone_module", py_clone_module, METH_VARARGS, "clone_module(module, memo): arena._clone_module in C"},
     {"bind_wreduce_tensors", py_bind_wreduce_tensors, METH_O, "bind dlsim_wreduce_tensors by address"},
+    {"bind_wreduce_batched", py_bind_wreduce_batched, METH_O, "bind dlsim_wreduce_batched by address"},
+    {"wreduce_rows_multi", py_wreduce_rows_multi, METH_VARARGS,
+     "wreduce_rows_multi(tasks, dtype, mode, stream, device): many tasks' tensor rows in one dlsim_wreduce_batched"},
     {"fill_param_views", py_fill_param_views, METH_VARARGS,
      "fill_param_views(memo, arena, specs, params, idx): memo[id(p)] = Parameter view of the arena"},
     {"checked_params", py_checked_params, METH_VARARGS, "module_params(module) if it matches signature, else None"},

@@ -579,6 +579,27 @@ def wreduce_rows(rows, idx: Sequence[int], numels: Sequence[int], weights_f32: n
     return True
 
 
+_BATCHED_BOUND = False
+
+
+def wreduce_rows_multi(tasks, dtype: int, mode: int, stream_handle: int, device: int = 0) -> bool:
+    """Many tasks' wreduce_rows in one dlsim_wreduce_batched call (sub-task =
+    one parameter tensor of one task), pointers collected in C
+    (csrc/pyhost.cpp). tasks: [(rows, idx, numels, weights_f32, out_base,
+    out_offsets)] as wreduce_rows takes them. Returns False, having launched
+    nothing, when a tensor is not contiguous or not on CUDA device `device`."""
+    global _BATCHED_BOUND
+    from . import _pyhost
+    if not _BATCHED_BOUND:
+        _pyhost.bind_wreduce_batched(ctypes.cast(load().dlsim_wreduce_batched, ctypes.c_void_p).value)
+        _BATCHED_BOUND = True
+    rc = _pyhost.wreduce_rows_multi(tasks, dtype, mode, stream_handle or 0, device)
+    if rc is None:
+        return False
+    _check("dlsim_wreduce_batched", rc)
+    return True
+
+
 def wreduce_tensors(inputs_by_model, weights_f32, outs, mode: int = DLSIM_EXACT, stream=None):
     """Tensor-list form: inputs_by_model[i][k] is tensor k of model i."""
     lib = load()

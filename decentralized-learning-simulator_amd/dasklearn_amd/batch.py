@@ -106,9 +106,9 @@ def aggregate_arena_tasks(prepared, mode: int = _native.DLSIM_EXACT,
     rows (optional): every model's parameter list. A dtype group whose arena
     list holds None (a model that keeps its parameters in separate device
     tensors, e.g. a device train task's deepcopy) is read from those tensors
-    in place: one dlsim_wreduce_tensors per task, pointers collected in C
-    (the single-task path's wreduce_rows), instead of copying each such model
-    into an arena first.
+    in place: every such task's tensors in one dlsim_wreduce_batched call per
+    dtype and device (one sub-task per tensor, pointers collected in C),
+    instead of copying each such model into an arena first.
 
     on_launched: called once every launch is queued, before the output
     modules are built; the list `prepared` is consumed while they are (each
@@ -117,6 +117,7 @@ def aggregate_arena_tasks(prepared, mode: int = _native.DLSIM_EXACT,
     made: the arenas stay alive through the launch views, and the stream
     orders any reuse of their memory after the kernels."""
     by_dtype = {}
+    by_rows = {}
     outs = []
     for entry in prepared:
         model0, layout, views, ws = entry[:4]
@@ -127,26 +128,33 @@ def aggregate_arena_tasks(prepared, mode: int = _native.DLSIM_EXACT,
                 dev = _rows_device(vs, rows, layout, dt)
                 out = torch.empty(layout.totals[dt], dtype=dt, device=dev)
                 o[dt] = out
-                stream = torch.cuda.current_stream(dev)
-                w = _native.weights_for_dtype(ws, dt)
                 idx = layout.groups[dt]
                 rows = [_row_on(rows[i], v, idx, layout.split_sizes[dt], dev) for i, v in enumerate(vs)]
-                if not _native.wreduce_rows(rows, idx, layout.split_sizes[dt], w, out.data_ptr(),
-                                            layout.byte_offsets[dt], _native.dtype_code(dt), mode,
-                                            stream.cuda_stream, dev.index):
-                    # a model's tensors are elsewhere (its arena was copied
-                    # here): flatten the in-place ones too, one reduce
-                    with torch.no_grad():
-                        flat = [v if v is not None else
-                                torch._C._nn.flatten_dense_tensors([rows[i][k] for k in idx]).to(dev)
-                                for i, v in enumerate(vs)]
-                    _native.wreduce(flat, w, out, mode, stream)
+                by_rows.setdefault((dt, dev), []).append(
+                    ((rows, idx, layout.split_sizes[dt], _native.weights_for_dtype(ws, dt), out.data_ptr(),
+                      layout.byte_offsets[dt]), vs, out))
                 continue
             dev = vs[0].device
             out = torch.empty(layout.totals[dt], dtype=dt, device=dev)
             o[dt] = out
             by_dtype.setdefault((dt, dev), []).append((vs, _native.weights_for_dtype(ws, dt), out))
         outs.append(o)
+    for (dt, dev), group in by_rows.items():
+        # every task read from separate tensors: one library call for all
+        stream = torch.cuda.current_stream(dev)
+        code = _native.dtype_code(dt)
+        if _native.wreduce_rows_multi([g[0] for g in group], code, mode, stream.cuda_stream, dev.index):
+            continue
+        for (rows, idx, sizes, w, out_ptr, offs), vs, out in group:
+            if not _native.wreduce_rows(rows, idx, sizes, w, out_ptr, offs, code, mode, stream.cuda_stream, dev.index):
+                # a model's tensors are elsewhere (its arena was copied
+                # here): flatten the in-place ones too, one reduce
+                with torch.no_grad():
+                    flat = [v if v is not None else
+                            torch._C._nn.flatten_dense_tensors([rows[i][k] for k in idx]).to(dev)
+                            for i, v in enumerate(vs)]
+                _native.wreduce(flat, w, out, mode, stream)
+    by_rows.clear()
     for (dt, dev), group in by_dtype.items():
         stream = torch.cuda.current_stream(dev)
         if dt == torch.float64:
