@@ -174,3 +174,43 @@ def test_round_executor_reads_device_trained_tensors_in_place(make):
                 xs, ys = x.detach().cpu().reshape(-1), y.detach().reshape(-1)
                 iv = {8: torch.int64, 4: torch.int32, 2: torch.int16}[xs.element_size()]
                 assert torch.equal(xs.view(iv), ys.view(iv)), (p, r, x.dtype)
+
+
+def test_wreduce_rows_multi_matches_per_task_and_refuses_strided_tensors():
+    """The executor's one-call path for many tasks' separate tensors: equal to
+    one wreduce_rows per task (bf16 and fp32, zero-element tensors skipped),
+    and it launches nothing when a tensor is not contiguous."""
+    from dasklearn_amd import _native
+    torch.manual_seed(31)
+    for dt in (torch.float32, torch.bfloat16):
+        shapes = [(7, 5), (0,), (130,), (3, 4, 5)]
+        tasks, exp = [], []
+        for t in range(5):
+            n = 2 + t
+            rows = [[(torch.randn(*s) * 0.1).to(dt).cuda() for s in shapes] for _ in range(n)]
+            w = _native.weights_for_dtype([0.1 * (i + 1) for i in range(n)], dt)
+            sizes = [int(torch.Size(s).numel()) for s in shapes]
+            offs, o = [], 0
+            for sz in sizes:
+                offs.append(o * rows[0][0].element_size())
+                o += sz
+            out = torch.full((o,), float("nan"), dtype=dt, device="cuda")
+            ref = torch.full((o,), float("nan"), dtype=dt, device="cuda")
+            idx = list(range(len(shapes)))
+            assert _native.wreduce_rows(rows, idx, sizes, w, ref.data_ptr(), offs, _native.dtype_code(dt),
+                                        _native.DLSIM_EXACT, torch.cuda.current_stream().cuda_stream, 0)
+            tasks.append((rows, idx, sizes, w, out.data_ptr(), offs))
+            exp.append((out, ref))
+        code = _native.dtype_code(dt)
+        stream = torch.cuda.current_stream().cuda_stream
+        bad = list(tasks)
+        r0 = [list(r) for r in bad[2][0]]
+        r0[1][3] = torch.randn(5, 4, 3).to(dt).cuda().permute(2, 1, 0)  # same shape, strided
+        bad[2] = (r0,) + bad[2][1:]
+        assert not _native.wreduce_rows_multi(bad, code, _native.DLSIM_EXACT, stream, 0)
+        torch.cuda.synchronize()
+        assert all(torch.isnan(out.float()).all() for out, _ in exp)  # nothing was launched
+        assert _native.wreduce_rows_multi(tasks, code, _native.DLSIM_EXACT, stream, 0)
+        for out, ref in exp:
+            assert torch.equal(out.view(torch.int16) if dt == torch.bfloat16 else out.view(torch.int32),
+                               ref.view(torch.int16) if dt == torch.bfloat16 else ref.view(torch.int32))
