@@ -122,6 +122,10 @@ def parse(argv=None):
                     help="process-group backend: nccl (= RCCL over xGMI, the real path); gloo only "
                          "to rehearse the multi-process flow on a box with fewer GPUs than ranks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--two-streams", action="store_true",
+                    help="diagnostic: also time the K steps alternating over two streams (field two_streams); "
+                         "off by default because those overlapping dispatches would enter a rocprof average "
+                         "of the same command")
     ap.add_argument("--no-single-gpu-reference", action="store_true",
                     help="N > 1: skip rank 0's timing of the whole config alone (the speed-up base)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
@@ -522,7 +526,9 @@ def run_rank(args, rank: int, world: int, local: int):
         probe = pattern_ceiling(wl, K, sync, new_event, achieved) if B == 1 else None
         floor = launch_floor(wl, n, dtype, w32, mode, dev, K, sync, new_event, ev_ms / K * 1e3) \
             if B == 1 else None
-        overlap = two_streams(wl, K, sync, dev) if B == 1 else None
+        # opt-in: its concurrent launches share the reduce's kernel name, so
+        # they would skew rocprof's per-dispatch average of the same command
+        overlap = two_streams(wl, K, sync, dev) if B == 1 and args.two_streams else None
         scaling = "weak" if args.weak and world > 1 else "strong"
         workload = args.config + ": " + desc
         if B > 1:
