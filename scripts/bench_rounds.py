@@ -218,6 +218,8 @@ def main():
     ap.add_argument("--model", choices=("gnlenet", "flat", "resnet18"), default="gnlenet",
                     help="gnlenet: the reference's module tree; flat: the same 14 tensors in one ParameterList; "
                          "resnet18: the north star's 62 ResNet-18 parameter tensors in one ParameterList")
+    ap.add_argument("--release-late", action="store_true",
+                    help="RoundExecutor drops a wave's inputs after the wave (release_early=False)")
     ap.add_argument("--flatten", action="store_true",
                     help="RoundExecutor copies device-trained models into arenas first (tensors_in_place=False)")
     ap.add_argument("--profile", default=None, help="cProfile the batched run into this file")
@@ -246,12 +248,14 @@ def main():
     # warm-up at full size (library load, kernels, and the device and pinned
     # allocator caches for a wave's buffers, so the timed rounds are steady state)
     wt, _ = dag(a.peers, 1)
-    RoundExecutor({"train": tr}, Settings(), device=dev, tensors_in_place=not a.flatten).run(
+    RoundExecutor({"train": tr}, Settings(), device=dev, tensors_in_place=not a.flatten,
+                  release_early=not a.release_late).run(
         wt, seed={"init": [init_x]})
     sequential(wt, aggregate, init_x, sync, tr)
 
     def run_batched(profile=None):
-        ex = RoundExecutor({"train": tr}, Settings(), device=dev, timing=True, tensors_in_place=not a.flatten)
+        ex = RoundExecutor({"train": tr}, Settings(), device=dev, timing=True, tensors_in_place=not a.flatten,
+                           release_early=not a.release_late)
         wave = ex._aggregate_wave
 
         def metered(aggs, *rest):  # the executor times the wave plus a sync
@@ -323,7 +327,8 @@ def main():
     def line(kind):
         per = statistics.median(samples[kind])
         return {"kind": kind + ("_host_models" if a.host and not kind.startswith("cpu") else "")
-                + ("_flatten" if a.flatten and kind == "batched" else ""), "model": a.model,
+                + ("_flatten" if a.flatten and kind == "batched" else "")
+                + ("_release_late" if a.release_late and kind == "batched" else ""), "model": a.model,
                 "peers": a.peers,
                 "fan_in": fan, "reps": len(samples[kind]), "params": p,
                 "ms_per_round": round(per * a.peers * 1e3, 3), "us_per_task": round(per * 1e6, 1),

@@ -28,15 +28,16 @@ def device_agnostic_train(settings, params):
     return [out]
 
 
+@pytest.mark.parametrize("release_early", [False, True])
 @pytest.mark.parametrize("n,rounds", [(4, 2), (10, 3)])
-def test_round_executor_matches_sequential_replay(n, rounds):
+def test_round_executor_matches_sequential_replay(n, rounds, release_early):
     torch.manual_seed(21)
     init = Shaped(GNLENET)
     with torch.no_grad():
         for p in init.parameters():
             p.copy_(torch.randn(p.shape) * 0.05)
     tasks, nb = build_dag(n, rounds)
-    ex = RoundExecutor({"train": device_agnostic_train}, Settings())
+    ex = RoundExecutor({"train": device_agnostic_train}, Settings(), release_early=release_early)
     got = ex.run(tasks, seed={"init": [init]})
     exp = replay(tasks, {"aggregate": oracle_aggregate, "train": device_agnostic_train}, init)
     # waves: all trains of a round, then all aggregates of that round
