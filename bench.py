@@ -582,6 +582,18 @@ def run_rank(args, rank: int, world: int, local: int):
             result["cpu_baseline"] = cpu_baseline(args.config, n, p, dtype, weights, args.cpu_seconds)
         else:
             result["cpu_baseline"] = None
+    if world > 1 and args.backend == "nccl" and strong:
+        # last, and under a watchdog: RCCL calls made by the library itself
+        def on_timeout():
+            if rank == 0:
+                result["allgather"]["dlsim_wreduce_sharded_error"] = \
+                    f"timed out after {SHARDED_TIMEOUT_S:.0f} s; line printed without it"
+                print(json.dumps(result), file=_RESULT_OUT or sys.stdout, flush=True)
+        sharded = _guarded(lambda: _time_sharded(wl, n, p_cfg, w32, mode, dtype, dev, cdev, stream, barrier),
+                           SHARDED_TIMEOUT_S, on_timeout)
+        if rank == 0:
+            result["allgather"].update(sharded)
+    if rank == 0:
         print(json.dumps(result), file=_RESULT_OUT or sys.stdout, flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -605,10 +617,9 @@ class _StreamEvent:
 
 def _time_gathers(args, wl, rank, world, p_cfg, p, n, w32, mode, dtype, dev, cdev, stream, strong, barrier):
     """The collective that would materialise the full output, timed apart
-    from `value`: (a) RCCL all_gather_into_tensor of width-padded slices
-    (torch), (b) on an RCCL group, the C ABI's dlsim_wreduce_sharded end to
-    end (this rank's reduce into the full buffer + grouped in-place
-    ncclBroadcast of every rank's slice, a variable-size all-gather)."""
+    from `value`: RCCL all_gather_into_tensor of width-padded slices (torch).
+    The C ABI's own gather (dlsim_wreduce_sharded) is timed at the end of the
+    run, under a watchdog (_time_sharded, _guarded)."""
     from dasklearn_amd import _native
     tdt = TORCH_DTYPE[dtype]
     esz = ELEM_BYTES[dtype]
@@ -634,34 +645,72 @@ def _time_gathers(args, wl, rank, world, p_cfg, p, n, w32, mode, dtype, dev, cde
            "note": ("RCCL" if args.backend == "nccl" else "gloo (rehearsal)")
                    + " collectives of the reduced slices; host clock over 20 back-to-back ops after a sync; "
                      "not in value"}
-    if args.backend == "nccl" and strong:
-        try:
-            pg = dist.distributed_c10d._get_default_group()
-            comm = int(pg._get_backend(dev)._comm_ptr())
-            slices = [wl.plans[0]._keep[0][i] for i in range(n)]
-            fullout = torch.empty(p_cfg, dtype=tdt, device=dev)
-            for _ in range(3):
-                _native.wreduce_sharded(slices, w32, fullout, comm, True, mode, stream)
-            torch.cuda.synchronize(dev)
-            barrier()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-            for _ in range(reps):
-                _native.wreduce_sharded(slices, w32, fullout, comm, True, mode, stream)
-            e1.record(stream)
-            torch.cuda.synchronize(dev)
-            out["dlsim_wreduce_sharded_gather_ms"] = e0.elapsed_time(e1) / reps
-            out["sharded_note"] = ("dlsim_wreduce_sharded(gather=1) on the group's RCCL communicator: local reduce "
-                                   "+ grouped in-place ncclBroadcast, HIP events on the launch stream")
-        except Exception as e:  # report, do not fail the bench line
-            out["dlsim_wreduce_sharded_error"] = f"{type(e).__name__}: {e}"[:300]
-    t = torch.tensor([out["all_gather_into_tensor_ms"], out.get("dlsim_wreduce_sharded_gather_ms", 0.0)],
-                     dtype=torch.float64, device=cdev)
+    t = torch.tensor([out["all_gather_into_tensor_ms"]], dtype=torch.float64, device=cdev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     out["all_gather_into_tensor_ms"] = round(float(t[0]), 4)
-    if "dlsim_wreduce_sharded_gather_ms" in out:
-        out["dlsim_wreduce_sharded_gather_ms"] = round(float(t[1]), 4)
     return out
+
+
+SHARDED_TIMEOUT_S = 90.0
+
+
+def _time_sharded(wl, n, p_cfg, w32, mode, dtype, dev, cdev, stream, barrier, reps: int = 20):
+    """The C ABI's dlsim_wreduce_sharded end to end on the group's own RCCL
+    communicator: this rank's reduce into the full buffer + grouped in-place
+    ncclBroadcast of every rank's slice (a variable-size all-gather), HIP
+    events on the launch stream, max over ranks."""
+    from dasklearn_amd import _native
+    out = {}
+    try:
+        pg = dist.distributed_c10d._get_default_group()
+        comm = int(pg._get_backend(dev)._comm_ptr())
+        slices = [wl.plans[0]._keep[0][i] for i in range(n)]
+        fullout = torch.empty(p_cfg, dtype=TORCH_DTYPE[dtype], device=dev)
+        for _ in range(3):
+            _native.wreduce_sharded(slices, w32, fullout, comm, True, mode, stream)
+        torch.cuda.synchronize(dev)
+        barrier()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            _native.wreduce_sharded(slices, w32, fullout, comm, True, mode, stream)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        ms = e0.elapsed_time(e1) / reps
+        out["sharded_note"] = ("dlsim_wreduce_sharded(gather=1) on the group's RCCL communicator: local reduce "
+                               "+ grouped in-place ncclBroadcast, HIP events on the launch stream, max over ranks")
+    except Exception as e:  # report, do not fail the bench line
+        ms = -1.0
+        out["dlsim_wreduce_sharded_error"] = f"{type(e).__name__}: {e}"[:300]
+    t = torch.tensor([ms], dtype=torch.float64, device=cdev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if ms >= 0:
+        out["dlsim_wreduce_sharded_gather_ms"] = round(float(t[0]), 4)
+    return out
+
+
+def _guarded(fn, timeout_s: float, on_timeout):
+    """fn() with a watchdog: a collective issued outside torch's own watchdog
+    (the C ABI's RCCL calls) must not hold the bench line hostage. If fn has
+    not returned after timeout_s, on_timeout() runs (rank 0 prints the line
+    it has) and the process exits."""
+    import threading
+    done = threading.Event()
+
+    def fire():
+        if not done.is_set():
+            try:
+                on_timeout()
+            finally:
+                os._exit(0)
+    timer = threading.Timer(timeout_s, fire)
+    timer.daemon = True
+    timer.start()
+    try:
+        return fn()
+    finally:
+        done.set()
+        timer.cancel()
 
 
 def main(argv=None):

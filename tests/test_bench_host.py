@@ -108,3 +108,24 @@ def test_rank_stdout_carries_only_the_result_line(tmp_path):
     assert r.returncode == 0, r.stderr
     assert r.stdout.splitlines() == ['{"value": 1}']
     assert "[Gloo] Rank 0" in r.stderr and "a stray print" in r.stderr
+
+
+def test_guarded_returns_or_prints_and_exits_on_timeout(tmp_path):
+    """bench._guarded: a call that returns in time gives its value; one that
+    hangs past the timeout runs on_timeout (rank 0 prints its line) and the
+    process exits 0 instead of holding the multi-GPU bench hostage."""
+    import subprocess
+    assert bench._guarded(lambda: 42, 5.0, lambda: None) == 42
+    script = tmp_path / "child.py"
+    script.write_text(textwrap.dedent(f"""
+        import sys, time
+        sys.path.insert(0, {ROOT!r})
+        import bench
+        bench._guarded(lambda: time.sleep(30), 0.5, lambda: print('{{"value": 7}}', flush=True))
+        print("not reached", flush=True)
+    """))
+    t0 = time.perf_counter()
+    r = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.splitlines() == ['{"value": 7}']
+    assert time.perf_counter() - t0 < 25
