@@ -103,24 +103,27 @@ class RoundExecutor:
             return {k: self._resolve(x) for k, x in v.items()}
         return v
 
-    def _layout_for(self, m: nn.Module) -> ParamLayout:
+    def _layout_for(self, m: nn.Module, params=None) -> ParamLayout:
         """m's ParamLayout; a model of a class seen before reuses that layout
         when the parameter signature matches (arena.layout_of)."""
-        return layout_of(m)
+        return layout_of(m, params)
 
-    def _arena_of(self, m: nn.Module, cache: dict):
+    def _arena_of(self, m: nn.Module, cache: dict, walked: Optional[dict] = None):
         """(layout over m's parameters, {dtype: flat device arena}) for one
         model, once per wave (`cache` keeps the model alive, so its id cannot
-        be reused while the entry exists)."""
+        be reused while the entry exists). walked: {id(m): (m, parameters)}
+        from this wave's upload scan, so the parameters are walked once."""
         hit = cache.get(id(m))
         if hit is not None and hit[0] is m:
             return hit[1], hit[2]
-        reg = registered_arenas(m)
+        w = walked.get(id(m)) if walked is not None else None
+        ps = w[1] if w is not None and w[0] is m else None
+        reg = registered_arenas(m, ps)
         if reg is not None:  # an aggregate output: its arenas as they are
             layout, ar = reg
             views = {dt: [ar[dt]] for dt in layout.groups}
         else:
-            layout = self._layout_for(m)
+            layout = self._layout_for(m, ps)
             views = {dt: None if (v := layout.arena_view(layout.params, dt)) is None else [v]
                      for dt in layout.groups}
         params = [layout.params]
@@ -160,7 +163,7 @@ class RoundExecutor:
             buf = self._stages[k] = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
         return buf
 
-    def _upload_host_models(self, models, cache: dict) -> None:
+    def _upload_host_models(self, models, cache: dict, walked: Optional[dict] = None) -> None:
         """Every host model of a wave (the reference's CPU-trained models) to
         the device in bounded groups: the library's threads pack a group's
         parameters into a persistent pinned buffer (dlsim_host_pack; one arena
@@ -169,16 +172,22 @@ class RoundExecutor:
         its own) and alternate between two pinned buffers, so the pack of
         group g+1 overlaps the copy of group g and pinned memory stays bounded
         by two groups, however many models a wave has. Fills `cache` as
-        _arena_of would (instead of one small H2D per parameter tensor)."""
+        _arena_of would (instead of one small H2D per parameter tensor).
+        walked: filled with {id(m): (m, parameters)} for the models it walks
+        and leaves to _arena_of."""
         pending, seen = [], set()
         for m in models:
-            if id(m) in seen or (id(m) in cache and cache[id(m)][0] is m) or registered_arenas(m) is not None:
+            if id(m) in seen or (id(m) in cache and cache[id(m)][0] is m):
                 continue
             seen.add(id(m))
             ps = module_params(m)
+            if walked is not None:
+                walked[id(m)] = (m, ps)
+            if registered_arenas(m, ps) is not None:
+                continue
             if not ps or any(p.get_device() != -1 for p in ps):
                 continue
-            pending.append((m, self._layout_for(m)))
+            pending.append((m, self._layout_for(m, ps)))
         if not pending:
             return
         dev = _target_device(pending[0][1].params, self.device)
@@ -232,9 +241,10 @@ class RoundExecutor:
             models = d["models"]
             ws = _resolve(models, d.get("weights"))  # fedavg.py:14-17 rules and exceptions
             resolved.append((models, ws))
-        self._upload_host_models([m for models, _ in resolved for m in models], cache)
+        walked: dict = {}
+        self._upload_host_models([m for models, _ in resolved for m in models], cache, walked)
         for models, ws in resolved:
-            ents = [self._arena_of(m, cache) for m in models]
+            ents = [self._arena_of(m, cache, walked) for m in models]
             layout0 = ents[0][0]
             sig = layout0._signature
             for i in range(1, len(ents)):
@@ -245,6 +255,7 @@ class RoundExecutor:
             prepared.append((models[0], layout0, views, ws, [lay.params for lay, _ in ents]))
         resolved.clear()
         cache.clear()
+        walked.clear()
         return aggregate_arena_tasks(prepared, self.mode, on_launched)
 
     def run(self, tasks: Sequence[Task], seed: Optional[Dict[str, list]] = None) -> Dict[str, list]:
