@@ -343,6 +343,15 @@ void add_nf(std::vector<Variant>& vs, int n) {
   vs.push_back({p + "_V4_nt_wave", launch_ts<Op, NF, 8, 4, 1, kStNT, true>, 0});
   vs.push_back({p + "_V1_plain", launch_ts<Op, NF, 8, 1, 1, kStPlain, true>, 0});
   vs.push_back({p + "_V1_sc1_ldplain", launch_ts<Op, NF, 8, 1, 0, 16, true>, 0});
+  // load cache-policy bits on the shipped large shape (round 2, session 2):
+  // buffer loads with sc0 = 1, nt = 2, sc1 = 16 combinations
+  vs.push_back({p + "_V4w_ldb_nt", launch_ts<Op, NF, 8, 4, kLdBuffer + 2, 16, true>, 0});
+  vs.push_back({p + "_V4w_ldb_sc0nt", launch_ts<Op, NF, 8, 4, kLdBuffer + 3, 16, true>, 0});
+  vs.push_back({p + "_V4w_ldb_sc1nt", launch_ts<Op, NF, 8, 4, kLdBuffer + 18, 16, true>, 0});
+  vs.push_back({p + "_V4w_ldb_sc01nt", launch_ts<Op, NF, 8, 4, kLdBuffer + 19, 16, true>, 0});
+  vs.push_back({p + "_V4w_ldb_sc1", launch_ts<Op, NF, 8, 4, kLdBuffer + 16, 16, true>, 0});
+  vs.push_back({p + "_V4w_ldb_sc01", launch_ts<Op, NF, 8, 4, kLdBuffer + 17, 16, true>, 0});
+  vs.push_back({p + "_V4w_ldb_plain", launch_ts<Op, NF, 8, 4, kLdBuffer + 0, 16, true>, 0});
 }
 
 template <class Op>
