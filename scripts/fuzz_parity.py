@@ -16,6 +16,10 @@ shapes, dtypes, alignments, weights and special values, for a time budget.
   host_reduce dlsim_host_wreduce (random host tensors at odd offsets, pipeline
               chunks, pack threads, side streams or not) vs the oracle
   host_chunk  dlsim_host_chunk_mean (random tasks, threads) vs PyTorch's CPU order
+  executor    RoundExecutor on random DAGs of random module trees, each train
+              output on the device or the host at random (in-place tensors,
+              registered arenas, uploaded host models, fp64 groups in one
+              wave), random release/in-place settings, vs an oracle replay
 
 Prints one JSON line with the case counts and the first failures (if any).
 
@@ -152,6 +156,69 @@ def rand_module(rng, seed):
     return Tree()
 
 
+def executor_case(rng):
+    """RoundExecutor on a random D-PSGD-like DAG against a host replay with the
+    oracle aggregate (the reference's op sequence). Training computes its
+    update on the host, so both sides train to the same bits; where each train
+    output lives (device or host) is drawn per task."""
+    import copy
+    from dasklearn_amd.rounds import RoundExecutor
+    from oracle import fedavg_torch
+    n = int(rng.integers(2, 7))
+    rounds = int(rng.integers(1, 3))
+    base = int(rng.integers(0, 1 << 30))
+    init = rand_module(np.random.default_rng(base), base)
+    place = {(p, r): str(rng.choice(["cuda", "cpu"])) for p in range(n) for r in range(1, rounds + 1)}
+    tasks = []
+    for r in range(1, rounds + 1):
+        for p in range(n):
+            src = ("init", 0) if r == 1 else (f"agg_{p}_{r - 1}", 0)
+            tasks.append((f"train_{p}_{r}", "train", {"model": src, "round": r, "peer": p}))
+        for p in range(n):
+            nb = sorted({int(q) for q in rng.choice(n, size=int(rng.integers(1, n + 1)))} - {p})
+            models = [(f"train_{q}_{r}", 0) for q in nb] + [(f"train_{p}_{r}", 0)]
+            if r > 1 and rng.random() < 0.3:
+                models.append((f"agg_{p}_{r - 1}", 0))  # a registered arena output too
+            data = {"models": models, "round": r, "peer": p}
+            if rng.random() < 0.6:
+                data["weights"] = [float(v) for v in rng.standard_normal(len(models))]
+            tasks.append((f"agg_{p}_{r}", "aggregate", data))
+
+    def make_train(host_only):
+        def train(settings, params):
+            r, p = params["round"], params["peer"]
+            out = copy.deepcopy(params["model"]).to("cpu" if host_only else place[(p, r)])
+            g = torch.Generator().manual_seed(1000 * r + p)
+            with torch.no_grad():
+                for q in out.parameters():
+                    q.copy_((q.detach().cpu() + (torch.randn(q.shape, generator=g) * 0.01).to(q.dtype)).to(q.device))
+            return [out]
+        return train
+
+    class S:
+        pass
+    ex = RoundExecutor({"train": make_train(False)}, S(), release_early=bool(rng.random() < 0.7),
+                       tensors_in_place=bool(rng.random() < 0.8))
+    got = ex.run(tasks, seed={"init": [copy.deepcopy(init).to(str(rng.choice(["cuda", "cpu"])))]})
+    results = {"init": [init]}
+    tr = make_train(True)
+    for name, func, data in tasks:
+        d = {k: ([results[x[0]][x[1]] for x in v] if k == "models" else
+                 (results[v[0]][v[1]] if isinstance(v, tuple) else v)) for k, v in data.items()}
+        results[name] = tr(None, d) if func == "train" else [fedavg_torch.aggregate_modules(d["models"],
+                                                                                            d.get("weights"))]
+    ok = True
+    for name, res in got.items():
+        if not name.startswith("agg_"):
+            continue
+        a, b = res[0], results[name][0]
+        for x, y in zip(a.parameters(), b.parameters()):
+            ok = ok and x.dtype == y.dtype and orc.same_bits(bits(x.detach().reshape(-1).cpu()),
+                                                             bits(y.detach().reshape(-1)))
+    return ok, dict(kind="executor", n=n, rounds=rounds, release_early=ex.release_early,
+                    in_place=ex.tensors_in_place)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=120.0)
@@ -159,7 +226,7 @@ def main():
     a = ap.parse_args()
     rng = np.random.default_rng(a.seed)
     counts = {"reduce": 0, "reduce_fast": 0, "tensors": 0, "batched": 0, "chunk_mean": 0, "modules": 0,
-              "reconstruct": 0, "host_reduce": 0, "host_chunk": 0}
+              "reconstruct": 0, "host_reduce": 0, "host_chunk": 0, "executor": 0}
     fails = []
     t_end = time.time() + a.seconds
     t_note = time.time() + 20
@@ -169,8 +236,8 @@ def main():
             t_note = time.time() + 20
         dtype = str(rng.choice(["f32", "bf16", "f16", "f64"]))
         which = rng.choice(["reduce", "tensors", "batched", "chunk_mean", "modules", "reconstruct",
-                            "host_reduce", "host_chunk"],
-                           p=[0.25, 0.1, 0.1, 0.2, 0.1, 0.1, 0.1, 0.05])
+                            "host_reduce", "host_chunk", "executor"],
+                           p=[0.22, 0.1, 0.1, 0.18, 0.1, 0.1, 0.1, 0.05, 0.05])
         if dtype == "f64" and which != "reduce":  # fp64 is the single-task entry (dlsim_wreduce_f64)
             dtype = "f32"
         try:
@@ -343,6 +410,9 @@ def main():
                 counts["host_reduce"] += 1
                 case = dict(kind="host_reduce", dtype=dtype, n=n, p=p, tensors=len(sizes), chunk=chunk,
                             threads=threads, side=side)
+            elif which == "executor":
+                ok, case = executor_case(rng)
+                counts["executor"] += 1
             elif which == "host_chunk":
                 from dasklearn_amd.arena import _side_streams
                 cpu_threads = int(rng.choice([1, 2, 4, 8, 16]))
