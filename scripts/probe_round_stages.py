@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--release-late", action="store_true", help="RoundExecutor(release_early=False)")
     ap.add_argument("--nogc", action="store_true", help="collector disabled inside the waves (diagnostic)")
+    ap.add_argument("--freeze", action="store_true", help="gc.freeze() once the models exist (application-level)")
     a = ap.parse_args()
     from dasklearn_amd import batch, rounds
 
@@ -80,6 +81,10 @@ def main():
 
     rounds.aggregate_arena_tasks = timed_arena_tasks
     rounds.RoundExecutor._aggregate_wave = timed_wave
+    if a.freeze:
+        import gc
+        gc.collect()
+        gc.freeze()  # everything alive now moves to the permanent generation
     try:
         for _ in range(2):
             rec.clear()
@@ -89,7 +94,7 @@ def main():
         rounds.aggregate_arena_tasks = orig_arena_tasks
         rounds.RoundExecutor._aggregate_wave = orig_wave
     out = {"model": a.model, "peers": a.peers, "fan_in": fan, "waves": len(rec), "release_early": not a.release_late,
-           "gc_in_waves": not a.nogc}
+           "gc_in_waves": not a.nogc, "gc_freeze": a.freeze}
     for k in ("resolve", "launch", "release", "modules", "drain"):
         out[k + "_us_per_task"] = round(statistics.median(r[k] / r["n"] for r in rec) * 1e6, 1)
     print(json.dumps(out), flush=True)
