@@ -16,7 +16,8 @@ contributors per index (success_fraction 1: the sample size).
   cpu_ref     the reference's arithmetic on the CPU: per index
               torch.mean(torch.stack(chunks), 0), then cat + copy, 4 threads
 
-    python scripts/bench_chunks.py
+    python scripts/bench_chunks.py            # flat 11 M model, m = 4 and 10
+    python scripts/bench_chunks.py --models   # ResNet-18 and GNLeNet state_dicts
 """
 from __future__ import annotations
 
@@ -190,6 +191,32 @@ def resnet_case(dev, m=4, k=10):
     return res
 
 
+def gnlenet_case(dev, m=4, k=10, reps=200):
+    """The same on the reference's default model (GNLeNet's module tree,
+    14 state_dict entries, 85,354 params): per-task cost, not bandwidth."""
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    from bench_rounds import GNLeNetTree
+    torch.manual_seed(0)
+    models = [GNLeNetTree() for _ in range(m)]
+    host_chunks = [ChunkManager.chunk_model(mdl, k) for mdl in models]
+    by_index = [[host_chunks[i][c] for i in range(m)] for c in range(k)]
+    dev_by_index = [[c.to(dev) for c in cs] for cs in by_index]
+    res = {"case": "gnlenet_state_dict", "k": k, "m": m, "entries": len(models[0].state_dict())}
+    tgt_d = GNLeNetTree().to(dev)
+    res["device_us"] = round(med(lambda: ChunkManager.reconstruct_model([list(c) for c in dev_by_index], tgt_d),
+                                 reps=reps) * 1e6, 1)
+    tgt_h = GNLeNetTree()
+    res["host_us"] = round(med(lambda: ChunkManager.reconstruct_model([list(c) for c in by_index], tgt_h),
+                               reps=reps) * 1e6, 1)
+    nt = torch.get_num_threads()
+    torch.set_num_threads(4)
+    tgt_c = GNLeNetTree()
+    res["cpu_ref_4t_us"] = round(med(lambda: cpu_reconstruct([list(c) for c in by_index], tgt_c), reps=reps,
+                                     sync=False) * 1e6, 1)
+    torch.set_num_threads(nt)
+    return res
+
+
 def _wrap(flat):
     m = Flat()
     m.w = nn.Parameter(flat, requires_grad=False)
@@ -197,5 +224,10 @@ def _wrap(flat):
 
 
 if __name__ == "__main__":
-    main()
+    if "--models" in sys.argv:  # the two real module trees only
+        d = torch.device("cuda", 0)
+        print(json.dumps(resnet_case(d)), flush=True)
+        print(json.dumps(gnlenet_case(d)), flush=True)
+    else:
+        main()
     print(json.dumps(resnet_case(torch.device("cuda", 0))), flush=True)
