@@ -104,6 +104,7 @@ typedef int rccl_result_t;  // ncclResult_t
 struct Rccl {
   void* lib = nullptr;
   rccl_result_t (*bcast)(const void*, void*, size_t, int, int, void*, hipStream_t) = nullptr;
+  rccl_result_t (*allreduce)(const void*, void*, size_t, int, int, void*, hipStream_t) = nullptr;
   rccl_result_t (*group_start)() = nullptr;
   rccl_result_t (*group_end)() = nullptr;
   rccl_result_t (*count)(void*, int*) = nullptr;
@@ -112,6 +113,7 @@ struct Rccl {
 };
 Rccl g_rccl;
 constexpr int kRcclFloat16 = 6, kRcclFloat32 = 7, kRcclBfloat16 = 9;  // ncclDataType_t (rccl.h)
+constexpr int kRcclInt64 = 4, kRcclMax = 2;                           // ncclInt64, ncclMax
 
 int rccl_fail(rccl_result_t r, const char* what) {
   return fail(DLSIM_E_RCCL, "%s: %s (ncclResult %d)", what, g_rccl.err ? g_rccl.err(r) : "?", r);
@@ -359,14 +361,58 @@ int dlsim_rccl_bind(const char* librccl_path) {
   Rccl r;
   r.lib = h;
   r.bcast = reinterpret_cast<decltype(r.bcast)>(dlsym(h, "ncclBroadcast"));
+  r.allreduce = reinterpret_cast<decltype(r.allreduce)>(dlsym(h, "ncclAllReduce"));
   r.group_start = reinterpret_cast<decltype(r.group_start)>(dlsym(h, "ncclGroupStart"));
   r.group_end = reinterpret_cast<decltype(r.group_end)>(dlsym(h, "ncclGroupEnd"));
   r.count = reinterpret_cast<decltype(r.count)>(dlsym(h, "ncclCommCount"));
   r.user_rank = reinterpret_cast<decltype(r.user_rank)>(dlsym(h, "ncclCommUserRank"));
   r.err = reinterpret_cast<decltype(r.err)>(dlsym(h, "ncclGetErrorString"));
-  if (!r.bcast || !r.group_start || !r.group_end || !r.count || !r.user_rank || !r.err)
+  if (!r.bcast || !r.allreduce || !r.group_start || !r.group_end || !r.count || !r.user_rank || !r.err)
     return fail(DLSIM_E_RCCL, "%s lacks an RCCL symbol", librccl_path);
   g_rccl = r;
+  return DLSIM_OK;
+}
+
+// The agreement step of dlsim_wreduce_sharded: one
+// int64 MAX all-reduce of [a failure slot per rank | n_elems, -n_elems,
+// dtype, -dtype, gather, -gather] on the caller's stream, read back by the
+// host. Every rank learns which ranks failed their local checks (or their
+// local reduce launch) and whether all ranks agree on the arguments that
+// shape the broadcast group, so either every rank enters the group or none
+// does. Sets *failed to the failing ranks and *mismatch to the disagreement.
+int sharded_agree(void* comm, int world, int rank, bool local_fail, size_t n_elems, int dtype, int gather,
+                  hipStream_t st, std::vector<int>* failed, bool* mismatch) {
+  const int nw = world + 6;
+  std::vector<int64_t> w(static_cast<size_t>(nw), 0);
+  w[rank] = local_fail ? 1 : 0;
+  const int64_t args[3] = {static_cast<int64_t>(n_elems), dtype, gather ? 1 : 0};
+  for (int k = 0; k < 3; ++k) {
+    w[world + 2 * k] = args[k];
+    w[world + 2 * k + 1] = -args[k];
+  }
+  void* d = nullptr;
+  const size_t bytes = sizeof(int64_t) * static_cast<size_t>(nw);
+  hipError_t e = hipMallocAsync(&d, bytes, st);
+  if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(agreement)");
+  int rc = DLSIM_OK;
+  e = hipMemcpyAsync(d, w.data(), bytes, hipMemcpyHostToDevice, st);
+  if (e != hipSuccess) rc = hip_fail(e, "hipMemcpyAsync(agreement H2D)");
+  if (rc == DLSIM_OK) {
+    const rccl_result_t rr = g_rccl.allreduce(d, d, static_cast<size_t>(nw), kRcclInt64, kRcclMax, comm, st);
+    if (rr != 0) rc = rccl_fail(rr, "ncclAllReduce(agreement)");
+  }
+  if (rc == DLSIM_OK) {
+    e = hipMemcpyAsync(w.data(), d, bytes, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) rc = hip_fail(e, "agreement D2H");
+  }
+  (void)hipFreeAsync(d, st);
+  if (rc != DLSIM_OK) return rc;
+  failed->clear();
+  for (int r = 0; r < world; ++r)
+    if (w[r] != 0) failed->push_back(r);
+  *mismatch = false;
+  for (int k = 0; k < 3; ++k) *mismatch |= w[world + 2 * k] != -w[world + 2 * k + 1];
   return DLSIM_OK;
 }
 
@@ -381,26 +427,48 @@ int dlsim_wreduce_sharded(const void* const* d_slices, size_t slice_elems, int n
   if (rr != 0) return rccl_fail(rr, "ncclCommCount");
   rr = g_rccl.user_rank(rccl_comm, &rank);
   if (rr != 0) return rccl_fail(rr, "ncclCommUserRank");
-  if (n_elems > 0 && !d_out) return fail(DLSIM_E_ARG, "null output pointer");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  // Rank-local checks and the local reduce: a failure here is not returned
+  // before the other ranks have heard of it (sharded_agree), so no rank is
+  // left waiting inside the broadcast group.
   size_t b = 0, e = 0;
-  int rc = dlsim_shard_range(n_elems, world, rank, 64, &b, &e);
-  if (rc != DLSIM_OK) return rc;
-  if (slice_elems != e - b)
-    return fail(DLSIM_E_ARG, "rank %d of %d: slices have %zu elements, its shard [%zu, %zu) has %zu", rank, world,
-                slice_elems, b, e, e - b);
-  const size_t esz = elem_bytes(dtype);
+  int rc = DLSIM_OK;
+  if (n_elems > 0 && !d_out) rc = fail(DLSIM_E_ARG, "null output pointer");
+  if (rc == DLSIM_OK) rc = dlsim_shard_range(n_elems, world, rank, 64, &b, &e);
+  if (rc == DLSIM_OK && slice_elems != e - b)
+    rc = fail(DLSIM_E_ARG, "rank %d of %d: slices have %zu elements, its shard [%zu, %zu) has %zu", rank, world,
+              slice_elems, b, e, e - b);
+  const size_t esz = known_dtype(dtype) ? elem_bytes(dtype) : 0;
   char* out = static_cast<char*>(d_out);
-  // this rank's slice of every model -> this rank's slice of the output
-  if (e > b) {
-    rc = dlsim_wreduce(d_slices, n, h_weights, out + b * esz, e - b, dtype, mode, stream);
-    if (rc != DLSIM_OK) return rc;
-  } else {
-    rc = check_args(d_slices, n, h_weights, nullptr, 0, dtype, mode);
-    if (rc != DLSIM_OK) return rc;
+  if (rc == DLSIM_OK) {
+    // this rank's slice of every model -> this rank's slice of the output
+    if (e > b) rc = dlsim_wreduce(d_slices, n, h_weights, out + b * esz, e - b, dtype, mode, stream);
+    else rc = check_args(d_slices, n, h_weights, nullptr, 0, dtype, mode);
+  }
+  if (world > 1) {
+    const std::string local_err = g_err;
+    std::vector<int> failed;
+    bool mismatch = false;
+    const int arc = sharded_agree(rccl_comm, world, rank, rc != DLSIM_OK, n_elems, dtype, gather, st, &failed,
+                                  &mismatch);
+    if (arc != DLSIM_OK) return arc;
+    if (rc != DLSIM_OK) {
+      g_err = local_err;
+      return rc;
+    }
+    if (!failed.empty()) {
+      std::string who;
+      for (int r : failed) who += (who.empty() ? "" : ",") + std::to_string(r);
+      return fail(DLSIM_E_PEER, "rank(s) %s of %d failed their checks; no rank entered the broadcast group",
+                  who.c_str(), world);
+    }
+    if (mismatch)
+      return fail(DLSIM_E_ARG, "ranks disagree on n_elems, dtype or gather; no rank entered the broadcast group");
+  } else if (rc != DLSIM_OK) {
+    return rc;
   }
   if (!gather || world == 1 || n_elems == 0) return DLSIM_OK;
   // variable-size all-gather: every rank broadcasts its slice in place
-  hipStream_t st = static_cast<hipStream_t>(stream);
   const int dt = dtype == DLSIM_BF16 ? kRcclBfloat16 : dtype == DLSIM_F16 ? kRcclFloat16 : kRcclFloat32;
   rr = g_rccl.group_start();
   if (rr != 0) return rccl_fail(rr, "ncclGroupStart");

@@ -22,6 +22,9 @@ DLSIM_F64 = 3
 DLSIM_EXACT = 0
 DLSIM_FAST = 1
 MAX_FUSED_INPUTS = 128
+DLSIM_E_ARG = -1
+DLSIM_E_RCCL = -4
+DLSIM_E_PEER = -5  # another rank failed (dlsim_wreduce_sharded's agreement step)
 
 # Every symbol include/dlsim.h declares (tests/test_abi.py checks the header
 # against this list and the library's exports).
@@ -533,6 +536,20 @@ def wreduce_sharded(slices, weights_f32, out, comm_ptr: int, gather: bool = True
                                      out.numel(), dtype_code(out.dtype), mode, ctypes.c_void_p(comm_ptr),
                                      1 if gather else 0, _stream_handle(out.device, stream)))
     return out
+
+
+def wreduce_sharded_failed(comm_ptr: int, n_elems: int, gather: bool, device, stream=None) -> None:
+    """Join dlsim_wreduce_sharded's agreement step as a rank whose arguments
+    already failed the caller's own checks (no slices, no output): the library
+    tells every other rank, so none enters the broadcast group, and this call
+    returns the library's own argument error (raised as DlsimError)."""
+    lib = load()
+    if _RCCL_BOUND is None:
+        rccl_bind()
+    _check("dlsim_wreduce_sharded",
+           lib.dlsim_wreduce_sharded(None, ctypes.c_size_t(-1 & 0xFFFFFFFFFFFFFFFF), 0, None, None, n_elems,
+                                     DLSIM_F32, DLSIM_EXACT, ctypes.c_void_p(comm_ptr), 1 if gather else 0,
+                                     _stream_handle(device, stream)))
 
 
 def chunk_mean_ilp_begin(m: int, n: int, threads: int) -> int:

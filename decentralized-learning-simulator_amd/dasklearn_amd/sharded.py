@@ -101,23 +101,83 @@ class ShardedAggregator:
     def aggregate_param_sharded(self, shard_inputs: Sequence[torch.Tensor], weights,
                                 n_elems: int, gather: bool = True,
                                 mode: int = _native.DLSIM_EXACT) -> torch.Tensor:
-        """shard_inputs[i] = this rank's slice (self.bounds(n_elems)) of model i."""
-        w32 = _resolve(len(shard_inputs), weights)
-        b, e = self.bounds(n_elems)
-        for x in shard_inputs:
-            if x.numel() != e - b:
-                raise ValueError(f"rank {self.rank}: shard has {x.numel()} elements, expected {e - b}")
-        comm = self._rccl_comm(shard_inputs[0].device)
-        if comm is not None:
-            # the C ABI end to end: local reduce into the full buffer, then the
-            # grouped in-place broadcasts on the caller's RCCL communicator
-            full = torch.empty(n_elems, dtype=shard_inputs[0].dtype, device=shard_inputs[0].device)
-            _native.wreduce_sharded(list(shard_inputs), w32, full, comm, gather, mode)
-            return full if gather else full[b:e]
-        out = torch.empty(e - b, dtype=shard_inputs[0].dtype, device=shard_inputs[0].device)
+        """shard_inputs[i] = this rank's slice (self.bounds(n_elems)) of model i.
+
+        Errors are collective: a rank whose arguments fail its checks does not
+        raise before the other ranks know, so none of them is left inside a
+        collective; every rank then raises the same error (the failing ranks'
+        messages, in rank order)."""
+        local = None
+        try:
+            if not shard_inputs:
+                raise IndexError("list index out of range")  # models[0] of fedavg.py:20
+            w32 = _resolve(len(shard_inputs), weights)
+            b, e = self.bounds(n_elems)
+            x0 = shard_inputs[0]
+            for x in shard_inputs:
+                if x.numel() != e - b:
+                    raise ValueError(f"rank {self.rank}: shard has {x.numel()} elements, expected {e - b}")
+                if x.dtype != x0.dtype or x.device != x0.device or not x.is_contiguous():
+                    raise ValueError(f"rank {self.rank}: shards must be contiguous tensors of one dtype and device")
+        except (AssertionError, ValueError, IndexError, TypeError) as ex:
+            local = ex
+        if self._uses_c_abi():
+            dev = shard_inputs[0].device if local is None else _default_device()
+            comm = self._rccl_comm(dev)
+            if comm is not None:
+                # the C ABI end to end: local reduce into the full buffer, the
+                # library's agreement step, then the grouped in-place broadcasts
+                # on the caller's RCCL communicator
+                failed = local
+                full = None
+                try:
+                    if local is None:
+                        full = torch.empty(n_elems, dtype=x0.dtype, device=x0.device)
+                        _native.wreduce_sharded(list(shard_inputs), w32, full, comm, gather, mode)
+                    else:  # join the library's agreement as a failed rank
+                        _native.wreduce_sharded_failed(comm, n_elems, gather, dev)
+                except _native.DlsimError as ex:
+                    failed = failed or ex
+                if failed is not None:
+                    self._raise_collectively(failed)
+                return full if gather else full[b:e]
+        self._agree(local, [n_elems, 1 if gather else 0, _native.dtype_code(x0.dtype) if local is None else 0])
+        out = torch.empty(e - b, dtype=x0.dtype, device=x0.device)
         if e > b:
             self.local_reduce(list(shard_inputs), w32, out, mode)
         return self.all_gather(out, n_elems) if gather else out
+
+    # ---- collective error handling ------------------------------------------------
+    def _uses_c_abi(self) -> bool:
+        return self.local_reduce is _hip_reduce and self.align == 64 and dist.get_backend(self.group) == "nccl"
+
+    def _agree(self, local: Optional[BaseException], args: Sequence[int]) -> None:
+        """One int64 MAX all-reduce of [a failure slot per rank | each argument
+        and its negation]: every rank learns which ranks failed and whether the
+        arguments that shape the collectives agree, before any of them enters
+        one. Raises the same error on every rank if anything is wrong (a
+        failed rank's arguments are not compared). The C ABI's
+        dlsim_wreduce_sharded runs the same step on RCCL."""
+        w = _max_allreduce(self.group, self.world, self.rank, local is not None, args)
+        if any(w[:self.world]):
+            self._raise_collectively(local)
+        if any(w[self.world + 2 * k] != -w[self.world + 2 * k + 1] for k in range(len(args))):
+            raise ValueError("ranks disagree on the model size, gather or dtype; no collective was entered")
+
+    def _raise_collectively(self, local: Optional[BaseException]) -> None:
+        """Every rank reaches this once some rank has failed (all of them know
+        it from the agreement step): gather the failing ranks' messages and
+        raise the same error everywhere, typed after the first failing rank's
+        (ValueError / AssertionError / IndexError / TypeError, else
+        RuntimeError, e.g. a library error)."""
+        mine = None if local is None else (type(local).__name__, str(local))
+        got: List = [None] * self.world
+        dist.all_gather_object(got, mine, group=self.group)
+        failed = [(r, g) for r, g in enumerate(got) if g is not None]
+        msg = "; ".join(f"rank {r} of {self.world}: {m}" for r, (_, m) in failed)
+        kinds = {"ValueError": ValueError, "AssertionError": AssertionError, "IndexError": IndexError,
+                 "TypeError": TypeError}
+        raise kinds.get(failed[0][1][0] if failed else "", RuntimeError)(msg or "a rank failed")
 
     def aggregate_model_sharded(self, local_models: Sequence[torch.Tensor], counts: Sequence[int],
                                 weights, exact: bool = True) -> torch.Tensor:
@@ -125,12 +185,18 @@ class ShardedAggregator:
         models rank r holds (global model order = rank order, then local
         order). weights: the global list (None/[] -> uniform)."""
         counts = list(counts)
-        if len(counts) != self.world or counts[self.rank] != len(local_models):
-            raise ValueError("counts must list every rank's model count, this rank's included")
-        n_total = sum(counts)
-        w32 = _resolve(n_total, weights)
-        ref = local_models[0] if local_models else None
-        n_elems = _agree_numel(ref, self.group)
+        local = None
+        try:
+            if len(counts) != self.world or counts[self.rank] != len(local_models):
+                raise ValueError("counts must list every rank's model count, this rank's included")
+            n_total = sum(counts)
+            w32 = _resolve(n_total, weights)
+        except (AssertionError, ValueError, TypeError) as ex:
+            local = ex
+        ref = local_models[0] if local_models and local is None else None
+        # every rank checks its arguments before the first collective; the
+        # agreement also tells ranks without models the model size
+        n_elems = _agree_numel(ref, self.group, self, local)
         dtype = ref.dtype if ref is not None else torch.float32
         device = ref.device if ref is not None else _default_device()
         first = sum(counts[:self.rank])
@@ -193,14 +259,46 @@ def _default_device():
     return torch.device("cpu")
 
 
-def _agree_numel(ref: Optional[torch.Tensor], group) -> int:
-    """Every rank must see the same model size; ranks without models learn it."""
-    dev = ref.device if ref is not None else _default_device()
+def _coll_device(group):
+    """Where a small control tensor for `group`'s backend lives."""
     if dist.get_backend(group) == "gloo":
-        dev = torch.device("cpu")
-    t = torch.tensor([ref.numel() if ref is not None else -1], dtype=torch.int64, device=dev)
+        return torch.device("cpu")
+    return _default_device()
+
+
+def _max_allreduce(group, world: int, rank: int, failed: bool, args: Sequence[int]) -> List[int]:
+    """[failure slot per rank | arg_0, -arg_0, arg_1, -arg_1, ...] reduced
+    with MAX over the group: slot r says rank r failed, and arg_k agrees on
+    every rank iff its max equals minus the max of its negation."""
+    t = torch.zeros(world + 2 * len(args), dtype=torch.int64, device=_coll_device(group))
+    t[rank] = 1 if failed else 0
+    for k, v in enumerate(args):
+        t[world + 2 * k] = int(v)
+        t[world + 2 * k + 1] = -int(v)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
-    n = int(t.item())
-    if ref is not None and ref.numel() != n:
+    return t.tolist()
+
+
+def _agree_numel(ref: Optional[torch.Tensor], group, agg: Optional["ShardedAggregator"] = None,
+                 local: Optional[BaseException] = None) -> int:
+    """Every rank must see the same model size; ranks without models learn
+    it. With `agg`, rank-local argument errors are agreed in the same
+    all-reduce (a failure slot per rank) and raised on every rank; a size
+    disagreement is raised on every rank too."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    # ranks without models contribute (-1, -2^62): neutral for both maxima
+    hi, neg_lo = (ref.numel(), -ref.numel()) if ref is not None else (-1, -2 ** 62)
+    t = torch.zeros(world + 2, dtype=torch.int64, device=_coll_device(group))
+    t[rank] = 1 if local is not None else 0
+    t[world], t[world + 1] = hi, neg_lo
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    w = t.tolist()
+    if any(w[:world]):
+        if agg is None:
+            raise RuntimeError("a rank failed its checks")
+        agg._raise_collectively(local)
+    n = int(w[world])
+    if w[world + 1] != -2 ** 62 and n != -w[world + 1]:
         raise ValueError("models differ in size across ranks")
     return n

@@ -62,6 +62,8 @@ enum dlsim_mode {
 #define DLSIM_E_DTYPE (-2)    /* dtype not in enum dlsim_dtype                */
 #define DLSIM_E_MODE (-3)     /* mode not in enum dlsim_mode                  */
 #define DLSIM_E_RCCL (-4)     /* RCCL not bound, or an RCCL call failed       */
+#define DLSIM_E_PEER (-5)     /* another rank of the communicator failed its
+                                 checks (dlsim_wreduce_sharded's agreement)   */
 #define DLSIM_E_HIP (-100)    /* a HIP call failed: code = -100 - hipError_t  */
 
 /* Fan-in carried in kernel arguments. Larger n (any n >= 1) reads its
@@ -251,6 +253,17 @@ int dlsim_rccl_bind(const char* librccl_path);
  *   grouped ncclBroadcast on `stream`), so every rank ends with the whole
  *   output. Each element's N terms stay on one GPU in input order: results
  *   are bit-identical to dlsim_wreduce on one GPU.
+ *   Errors are collective when W > 1: the rank-local checks (slice length,
+ *   pointers, dtype, fan-in, weights) and the local reduce's launch run
+ *   first, then every rank joins one agreement all-reduce (int64 MAX of a
+ *   failure slot per rank plus n_elems, dtype and gather, on `stream`, read
+ *   back by the host: the call waits for the stream once). A rank whose own
+ *   checks failed returns its own error; every other rank returns
+ *   DLSIM_E_PEER naming the failed ranks, or DLSIM_E_ARG if the ranks
+ *   disagree on n_elems, dtype or gather; in both cases no rank enters the
+ *   broadcast group, so none is left waiting in it. Only a failure before the
+ *   communicator can be queried (RCCL not bound, null communicator) is
+ *   rank-local.
  */
 int dlsim_wreduce_sharded(const void* const* d_slices, size_t slice_elems, int n, const float* h_weights,
                           void* d_out, size_t n_elems, int dtype, int mode, void* rccl_comm, int gather,

@@ -1,6 +1,6 @@
-// stub_rccl.hip — TEST INFRASTRUCTURE: a stand-in for the five RCCL entry
-// points dlsim_wreduce_sharded binds (dlsim_rccl_bind dlopens this file), so
-// its gather path runs with W > 1 ranks on ONE GPU.
+// stub_rccl.hip — TEST INFRASTRUCTURE: a stand-in for the RCCL entry points
+// dlsim_wreduce_sharded binds (dlsim_rccl_bind dlopens this file), so its
+// agreement step and gather path run with W > 1 ranks on ONE GPU.
 //
 // A stub communicator names a world size W, this rank r, this rank's full
 // output buffer and the full output buffers the other W - 1 ranks would hold
@@ -28,6 +28,10 @@ struct StubComm {
     int dtype;
   };
   std::vector<Call> calls;
+  // the other ranks' contributions to an int64 MAX all-reduce (already
+  // max-combined), set by the test; empty = they contribute this rank's words
+  std::vector<int64_t> peer_words;
+  int allreduces = 0;
   int group_depth = 0;
   int max_group_depth = 0;
 };
@@ -93,6 +97,23 @@ int ncclBroadcast(const void* sendbuff, void* recvbuff, size_t count, int dataty
   return e == hipSuccess ? 0 : 1;  // ncclUnhandledCudaError
 }
 
+// int64 MAX only (the agreement step): this rank's words, max-combined with
+// the peers' words the test set. Host-synchronous (test infrastructure).
+int ncclAllReduce(const void* sendbuff, void* recvbuff, size_t count, int datatype, int op, void* comm,
+                  hipStream_t stream) {
+  StubComm* c = static_cast<StubComm*>(comm);
+  if (!c || datatype != 4 || op != 2) return 4;  // ncclInt64, ncclMax
+  if (g_depth > 0) return 5;                     // not inside the broadcast group
+  std::vector<int64_t> w(count);
+  if (hipMemcpyAsync(w.data(), sendbuff, count * 8, hipMemcpyDeviceToHost, stream) != hipSuccess) return 1;
+  if (hipStreamSynchronize(stream) != hipSuccess) return 1;
+  for (size_t k = 0; k < count && k < c->peer_words.size(); ++k)
+    if (c->peer_words[k] > w[k]) w[k] = c->peer_words[k];
+  ++c->allreduces;
+  if (hipMemcpyAsync(recvbuff, w.data(), count * 8, hipMemcpyHostToDevice, stream) != hipSuccess) return 1;
+  return hipStreamSynchronize(stream) == hipSuccess ? 0 : 1;
+}
+
 // ---- test helpers ------------------------------------------------------------
 void* stub_comm_create(int world, int rank, void* own_out, void* const* peer_out) {
   StubComm* c = new StubComm;
@@ -118,5 +139,11 @@ int stub_comm_calls(void* comm, int* roots, size_t* offsets, size_t* counts, int
 }
 
 int stub_comm_max_group_depth(void* comm) { return static_cast<StubComm*>(comm)->max_group_depth; }
+
+void stub_comm_set_peer_words(void* comm, const int64_t* w, int n) {
+  static_cast<StubComm*>(comm)->peer_words.assign(w, w + n);
+}
+
+int stub_comm_allreduces(void* comm) { return static_cast<StubComm*>(comm)->allreduces; }
 
 }  // extern "C"

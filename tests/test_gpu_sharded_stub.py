@@ -45,6 +45,9 @@ def stub():
     lib.stub_comm_calls.restype = ctypes.c_int
     lib.stub_comm_max_group_depth.argtypes = [vp]
     lib.stub_comm_max_group_depth.restype = ctypes.c_int
+    lib.stub_comm_set_peer_words.argtypes = [vp, ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
+    lib.stub_comm_allreduces.argtypes = [vp]
+    lib.stub_comm_allreduces.restype = ctypes.c_int
     _native.rccl_bind(STUB)
     yield lib
     _native.rccl_bind()  # back to torch's RCCL for the other tests
@@ -92,6 +95,7 @@ def test_sharded_gather_assembles_the_whole_output(stub, world, p, dtype):
             want = [(q, bq * esz, eq - bq) for q, (bq, eq) in enumerate(bounds) if eq > bq]
             assert [(roots[i], offs[i], cnts[i]) for i in range(m)] == want
             assert stub.stub_comm_max_group_depth(comm) == 1  # one ncclGroupStart/End around them
+            assert stub.stub_comm_allreduces(comm) == 1  # the agreement step, before the group
         finally:
             stub.stub_comm_destroy(comm)
 
@@ -126,5 +130,68 @@ def test_sharded_rejects_a_slice_of_the_wrong_length(stub):
     try:
         with pytest.raises(_native.DlsimError, match="slices have"):
             _native.wreduce_sharded([x[:500]], orc.reference_weights(1, None), out, comm)
+        # the failure was agreed with the other rank before returning, and no
+        # broadcast was requested
+        assert stub.stub_comm_allreduces(comm) == 1
+        assert stub.stub_comm_calls(comm, None, None, None, 0) == 0
+    finally:
+        stub.stub_comm_destroy(comm)
+
+
+def _agree_words(world, failed, n_elems, dtype, gather):
+    w = [1 if r in failed else 0 for r in range(world)]
+    for v in (n_elems, dtype, 1 if gather else 0):
+        w += [v, -v]
+    return (ctypes.c_int64 * len(w))(*w), len(w)
+
+
+@pytest.mark.parametrize("case", ["peer_failed", "n_elems", "gather"])
+def test_sharded_peer_failure_is_agreed_before_the_group(stub, case):
+    """when another rank failed its checks, or the ranks
+    disagree on the arguments that shape the broadcast group, this rank
+    returns an error without entering the group (no broadcast requested), its
+    own slice still reduced."""
+    world, p, n = 3, 64 * 20 * 3 + 5, 4
+    rows = make_rows(n, p, 77, "f32")
+    w = orc.reference_weights(n, None)
+    xs = to_dev(list(rows), "f32")
+    expected = orc.wreduce(list(rows), w, "f32")
+    out = _nan_like(xs[0])
+    comm = stub.stub_comm_create(world, 0, out.data_ptr(), (ctypes.c_void_p * world)(*[out.data_ptr()] * world))
+    try:
+        if case == "peer_failed":
+            words, k = _agree_words(world, {2}, p, _native.DLSIM_F32, True)
+        elif case == "n_elems":
+            words, k = _agree_words(world, set(), p + 64, _native.DLSIM_F32, True)
+        else:
+            words, k = _agree_words(world, set(), p, _native.DLSIM_F32, False)
+        stub.stub_comm_set_peer_words(comm, words, k)
+        b, e = _native.shard_range(p, world, 0, 64)
+        with pytest.raises(_native.DlsimError) as ei:
+            _native.wreduce_sharded([x[b:e] for x in xs], w, out, comm, gather=True)
+        if case == "peer_failed":
+            assert ei.value.rc == _native.DLSIM_E_PEER and "rank(s) 2 of 3" in str(ei.value)
+        else:
+            assert ei.value.rc == _native.DLSIM_E_ARG and "disagree" in str(ei.value)
+        assert stub.stub_comm_allreduces(comm) == 1
+        assert stub.stub_comm_calls(comm, None, None, None, 0) == 0
+        assert orc.same_bits(from_dev(out)[b:e], expected[b:e])
+    finally:
+        stub.stub_comm_destroy(comm)
+
+
+def test_sharded_failed_rank_joins_the_agreement(stub):
+    """A caller whose own checks failed (ShardedAggregator) joins the
+    agreement through wreduce_sharded_failed: the library counts it as a
+    failed rank and returns its argument error."""
+    world, p = 2, 1000
+    out = torch.empty(p, device=dev())
+    comm = stub.stub_comm_create(world, 1, out.data_ptr(), (ctypes.c_void_p * 2)(out.data_ptr(), out.data_ptr()))
+    try:
+        with pytest.raises(_native.DlsimError) as ei:
+            _native.wreduce_sharded_failed(comm, p, True, dev())
+        assert ei.value.rc == _native.DLSIM_E_ARG
+        assert stub.stub_comm_allreduces(comm) == 1
+        assert stub.stub_comm_calls(comm, None, None, None, 0) == 0
     finally:
         stub.stub_comm_destroy(comm)

@@ -1,0 +1,62 @@
+"""Exactness guard at build time: the gfx950 ISA of every
+exact-policy kernel in the BUILT libdlsim_hip.so has no fused multiply-add and
+no mixed-precision instruction. The reference rounds every product and every
+sum separately (fedavg.py:25), so a launch-shape change that
+lets the backend contract `acc + w*x` fails this CPU test before any GPU run.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+sys.path.insert(0, os.path.join(ROOT, "scripts"))
+import audit_isa  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def report():
+    if not os.path.exists(audit_isa.LIB):
+        pytest.fail("libdlsim_hip.so is not built (run __graft_entry__.build())")
+    return audit_isa.audit()
+
+
+def test_every_translation_unit_with_device_code_is_audited(report):
+    # one code object per inst_*.hip unit (dlsim_abi.hip carries no kernels)
+    units = [f for f in os.listdir(os.path.join(ROOT, "decentralized-learning-simulator_amd", "csrc"))
+             if f.startswith("inst_") and f.endswith(".hip")]
+    assert report["code_objects"] == len(units)
+
+
+def test_exact_kernels_have_no_fused_or_mixed_ops(report):
+    assert report["exact_policies_clean"], json.dumps(report["offending_kernels"][:10], indent=1)
+    for pol in ("F32Exact", "BF16Exact", "F16Exact", "F64Exact"):
+        assert report["per_policy"][pol]["kernels"] > 40, pol
+
+
+def test_audit_sees_the_round2_shapes():
+    """The fixed VPT-2 block-map and grouped VPT-1 wave-map shapes
+    (dispatch.hpp fixed_shape / grouped_shape) are among the audited kernels."""
+    names = set()
+    for co in audit_isa.code_objects(audit_isa.LIB):
+        names |= set(audit_isa.kernels(audit_isa.disassemble(co)))
+    exact = [n for n in names if "8F32Exact" in n and "k_wreduce_tiles" in n]
+    # template args <Op, S, NF, G, VPT, NT, STP, WAVE>: ...ELi<VPT>ELi1ELi16ELb<wave>E
+    assert any("ELi2ELi1ELi16ELb0E" in n for n in exact), "fixed VPT 2 block map missing"
+    assert any("ELi0ELi8ELi1ELi1ELi16ELb1E" in n for n in exact), "grouped VPT 1 wave map missing"
+    assert any("ELi4ELi1ELi16ELb1E" in n for n in exact), "VPT 4 wave map missing"
+
+
+def test_detector_catches_contraction(report):
+    # positive controls: the FAST policies fuse by design, and the patterns
+    # match the instructions a contraction would produce
+    assert report["per_policy"]["F32Fast"]["fma"] > 0
+    assert report["per_policy"]["F64Fast"]["fma"] > 0
+    for ins in ("v_fma_f32 v1, v2, v3, v4", "v_fmac_f32_e32 v1, v2, v3", "v_pk_fma_f32 v[0:1], v[2:3], v[4:5], v[6:7]",
+                "v_fma_f64 v[0:1], v[2:3], v[4:5], v[6:7]"):
+        assert audit_isa.FMA_RE.search(ins), ins
+    assert audit_isa.MIX_RE.search("v_fma_mixlo_f16 v1, v2, v3, v4")

@@ -124,3 +124,81 @@ def test_sharded_paths_gloo(world, p, dtype):
     for r in range(world):
         assert "error" not in results[r], results[r].get("error")
         assert all(results[r].values()), (r, results[r])
+
+
+def _err_worker(rank, world, port, case, q):
+    """One rank misbehaves; every rank must raise the same error promptly
+    (no rank left waiting inside a collective), and the group stays usable."""
+    import datetime
+    import time
+    for path in PATHS:
+        sys.path.insert(0, path)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
+    try:
+        from dasklearn_amd.sharded import ShardedAggregator
+        agg = ShardedAggregator(local_reduce=oracle_reduce)
+        n, p = 3, 1000
+        xs = models(n, p, torch.float32)
+        b, e = agg.bounds(p)
+        shards = [x[b:e].contiguous() for x in xs]
+        counts = [2, 1] if world == 2 else [1] * world
+        first = sum(counts[:rank])
+        mine = xs[first:first + counts[rank]]
+        t0 = time.perf_counter()
+        err = None
+        try:
+            if case == "bad_shard":
+                agg.aggregate_param_sharded(shards if rank != 1 else [s[:-1] for s in shards], None, p)
+            elif case == "bad_weights":
+                agg.aggregate_param_sharded(shards, [0.5, 0.5] if rank == 1 else None, p)
+            elif case == "gather_mismatch":
+                agg.aggregate_param_sharded(shards, None, p, gather=(rank == 0))
+            elif case == "bad_counts":
+                agg.aggregate_model_sharded(mine, counts if rank != 1 else counts[::-1] + [0], None)
+            elif case == "size_mismatch":
+                agg.aggregate_model_sharded([m[:-64] for m in mine] if rank == 1 else mine, counts, None)
+        except Exception as ex:  # noqa: BLE001 - the error is the result
+            err = (type(ex).__name__, str(ex))
+        secs = time.perf_counter() - t0
+        # the group is still usable afterwards
+        ok = agg.aggregate_param_sharded(shards, None, p)
+        q.put((rank, {"err": err, "secs": secs, "after_ok": ok.numel() == p}))
+    except Exception:
+        import traceback
+        q.put((rank, {"error": traceback.format_exc()}))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case,kind,text", [
+    ("bad_shard", "ValueError", "rank 1 of 2: rank 1: shard has"),
+    ("bad_weights", "AssertionError", "rank 1 of 2"),
+    ("gather_mismatch", "ValueError", "disagree"),
+    ("bad_counts", "ValueError", "rank 1 of 2: counts must list"),
+    ("size_mismatch", "ValueError", "differ in size"),
+])
+def test_sharded_errors_are_collective_gloo(case, kind, text):
+    """a rank-local argument error (a wrong-length shard,
+    a weight-count mismatch, disagreeing arguments) makes every rank raise the
+    same error, with no rank left inside a collective."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_err_worker, args=(r, world, port, case, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    results = {}
+    for _ in range(world):
+        r, res = q.get(timeout=120)
+        results[r] = res
+    for pr in procs:
+        pr.join(timeout=60)
+    for r in range(world):
+        assert "error" not in results[r], results[r].get("error")
+        assert results[r]["err"] is not None, (r, case)
+        assert results[r]["err"][0] == kind and text in results[r]["err"][1], (r, results[r]["err"])
+        assert results[r]["secs"] < 20, (r, results[r]["secs"])
+        assert results[r]["after_ok"]
+    assert results[0]["err"] == results[1]["err"]  # the same error on every rank
