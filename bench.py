@@ -353,9 +353,15 @@ def pmc_traffic(config: str, mode: str, split: int):
     rocprofv3 --pmc runs of this same command; FETCH_SIZE doubled per the
     gfx950 rule). Returns (bytes, source file) or (None, reason)."""
     import glob
+    import re
     best, src = None, None
     key = config if split <= 1 else f"{config}@slice{split}"
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+
+    def newest_last(path):  # r01 < r01_s4 < r02 < r02s2 < r03 ...: round, then session, then name
+        m = re.match(r"r(\d+)(?:_?s(\d+))?", os.path.basename(path))
+        return (int(m.group(1)), int(m.group(2) or 0), path) if m else (-1, 0, path)
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "*pmc*.json"), recursive=True),
+                       key=newest_last):
         try:
             with open(path) as f:
                 d = json.load(f)
@@ -375,6 +381,27 @@ def _host_threads() -> int:
     n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
     omp = os.environ.get("OMP_NUM_THREADS")
     return max(1, min(n, int(omp))) if omp and omp.isdigit() else n
+
+
+def box_info() -> dict:
+    """The host the CPU baseline ran on (its numbers move with the box's CPU
+    share and memory; VERDICT r02 weak #9)."""
+    info = {"host_cpus": os.cpu_count(), "threads_usable": _host_threads(),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+    if hasattr(os, "sched_getaffinity"):
+        info["affinity_cpus"] = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()
+        info["cgroup_cpu_quota"] = None if quota == "max" else round(int(quota) / int(period), 2)
+    except (OSError, ValueError):
+        info["cgroup_cpu_quota"] = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            info["cpu_model"] = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), None)
+    except OSError:
+        pass
+    return info
 
 
 def cpu_baseline(config, n, p, dtype, weights, budget_s):
@@ -431,6 +458,7 @@ def cpu_baseline(config, n, p, dtype, weights, budget_s):
         out["all_cores"] = {"value": round(bytes_ * reps2 / el2 / 1e9, 3), "unit": "GB/s", "cores": all_t,
                             "ms_per_step": round(el2 / reps2 * 1e3, 3),
                             "sample": f"{reps2} x the same aggregate in {el2:.1f} s at {all_t} threads"}
+    out["box"] = box_info()
     return out
 
 
@@ -689,11 +717,16 @@ def _time_sharded(wl, n, p_cfg, w32, mode, dtype, dev, cdev, stream, barrier, re
     return out
 
 
+WATCHDOG_EXIT = 3  # exit code of a rank whose guarded collective timed out
+
+
 def _guarded(fn, timeout_s: float, on_timeout):
     """fn() with a watchdog: a collective issued outside torch's own watchdog
     (the C ABI's RCCL calls) must not hold the bench line hostage. If fn has
     not returned after timeout_s, on_timeout() runs (rank 0 prints the line
-    it has) and the process exits."""
+    it has, with the timeout recorded in it) and the process exits with
+    WATCHDOG_EXIT, so spawn_ranks and the driver see the run as failed
+    (a hung collective must not read as a successful bench)."""
     import threading
     done = threading.Event()
 
@@ -702,7 +735,7 @@ def _guarded(fn, timeout_s: float, on_timeout):
             try:
                 on_timeout()
             finally:
-                os._exit(0)
+                os._exit(WATCHDOG_EXIT)
     timer = threading.Timer(timeout_s, fire)
     timer.daemon = True
     timer.start()

@@ -22,6 +22,9 @@
 //            lanes l, each the ilp order over rows l, l+8, ...; the m mod 8
 //            remaining rows summed from +0, then the eight lanes added in turn.
 //
+// fp64 chunks (F64Mean) run the same orders in double with Vectorized<double>'s
+// 4 lanes: 16-column cascade blocks and rounding, the inner order from m >= 4.
+//
 // Layout of the work: every chunk index is one task of a batched grid (the
 // kernel-argument batches of k_wreduce_batch). The cascade columns stream in
 // tiles of 256 lanes x VPT 16-byte vectors, one lane folding its elements'
@@ -62,12 +65,18 @@ struct PtrArgs {
   __device__ const void* ptr(int i) const { return p[i]; }
 };
 
-// One element's cascade (multi_row_sum with 16-value blocks and 4 levels).
+// Lanes of ATen's Vectorized<acc> in the sum kernel (the inner order and the
+// column blocks): 8 floats, 4 doubles.
+template <class Op> constexpr int cm_lanes() { return Op::kBytes == 8 ? 4 : 8; }
+
+// One element's cascade (multi_row_sum with 16-value blocks and 4 levels),
+// in the accumulator type T (float; double for fp64 chunks).
+template <class T>
 struct CascadeSum {
-  float a[4];
-  __device__ void init() { a[0] = a[1] = a[2] = a[3] = 0.0f; }
+  T a[4];
+  __device__ void init() { a[0] = a[1] = a[2] = a[3] = T(0); }
   // value number i (0-based) of the sequence, in order
-  __device__ void add(long long i, float x) {
+  __device__ void add(long long i, T x) {
     a[0] = a[0] + x;
     if (((i + 1) & 15) == 0) flush(i + 1);
   }
@@ -75,17 +84,18 @@ struct CascadeSum {
 #pragma unroll
     for (int l = 1; l < 4; ++l) {
       a[l] = a[l] + a[l - 1];
-      a[l - 1] = 0.0f;
+      a[l - 1] = T(0);
       if ((i & (15LL << (4 * l))) != 0) break;
     }
   }
-  __device__ float result() const { return ((a[0] + a[1]) + a[2]) + a[3]; }
+  __device__ T result() const { return ((a[0] + a[1]) + a[2]) + a[3]; }
 };
 
 // One element's row_sum (ilp) order over a sequence of `len` values.
+template <class T>
 struct IlpSum {
-  float a[4][4];  // [level][k]
-  float p[4];
+  T a[4][4];  // [level][k]
+  T p[4];
   long long s;    // values per interleaved cascade (len / 4)
   bool done;
   __device__ void init(long long len) {
@@ -94,11 +104,11 @@ struct IlpSum {
 #pragma unroll
     for (int l = 0; l < 4; ++l)
 #pragma unroll
-      for (int k = 0; k < 4; ++k) a[l][k] = 0.0f;
+      for (int k = 0; k < 4; ++k) a[l][k] = T(0);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) p[k] = 0.0f;
+    for (int k = 0; k < 4; ++k) p[k] = T(0);
   }
-  __device__ void add(long long idx, float x) {
+  __device__ void add(long long idx, T x) {
     if (idx < 4 * s) {
       const int k = static_cast<int>(idx & 3);
 #pragma unroll
@@ -111,7 +121,7 @@ struct IlpSum {
 #pragma unroll
           for (int kk = 0; kk < 4; ++kk) {
             a[l][kk] = a[l][kk] + a[l - 1][kk];
-            a[l - 1][kk] = 0.0f;
+            a[l - 1][kk] = T(0);
           }
           if ((i & (15LL << (4 * l))) != 0) break;
         }
@@ -126,7 +136,7 @@ struct IlpSum {
     for (int k = 0; k < 4; ++k) p[k] = ((a[0][k] + a[1][k]) + a[2][k]) + a[3][k];
     done = true;
   }
-  __device__ float result() {
+  __device__ T result() {
     if (!done) finish();
     return ((p[0] + p[1]) + p[2]) + p[3];
   }
@@ -138,7 +148,15 @@ template <class Op>
 __device__ __forceinline__ u32x4 ld_slot_scalar(const void* base, size_t v, size_t lim) {
   u32x4 r = {0u, 0u, 0u, 0u};
   const size_t j0 = v * Op::E;
-  if constexpr (Op::kBytes == 4) {
+  if constexpr (Op::kBytes == 8) {
+    const uint64_t* q = static_cast<const uint64_t*>(base);
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+      if (j0 + e < lim) {
+        r[2 * e] = static_cast<uint32_t>(q[j0 + e]);
+        r[2 * e + 1] = static_cast<uint32_t>(q[j0 + e] >> 32);
+      }
+  } else if constexpr (Op::kBytes == 4) {
     const uint32_t* q = static_cast<const uint32_t*>(base);
 #pragma unroll
     for (int e = 0; e < 4; ++e)
@@ -173,13 +191,14 @@ template <class Op, class A, class SH, int LV, bool VEC, bool CHECK>
 __device__ __forceinline__ void cm_tile(const A& a, int m, const OutRef& o, size_t v0, size_t nvec,
                                         size_t ncol, float div) {
   constexpr int VPT = SH::VPT, RF = SH::RF;
-  float acc[LV][VPT][Op::E];
+  using T = acc_t<Op>;
+  T acc[LV][VPT][Op::E];
 #pragma unroll
   for (int l = 0; l < LV; ++l)
 #pragma unroll
     for (int v = 0; v < VPT; ++v)
 #pragma unroll
-      for (int e = 0; e < Op::E; ++e) acc[l][v][e] = 0.0f;
+      for (int e = 0; e < Op::E; ++e) acc[l][v][e] = T(0);
   for (int i0 = 0; i0 < m; i0 += 16) {
     const int cnt = m - i0 < 16 ? m - i0 : 16;
 #pragma unroll
@@ -207,7 +226,7 @@ __device__ __forceinline__ void cm_tile(const A& a, int m, const OutRef& o, size
           if (h + g < cnt) {
 #pragma unroll
             for (int v = 0; v < VPT; ++v) {
-              float x[Op::E];
+              T x[Op::E];
               unpack<Op>(r[g][v], x);
 #pragma unroll
               for (int e = 0; e < Op::E; ++e) acc[0][v][e] = acc[0][v][e] + x[e];
@@ -225,7 +244,7 @@ __device__ __forceinline__ void cm_tile(const A& a, int m, const OutRef& o, size
 #pragma unroll
           for (int e = 0; e < Op::E; ++e) {
             acc[l][v][e] = acc[l][v][e] + acc[l - 1][v][e];
-            acc[l - 1][v][e] = 0.0f;
+            acc[l - 1][v][e] = T(0);
           }
         if ((i & (15 << (4 * l))) != 0) break;
       }
@@ -242,7 +261,7 @@ __device__ __forceinline__ void cm_tile(const A& a, int m, const OutRef& o, size
     const size_t idx = v0 + static_cast<size_t>(v) * SH::VS;
     if (CHECK && idx >= nvec) continue;
     if constexpr (VEC) {
-      store_vec<Op::kBytes == 4 ? 16 : kStNT>(o, idx, pack<Op>(acc[0][v], div));
+      store_vec<Op::kBytes >= 4 ? 16 : kStNT>(o, idx, pack<Op>(acc[0][v], div));
     } else {
 #pragma unroll
       for (int e = 0; e < Op::E; ++e) {
@@ -259,17 +278,19 @@ __device__ __forceinline__ void cm_tile(const A& a, int m, const OutRef& o, size
 template <class Op, class A>
 __device__ __forceinline__ void cm_scalar_cols(const A& a, int m, void* out, size_t c0, size_t n,
                                                size_t ilp_begin, bool inner, float div) {
-  __shared__ float st[kCmTailRows][kCmTailCols];
+  using T = acc_t<Op>;
+  constexpr int VW = cm_lanes<Op>();
+  __shared__ T st[kCmTailRows][kCmTailCols];
   const int W = static_cast<int>(n - c0);  // block-uniform, <= kCmTailCols
   const int tid = threadIdx.x;
   const size_t col = c0 + static_cast<size_t>(tid);
   const bool is_ilp = col >= ilp_begin;
-  const long long vs = m / 8;  // inner: 8-lane vectors
-  CascadeSum cs;
-  IlpSum il;
+  const long long vs = m / VW;  // inner: VW-lane vectors
+  CascadeSum<T> cs;
+  IlpSum<T> il;
   cs.init();
   il.init(inner ? vs : m);
-  float fin = 0.0f;  // inner: the m mod 8 trailing rows, from +0
+  T fin = T(0);  // inner: the m mod VW trailing rows, from +0
   for (int r0 = 0; r0 < m; r0 += kCmTailRows) {
     const int rc = m - r0 < kCmTailRows ? m - r0 : kCmTailRows;
     for (int idx = tid; idx < rc * W; idx += kBlock) {
@@ -280,16 +301,16 @@ __device__ __forceinline__ void cm_scalar_cols(const A& a, int m, void* out, siz
     if (!inner) {
       if (tid < W) {
         for (int rr = 0; rr < rc; ++rr) {
-          const float x = st[rr][tid];
+          const T x = st[rr][tid];
           if (is_ilp) il.add(r0 + rr, x);
           else cs.add(r0 + rr, x);
         }
       }
-    } else if (tid < 8) {
+    } else if (tid < VW) {
       for (int rr = 0; rr < rc; ++rr) {
         const long long i = r0 + rr;
-        if (i < 8 * vs && (i & 7) == tid) il.add(i >> 3, st[rr][0]);
-        if (tid == 0 && i >= 8 * vs) fin = fin + st[rr][0];
+        if (i < VW * vs && (i % VW) == tid) il.add(i / VW, st[rr][0]);
+        if (tid == 0 && i >= VW * vs) fin = fin + st[rr][0];
       }
     }
     __syncthreads();
@@ -298,11 +319,11 @@ __device__ __forceinline__ void cm_scalar_cols(const A& a, int m, void* out, siz
     if (tid < W) store_elem<Op>(out, col, is_ilp ? il.result() : cs.result(), div);
     return;
   }
-  if (tid < 8) st[0][tid] = il.result();
+  if (tid < VW) st[0][tid] = il.result();
   __syncthreads();
   if (tid == 0) {
 #pragma unroll
-    for (int l = 0; l < 8; ++l) fin = fin + st[0][l];
+    for (int l = 0; l < VW; ++l) fin = fin + st[0][l];
     store_elem<Op>(out, 0, fin, div);
   }
 }
@@ -317,7 +338,7 @@ __device__ __forceinline__ void cm_task(const A& a, int m, void* out, size_t n, 
   constexpr size_t kTile = static_cast<size_t>(kBlock) * SH::VPT;
   const size_t full = nvec / kTile;
   const bool vec = (flags & kCmVec) != 0;
-  const OutRef o = make_out<Op::kBytes == 4 ? 16 : kStNT>(out, vec ? nvec : 0);
+  const OutRef o = make_out<Op::kBytes >= 4 ? 16 : kStNT>(out, vec ? nvec : 0);
   if (local == 0) {
     if (full * kTile < nvec) {  // the partial tile, block map (bounds-checked)
       using PT = CmShape<SH::VPT, false, SH::RF>;

@@ -537,8 +537,13 @@ int table_launch(const void* h_table, const void* d_table, hipStream_t st) {
 // (parallel_dim_reduction's column split, 32-column rounding; the 8-wide
 // vectorized_outer_sum blocks of 32 columns; scalar_outer_sum's groups of 4
 // under 8 columns). n == 1 is the inner reduction (all "ilp"/inner).
-inline size_t chunk_mean_ilp_begin(int m, size_t n, int threads) {
+// esz / vw: the summed element's bytes and its Vectorized<> lanes (fp32 and
+// the widened 16-bit types: 4 / 8; fp64: 8 / 4): ranges round to 128 B of
+// columns, cascade blocks are 4 * vw columns, the vectorized path starts at
+// vw columns (oracle/fedavg_oracle.c ilp_begin_gen).
+inline size_t chunk_mean_ilp_begin(int m, size_t n, int threads, size_t esz = 4, size_t vw = 8) {
   if (n <= 1) return 0;
+  const size_t rnd = 128 / esz;
   size_t b = 0, e = n;
   if (!(static_cast<unsigned long long>(m) * n < 32768ULL || threads <= 1)) {
     const size_t tp = static_cast<size_t>(threads) < n ? static_cast<size_t>(threads) : n;
@@ -547,8 +552,8 @@ inline size_t chunk_mean_ilp_begin(int m, size_t n, int threads) {
       size_t tb = t * cs;
       if (tb >= n) break;
       size_t te = tb + cs < n ? tb + cs : n;
-      tb -= tb % 32;
-      if (te != n) te -= te % 32;
+      tb -= tb % rnd;
+      if (te != n) te -= te % rnd;
       if (tb < te) {
         b = tb;
         e = te;
@@ -556,7 +561,7 @@ inline size_t chunk_mean_ilp_begin(int m, size_t n, int threads) {
     }
   }
   const size_t s1 = e - b;
-  return b + (s1 >= 8 ? s1 / 32 * 32 : s1 / 4 * 4);
+  return b + (s1 >= vw ? s1 / (4 * vw) * (4 * vw) : s1 / 4 * 4);
 }
 
 // Chunk mean tiles: VPT 4, wave map, 8 rows per load group. Block and wave
@@ -583,7 +588,7 @@ int run_chunk_mean(int b, const int* fan_in, const void* const* in, void* const*
     bool vec = aligned16(outs[t]);
     for (int i = 0; i < fan_in[t] && vec; ++i) vec = aligned16(in[off[t] + i]);
     uint8_t f = vec ? dlsim::kCmVec : 0;
-    if (nelem[t] == 1 && fan_in[t] >= 8) f |= dlsim::kCmInner;
+    if (nelem[t] == 1 && fan_in[t] >= dlsim::cm_lanes<Op>()) f |= dlsim::kCmInner;
     return f;
   };
   auto task_blocks = [&](int t, size_t ib) { return ib / Op::E / tile + 1; };
@@ -608,7 +613,7 @@ int run_chunk_mean(int b, const int* fan_in, const void* const* in, void* const*
     const size_t n = nelem[t];
     if (n == 0) continue;
     const int m = fan_in[t];
-    const size_t ib = chunk_mean_ilp_begin(m, n, threads);
+    const size_t ib = chunk_mean_ilp_begin(m, n, threads, Op::kBytes == 8 ? 8 : 4, dlsim::cm_lanes<Op>());
     const uint8_t flags = task_flags(t);
     const size_t tb = task_blocks(t, ib);
     if (m > dlsim::kCmMaxPtrs) {
@@ -670,6 +675,9 @@ int run_chunk_mean(int b, const int* fan_in, const void* const* in, void* const*
   X int dlsim_host::run<Op>(const void* const*, int, const float*, void*, size_t, hipStream_t, float);
 #define DLSIM_F64_ENTRIES(X, Op) \
   X int dlsim_host::run<Op>(const void* const*, int, const double*, void*, size_t, hipStream_t, float);
+#define DLSIM_CHUNK_ENTRIES(X, Op)                                                                       \
+  X int dlsim_host::run_chunk_mean<Op>(int, const int*, const void* const*, void* const*, const size_t*, \
+                                       int, hipStream_t);
 
 // every policy's entries, with X = `extern template` (declare) or `template` (define)
 #define DLSIM_ALL_ENTRIES(X)                  \
@@ -685,4 +693,5 @@ int run_chunk_mean(int b, const int* fan_in, const void* const* in, void* const*
   DLSIM_PROBE_ENTRIES(X, dlsim::XorProbe<4>)  \
   DLSIM_PROBE_ENTRIES(X, dlsim::XorProbe<2>)  \
   DLSIM_F64_ENTRIES(X, dlsim::F64Exact)       \
-  DLSIM_F64_ENTRIES(X, dlsim::F64Fast)
+  DLSIM_F64_ENTRIES(X, dlsim::F64Fast)        \
+  DLSIM_CHUNK_ENTRIES(X, dlsim::F64Mean)

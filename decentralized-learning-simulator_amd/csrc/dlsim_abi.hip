@@ -67,6 +67,13 @@ int with_mean_policy(int dtype, F&& f) {
   return f(dlsim::F16Mean{});
 }
 
+// The chunk mean's policies: the mean ones plus fp64 (chunk_mean_kernels.hpp).
+template <class F>
+int with_chunk_policy(int dtype, F&& f) {
+  if (dtype == DLSIM_F64) return f(dlsim::F64Mean{});
+  return with_mean_policy(dtype, f);
+}
+
 int check_args(const void* const* in, int n, const void* w, const void* out, size_t nelem,
                int dtype, int mode, bool need_w = true, bool f64_ok = false) {
   if (!known_dtype(dtype) && !(f64_ok && dtype == DLSIM_F64)) return dtype_fail(dtype);
@@ -167,6 +174,10 @@ void pack_and_dispatch(dlsim::PackJob& job, int threads, size_t in_bytes, F&& on
   }
   if (helpers > 0) pool.join();
 }
+
+// dlsim_host_chunk_mean jobs below this many staged bytes take the one-DMA
+// path (pack all, one H2D, one batched launch, one D2H).
+constexpr size_t kSmallHostJobBytes = size_t{4} << 20;
 
 // Staging layout of dlsim_host_chunk_mean: input rows back to back, each at
 // a 256-B aligned offset.
@@ -340,7 +351,7 @@ int dlsim_chunk_mean_batched(int b, const int* fan_in, const void* const* d_inpu
   if (cpu_threads < 1) return fail(DLSIM_E_ARG, "cpu_threads must be >= 1 (got %d)", cpu_threads);
   size_t off = 0;
   for (int t = 0; t < b; ++t) {
-    int rc = check_args(d_inputs + off, fan_in[t], nullptr, d_outs[t], n_elems[t], dtype, DLSIM_EXACT, false);
+    int rc = check_args(d_inputs + off, fan_in[t], nullptr, d_outs[t], n_elems[t], dtype, DLSIM_EXACT, false, true);
     if (rc != DLSIM_OK) return fail(rc, "task %d: %s", t, g_err.c_str());
     if (fan_in[t] > 65535) return fail(DLSIM_E_ARG, "task %d: fan-in %d > 65535", t, fan_in[t]);
     if (n_elems[t] * elem_bytes(dtype) >= kMaxLaunchOutBytes)
@@ -348,7 +359,7 @@ int dlsim_chunk_mean_batched(int b, const int* fan_in, const void* const* d_inpu
     off += static_cast<size_t>(fan_in[t]);
   }
   hipStream_t st = static_cast<hipStream_t>(stream);
-  return with_mean_policy(dtype, [&](auto op) {
+  return with_chunk_policy(dtype, [&](auto op) {
     return run_chunk_mean<decltype(op)>(b, fan_in, d_inputs, d_outs, n_elems, cpu_threads, st);
   });
 }
@@ -598,7 +609,7 @@ int dlsim_host_chunk_mean(int b, const int* fan_in, const void* const* h_inputs,
   if (b < 0) return fail(DLSIM_E_ARG, "b must be >= 0 (got %d)", b);
   if (b == 0) return DLSIM_OK;
   if (!fan_in || !h_inputs || !d_outs || !n_elems) return fail(DLSIM_E_ARG, "null array argument");
-  if (!known_dtype(dtype)) return dtype_fail(dtype);
+  if (!known_dtype(dtype) && dtype != DLSIM_F64) return dtype_fail(dtype);
   if (cpu_threads < 1) return fail(DLSIM_E_ARG, "cpu_threads must be >= 1 (got %d)", cpu_threads);
   const size_t esz = elem_bytes(dtype);
   size_t need = 0, rows_total = 0;
@@ -644,6 +655,46 @@ int dlsim_host_chunk_mean(int b, const int* fan_in, const void* const* h_inputs,
       }
     job.seal(rows_total);
   }
+  if (need * esz < kSmallHostJobBytes) {
+    // Small job (GNLeNet's Conflux reconstruct: ~1.4 MB):
+    // a DMA costs ~15 us of copy-engine time whatever its size, so pack every
+    // row first, then ONE H2D of the staging, ONE batched launch of every
+    // task's mean and, when the outputs sit at the same offsets on both
+    // sides (the ChunkManager's back-to-back layout), ONE D2H; all on
+    // `stream`.
+    pack_and_dispatch(job, threads, need * esz, [](size_t, size_t) {});
+    hipError_t e = hipMemcpyAsync(ds, hs, need * esz, hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) return hip_fail(e, "staging H2D");
+    std::vector<const void*> ins_all(rows_total);
+    for (size_t r = 0; r < rows_total; ++r) ins_all[r] = ds + row_off[r] * esz;
+    int rc = with_chunk_policy(dtype, [&](auto op) {
+      return run_chunk_mean<decltype(op)>(b, fan_in, ins_all.data(), d_outs, n_elems, cpu_threads, st);
+    });
+    if (rc != DLSIM_OK || !h_outs) return rc;
+    // one D2H if every task's output keeps its offset from task 0's on both
+    // sides; else one per task
+    const char* d0 = static_cast<const char*>(d_outs[0]);
+    char* h0 = static_cast<char*>(h_outs[0]);
+    bool one = h0 != nullptr;
+    size_t span = 0;
+    for (int t = 0; t < b && one; ++t) {
+      if (n_elems[t] == 0) continue;
+      const ptrdiff_t dd = static_cast<const char*>(d_outs[t]) - d0;
+      one = h_outs[t] && dd >= 0 && static_cast<char*>(h_outs[t]) - h0 == dd;
+      span = std::max(span, static_cast<size_t>(dd) + n_elems[t] * esz);
+    }
+    if (one) {
+      if (span > 0 && (e = hipMemcpyAsync(h0, d0, span, hipMemcpyDeviceToHost, st)) != hipSuccess)
+        return hip_fail(e, "result D2H");
+      return DLSIM_OK;
+    }
+    for (int t = 0; t < b; ++t) {
+      if (n_elems[t] == 0 || !h_outs[t]) continue;
+      e = hipMemcpyAsync(h_outs[t], d_outs[t], n_elems[t] * esz, hipMemcpyDeviceToHost, st);
+      if (e != hipSuccess) return hip_fail(e, "result D2H");
+    }
+    return DLSIM_OK;
+  }
   StreamLinks ln;
   ln.link(st, h2d, "order H2D after stream");
   if (h_outs) ln.link(st, d2h, "order D2H after stream");
@@ -664,7 +715,7 @@ int dlsim_host_chunk_mean(int b, const int* fan_in, const void* const* h_inputs,
     ins.assign(static_cast<size_t>(fan_in[t]), nullptr);
     for (int i = 0; i < fan_in[t]; ++i) ins[i] = ds + row_off[first + i] * esz;
     void* out = d_outs[t];
-    ln.rc = with_mean_policy(dtype, [&](auto op) {
+    ln.rc = with_chunk_policy(dtype, [&](auto op) {
       return run_chunk_mean<decltype(op)>(1, &fan_in[t], ins.data(), &out, &n_elems[t], cpu_threads, st);
     });
     if (ln.rc != DLSIM_OK || !h_outs || !h_outs[t]) return;

@@ -4,3 +4,4 @@
 
 DLSIM_F64_ENTRIES(template, dlsim::F64Exact)
 DLSIM_F64_ENTRIES(template, dlsim::F64Fast)
+DLSIM_CHUNK_ENTRIES(template, dlsim::F64Mean)

@@ -869,10 +869,19 @@ PyObject* clone(PyObject* m, PyObject* memo, int depth) {
     if (!d) break;
     state = PyDict_Copy(d);
     if (!state) break;
-    Py_ssize_t pos = 0;
-    PyObject *k, *v;
+    // Walk the copy's entries through an owned snapshot: clone_attr runs
+    // arbitrary Python (copy.deepcopy, __setstate__), which may mutate the
+    // module's dict; borrowed PyDict_Next references into it could then be
+    // freed mid-walk. A size change raises as the Python
+    // specification's `for k, v in d.items()` does.
+    PyObject* items = PyDict_Items(state);
+    if (!items) break;
+    const Py_ssize_t n0 = PyDict_Size(d);
     ok = 0;
-    while (ok == 0 && PyDict_Next(d, &pos, &k, &v)) {
+    for (Py_ssize_t i = 0; ok == 0 && i < PyList_GET_SIZE(items); ++i) {
+      PyObject* kv = PyList_GET_ITEM(items, i);  // owned by `items`
+      PyObject* k = PyTuple_GET_ITEM(kv, 0);
+      PyObject* v = PyTuple_GET_ITEM(kv, 1);
       if (key_is(k, s_compiled_key)) {
         ok = PyDict_DelItem(state, k);
         continue;
@@ -883,7 +892,12 @@ PyObject* clone(PyObject* m, PyObject* memo, int depth) {
         ok = PyDict_SetItem(state, k, nv);
         Py_DECREF(nv);
       }
+      if (ok == 0 && PyDict_Size(d) != n0) {
+        PyErr_SetString(PyExc_RuntimeError, "dictionary changed size during iteration");
+        ok = -1;
+      }
     }
+    Py_DECREF(items);
     if (ok < 0) break;
     // Module.__setstate__ is __dict__.update(state) when the state already has
     // every attribute it would add; a class's own __setstate__ is called
@@ -985,5 +999,17 @@ PyMODINIT_FUNC PyInit__pyhost(void) {
   s_setstate = PyUnicode_InternFromString("__setstate__");
   if (!s_parameters || !s_modules || !s_compiled_key || !s_new || !s_setstate)
     return nullptr;
-  return PyModule_Create(&kModule);
+  PyObject* mod = PyModule_Create(&kModule);
+  if (!mod) return nullptr;
+  // The torch build this file was compiled against (torch.__version__ at
+  // build time): it reads at::Tensor fields and restates deepcopy against
+  // that torch's internals, so arena.py refuses to use it under another.
+#ifndef DLSIM_TORCH_VERSION
+#error "build with -DDLSIM_TORCH_VERSION=\"<torch.__version__>\" (__graft_entry__.build())"
+#endif
+  if (PyModule_AddStringConstant(mod, "BUILT_FOR_TORCH", DLSIM_TORCH_VERSION) < 0) {
+    Py_DECREF(mod);
+    return nullptr;
+  }
+  return mod;
 }

@@ -444,6 +444,35 @@ void add_r03(std::vector<Variant>& vs, int n) {
   }
 }
 
+// Round 3 layout sweep (DLSIM_TUNE_LAYOUT): the shipped launch shapes of
+// every size class for fan-in n (fixed kernels for n = 2 and 8, the grouped
+// kernel for any n), to time one layout of the inputs and outputs.
+template <class Op, int NF>
+void add_fixed_shapes(std::vector<Variant>& vs, int n) {
+  if (n != NF) return;
+  const std::string p = "NF" + std::to_string(NF);
+  if constexpr (Op::kBytes >= 4) {
+    vs.push_back({p + "_V2_sc1_blk", launch_ts<Op, NF, 8, 2, 1, 16, false>, 0});
+    vs.push_back({p + "_V4_sc1_blk", launch_ts<Op, NF, 8, 4, 1, 16, false>, 0});
+    vs.push_back({p + "_V4_sc1_wave", launch_ts<Op, NF, 8, 4, 1, 16, true>, 0});
+  } else {
+    vs.push_back({p + "_V1_sc1_wave", launch_ts<Op, NF, 4, 1, 1, 16, true>, 0});
+    vs.push_back({p + "_V4_nt_blk", launch_ts<Op, NF, 4, 4, 1, kStNT, false>, 0});
+  }
+}
+template <class Op>
+void add_layout(std::vector<Variant>& vs, int n) {
+  add_fixed_shapes<Op, 2>(vs, n);
+  add_fixed_shapes<Op, 8>(vs, n);
+  if constexpr (Op::kBytes >= 4) {
+    vs.push_back({"T_G8_V1_sc1_wave", launch_ts<Op, 0, 8, 1, 1, 16, true>, 0});
+    vs.push_back({"T_G8_V4_sc1_blk", launch_ts<Op, 0, 8, 4, 1, 16, false>, 0});
+  } else {
+    vs.push_back({"T_G4_V1_sc1_wave", launch_ts<Op, 0, 4, 1, 1, 16, true>, 0});
+    vs.push_back({"T_G4_V4_nt_blk", launch_ts<Op, 0, 4, 4, 1, kStNT, false>, 0});
+  }
+}
+
 template <class Op, int NF>
 void add_nf(std::vector<Variant>& vs, int n) {
   if (n != NF) return;
@@ -560,7 +589,14 @@ int run(int n, size_t P, int reps, double peak_gbs) {
     for (auto& p : in) CK(hipMalloc(&p, bytes + 256));
     printf("layout=separate\n");
   }
-  for (auto& p : out) CK(hipMalloc(&p, bytes + 256));
+  // DLSIM_TUNE_OUT_OFFSET=B: each output starts B bytes past its (2 MiB
+  // aligned) allocation
+  const size_t out_off = getenv("DLSIM_TUNE_OUT_OFFSET") ? strtoull(getenv("DLSIM_TUNE_OUT_OFFSET"), nullptr, 10) & ~(size_t)15 : 0;
+  std::vector<void*> out_alloc(sets);
+  for (int k = 0; k < sets; ++k) {
+    CK(hipMalloc(&out_alloc[k], bytes + 256 + out_off));
+    out[k] = (char*)out_alloc[k] + out_off;
+  }
   printf("addr_mod_2MiB in0=%zu in1=%zu out0=%zu\n", (size_t)((uintptr_t)in[0] % (2u << 20)),
          (size_t)((uintptr_t)in[n > 1 ? 1 : 0] % (2u << 20)), (size_t)((uintptr_t)out[0] % (2u << 20)));
   for (size_t k = 0; k < in.size(); ++k)
@@ -581,9 +617,11 @@ int run(int n, size_t P, int reps, double peak_gbs) {
   for (auto& e : ev) CK(hipEventCreate(&e));
   const double alg_bytes = (double)(n + 1) * bytes;
 
-  const bool r03 = getenv("DLSIM_TUNE_R03") != nullptr;
+  const bool r03 = getenv("DLSIM_TUNE_R03") != nullptr || getenv("DLSIM_TUNE_LAYOUT") != nullptr;
   std::vector<Variant> vs;
-  if (r03) {
+  if (getenv("DLSIM_TUNE_LAYOUT")) {
+    add_layout<Op>(vs, n);
+  } else if (r03) {
     add_r03<Op, 8>(vs, n);
     if (vs.empty()) {
       fprintf(stderr, "DLSIM_TUNE_R03 needs f32 exact, n = 8\n");
@@ -704,7 +742,7 @@ int run(int n, size_t P, int reps, double peak_gbs) {
   if (arena) CK(hipFree(arena));
   else
     for (auto& p : in) CK(hipFree(p));
-  for (auto& p : out) CK(hipFree(p));
+  for (auto& p : out_alloc) CK(hipFree(p));
   return 0;
 }
 
@@ -719,12 +757,12 @@ int main(int argc, char** argv) {
     return 1;
   }
   const double peak = 8000.0;  // GB/s, MI355X HBM3E spec
-#ifdef DLSIM_TUNE_F32_ONLY  // the fp32 exact policy alone (fast to build: csrc/build/tune_f32)
-  if (dt != "f32" || mode != "exact") {
-    fprintf(stderr, "this build times f32 exact only\n");
+#ifdef DLSIM_TUNE_F32_ONLY  // the fp32 / bf16 exact policies alone (fast to build: csrc/build/tune_f32)
+  if (mode != "exact") {
+    fprintf(stderr, "this build times the exact policies only\n");
     return 1;
   }
-  return run<F32Exact>(n, P, reps, peak);
+  return dt == "f32" ? run<F32Exact>(n, P, reps, peak) : run<BF16Exact>(n, P, reps, peak);
 #endif
   if (dt == "f32")
     return mode == "exact" ? run<F32Exact>(n, P, reps, peak) : run<F32Fast>(n, P, reps, peak);

@@ -289,6 +289,23 @@ struct F16Mean {
   __device__ static float finish(float a, float div) { return f16_round(pin_f32(a / div)); }
 };
 
+// fp64 chunk mean (ChunkManager on a double model, chunk_manager.py:40): the
+// sum in double (chunk_mean_kernels.hpp's orders), one double division by m.
+struct F64Mean {
+  using T = double;
+  using W = double;
+  static constexpr int E = 2;
+  static constexpr int kBytes = 8;
+  static constexpr int kFmt = kFmtF32;
+  __device__ static double init(double) { return 0.0; }
+  __device__ static double step(double acc, double, double x) { return acc + x; }
+  __device__ static void step2(double& a0, double& a1, double, double x0, double x1) {
+    a0 = a0 + x0;
+    a1 = a1 + x1;
+  }
+  __device__ static double finish(double a, float div) { return a / static_cast<double>(div); }
+};
+
 // ---- 16-byte vector <-> E floats --------------------------------------------
 template <class Op>
 __device__ __forceinline__ void unpack(const u32x4& r, acc_t<Op> (&x)[Op::E]) {

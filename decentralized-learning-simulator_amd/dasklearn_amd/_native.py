@@ -173,9 +173,9 @@ def weights_for_dtype(weights: Sequence[float], torch_dtype) -> np.ndarray:
 
 
 def dtype_code(torch_dtype, single_task: bool = False) -> int:
-    """ABI dtype of a parameter dtype. fp64 has one entry point
-    (dlsim_wreduce_f64, single task); the batched, tensor-list, mean and host
-    entries take fp32/bf16/fp16 only."""
+    """ABI dtype of a parameter dtype. fp64 (single_task=True) has the
+    single-task reduce (dlsim_wreduce_f64) and the chunk means; the batched,
+    tensor-list, mean and host-reduce entries take fp32/bf16/fp16 only."""
     import torch
     if torch_dtype == torch.float32:
         return DLSIM_F32
@@ -374,7 +374,7 @@ def mean_batched(tasks, stream=None):
     if b == 0:
         return []
     out0 = tasks[0][1]
-    dt = dtype_code(out0.dtype)
+    dt = dtype_code(out0.dtype, single_task=True)  # fp64 chunks too (PyTorch's double order)
     fan, ptrs, outs, numels = [], [], [], []
     for inputs, out in tasks:
         if len(inputs) < 1:
@@ -408,7 +408,7 @@ def chunk_mean_batched(tasks, threads=None, stream=None):
         import torch
         threads = torch.get_num_threads()
     out0 = tasks[0][1]
-    dt = dtype_code(out0.dtype)
+    dt = dtype_code(out0.dtype, single_task=True)  # fp64 chunks too (PyTorch's double order)
     fan, ptrs, outs, numels = [], [], [], []
     for inputs, out in tasks:
         if len(inputs) < 1:
@@ -482,7 +482,8 @@ def host_chunk_mean(tasks, staging, d_staging, host_outs=None, threads=None, cpu
            lib.dlsim_host_chunk_mean(b, (ctypes.c_int * b)(*fan), (ctypes.c_void_p * len(ptrs))(*ptrs),
                                      (ctypes.c_size_t * b)(*numels), staging.data_ptr(), d_staging.data_ptr(),
                                      min(staging.numel(), d_staging.numel()), (ctypes.c_void_p * b)(*outs), hptrs,
-                                     dtype_code(dt), int(torch.get_num_threads() if cpu_threads is None else cpu_threads),
+                                     dtype_code(dt, single_task=True),  # fp64 chunks too
+                                     int(torch.get_num_threads() if cpu_threads is None else cpu_threads),
                                      int(torch.get_num_threads() if threads is None else threads),
                                      _stream_handle(out0.device, stream),
                                      None if h2d_stream is None else h2d_stream.cuda_stream,

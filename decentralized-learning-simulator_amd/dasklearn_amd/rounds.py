@@ -60,7 +60,7 @@ class RoundExecutor:
 
     def __init__(self, funcs: Dict[str, Callable], settings, device=None,
                  mode: int = _native.DLSIM_EXACT, timing: bool = False, keep_all: bool = False,
-                 tensors_in_place: bool = True, release_early: bool = True):
+                 tensors_in_place: bool = True, release_early: bool = True, foreign_streams: bool = False):
         """timing: accumulate wall seconds per kind of wave work in
         `self.stats` ("aggregate", "other"); the stream is synchronised after
         every batched aggregate so its kernels count (measurement only).
@@ -79,11 +79,20 @@ class RoundExecutor:
         box: 96 against 217 µs per task, collector passes 87/6/0 against
         468/45/3 by generation, profiles/r02_release_ab/). False drops them
         after the wave, as the broker drops a task's inputs after the task
-        returns (broker.py:221)."""
+        returns (broker.py:221).
+        foreign_streams: results are dropped while the wave's kernels may
+        still be queued; the caching allocator keeps that safe for tensors
+        allocated on the stream the reduce runs on (torch's current stream,
+        where train functions allocate unless they switch streams). A train
+        function that allocates its outputs under another stream must set
+        foreign_streams=True: every released device parameter is then
+        recorded on the current stream (Tensor.record_stream), so its block
+        is not reused before the reduce has read it."""
         self.timing = timing
         self.keep_all = keep_all
         self.tensors_in_place = tensors_in_place
         self.release_early = release_early
+        self.foreign_streams = foreign_streams
         self.stats: Dict[str, float] = {"aggregate": 0.0, "other": 0.0, "aggregate_tasks": 0}
         self.funcs = dict(funcs)
         self.settings = settings
@@ -128,7 +137,7 @@ class RoundExecutor:
                      for dt in layout.groups}
         params = [layout.params]
         dev = _device_views(views)
-        if dev is not None and (self.device is None or dev == torch.device(self.device)):
+        if dev is not None and (self.device is None or dev == _target_device((), self.device)):
             arenas = {dt: vs[0] for dt, vs in views.items()}
         else:
             dev = _target_device(params[0], self.device)
@@ -289,7 +298,9 @@ class RoundExecutor:
 
             def release():
                 for r in dying:
-                    self.results.pop(r, None)
+                    res = self.results.pop(r, None)
+                    if self.foreign_streams and res is not None:
+                        _record_on_current_stream(res)
                 dying.clear()
             t0 = time.perf_counter()
             for name, func, data in ready:
@@ -317,3 +328,13 @@ class RoundExecutor:
             release()
             pending = [t for t in pending if t[0] not in done]
         return self.results
+
+
+def _record_on_current_stream(objs) -> None:
+    """Tensor.record_stream(current stream) on every device parameter of the
+    modules (and device tensors) in `objs` (RoundExecutor foreign_streams)."""
+    for o in objs:
+        ts = module_params(o) if isinstance(o, nn.Module) else [o] if isinstance(o, torch.Tensor) else []
+        for t in ts:
+            if t.is_cuda:
+                t.record_stream(torch.cuda.current_stream(t.device))

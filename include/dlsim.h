@@ -40,7 +40,9 @@ enum dlsim_dtype {
   DLSIM_F32 = 0,  /* IEEE binary32                                      */
   DLSIM_BF16 = 1, /* bfloat16 (upper 16 bits of binary32), RNE rounding  */
   DLSIM_F16 = 2,  /* IEEE binary16, RNE rounding                        */
-  DLSIM_F64 = 3   /* IEEE binary64: dlsim_wreduce_f64 only (double weights) */
+  DLSIM_F64 = 3   /* IEEE binary64: dlsim_wreduce_f64 (double weights) and
+                     the chunk means (dlsim_chunk_mean_batched,
+                     dlsim_host_chunk_mean) only */
 };
 
 enum dlsim_mode {
@@ -215,7 +217,9 @@ int dlsim_mean_batched(int b, const int* fan_in, const void* const* d_inputs, vo
  * averages fan_in[t] buffers d_inputs[o_t .. o_t + fan_in[t]) (o_t the prefix
  * sum of fan_in) into d_outs[t] (n_elems[t] elements, < 2 GiB). The order is
  * ATen's cascade_sum (chunk_mean_kernels.hpp); bf16 chunks are summed in
- * fp32, divided and rounded once. Any fan-in up to 65535: up to 192 inputs
+ * fp32, divided and rounded once; DLSIM_F64 chunks are summed and divided in
+ * double in PyTorch's double order (Vectorized<double>'s 4 lanes: 16-column
+ * blocks and rounding). Any fan-in up to 65535: up to 192 inputs
  * per launch travel as kernel arguments, larger ones through a stream-ordered
  * device array (hipMallocAsync / hipFreeAsync on `stream`). Tasks whose
  * outputs overlap another task's buffers run one launch each, in order.

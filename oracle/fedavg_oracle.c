@@ -301,6 +301,96 @@ static float inner_sum(const float* x, long long m) {
   return fin;
 }
 
+/* The column split for an element of `esz` bytes whose Vectorized<acc> has
+ * `vw` lanes (fp32: 4 B, 8 lanes; fp64: 8 B, 4 lanes): ranges rounded to
+ * 128 B of columns, whole blocks of 4 vectors (nrows = 4 of
+ * vectorized_outer_sum) in the cascade order, the vectorized path from vw
+ * columns up, scalar_outer_sum's 4-column groups below. */
+static size_t ilp_begin_gen(int m, size_t n, int threads, size_t esz, size_t vw) {
+  if (n <= 1) return 0;
+  const size_t rnd = 128 / esz;
+  size_t b = 0, e = n;
+  if (!((unsigned long long)m * n < 32768ULL || threads <= 1)) {
+    const size_t tp = (size_t)threads < n ? (size_t)threads : n;
+    const size_t cs = (n + tp - 1) / tp;
+    for (size_t t = 0; t < tp; ++t) {
+      size_t tb = t * cs;
+      if (tb >= n) break;
+      size_t te = tb + cs < n ? tb + cs : n;
+      tb -= tb % rnd;
+      if (te != n) te -= te % rnd;
+      if (tb < te) { b = tb; e = te; }
+    }
+  }
+  const size_t s1 = e - b;
+  const size_t main = s1 >= vw ? s1 / (4 * vw) * (4 * vw) : s1 / 4 * 4;
+  return b + main;
+}
+
+/* fp64 (chunk_manager.py:40 on a double model): the same orders in double,
+ * with SumKernel's Vectorized<double> (4 lanes) and 16-column (128 B)
+ * rounding; restated per function from the fp32 ones above. */
+static double cascade_sum_f64(const double* x, long long S, long long st) {
+  int lp = ceil_log2_i64(S) / 4;
+  if (lp < 4) lp = 4;
+  const long long step = 1LL << lp, mask = step - 1;
+  double a[4] = {0.0, 0.0, 0.0, 0.0};
+  long long i = 0;
+  while (i + step <= S) {
+    for (long long j = 0; j < step; ++j, ++i) a[0] = a[0] + x[i * st];
+    for (int l = 1; l < 4; ++l) {
+      a[l] = a[l] + a[l - 1];
+      a[l - 1] = 0.0;
+      if ((i & (mask << (l * lp))) != 0) break;
+    }
+  }
+  for (; i < S; ++i) a[0] = a[0] + x[i * st];
+  for (int l = 1; l < 4; ++l) a[0] = a[0] + a[l];
+  return a[0];
+}
+
+static double ilp_sum_f64(const double* x, long long len, long long st) {
+  const long long s = len / 4;
+  double p[4];
+  for (int k = 0; k < 4; ++k) p[k] = cascade_sum_f64(x + k * st, s, 4 * st);
+  for (long long i = 4 * s; i < len; ++i) p[0] = p[0] + x[i * st];
+  return ((p[0] + p[1]) + p[2]) + p[3];
+}
+
+static double inner_sum_f64(const double* x, long long m) {  /* 4 lanes */
+  const long long vs = m / 4;
+  double fin = 0.0;
+  for (long long k = vs * 4; k < m; ++k) fin = fin + x[k];
+  for (int l = 0; l < 4; ++l) fin = fin + ilp_sum_f64(x + l, vs, 4);
+  return fin;
+}
+
+size_t oracle_chunk_mean_ilp_begin_f64(int m, size_t n, int threads) { return ilp_begin_gen(m, n, threads, 8, 4); }
+
+int oracle_chunk_mean_f64(const double* const* in, int m, double* out, size_t n, int threads) {
+  if (m < 1 || !in || !out) return -1;
+  const size_t cb = 4096;
+  double* col = (double*)malloc(sizeof(double) * (size_t)m * cb);
+  if (!col) return -2;
+  const size_t ib = oracle_chunk_mean_ilp_begin_f64(m, n, threads);
+  for (size_t j0 = 0; j0 < n; j0 += cb) {
+    const size_t c = n - j0 < cb ? n - j0 : cb;
+    for (size_t j = 0; j < c; ++j)
+      for (int i = 0; i < m; ++i) col[j * (size_t)m + i] = in[i][j0 + j];
+    for (size_t j = 0; j < c; ++j) {
+      const double* x = col + j * (size_t)m;
+      const size_t g = j0 + j;
+      double s;
+      if (n == 1) s = m >= 4 ? inner_sum_f64(x, m) : ilp_sum_f64(x, m, 1);
+      else if (g < ib) s = cascade_sum_f64(x, m, 1);
+      else s = ilp_sum_f64(x, m, 1);
+      out[g] = s / (double)m;
+    }
+  }
+  free(col);
+  return 0;
+}
+
 size_t oracle_chunk_mean_ilp_begin(int m, size_t n, int threads) {
   if (n == 0) return 0;
   if (n == 1) return 0;

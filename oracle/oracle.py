@@ -51,12 +51,14 @@ def _load():
         fn = getattr(lib, name)
         fn.argtypes = [pp, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t]
         fn.restype = ctypes.c_int
-    for name in ("oracle_chunk_mean_f32", "oracle_chunk_mean_bf16", "oracle_chunk_mean_f16"):
+    for name in ("oracle_chunk_mean_f32", "oracle_chunk_mean_bf16", "oracle_chunk_mean_f16", "oracle_chunk_mean_f64"):
         fn = getattr(lib, name)
         fn.argtypes = [pp, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
         fn.restype = ctypes.c_int
     lib.oracle_chunk_mean_ilp_begin.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int]
     lib.oracle_chunk_mean_ilp_begin.restype = ctypes.c_size_t
+    lib.oracle_chunk_mean_ilp_begin_f64.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int]
+    lib.oracle_chunk_mean_ilp_begin_f64.restype = ctypes.c_size_t
     for name in ("oracle_wreduce_f64", "oracle_wreduce_fast_f64"):
         fn = getattr(lib, name)
         fn.argtypes = [pp, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
@@ -178,6 +180,10 @@ def chunk_mean(xs, dtype: str = "f32", threads: int = 4) -> np.ndarray:
         rows, p = _as_rows(xs, np.uint16)
         out = np.empty(p, dtype=np.uint16)
         fn = getattr(lib, f"oracle_chunk_mean_{dtype}")
+    elif dtype == "f64":  # Vectorized<double>: 4 lanes, 16-column rounding
+        rows, p = _as_rows(xs, np.float64)
+        out = np.empty(p, dtype=np.float64)
+        fn = lib.oracle_chunk_mean_f64
     else:
         raise ValueError(f"unsupported dtype {dtype}")
     ptrs = (ctypes.c_void_p * n)(*[r.ctypes.data for r in rows])
@@ -186,8 +192,10 @@ def chunk_mean(xs, dtype: str = "f32", threads: int = 4) -> np.ndarray:
     return out.view(np.float16) if dtype == "f16" else out
 
 
-def chunk_mean_ilp_begin(m: int, n: int, threads: int) -> int:
+def chunk_mean_ilp_begin(m: int, n: int, threads: int, dtype: str = "f32") -> int:
     """First column that PyTorch's CPU sum folds in row_sum (ILP) order."""
+    if dtype == "f64":
+        return int(_load().oracle_chunk_mean_ilp_begin_f64(m, n, threads))
     return int(_load().oracle_chunk_mean_ilp_begin(m, n, threads))
 
 

@@ -10,6 +10,8 @@ inputs and outputs as .npz data next to this script. Skips when
 
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_chunks.py
 
+fp64 cases (double models) go to chunks_f64/ with meta dtype "f64".
+
 Per case (np.load(..., allow_pickle=False)):
     meta       JSON: case, num_chunks k, contributors per chunk index, shapes,
                torch_version / cpu_capability of the generating process (the
@@ -79,6 +81,41 @@ def main() -> int:
         for p in range(mmax):
             arrays[f"flat_{p}"] = ChunkManager.get_flat_params(models[p]).numpy().copy()
         path = os.path.join(HERE, "chunks", case + ".npz")
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        np.savez_compressed(path, **arrays)
+        written.append(path)
+    # fp64 models: the same tasks on double parameters,
+    # whose torch.mean runs PyTorch's double order (Vectorized<double>: 4
+    # lanes, 16-column blocks and rounding). The last case has enough columns
+    # that the worker's 4 threads split them (m * n >= 32768).
+    shapes64 = [[9001], [50, 50], [7]]  # 11,508 parameters
+    for k, counts, shp in [(1, [2], shapes), (3, [1, 2, 3], shapes), (4, [4, 4, 4, 4], shapes),
+                           (2, [5, 8], shapes), (3, [16, 3, 7], shapes), (2, [4, 9], shapes64)]:
+        mmax = max(counts)
+        g = torch.Generator().manual_seed(700 + k * 10 + mmax)
+        models = []
+        for p in range(mmax):
+            m = Net(shp).double()
+            with torch.no_grad():
+                for q in m.parameters():
+                    q.copy_(torch.randn(q.shape, generator=g, dtype=torch.float64) * 0.05)
+            models.append(m)
+        chunked = [ChunkManager.chunk_model(m, k) for m in models]
+        chunks = [[chunked[p][c].clone() for p in range(counts[c])] for c in range(k)]
+        chunk_arrays = {f"chunks_{c}": torch.stack(chunks[c]).numpy().copy() for c in range(k)}
+        target = Net(shp).double()
+        out = ChunkManager.reconstruct_model([list(cs) for cs in chunks], target)
+        expected = ChunkManager.get_flat_params(out).numpy().copy()
+        assert expected.dtype == np.float64
+        case = f"chunks_f64_k{k}_m{'-'.join(map(str, counts))}"
+        meta = dict(case=case, num_chunks=k, counts=counts, shapes=shp, torch_threads=4, dtype="f64",
+                    source="seeded randn*0.05 double models (stored)",
+                    torch_version=torch.__version__,
+                    cpu_capability=torch.backends.cpu.get_cpu_capability())
+        arrays = dict(meta=np.array(json.dumps(meta)), expected=expected, **chunk_arrays)
+        for p in range(mmax):
+            arrays[f"flat_{p}"] = ChunkManager.get_flat_params(models[p]).numpy().copy()
+        path = os.path.join(HERE, "chunks_f64", case + ".npz")
         os.makedirs(os.path.dirname(path), exist_ok=True)
         np.savez_compressed(path, **arrays)
         written.append(path)

@@ -113,7 +113,8 @@ def test_rank_stdout_carries_only_the_result_line(tmp_path):
 def test_guarded_returns_or_prints_and_exits_on_timeout(tmp_path):
     """bench._guarded: a call that returns in time gives its value; one that
     hangs past the timeout runs on_timeout (rank 0 prints its line) and the
-    process exits 0 instead of holding the multi-GPU bench hostage."""
+    process exits with bench.WATCHDOG_EXIT (non-zero: the run is reported as
+    failed) instead of holding the multi-GPU bench hostage."""
     import subprocess
     assert bench._guarded(lambda: 42, 5.0, lambda: None) == 42
     script = tmp_path / "child.py"
@@ -126,6 +127,27 @@ def test_guarded_returns_or_prints_and_exits_on_timeout(tmp_path):
     """))
     t0 = time.perf_counter()
     r = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, timeout=120)
-    assert r.returncode == 0, r.stderr
+    assert r.returncode == bench.WATCHDOG_EXIT != 0, r.stderr
     assert r.stdout.splitlines() == ['{"value": 7}']
     assert time.perf_counter() - t0 < 25
+
+
+def test_pmc_traffic_takes_the_newest_round(tmp_path, monkeypatch):
+    """with several PMC summaries for one config the
+    newest round/session wins (r01 < r01_s4 < r02 < r02s2 < r03)."""
+    prof = tmp_path / "profiles"
+    (prof / "r03_sub").mkdir(parents=True)
+    for name, val in [("r02s2_pmc_traffic.json", 2), ("r01_s4_pmc_traffic.json", 1), ("r02_pmc_traffic.json", 3),
+                      ("r03_sub/r03_pmc_traffic.json", 4)]:
+        (prof / name).write_text(json.dumps({"north_star": {"exact": {"hbm_bytes_per_launch": val}}}))
+    (prof / "r03_other_pmc.json").write_text(json.dumps({"cfg2": {"exact": {"hbm_bytes_per_launch": 9}}}))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    b, src = bench.pmc_traffic("north_star", "exact", 1)
+    assert b == 4 and src.startswith("profiles/r03_sub/r03_pmc_traffic.json")
+    assert bench.pmc_traffic("cfg3", "exact", 1)[0] is None
+
+
+def test_box_info_names_the_host():
+    info = bench.box_info()
+    assert info["host_cpus"] >= 1 and info["threads_usable"] >= 1
+    assert "cgroup_cpu_quota" in info and "omp_num_threads" in info

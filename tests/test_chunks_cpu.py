@@ -142,3 +142,64 @@ def test_reconstruction_warns_once_outside_the_pinned_build(monkeypatch):
     with warnings.catch_warnings():
         warnings.simplefilter("error")
         cm._check_order_scope()  # once per process
+
+
+# ---- fp64 chunks ---------------------------------------
+CHUNK_FIXTURES_F64 = sorted(glob.glob(os.path.join(GOLDEN, "chunks_f64", "*.npz")))
+
+
+def net64(shapes):
+    return Net(shapes).double()
+
+
+def test_f64_fixtures_exist():
+    assert len(CHUNK_FIXTURES_F64) >= 6
+
+
+@pytest.mark.parametrize("path", CHUNK_FIXTURES_F64, ids=lambda p: os.path.basename(p)[:-4])
+def test_f64_chunking_matches_reference(path):
+    d = load(path)
+    assert d["meta"]["dtype"] == "f64" and d["expected"].dtype == np.float64
+    k, counts = d["meta"]["num_chunks"], d["meta"]["counts"]
+    for p in range(max(counts)):
+        m = net64(d["meta"]["shapes"])
+        off = 0
+        with torch.no_grad():
+            for q in m.parameters():
+                q.copy_(torch.from_numpy(d[f"flat_{p}"][off:off + q.numel()].copy()).view_as(q))
+                off += q.numel()
+        chunks = ChunkManager.chunk_model(m, k)
+        for c in range(k):
+            if p < counts[c]:
+                assert np.array_equal(chunks[c].numpy(), d[f"chunks_{c}"][p])
+
+
+@pytest.mark.parametrize("path", CHUNK_FIXTURES_F64, ids=lambda p: os.path.basename(p)[:-4])
+def test_f64_chunk_mean_oracle_bit_exact_vs_reference(path):
+    """oracle.chunk_mean(..., "f64"): PyTorch's double order (4-lane vectors,
+    16-column blocks and rounding) reproduces every mean the reference's
+    ChunkManager produced on double models."""
+    d = load(path)
+    k = d["meta"]["num_chunks"]
+    got = np.concatenate([orc.chunk_mean(list(d[f"chunks_{c}"]), "f64", d["meta"]["torch_threads"])
+                          for c in range(k)])
+    assert np.array_equal(got.view(np.int64), d["expected"].view(np.int64))
+
+
+@pytest.mark.parametrize("threads", [1, 2, 3, 4, 8])
+def test_f64_chunk_mean_oracle_matches_torch(threads):
+    """The double order against torch.mean itself across the branches: the
+    vectorized (>= 4 columns) and scalar paths, 16-column blocks, the row_sum
+    tail, the 4-lane inner reduction, the thread split, multi-level cascades."""
+    rng = np.random.default_rng(threads + 64)
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        for m in (1, 2, 3, 4, 5, 7, 8, 16, 17, 33, 300):
+            for n in (1, 2, 3, 4, 5, 15, 16, 17, 31, 33, 100, 8193, 40001):
+                x = rng.standard_normal((m, n)) * np.exp(rng.standard_normal((m, n)) * 2)
+                exp = torch.mean(torch.stack(list(torch.from_numpy(x))), 0).numpy()
+                got = orc.chunk_mean(list(x), "f64", threads)
+                assert np.array_equal(got.view(np.int64), exp.view(np.int64)), (m, n)
+    finally:
+        torch.set_num_threads(prev)

@@ -147,12 +147,13 @@ def test_mean_chunk_indices_one_launch_per_dtype(where):
 def _rows_t(rng, m, n, dtype, offset=0):
     """m rows of n elements as device tensors, `offset` elements into their
     buffers (offset 1: not 16-byte aligned)."""
-    x = (rng.standard_normal((m, n)) * np.exp(rng.standard_normal((m, n)) * 2)).astype(np.float32)
+    x = (rng.standard_normal((m, n)) * np.exp(rng.standard_normal((m, n)) * 2))
+    x = x if dtype == "f64" else x.astype(np.float32)
     rows = orc.f32_to_bf16_bits(x) if dtype == "bf16" else orc.f32_to_f16_bits(x) if dtype == "f16" else x
     tdt = torch.bfloat16 if dtype == "bf16" else torch.float16
     ts = []
     for r in rows:
-        h = torch.from_numpy(r.view(np.int16).copy()).view(tdt) if dtype != "f32" \
+        h = torch.from_numpy(r.view(np.int16).copy()).view(tdt) if dtype in ("bf16", "f16") \
             else torch.from_numpy(r.copy())
         buf = torch.empty(n + offset, dtype=h.dtype, device=dev())
         buf[offset:].copy_(h)
@@ -165,7 +166,7 @@ def _bits(t):
     return t.view(torch.int16).numpy().view(np.uint16) if t.dtype == torch.bfloat16 else t.numpy()
 
 
-@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16"])
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16", "f64"])
 @pytest.mark.parametrize("threads", [1, 4, 8])
 def test_chunk_mean_matches_torch_order(dtype, threads):
     """Every (m, n) class of PyTorch's CPU sum order — cascade blocks, the
@@ -173,7 +174,7 @@ def test_chunk_mean_matches_torch_order(dtype, threads):
     reduction, the level-1 flush at 16 rows — in batches that cross the
     32-task / 192-input launch limits: each task bit-identical to the
     order-exact oracle (pinned against torch.mean on the CPU)."""
-    rng = np.random.default_rng(threads * 10 + ["f32", "bf16", "f16"].index(dtype))
+    rng = np.random.default_rng(threads * 10 + ["f32", "bf16", "f16", "f64"].index(dtype))
     tasks, exp = [], []
     for m in (1, 2, 3, 4, 5, 8, 9, 16, 17, 18, 33, 100):
         for n in (1, 2, 3, 5, 7, 8, 9, 31, 33, 65, 1000, 4099, 40001):
@@ -185,7 +186,7 @@ def test_chunk_mean_matches_torch_order(dtype, threads):
         assert orc.same_bits(_bits(out), e), (len(ts), out.numel())
 
 
-@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16"])
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16", "f64"])
 def test_chunk_mean_unaligned_and_aliased(dtype):
     """Rows one element into their buffers (scalar path), and the output
     aliasing input 0."""
@@ -200,16 +201,17 @@ def test_chunk_mean_unaligned_and_aliased(dtype):
         assert orc.same_bits(_bits(ts[0]), e)
 
 
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
 @pytest.mark.parametrize("m", [193, 256, 300])
-def test_chunk_mean_large_fan_in(m):
+def test_chunk_mean_large_fan_in(m, dtype):
     """More inputs than a kernel-argument batch holds: the device pointer
     array path, with the level-2 flush of the cascade at 256 rows."""
     rng = np.random.default_rng(m)
     for n in (1, 9, 5000):
-        rows, ts = _rows_t(rng, m, n, "f32")
-        out = torch.empty(n, device=dev())
+        rows, ts = _rows_t(rng, m, n, dtype)
+        out = torch.empty(n, dtype=ts[0].dtype, device=dev())
         _native.chunk_mean_batched([(ts, out)], threads=4)
-        assert orc.same_bits(_bits(out), orc.chunk_mean(list(rows), "f32", 4)), n
+        assert orc.same_bits(_bits(out), orc.chunk_mean(list(rows), dtype, 4)), n
 
 
 def test_chunk_mean_resnet18_chunks_full_size():
@@ -235,7 +237,7 @@ def test_chunk_mean_errors():
         _native.chunk_mean_batched([([x], torch.empty(8, device=dev()))], threads=0)
 
 
-@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16"])
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16", "f64"])
 @pytest.mark.parametrize("threads,cpu_threads,side", [(1, 1, False), (4, 4, True), (8, 8, True), (3, 16, False)])
 def test_host_chunk_mean_matches_torch_order(dtype, threads, cpu_threads, side):
     """dlsim_host_chunk_mean (host chunks packed on `threads` library threads,
@@ -247,11 +249,12 @@ def test_host_chunk_mean_matches_torch_order(dtype, threads, cpu_threads, side):
     rng = np.random.default_rng(threads * 100 + cpu_threads)
     tasks, exp, hosts = [], [], []
     for m, n in [(4, 300_001), (1, 7), (40, 4099), (3, 0), (17, 1), (2, 65), (9, 1_000_003), (5, 33)]:
-        x = (rng.standard_normal((m, n)) * 0.1).astype(np.float32)
+        x = rng.standard_normal((m, n)) * 0.1
+        x = x if dtype == "f64" else x.astype(np.float32)
         rows = orc.f32_to_bf16_bits(x) if dtype == "bf16" else orc.f32_to_f16_bits(x) if dtype == "f16" else x
         ts = []
         for i, r in enumerate(rows):
-            if dtype == "f32":
+            if dtype in ("f32", "f64"):
                 h = torch.from_numpy(r.copy())
             else:
                 h = torch.from_numpy(r.view(np.int16).copy()).view(torch.bfloat16 if dtype == "bf16" else torch.float16)
@@ -286,3 +289,73 @@ def test_host_chunk_mean_rejects_small_staging():
     stage = torch.empty(64, pin_memory=True)
     with pytest.raises(ValueError):
         _native.host_chunk_mean([(x, out)], stage, torch.empty(64, device=dev()))
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f64"])
+@pytest.mark.parametrize("tight", [True, False])
+def test_host_chunk_mean_small_job_one_dma(dtype, tight):
+    """a job under 4 MiB (GNLeNet's Conflux reconstruct:
+    k = 10 chunk indices of ~8.5 K elements, m = 4) packs every row, sends ONE
+    H2D, runs ONE batched launch and, when the outputs keep the same offsets
+    on the device and the host (ChunkManager's back-to-back layout), ONE D2H;
+    every mean bit-identical to the order-exact oracle, with outputs back to
+    back and at padded device offsets."""
+    rng = np.random.default_rng(17)
+    k, m, size = 10, 4, 85_354 // 10
+    sizes = [size] * (k - 1) + [85_354 - size * (k - 1)]
+    tdt = {"f32": torch.float32, "bf16": torch.bfloat16, "f64": torch.float64}[dtype]
+    esz = torch.empty((), dtype=tdt).element_size()
+    al = 256 // esz
+    tasks, exp, hosts = [], [], []
+    total = sum(sizes) if tight else sum((n + al - 1) // al * al for n in sizes)
+    d_out = torch.empty(total, dtype=tdt, device=dev())
+    host = torch.empty(sum(sizes), dtype=tdt, pin_memory=True)
+    off = hoff = 0
+    for n in sizes:
+        x = rng.standard_normal((m, n)) * 0.1
+        x = x if dtype == "f64" else x.astype(np.float32)
+        rows = orc.f32_to_bf16_bits(x) if dtype == "bf16" else x
+        ts = [torch.from_numpy(r.view(np.int16).copy()).view(tdt) if dtype == "bf16" else torch.from_numpy(r.copy())
+              for r in rows]
+        tasks.append((ts, d_out[off:off + n]))
+        hosts.append(host[hoff:hoff + n])
+        exp.append(orc.chunk_mean(list(rows), dtype, 4))
+        off += n if tight else (n + al - 1) // al * al
+        hoff += n
+    need = _native.staged_rows_elems(sizes, [m] * k, esz)
+    assert need * esz < 4 << 20
+    stage = torch.empty(need, dtype=tdt, pin_memory=True)
+    d_in = torch.empty(need, dtype=tdt, device=dev())
+    stream = torch.cuda.current_stream(dev())
+    _native.host_chunk_mean(tasks, stage, d_in, host_outs=hosts, threads=4, cpu_threads=4, stream=stream)
+    stream.synchronize()
+    for (ts, out), h, e in zip(tasks, hosts, exp):
+        assert orc.same_bits(_bits(out), e)
+        assert orc.same_bits(_bits(h), e)
+
+
+CHUNK_FIXTURES_F64 = sorted(__import__("glob").glob(os.path.join(os.path.dirname(CHUNK_FIXTURES[0]), "..",
+                                                                   "chunks_f64", "*.npz")))
+
+
+@pytest.mark.parametrize("path", CHUNK_FIXTURES_F64, ids=lambda p: os.path.basename(p)[:-4])
+@pytest.mark.parametrize("where", ["host", "device"])
+def test_reconstruct_f64_matches_reference(path, where):
+    """ChunkManager.reconstruct_model on double models,
+    bit-identical to the reference's own (PyTorch's double order)."""
+    d = load(path)
+    k, counts = d["meta"]["num_chunks"], d["meta"]["counts"]
+    chunks = [[torch.from_numpy(d[f"chunks_{c}"][p].copy()) for p in range(counts[c])] for c in range(k)]
+    target = Net(d["meta"]["shapes"]).double()
+    if where == "device":
+        chunks = [[t.to(dev()) for t in cs] for cs in chunks]
+        target = target.to(dev())
+    prev = torch.get_num_threads()
+    torch.set_num_threads(d["meta"]["torch_threads"])
+    try:
+        out = ChunkManager.reconstruct_model(chunks, target)
+    finally:
+        torch.set_num_threads(prev)
+    got = ChunkManager.get_flat_params(out).cpu().numpy()
+    assert got.dtype == np.float64
+    assert np.array_equal(got.view(np.int64), d["expected"].view(np.int64)), counts

@@ -215,3 +215,67 @@ def test_wreduce_rows_multi_matches_per_task_and_refuses_strided_tensors():
         for out, ref in exp:
             assert torch.equal(out.view(torch.int16) if dt == torch.bfloat16 else out.view(torch.int32),
                                ref.view(torch.int16) if dt == torch.bfloat16 else ref.view(torch.int32))
+
+
+_SIDE = {}
+
+
+def side_stream_train(settings, params):
+    """device_agnostic_train whose outputs are allocated and written under a
+    side stream (then ordered before the current stream's work), followed by
+    scratch allocations on that stream that may reuse freed blocks."""
+    dev = torch.device("cuda", torch.cuda.current_device())
+    s = _SIDE.setdefault(dev, torch.cuda.Stream(dev))
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        out = device_agnostic_train(settings, params)[0]
+        junk = [torch.full((p.numel(),), float("nan"), device=dev) for p in out.parameters()]
+        del junk
+    torch.cuda.current_stream(dev).wait_stream(s)
+    return [out]
+
+
+def test_round_executor_foreign_streams():
+    """ADVICE r02 (batch.py release_early): a train function that allocates
+    its outputs under another stream runs with foreign_streams=True: released
+    inputs are recorded on the reduce's stream, and the rounds stay
+    bit-identical to the oracle replay."""
+    torch.manual_seed(31)
+    init = Shaped(GNLENET).cuda()
+    with torch.no_grad():
+        for p in init.parameters():
+            p.copy_(torch.randn(p.shape, device=p.device) * 0.05)
+    tasks, nb = build_dag(8, 3)
+    ex = RoundExecutor({"train": side_stream_train}, Settings(), foreign_streams=True)
+    got = ex.run(tasks, seed={"init": [init]})
+    exp = replay(tasks, {"aggregate": oracle_aggregate, "train": device_agnostic_train}, init.cpu())
+    for p in range(8):
+        a = got[f"agg_{p}_3"][0]
+        b = exp[f"agg_{p}_3"][0]
+        assert orc.same_bits(torch.cat([q.detach().reshape(-1).cpu() for q in a.parameters()]).numpy(), flat(b))
+
+
+def test_round_executor_device_cuda_without_index():
+    """ADVICE r02 (arena._target_device): device='cuda' (no index) means the
+    current device, so device-resident models are read where they are (no
+    flatten copy) and the results stay bit-identical."""
+    torch.manual_seed(37)
+    init = Shaped(GNLENET).cuda()
+    tasks, nb = build_dag(4, 2)
+    flattened = []
+    orig = torch._C._nn.flatten_dense_tensors
+
+    def spy(ts):
+        flattened.append(len(ts))
+        return orig(ts)
+    torch._C._nn.flatten_dense_tensors = spy
+    try:
+        ex = RoundExecutor({"train": device_agnostic_train}, Settings(), device="cuda")
+        got = ex.run(tasks, seed={"init": [init]})
+    finally:
+        torch._C._nn.flatten_dense_tensors = orig
+    assert not flattened
+    exp = replay(tasks, {"aggregate": oracle_aggregate, "train": device_agnostic_train}, init.cpu())
+    for p in range(4):
+        a, b = got[f"agg_{p}_2"][0], exp[f"agg_{p}_2"][0]
+        assert orc.same_bits(torch.cat([q.detach().reshape(-1).cpu() for q in a.parameters()]).numpy(), flat(b))

@@ -274,6 +274,38 @@ def test_c_clone_propagates_errors():
         arena._clone_module(m, {})
 
 
+def test_c_clone_survives_an_attribute_that_mutates_the_module():
+    """an attribute whose __deepcopy__ changes the module's dict
+    while the C clone walks it must not leave the walk holding freed
+    references; like the Python specification (`for k, v in d.items()`) the
+    clone raises RuntimeError, and with the values replaced in place (no size
+    change) both finish."""
+    class Grow:
+        def __init__(self, owner, add):
+            self.owner, self.add = owner, add
+
+        def __deepcopy__(self, memo):
+            if self.add:
+                self.owner.__dict__[f"grown_{len(self.owner.__dict__)}"] = object()
+            else:
+                for k in list(self.owner.__dict__):
+                    if k.startswith("victim"):
+                        self.owner.__dict__[k] = [0]  # drops the old value's last reference
+            return Grow(None, False)
+
+    for spec in (arena._clone_module, arena._clone_module_py):
+        m = nn.Linear(2, 2)
+        m.a_grow = Grow(m, True)
+        m.z_victim = [object() for _ in range(3)]
+        with pytest.raises(RuntimeError, match="changed size"):
+            spec(m, {})
+        m = nn.Linear(2, 2)
+        m.a_swap = Grow(m, False)
+        m.victim = [object() for _ in range(3)]
+        out = spec(m, {})
+        assert isinstance(out.a_swap, Grow)
+
+
 def test_fast_clone_respects_custom_deepcopy():
     m = nn.Sequential(_CustomCopy(3, 2))
     lay = arena.ParamLayout(m)
@@ -295,6 +327,15 @@ def test_registered_arenas_invalidated_by_reassignment():
     out2[0].weight = nn.Parameter(torch.ones(3, 4))  # replaced
     assert arena.registered_arenas(out2) is None
     assert arena.registered_arenas(m) is None  # never registered
+    # same address and shape, other strides (a square weight
+    # re-viewed transposed): the arena no longer holds p's logical values
+    sq = nn.Sequential(nn.Linear(3, 3))
+    lsq = arena.ParamLayout(sq)
+    out3 = arena.module_from_arenas(sq, lsq, {torch.float32: torch.arange(float(lsq.totals[torch.float32]))})
+    assert arena.registered_arenas(out3) is not None
+    out3[0].weight.data = out3[0].weight.data.t()
+    assert out3[0].weight.data_ptr() == arena._arena_entry(out3).bases[torch.float32]
+    assert arena.registered_arenas(out3) is None
 
 
 def test_input_arenas_mixes_registered_and_plain():
@@ -587,3 +628,15 @@ def test_param_views_match_make_subclass(offset):
     loss.backward()
     assert torch.equal(w.grad, torch.full_like(w, 3.0))
     assert got[id(m.a.bias)].grad is None and not got[id(m.a.bias)].requires_grad
+
+
+def test_pyhost_torch_version_guard():
+    """_pyhost is compiled against one torch's internals;
+    the package refuses it under another torch instead of mis-cloning."""
+    from dasklearn_amd import _pyhost
+    assert _pyhost.BUILT_FOR_TORCH == torch.__version__
+    arena.check_pyhost_build(torch.__version__, torch.__version__)
+    with pytest.raises(ImportError, match="built for torch 2.1.2"):
+        arena.check_pyhost_build("2.1.2", torch.__version__)
+    with pytest.raises(ImportError, match="rebuild"):
+        arena.check_pyhost_build(torch.__version__, torch.__version__ + "-other")
