@@ -212,29 +212,38 @@ class ReduceWorkload:
 
     def __init__(self, n, p, dtype, w32, mode, batch, dev, seed, stream):
         from dasklearn_amd import _native
-        from dasklearn_amd.arena import row_stride
+        from dasklearn_amd.arena import aligned_empty, arena_empty, base_align, row_stride
         tdt = TORCH_DTYPE[dtype]
         esz = ELEM_BYTES[dtype]
         self.stream = stream
         self.bytes_per_step = (n + 1) * p * esz * batch
         self.sets = n_sets(self.bytes_per_step)
         g = torch.Generator(device=dev).manual_seed(seed)
-        # rows padded to 256 B so every model's arena starts 16-byte aligned
-        # (the vector kernel's requirement), at the staging arena's stride
+        # the models are rows of one arena laid out as the product's staging
+        # and round uploads lay them out (arena.row_stride / base_align: 256 B
+        # rows, or 2 MiB-aligned rows for >= 16 MiB of 4/8-byte elements), the
+        # outputs as the product allocates aggregate outputs (arena_empty)
         p_pad = row_stride(p, esz)
+        al = base_align(p * esz, esz)
         self.plans, self.probe_plans, self.outs, self._keep = [], [], [], []
+        # every set's rows in ONE allocation, as the staging buffer holds a
+        # call's rows: rows in separate per-set allocations measured 0.5-2.5 %
+        # slower and varied with where the driver placed them
+        # (profiles/r03_bench_gap.jsonl)
+        rows = aligned_empty(self.sets * batch * n * p_pad, tdt, dev, al).view(self.sets, batch, n, p_pad)
+        self._keep.append(rows)
         for s in range(self.sets):
             if batch == 1:
-                x = torch.empty((n, p_pad), dtype=tdt, device=dev)
+                x = rows[s, 0]
                 x[:, :p].copy_((torch.randn((n, p), generator=g, device=dev) * 0.05).to(tdt))
-                out = torch.empty(p, dtype=tdt, device=dev)
+                out = arena_empty(p, tdt, dev)
                 plan = _native.ReducePlan([x[i, :p] for i in range(n)], w32, out, mode)
                 assert all(t.data_ptr() % 16 == 0 for t in plan._keep[0]), "arena rows must be 16-B aligned"
                 self.outs.append(out)
             else:
-                x = torch.empty((batch, n, p_pad), dtype=tdt, device=dev)
+                x = rows[s]
                 x[:, :, :p].copy_((torch.randn((batch, n, p), generator=g, device=dev) * 0.05).to(tdt))
-                ob = torch.empty((batch, p_pad), dtype=tdt, device=dev)
+                ob = aligned_empty(batch * p_pad, tdt, dev, al).view(batch, p_pad)
                 plan = _native.BatchPlan([([x[b, i, :p] for i in range(n)], w32, ob[b, :p]) for b in range(batch)],
                                          mode)
                 self.outs.append(ob[0, :p])

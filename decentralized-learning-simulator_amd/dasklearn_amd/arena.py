@@ -202,20 +202,64 @@ def _elem_size(dt: torch.dtype) -> int:
     return esz
 
 
+# Arena rows of 4- and 8-byte elements of at least ROW_ALIGN_MIN bytes start
+# ROW_ALIGN-aligned (round 3; profiles/r03_layout*/, r03_rowrule/).
+ROW_ALIGN = 2 << 20
+ROW_ALIGN_MIN = 16 << 20
+
+
 def row_stride(numel: int, elem_bytes: int) -> int:
-    """Elements between consecutive model rows of a staging arena: `numel`
-    rounded up to 256 B (every row 16-byte aligned for the vector kernel),
-    plus 4 KiB when that leaves a stride that is a multiple of 64 KiB. Rows
-    at power-of-two strides contend for the same HBM channels: 8 x 8 M fp32
-    rows run at 0.75 of peak at a 32 MiB stride and 0.80 with 4 KiB added
-    (profiles/r01_tune_pow2.log); other strides are left alone (the 11 M
-    ResNet-18 rows measured the same with any stagger,
-    profiles/r01_tune_layout.log)."""
+    """Elements between consecutive model rows of an arena of rows (staging,
+    a round's uploads, bench inputs).
+
+    * 4/8-byte rows of >= 16 MiB: a whole number k of 2 MiB units, with
+      k + 1 when k is a multiple of 4 (rows 8 MiB apart share HBM channels);
+      the buffer's base is 2 MiB-aligned (aligned_empty). Measured for the
+      fixed and grouped launch shapes with >= 1 GiB rotating: the north
+      star's 8 x 11.2 M fp32 63.2 -> 61.7 us, 1.5-2.5 % at 6-25 M x 8, n = 4,
+      17 and 100 at 11.2 M; n = 2 fp32 and bf16 rows: neutral (+-0.6 %), so
+      2-byte rows keep the rule below (profiles/r03_rowrule/).
+    * otherwise `numel` rounded up to 256 B (every row 16-byte aligned for the
+      vector kernel), plus 4 KiB when that leaves a stride that is a multiple
+      of 64 KiB: 8 x 8 M fp32 rows ran at 0.75 of peak at a 32 MiB stride and
+      0.80 with 4 KiB added (profiles/r01_tune_pow2.log). Below 16 MiB 2 MiB
+      alignment measured neutral to 2.4 % slower (2.8 M x 8 fp32,
+      profiles/r03_layout_sweep/)."""
+    nbytes = numel * elem_bytes
+    if elem_bytes >= 4 and nbytes >= ROW_ALIGN_MIN:
+        k = (nbytes + ROW_ALIGN - 1) // ROW_ALIGN
+        if k % 4 == 0:
+            k += 1
+        return k * ROW_ALIGN // elem_bytes
     per256 = 256 // elem_bytes
     padded = (numel + per256 - 1) // per256 * per256
     if (padded * elem_bytes) % 65536 == 0:
         padded += 4096 // elem_bytes
     return padded
+
+
+def base_align(nbytes: int, elem_bytes: int) -> int:
+    """Alignment (bytes) of a device buffer that holds rows of `nbytes` each
+    (row_stride) or one arena of `nbytes`: ROW_ALIGN under row_stride's
+    2 MiB rule, else 256."""
+    return ROW_ALIGN if elem_bytes >= 4 and nbytes >= ROW_ALIGN_MIN else 256
+
+
+def aligned_empty(numel: int, dtype: torch.dtype, device, align: int) -> torch.Tensor:
+    """torch.empty(numel) on `device` starting at an `align`-byte boundary
+    (over-allocates align bytes; the view keeps the storage alive)."""
+    if align <= 256:
+        return torch.empty(numel, dtype=dtype, device=device)
+    esz = _elem_size(dtype)
+    raw = torch.empty(numel + align // esz, dtype=dtype, device=device)
+    skip = (-raw.data_ptr()) % align // esz
+    return raw[skip:skip + numel]
+
+
+def arena_empty(numel: int, dtype: torch.dtype, device) -> torch.Tensor:
+    """A fresh aggregate output (one dtype arena of a model), aligned like a
+    row of its size (base_align)."""
+    return aligned_empty(numel, dtype, device, base_align(numel * _elem_size(dtype), _elem_size(dtype)))
 
 
 class _Staging:
@@ -256,9 +300,9 @@ class _Staging:
             return lk
 
     @staticmethod
-    def _grow(pool: Dict[Tuple, torch.Tensor], key, need: int, make) -> torch.Tensor:
+    def _grow(pool: Dict[Tuple, torch.Tensor], key, need: int, make, align: int = 0) -> torch.Tensor:
         buf = pool.get(key)
-        if buf is None or buf.numel() < need:
+        if buf is None or buf.numel() < need or (align and buf.data_ptr() % align):
             pool.pop(key, None)  # drop the old one first (device memory returns to torch's cache)
             buf = pool[key] = make(need)
         return buf
@@ -271,9 +315,11 @@ class _Staging:
             ev = self.last_use.pop(key, None)
             if ev is not None:
                 ev.synchronize()
-            stride = row_stride(numel, _elem_size(dt))
+            esz = _elem_size(dt)
+            stride = row_stride(numel, esz)
             need = max(1, n * stride)
-            flat = self._grow(self.dev, key, need, lambda k: torch.empty(k, dtype=dt, device=device))
+            al = base_align(numel * esz, esz)
+            flat = self._grow(self.dev, key, need, lambda k: aligned_empty(k, dt, device, ROW_ALIGN), align=al)
             hflat = self._grow(self.host, key, need, lambda k: torch.empty(k, dtype=dt, pin_memory=True)) \
                 if pinned else None
             last = self._views.get(key)
@@ -490,7 +536,7 @@ def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, m
             f64 = dt == torch.float64
             w = (_native.f64_weights(weights_f64) if weights_f64 is not None else weights_f32.astype(np.float64)) \
                 if f64 else weights_f32
-            out = torch.empty(total, dtype=dt, device=dev)
+            out = arena_empty(total, dt, dev)
             outs[dt] = out
             if total == 0:
                 if piped:
@@ -801,7 +847,7 @@ def to_device_arena(model: nn.Module, device=None) -> nn.Module:
     arenas = {}
     with torch.no_grad():
         for dt, idx in layout.groups.items():
-            flat = torch.empty(layout.totals[dt], dtype=dt, device=dev)
+            flat = arena_empty(layout.totals[dt], dt, dev)
             for k in idx:
                 off = layout.offsets[k]
                 p = layout.params[k]

@@ -17,7 +17,7 @@ import torch
 from torch import nn
 
 from . import _native
-from .arena import aggregate_modules, input_arenas, module_from_arenas
+from .arena import aggregate_modules, arena_empty, input_arenas, module_from_arenas
 
 
 def _resolve(models, weights) -> List[float]:
@@ -126,7 +126,7 @@ def aggregate_arena_tasks(prepared, mode: int = _native.DLSIM_EXACT,
             if any(v is None for v in vs):
                 rows = entry[4]
                 dev = _rows_device(vs, rows, layout, dt)
-                out = torch.empty(layout.totals[dt], dtype=dt, device=dev)
+                out = arena_empty(layout.totals[dt], dt, dev)
                 o[dt] = out
                 idx = layout.groups[dt]
                 rows = [_row_on(rows[i], v, idx, layout.split_sizes[dt], dev) for i, v in enumerate(vs)]
@@ -135,7 +135,7 @@ def aggregate_arena_tasks(prepared, mode: int = _native.DLSIM_EXACT,
                       layout.byte_offsets[dt]), vs, out))
                 continue
             dev = vs[0].device
-            out = torch.empty(layout.totals[dt], dtype=dt, device=dev)
+            out = arena_empty(layout.totals[dt], dt, dev)
             o[dt] = out
             by_dtype.setdefault((dt, dev), []).append((vs, _native.weights_for_dtype(ws, dt), out))
         outs.append(o)

@@ -30,7 +30,8 @@ import torch
 from torch import nn
 
 from . import _native
-from .arena import ParamLayout, _target_device, layout_of, module_params, registered_arenas
+from .arena import (ParamLayout, _target_device, aligned_empty, base_align, layout_of, module_params,
+                    registered_arenas, row_stride)
 from .batch import _device_views, _resolve, aggregate_arena_tasks
 
 Task = Tuple[str, str, dict]  # (task_name, func_name, data with placeholders)
@@ -202,9 +203,12 @@ class RoundExecutor:
         dev = _target_device(pending[0][1].params, self.device)
         stream = torch.cuda.current_stream(dev)
         groups, cur, cur_bytes = [], [], 0
+        def span_bytes(layout, dt, idx):  # one dtype arena, at the row rule's stride
+            esz = layout.params[idx[0]].element_size()
+            return row_stride(layout.totals[dt], esz) * esz
+
         for m, layout in pending:
-            nb = sum((layout.totals[dt] * layout.params[idx[0]].element_size() + 255) // 256 * 256
-                     for dt, idx in layout.groups.items())
+            nb = sum(span_bytes(layout, dt, idx) for dt, idx in layout.groups.items())
             if cur and cur_bytes + nb > UPLOAD_GROUP_BYTES:
                 groups.append(cur)
                 cur, cur_bytes = [], 0
@@ -213,22 +217,27 @@ class RoundExecutor:
         groups.append(cur)
         for g, group in enumerate(groups):
             srcs, offs, spans, off = [], [], [], 0
+            align = 256
             for m, layout in group:
                 span = {}
                 for dt, idx in layout.groups.items():
                     esz = layout.params[idx[0]].element_size()
                     span[dt] = (off, layout.totals[dt], esz)
+                    start = off
                     for k in idx:
                         p = layout.params[k]
                         srcs.append(p.detach() if p.is_contiguous() else p.detach().contiguous())
                         offs.append(off)
                         off += p.numel() * esz
-                    off = (off + 255) // 256 * 256
+                    # the next arena one row stride on (arena.row_stride: large
+                    # 4/8-byte arenas 2 MiB-aligned in a 2 MiB-aligned buffer)
+                    off = start + span_bytes(layout, dt, idx)
+                    align = max(align, base_align(layout.totals[dt] * esz, esz))
                 spans.append(span)
             size = max(off, 1)
             stage = self._stage(g % 2, size)
             _native.host_pack(srcs, offs, stage[:size])
-            buf = torch.empty(size, dtype=torch.uint8, device=dev)
+            buf = aligned_empty(size, torch.uint8, dev, align)
             buf.copy_(stage[:size], non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(stream)

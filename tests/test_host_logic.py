@@ -379,10 +379,10 @@ def test_task_function_is_star_exported():
 
 
 @pytest.mark.parametrize("numel,esz,expect", [
-    (11_181_642, 4, 11_181_696),        # ResNet-18 fp32: 256 B padding only
     (125_000_000, 2, 125_000_064),      # cfg4 bf16: 256 B padding, not a 64 KiB multiple
     (1 << 20, 4, (1 << 20) + 1024),     # 4 MiB stride -> +4 KiB
     (1 << 23, 2, (1 << 23) + 2048),
+    (2_795_456, 4, 2_795_456),          # 11 MiB fp32 (< 16 MiB): 256 B rule
     (85_354, 4, 85_376),
     (1, 4, 64),
 ])
@@ -391,6 +391,36 @@ def test_staging_row_stride(numel, esz, expect):
     assert s == expect
     assert (s * esz) % 256 == 0 and s >= numel
     assert (s * esz) % 65536 != 0
+
+
+@pytest.mark.parametrize("numel,esz,units", [
+    (11_181_642, 4, 22),    # the north star's rows: 44.7 MB -> 22 x 2 MiB
+    (1 << 22, 4, 9),        # 16 MiB exactly: 8 units -> 9 (8 MiB multiple avoided)
+    (6_291_456, 4, 13),     # 24 MiB: 12 -> 13
+    (10_000_000, 4, 21),    # 40 MB: 20 units -> 21
+    (25_000_000, 4, 49),    # 100 MB: 48 -> 49
+    (30_000_000, 4, 58),
+    (2_200_000, 8, 9),      # fp64 17.6 MB -> 9 units
+    (2_000_000, 8, 0),      # fp64 16.0 MB < 16 MiB: the 256 B rule
+])
+def test_row_stride_2mib_rule(numel, esz, units):
+    """Round 3 (profiles/r03_rowrule/): 4/8-byte rows of >= 16 MiB are whole
+    2 MiB units, never a multiple of 8 MiB apart."""
+    s = arena.row_stride(numel, esz)
+    if numel * esz < arena.ROW_ALIGN_MIN:
+        assert s * esz % 256 == 0 and s * esz < arena.ROW_ALIGN_MIN + 4096
+        return
+    assert s * esz == units * arena.ROW_ALIGN and units % 4 != 0 and s >= numel
+    assert arena.base_align(numel * esz, esz) == arena.ROW_ALIGN
+    assert arena.base_align(numel * 2, 2) == 256  # 2-byte rows keep the 256 B rule
+
+
+def test_aligned_empty_starts_on_the_boundary():
+    for n in (1, 1000, 3 << 20):
+        t = arena.aligned_empty(n, torch.float32, "cpu", arena.ROW_ALIGN)
+        assert t.numel() == n and t.data_ptr() % arena.ROW_ALIGN == 0 and t.is_contiguous()
+    assert arena.arena_empty(5 << 20, torch.float32, "cpu").data_ptr() % arena.ROW_ALIGN == 0
+    assert arena.arena_empty(100, torch.float32, "cpu").numel() == 100
 
 
 @pytest.mark.parametrize("total,esz", [(1000, 4), (11_181_642, 4), (11_181_642, 2), (3 << 20, 4), (10 ** 9, 4)])
