@@ -1,13 +1,13 @@
-# rocprofv3 evidence for the round-3 bench lines: for the north star at N=1
+# rocprofv3 evidence for the round-2 bench lines: for the north star at N=1
 # and rank 0's slice of the 2/4/8-rank strong split (the per-rank work of the
 # driver's multi-GPU run), plus cfg3/cfg4/cfg5: a kernel trace with --stats,
 # then FETCH_SIZE and WRITE_SIZE in separate --pmc passes (no trace domains),
 # summarised per config by scripts/pmc_summary.py (gfx950 FETCH_SIZE x2).
-# usage: bash scripts/gpu_profile_r03.sh <outdir> ["name:config:slice ..."]
+# usage: bash scripts/probes/gpu_profile_r02.sh <outdir> ["name:config:slice ..."]
 set -u
 export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=$R/gpurun_out/${1:-prof_r03}
+O=$R/gpurun_out/${1:-prof_r02}
 mkdir -p $O
 step() { echo "[$(date +%T)] $*"; }
 run() {  # name config slice
@@ -26,7 +26,7 @@ print((n + 1) * (e - b) * bench.ELEM_BYTES[dt])")
   step "$NAME fetch";  timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -f csv -d $O/fetch_$NAME -o run -- python3 $R/bench.py $ARGS --steps 50 --warmup 5 > $O/fetch_$NAME.log 2>&1 || return 1
   step "$NAME write";  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -f csv -d $O/write_$NAME -o run -- python3 $R/bench.py $ARGS --steps 50 --warmup 5 > $O/write_$NAME.log 2>&1 || return 1
   python3 scripts/pmc_summary.py --trace $O/trace_$NAME --fetch $O/fetch_$NAME --write $O/write_$NAME \
-    --config $KEY --mode exact --bytes-per-launch $BYTES --out $O/r03_pmc_traffic.json > /dev/null || return 1
+    --config $KEY --mode exact --bytes-per-launch $BYTES --out $O/r02_pmc_traffic.json > /dev/null || return 1
 }
 if [ $# -ge 2 ]; then  # a chosen list: "name:config:slice ..."
   for spec in $2; do

@@ -1,0 +1,26 @@
+# XCD-aware tile map and small-VPT wave-map variants against the shipped
+# shape (csrc/tune_wreduce.hip; arena layout as in bench.py), repeated.
+# usage: bash scripts/probes/gpu_xcd.sh <outdir>
+set -u
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/${1:-xcd}
+mkdir -p $O
+T=$R/decentralized-learning-simulator_amd/csrc/build/tune_wreduce
+export DLSIM_TUNE_STAGGER=0
+step() { echo "[$(date +%T)] $*"; }
+for rep in 1 2; do
+  for p in 1048576 4194304 11182080; do
+    step "f32 n8 P=$p rep $rep"
+    DLSIM_TUNE_ONLY=NF8_V4_sc1,NF8_V4_sc1_wave,NF8_V2_sc1_wave,NF8_V1_sc1_wave,NF8_xcd_V4,NF8_xcd_V2 \
+      timeout -k 10 120 $T 8 $p f32 exact 200 > $O/f32_n8_${p}_$rep.log 2>&1 || exit $?
+  done
+  step "f32 n17 rep $rep"
+  DLSIM_TUNE_ONLY=NF17_V4_sc1,NF17_V4_sc1_wave,NF17_V2_sc1_wave,NF17_xcd_V4 \
+    timeout -k 10 120 $T 17 11182080 f32 exact 100 > $O/f32_n17_$rep.log 2>&1 || exit $?
+  for p in 11182080 125001728; do
+    step "bf16 n2 P=$p rep $rep"
+    DLSIM_TUNE_ONLY=NF2_V4,NF2_V4_sc1,NF2_V4_sc1_wave,NF2_V2_sc1_wave,NF2_V1_sc1_wave,NF2_B512_V4,NF2_xcd_V4,NF2_xcd_V2 \
+      timeout -k 10 120 $T 2 $p bf16 exact 100 > $O/bf16_n2_${p}_$rep.log 2>&1 || exit $?
+  done
+done
+step done
