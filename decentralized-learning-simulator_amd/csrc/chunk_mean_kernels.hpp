@@ -35,6 +35,8 @@
 // through LDS 64 at a time so one thread per column folds them at LDS speed.
 #pragma once
 
+#include <type_traits>
+
 #include "wreduce_kernels.hpp"
 
 #pragma clang fp contract(off)
@@ -64,6 +66,17 @@ struct PtrArgs {
   const void* const* p;
   __device__ const void* ptr(int i) const { return p[i]; }
 };
+
+// The add of the cascade tiles: `a + b`, or for the memory-only probe
+// (XorProbe, csrc/tune_wreduce.hip's chunk-mean pattern ceiling) its pinned
+// XOR, so the probe runs exactly this dispatch with the arithmetic removed.
+template <class Op> struct CmIsProbe : std::false_type {};
+template <int B> struct CmIsProbe<XorProbe<B>> : std::true_type {};
+template <class Op, class T>
+__device__ __forceinline__ T cm_add(T a, T b) {
+  if constexpr (CmIsProbe<Op>::value) return Op::step(a, 0.0f, b);
+  else return a + b;
+}
 
 // Lanes of ATen's Vectorized<acc> in the sum kernel (the inner order and the
 // column blocks): 8 floats, 4 doubles.
@@ -229,7 +242,7 @@ __device__ __forceinline__ void cm_tile(const A& a, int m, const OutRef& o, size
               T x[Op::E];
               unpack<Op>(r[g][v], x);
 #pragma unroll
-              for (int e = 0; e < Op::E; ++e) acc[0][v][e] = acc[0][v][e] + x[e];
+              for (int e = 0; e < Op::E; ++e) acc[0][v][e] = cm_add<Op>(acc[0][v][e], x[e]);
             }
           }
         }
@@ -243,7 +256,7 @@ __device__ __forceinline__ void cm_tile(const A& a, int m, const OutRef& o, size
         for (int v = 0; v < VPT; ++v)
 #pragma unroll
           for (int e = 0; e < Op::E; ++e) {
-            acc[l][v][e] = acc[l][v][e] + acc[l - 1][v][e];
+            acc[l][v][e] = cm_add<Op>(acc[l][v][e], acc[l - 1][v][e]);
             acc[l - 1][v][e] = T(0);
           }
         if ((i & (15 << (4 * l))) != 0) break;
@@ -255,7 +268,7 @@ __device__ __forceinline__ void cm_tile(const A& a, int m, const OutRef& o, size
 #pragma unroll
     for (int v = 0; v < VPT; ++v)
 #pragma unroll
-      for (int e = 0; e < Op::E; ++e) acc[0][v][e] = acc[0][v][e] + acc[l][v][e];
+      for (int e = 0; e < Op::E; ++e) acc[0][v][e] = cm_add<Op>(acc[0][v][e], acc[l][v][e]);
 #pragma unroll
   for (int v = 0; v < VPT; ++v) {
     const size_t idx = v0 + static_cast<size_t>(v) * SH::VS;

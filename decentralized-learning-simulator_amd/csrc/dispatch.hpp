@@ -564,11 +564,14 @@ inline size_t chunk_mean_ilp_begin(int m, size_t n, int threads, size_t esz = 4,
   return b + (s1 >= vw ? s1 / (4 * vw) * (4 * vw) : s1 / 4 * 4);
 }
 
-// Chunk mean tiles: VPT 4, wave map, 8 rows per load group. Block and wave
-// maps, VPT 2/4 and 8/16 rows in flight measured within +-3% of each other
-// (profiles/r01_tune_chunk_mean_shapes.log); the wave map matches the fp32
-// reduce's shape.
+// Chunk mean tiles: VPT 4, wave map, 8 rows per load group (the kernel runs at
+// its own memory-only probe from m = 6 up: profiles/r03_chunks_m/); a launch
+// whose tasks all have m <= 6 contributors loads 4 rows per group instead:
+// 26.5 against 29.3 us at m = 2, 36.2 against 38.0 at m = 4, 49.6 against
+// 50.0 at m = 6 (ResNet-18 chunks, k = 10; RF 4 is slower from m = 7).
 using CmDefault = dlsim::CmShape<4, true, 8>;
+using CmFewRows = dlsim::CmShape<4, true, 4>;
+constexpr int kCmFewRowsMax = 6;
 
 template <class Op>
 int run_chunk_mean(int b, const int* fan_in, const void* const* in, void* const* outs, const size_t* nelem,
@@ -592,6 +595,12 @@ int run_chunk_mean(int b, const int* fan_in, const void* const* in, void* const*
     return f;
   };
   auto task_blocks = [&](int t, size_t ib) { return ib / Op::E / tile + 1; };
+  // RF by the call's largest contributor count (both shapes use VPT 4, so the
+  // block layout is the same)
+  int mmax = 0;
+  for (int t = 0; t < b; ++t) mmax = fan_in[t] > mmax ? fan_in[t] : mmax;
+  const bool few_rows = mmax <= kCmFewRowsMax;
+  static_assert(CmFewRows::VPT == CmDefault::VPT, "one block layout for both tile shapes");
   dlsim::ChunkMeanSlots s;
   std::memset(&s, 0, sizeof(s));
   int nt = 0, np = 0;
@@ -600,8 +609,12 @@ int run_chunk_mean(int b, const int* fan_in, const void* const* in, void* const*
     if (nt == 0) return DLSIM_OK;
     s.ntasks = nt;
     s.block_start[nt] = static_cast<uint32_t>(blocks);
-    hipLaunchKernelGGL((dlsim::k_chunk_mean_batch<Op, CmDefault>), dim3(static_cast<unsigned>(blocks)),
-                       dim3(dlsim::kBlock), 0, st, s);
+    if (few_rows)
+      hipLaunchKernelGGL((dlsim::k_chunk_mean_batch<Op, CmFewRows>), dim3(static_cast<unsigned>(blocks)),
+                         dim3(dlsim::kBlock), 0, st, s);
+    else
+      hipLaunchKernelGGL((dlsim::k_chunk_mean_batch<Op, CmDefault>), dim3(static_cast<unsigned>(blocks)),
+                         dim3(dlsim::kBlock), 0, st, s);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "chunk mean batch launch");
     std::memset(&s, 0, sizeof(s));

@@ -869,35 +869,40 @@ PyObject* clone(PyObject* m, PyObject* memo, int depth) {
     if (!d) break;
     state = PyDict_Copy(d);
     if (!state) break;
-    // Walk the copy's entries through an owned snapshot: clone_attr runs
-    // arbitrary Python (copy.deepcopy, __setstate__), which may mutate the
-    // module's dict; borrowed PyDict_Next references into it could then be
-    // freed mid-walk. A size change raises as the Python
-    // specification's `for k, v in d.items()` does.
-    PyObject* items = PyDict_Items(state);
-    if (!items) break;
+    // Walk the entries of `state`, this function's private copy of the
+    // module's dict: clone_attr runs arbitrary Python (copy.deepcopy,
+    // __setstate__) that may mutate the module's dict, but cannot reach
+    // `state`, and replacing a value of an existing key keeps PyDict_Next
+    // valid (the walk used to hold borrowed references into the
+    // module's own dict). k and v are held across the call; a size change of
+    // the module's dict raises as the Python specification's
+    // `for k, v in d.items()` does; the compiled-call key goes after the walk.
     const Py_ssize_t n0 = PyDict_Size(d);
+    Py_ssize_t pos = 0;
+    PyObject *k, *v;
+    bool drop_compiled = false;
     ok = 0;
-    for (Py_ssize_t i = 0; ok == 0 && i < PyList_GET_SIZE(items); ++i) {
-      PyObject* kv = PyList_GET_ITEM(items, i);  // owned by `items`
-      PyObject* k = PyTuple_GET_ITEM(kv, 0);
-      PyObject* v = PyTuple_GET_ITEM(kv, 1);
+    while (ok == 0 && PyDict_Next(state, &pos, &k, &v)) {
       if (key_is(k, s_compiled_key)) {
-        ok = PyDict_DelItem(state, k);
+        drop_compiled = true;
         continue;
       }
+      Py_INCREF(k);
+      Py_INCREF(v);
       PyObject* nv = clone_attr(k, v, memo, depth);
       if (!nv) ok = -1;
       else if (nv != kKeep) {
         ok = PyDict_SetItem(state, k, nv);
         Py_DECREF(nv);
       }
+      Py_DECREF(v);
+      Py_DECREF(k);
       if (ok == 0 && PyDict_Size(d) != n0) {
         PyErr_SetString(PyExc_RuntimeError, "dictionary changed size during iteration");
         ok = -1;
       }
     }
-    Py_DECREF(items);
+    if (ok == 0 && drop_compiled) ok = PyDict_DelItem(state, s_compiled_key);
     if (ok < 0) break;
     // Module.__setstate__ is __dict__.update(state) when the state already has
     // every attribute it would add; a class's own __setstate__ is called

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "wreduce_kernels.hpp"
+#include "chunk_mean_kernels.hpp"
 
 namespace dlsim {
 // Experimental bf16-exact element policies (compared against the shipped
@@ -746,7 +747,160 @@ int run(int n, size_t P, int reps, double peak_gbs) {
   return 0;
 }
 
+// ---- round 3: the chunk mean's shapes and its memory-only ceiling ----------------
+//  DLSIM_TUNE_CHUNK=1: `tasks` chunk indices of n
+// elements each, m contributors, one k_chunk_mean_batch launch per step, as
+// ChunkManager.reconstruct_model runs them: contributor p's flat model is one
+// arena row (the product's row rule), chunk c its slice [c n, (c+1) n), the
+// means back to back. Variants: cascade tile shapes, and the XOR pattern probe
+// of the shipped shape (same dispatch, arithmetic removed).
+static size_t cm_ilp_begin(int m, size_t n, int threads) {  // dispatch.hpp chunk_mean_ilp_begin, fp32
+  if (n <= 1) return 0;
+  size_t b = 0, e = n;
+  if (!((unsigned long long)m * n < 32768ULL || threads <= 1)) {
+    const size_t tp = (size_t)threads < n ? (size_t)threads : n;
+    const size_t cs = (n + tp - 1) / tp;
+    for (size_t t = 0; t < tp; ++t) {
+      size_t tb = t * cs;
+      if (tb >= n) break;
+      size_t te = tb + cs < n ? tb + cs : n;
+      tb -= tb % 32;
+      if (te != n) te -= te % 32;
+      if (tb < te) { b = tb; e = te; }
+    }
+  }
+  const size_t s1 = e - b;
+  return b + (s1 >= 8 ? s1 / 32 * 32 : s1 / 4 * 4);
+}
+
+struct CmVariant {
+  std::string name;
+  void (*launch)(const ChunkMeanSlots&, unsigned, hipStream_t);
+  int vpt;
+  bool probe;
+};
+template <class Op, class SH>
+void cm_launch(const ChunkMeanSlots& s, unsigned blocks, hipStream_t st) {
+  hipLaunchKernelGGL((k_chunk_mean_batch<Op, SH>), dim3(blocks), dim3(kBlock), 0, st, s);
+}
+
+static size_t row_rule_bytes(size_t bytes) {  // arena.row_stride for 4-byte rows
+  const size_t mib2 = size_t{2} << 20;
+  if (bytes >= (size_t{16} << 20)) {
+    size_t k = (bytes + mib2 - 1) / mib2;
+    if (k % 4 == 0) ++k;
+    return k * mib2;
+  }
+  size_t r = (bytes + 255) / 256 * 256;
+  if (r % 65536 == 0) r += 4096;
+  return r;
+}
+
+int run_chunk(int m, size_t n, int tasks, int reps) {
+  const double peak = 8000.0;
+  std::vector<CmVariant> vs = {
+      {"cm_V4_wave_RF8", cm_launch<F32Mean, CmShape<4, true, 8>>, 4, false},
+      {"cm_V4_blk_RF8", cm_launch<F32Mean, CmShape<4, false, 8>>, 4, false},
+      {"cm_V2_wave_RF8", cm_launch<F32Mean, CmShape<2, true, 8>>, 2, false},
+      {"cm_V1_wave_RF8", cm_launch<F32Mean, CmShape<1, true, 8>>, 1, false},
+      {"cm_V4_wave_RF4", cm_launch<F32Mean, CmShape<4, true, 4>>, 4, false},
+      {"cm_V4_wave_RF16", cm_launch<F32Mean, CmShape<4, true, 16>>, 4, false},
+      {"cm_V2_wave_RF16", cm_launch<F32Mean, CmShape<2, true, 16>>, 2, false},
+      {"cm_V1_wave_RF16", cm_launch<F32Mean, CmShape<1, true, 16>>, 1, false},
+      {"cm_xorprobe_V4_wave_RF8", cm_launch<XorProbe<4>, CmShape<4, true, 8>>, 4, true},
+  };
+  if (m > kCmMaxPtrs / tasks || tasks > kCmMaxTasks) {
+    fprintf(stderr, "m * tasks must fit one kernel-argument batch\n");
+    return 1;
+  }
+  const size_t model_bytes = (size_t)tasks * n * 4;
+  const size_t stride = row_rule_bytes(model_bytes);
+  const double alg = (double)tasks * n * (m + 1) * 4;
+  const int sets = std::max(3, std::min(64, (int)((1ull << 30) / ((double)m * stride + model_bytes)) + 1));
+  void* arena = nullptr;
+  const size_t al = size_t{2} << 20;
+  CK(hipMalloc(&arena, stride * (size_t)m * sets + al));
+  char* base = (char*)((((uintptr_t)arena) + al - 1) / al * al);
+  std::vector<void*> outs(sets);
+  for (auto& o : outs) CK(hipMalloc(&o, model_bytes + 256));
+  for (size_t k = 0; k < (size_t)m * sets; ++k)
+    hipLaunchKernelGGL(k_fill, dim3(2048), dim3(256), 0, 0, (uint32_t*)(base + k * stride), model_bytes / 4,
+                       (uint32_t)(k * 7919 + 1), 0);
+  CK(hipDeviceSynchronize());
+  printf("chunk m=%d n=%zu tasks=%d sets=%d stride=%zu bytes=%.1fMB\n", m, n, tasks, sets, stride, alg / 1e6);
+  hipStream_t st;
+  CK(hipStreamCreate(&st));
+  auto slots = [&](int set, int vpt) {
+    ChunkMeanSlots s;
+    memset(&s, 0, sizeof(s));
+    const size_t tile = (size_t)kBlock * vpt;
+    size_t blocks = 0;
+    int np = 0;
+    for (int t = 0; t < tasks; ++t) {
+      s.ptr_off[t] = (uint16_t)np;
+      for (int i = 0; i < m; ++i) s.p[np++] = base + ((size_t)set * m + i) * stride + (size_t)t * n * 4;
+      s.out[t] = (char*)outs[set] + (size_t)t * n * 4;
+      s.nelem[t] = n;
+      s.m[t] = (uint16_t)m;
+      const size_t ib = cm_ilp_begin(m, n, 4);
+      s.ilp_begin[t] = ib;
+      s.flags[t] = (n * 4) % 16 == 0 ? kCmVec : 0;
+      s.block_start[t] = (uint32_t)blocks;
+      blocks += ib / 4 / tile + 1;
+    }
+    s.block_start[tasks] = (uint32_t)blocks;
+    s.ntasks = tasks;
+    return std::make_pair(s, (unsigned)blocks);
+  };
+  std::vector<char> ref(model_bytes), got(model_bytes);
+  {
+    auto sb = slots(0, vs[0].vpt);
+    vs[0].launch(sb.first, sb.second, st);
+    CK(hipStreamSynchronize(st));
+    CK(hipMemcpy(ref.data(), outs[0], model_bytes, hipMemcpyDeviceToHost));
+  }
+  std::vector<hipEvent_t> ev(2);
+  for (auto& e : ev) CK(hipEventCreate(&e));
+  const int rounds = 3;
+  std::vector<std::vector<double>> bat(vs.size());
+  for (int r = 0; r < rounds; ++r)
+    for (size_t v = 0; v < vs.size(); ++v) {
+      std::vector<std::pair<ChunkMeanSlots, unsigned>> sb;
+      for (int k = 0; k < sets; ++k) sb.push_back(slots(k, vs[v].vpt));
+      for (int w = 0; w < 10; ++w) vs[v].launch(sb[w % sets].first, sb[w % sets].second, st);
+      CK(hipEventRecord(ev[0], st));
+      for (int k = 0; k < reps; ++k) vs[v].launch(sb[k % sets].first, sb[k % sets].second, st);
+      CK(hipEventRecord(ev[1], st));
+      CK(hipEventSynchronize(ev[1]));
+      float ms;
+      CK(hipEventElapsedTime(&ms, ev[0], ev[1]));
+      bat[v].push_back(ms * 1e3 / reps);
+    }
+  for (size_t v = 0; v < vs.size(); ++v) {
+    auto sb = slots(0, vs[v].vpt);
+    vs[v].launch(sb.first, sb.second, st);
+    CK(hipStreamSynchronize(st));
+    CK(hipMemcpy(got.data(), outs[0], model_bytes, hipMemcpyDeviceToHost));
+    std::sort(bat[v].begin(), bat[v].end());
+    const double us = bat[v][rounds / 2];
+    printf("variant=%-24s m=%d n=%zu tasks=%d batch_us=%.2f GBps=%.0f frac=%.3f same=%d\n", vs[v].name.c_str(), m, n,
+           tasks, us, alg / (us * 1e-6) / 1e9, alg / (us * 1e-6) / 1e9 / peak,
+           (int)(memcmp(ref.data(), got.data(), model_bytes) == 0));
+  }
+  CK(hipFree(arena));
+  for (auto& o : outs) CK(hipFree(o));
+  return 0;
+}
+
 int main(int argc, char** argv) {
+  if (getenv("DLSIM_TUNE_CHUNK")) {  // tune_* chunk m n tasks reps
+    const int m = argc > 1 ? atoi(argv[1]) : 4;
+    const size_t n = argc > 2 ? strtoull(argv[2], nullptr, 10) : 1118164;
+    const int tasks = argc > 3 ? atoi(argv[3]) : 10;
+    const int reps = argc > 4 ? atoi(argv[4]) : 100;
+    if (m < 1 || tasks < 1 || reps < 1 || n < 1) return 1;
+    return run_chunk(m, n, tasks, reps);
+  }
   int n = argc > 1 ? atoi(argv[1]) : 8;
   size_t P = argc > 2 ? strtoull(argv[2], nullptr, 10) : 11181642ull;
   std::string dt = argc > 3 ? argv[3] : "f32";

@@ -35,6 +35,7 @@ import torch  # noqa: E402
 from torch import nn  # noqa: E402
 
 from dasklearn_amd import _native  # noqa: E402
+from dasklearn_amd.arena import aligned_empty, arena_empty, base_align, row_stride  # noqa: E402
 from dasklearn_amd.chunk_manager import ChunkManager  # noqa: E402
 
 P = 11_181_642
@@ -87,10 +88,24 @@ def main():
         # kernel only: one batched launch per reconstruction over rotating
         # sets of inputs and outputs whose footprint is >= 1 GiB, so that no
         # launch finds its chunks in the 256 MiB Infinity Cache
+        # (round 3) every set lays the m contributors' flat models out as the
+        # rows of one allocation (arena.row_stride), each chunk a slice of its
+        # model, the means back to back in one output arena, as
+        # ChunkManager.reconstruct_model sees them; round 2 cloned each chunk
+        # into its own small allocation, which measured 38-62 us for the same
+        # m = 4 launch depending on where the allocator put the clones
         sets = max(3, -(-(1 << 30) // byts))
         res = {"k": k, "m": m, "params": P, "bytes": byts, "rotating_sets": sets}
-        in_sets = [dev_by_index] + [[[c.clone() for c in cs] for cs in dev_by_index] for _ in range(sets - 1)]
-        outs = [[torch.empty(cs[0].numel(), device=dev) for cs in dev_by_index] for _ in range(sets)]
+        stride = row_stride(P, 4)
+        rows = aligned_empty(sets * m * stride, torch.float32, dev, base_align(P * 4, 4)).view(sets, m, stride)
+        bounds = [(c * (P // k), (c + 1) * (P // k) if c < k - 1 else P) for c in range(k)]
+        in_sets, outs = [], []
+        for s_ in range(sets):
+            for i in range(m):
+                rows[s_, i, :P].copy_(dflats[i])
+            in_sets.append([[rows[s_, i, b:e] for i in range(m)] for b, e in bounds])
+            o = arena_empty(P, torch.float32, dev)
+            outs.append([o[b:e] for b, e in bounds])
         tasks = [[(cs, o) for cs, o in zip(in_sets[s], outs[s])] for s in range(sets)]
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         reps = 50
