@@ -524,9 +524,16 @@ def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, m
     dev = _target_device(all_params[0], device)
     n = len(models)
     outs: Dict[torch.dtype, torch.Tensor] = {}
-    stream = torch.cuda.current_stream(dev)
-    raw_stream = stream.cuda_stream
-    st = _Stages(timing, stream)
+    # the raw handle from C (torch.cuda.current_stream costs a few us of
+    # Python per call); the Stream object only where a path needs it
+    raw_stream = torch._C._cuda_getCurrentRawStream(dev.index)
+    _stream = []
+
+    def get_stream():
+        if not _stream:
+            _stream.append(torch.cuda.current_stream(dev))
+        return _stream[0]
+    st = _Stages(timing, get_stream() if timing is not None else None)
     host_models = all(not all_params[i][idx[0]].is_cuda
                       for idx in layout.groups.values() for i in range(n))
     piped = host_out and host_models and len(layout.groups) > 0
@@ -552,7 +559,7 @@ def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, m
                     st.mark("kernel")
                     continue
                 if f64:  # one task through dlsim_wreduce_f64
-                    _staged_reduce(all_params, idx, dt, dev, out, w, mode, stream)
+                    _staged_reduce(all_params, idx, dt, dev, out, w, mode, get_stream())
                     st.mark("kernel")
                     continue
                 # separate device tensors, read in place: the layout checked
@@ -563,14 +570,14 @@ def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, m
                                             raw_stream, dix):
                     # a tensor is not contiguous, or (in a model whose first
                     # tensor is here) on another device: stage them all
-                    _staged_reduce(all_params, idx, dt, dev, out, w, mode, stream)
+                    _staged_reduce(all_params, idx, dt, dev, out, w, mode, get_stream())
                 st.mark("kernel")
                 continue
             if not f64 and not any(all_params[i][idx[0]].is_cuda for i in range(n)):
                 # host models (the reference's case): chunked pack / H2D /
                 # reduce (/ D2H) pipeline
                 st.mark("layout")
-                h = _host_pipeline(all_params, idx, layout, dt, dev, out, weights_f32, mode, stream, piped)
+                h = _host_pipeline(all_params, idx, layout, dt, dev, out, weights_f32, mode, get_stream(), piped)
                 if h is not None:
                     outs[dt] = h
                 st.mark("pipeline")
@@ -578,15 +585,15 @@ def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, m
             # models on another GPU (or fp64 host models): gather onto this
             # one, then reduce
             st.mark("layout")
-            _staged_reduce(all_params, idx, dt, dev, out, w, mode, stream)
+            _staged_reduce(all_params, idx, dt, dev, out, w, mode, get_stream())
             st.mark("kernel")
     if piped:
         left = {dt: a for dt, a in outs.items() if a.is_cuda}
         if left:  # single-chunk groups: their D2H now
-            outs.update(arenas_to_host(left, stream))
+            outs.update(arenas_to_host(left, get_stream()))
             st.mark("d2h")
         else:
-            stream.synchronize()
+            get_stream().synchronize()
     return layout, outs, dev, piped, host_out
 
 
