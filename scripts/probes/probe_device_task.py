@@ -53,6 +53,16 @@ def main():
             functions.aggregate(Settings(), params)
             sync()
             ts.append(time.perf_counter() - t0)
+        # back to back without a sync per call (one at the end): the rate a
+        # worker's loop sustains when nothing waits on each result
+        bb = []
+        for _ in range(5):
+            sync()
+            t0 = time.perf_counter()
+            for _ in range(200):
+                functions.aggregate(Settings(), params)
+            sync()
+            bb.append((time.perf_counter() - t0) / 200)
         stages = {}
         for _ in range(300):
             st = {}
@@ -70,6 +80,7 @@ def main():
         pstats.Stats(prof, stream=s).sort_stats("tottime").print_stats(18)
         print(json.dumps({"model": kind, "us_call_median": round(statistics.median(ts) * 1e6, 1),
                           "us_call_min": round(min(ts) * 1e6, 1),
+                          "us_call_back_to_back": round(statistics.median(bb) * 1e6, 1),
                           "stages_us_median": {k: round(statistics.median(v) * 1e6, 1) for k, v in stages.items()}}),
               flush=True)
         print(s.getvalue(), file=sys.stderr, flush=True)
