@@ -18,6 +18,9 @@ contributors per index (success_fraction 1: the sample size).
 
     python scripts/bench_chunks.py            # flat 11 M model, m = 4 and 10
     python scripts/bench_chunks.py --models   # ResNet-18 and GNLeNet state_dicts
+    python scripts/bench_chunks.py --kernel-only [--m 4]
+                      # the batched chunk-mean launches alone (for rocprofv3
+                      # kernel stats and PMC passes of k_chunk_mean_batch)
 """
 from __future__ import annotations
 
@@ -73,10 +76,10 @@ def cpu_reconstruct(chunks, model):
     return model
 
 
-def main():
+def main(ms=(4, 10), kernel_only=False, reps=50):
     dev = torch.device("cuda", 0)
     k = 10
-    for m in (4, 10):
+    for m in ms:
         g = torch.Generator().manual_seed(m)
         flats = [torch.randn(P, generator=g) * 0.05 for _ in range(m)]
         host_chunks = [ChunkManager.chunk_model(_wrap(f), k) for f in flats]  # [model][index]
@@ -108,9 +111,9 @@ def main():
             outs.append([o[b:e] for b, e in bounds])
         tasks = [[(cs, o) for cs, o in zip(in_sets[s], outs[s])] for s in range(sets)]
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        reps = 50
-        for key, fn in (("kernel", lambda ts: _native.chunk_mean_batched(ts, threads=4)),
-                        ("seq_kernel", _native.mean_batched)):
+        legs = (("kernel", lambda ts: _native.chunk_mean_batched(ts, threads=4)),
+                ("seq_kernel", _native.mean_batched))
+        for key, fn in legs[:1] if kernel_only else legs:
             for s in range(sets):
                 fn(tasks[s])
             torch.cuda.synchronize()
@@ -123,6 +126,10 @@ def main():
             res[key + "_us"] = round(us, 2)
             res[key + "_GBps"] = round(byts / us / 1e3, 1)
             res[key + "_frac_of_8TBps"] = round(byts / us / 1e3 / 8000.0, 4)
+        if kernel_only:
+            print(json.dumps(res), flush=True)
+            del dflats, dev_chunks, dev_by_index, in_sets, outs, tasks
+            continue
         # per-index launches (the unbatched form) for comparison
         torch.cuda.synchronize()
         e0.record()
@@ -239,6 +246,11 @@ def _wrap(flat):
 
 
 if __name__ == "__main__":
+    if "--kernel-only" in sys.argv:
+        ms = [int(sys.argv[sys.argv.index("--m") + 1])] if "--m" in sys.argv else [4, 10]
+        reps = int(sys.argv[sys.argv.index("--reps") + 1]) if "--reps" in sys.argv else 200
+        main(ms, kernel_only=True, reps=reps)
+        sys.exit(0)
     if "--models" in sys.argv:  # the two real module trees only
         d = torch.device("cuda", 0)
         print(json.dumps(resnet_case(d)), flush=True)

@@ -238,8 +238,8 @@ def main():
         which = rng.choice(["reduce", "tensors", "batched", "chunk_mean", "modules", "reconstruct",
                             "host_reduce", "host_chunk", "executor"],
                            p=[0.22, 0.1, 0.1, 0.18, 0.1, 0.1, 0.1, 0.05, 0.05])
-        if dtype == "f64" and which != "reduce":  # fp64 is the single-task entry (dlsim_wreduce_f64)
-            dtype = "f32"
+        if dtype == "f64" and which not in ("reduce", "chunk_mean", "host_chunk"):
+            dtype = "f32"  # fp64 reduces are the single-task entry (dlsim_wreduce_f64); chunk means take fp64
         try:
             if which == "reduce":
                 n = int(rng.choice([1, 2, 3, 5, 8, 9, 14, 15, 16, 17, 33, 128, 129, 200]))

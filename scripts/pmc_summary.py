@@ -1,4 +1,4 @@
-"""Summarise rocprofv3 output for the reduce kernel.
+"""Summarise rocprofv3 output for the reduce kernel (or another, --kernel).
 
     python scripts/pmc_summary.py --trace DIR --fetch DIR --write DIR \
         --config north_star --mode exact --bytes-per-launch B --out profiles/r01_pmc_traffic.json
@@ -62,6 +62,7 @@ def trace_avg_ns(dirpath):
 
 
 def main():
+    global KERNEL_RE
     ap = argparse.ArgumentParser()
     ap.add_argument("--trace")
     ap.add_argument("--fetch")
@@ -70,9 +71,12 @@ def main():
     ap.add_argument("--mode", default="exact")
     ap.add_argument("--bytes-per-launch", type=float, required=True)
     ap.add_argument("--out", required=True)
+    ap.add_argument("--kernel", default=KERNEL_RE,
+                    help="substring of the kernel to summarise (k_chunk_mean_batch for bench_chunks.py)")
     a = ap.parse_args()
+    KERNEL_RE = a.kernel
 
-    ent = {"algorithmic_bytes_per_launch": a.bytes_per_launch}
+    ent = {"algorithmic_bytes_per_launch": a.bytes_per_launch, "kernel": a.kernel}
     if a.trace:
         avg, cnt = trace_avg_ns(a.trace)
         if avg:
