@@ -59,12 +59,22 @@ struct ChunkMeanSlots {
   uint16_t ptr_off[kCmMaxTasks];
   uint16_t m[kCmMaxTasks];
   uint8_t flags[kCmMaxTasks];
+  uint8_t head[kCmMaxTasks];  // leading columns folded by block 0 (see cm_task)
   int ntasks;
 };
 
 struct PtrArgs {
   const void* const* p;
   __device__ const void* ptr(int i) const { return p[i]; }
+};
+
+// The same inputs `off` bytes further on (the cascade tiles of a task whose
+// leading columns are peeled off, cm_task).
+template <class A>
+struct ShiftArgs {
+  A a;
+  size_t off;
+  __device__ const void* ptr(int i) const { return static_cast<const char*>(a.ptr(i)) + off; }
 };
 
 // The add of the cascade tiles: `a + b`, or for the memory-only probe
@@ -343,28 +353,38 @@ __device__ __forceinline__ void cm_scalar_cols(const A& a, int m, void* out, siz
 
 // One task's share of the grid: local block 0 does the ragged end, local
 // block b >= 1 the full tile b - 1 of the cascade columns.
+// `head` (< kCmTailCols, below ilp_begin) leading columns are folded by block
+// 0 too, so that the tiles start on a 128-B line of every input and of the
+// output: a chunk of a flat model starts wherever P / k puts it, and tiles
+// laid from a misaligned start straddle lines (+1.2-1.4 % HBM traffic at
+// ResNet-18 chunks, profiles/r03s3_chunk_pmc/). Every column keeps its own
+// order (the cascade order does not depend on where a column sits).
 template <class Op, class A, class SH, int LV>
 __device__ __forceinline__ void cm_task(const A& a, int m, void* out, size_t n, size_t ilp_begin,
-                                        uint8_t flags, uint32_t local) {
+                                        uint8_t flags, uint32_t local, uint32_t head) {
   const float div = static_cast<float>(m);
-  const size_t nvec = ilp_begin / Op::E;  // whole vectors of cascade columns
+  const size_t hb = static_cast<size_t>(head) * Op::kBytes;
+  const ShiftArgs<A> sa{a, hb};
+  const size_t nvec = (ilp_begin - head) / Op::E;  // whole vectors of cascade columns past the head
   constexpr size_t kTile = static_cast<size_t>(kBlock) * SH::VPT;
   const size_t full = nvec / kTile;
   const bool vec = (flags & kCmVec) != 0;
-  const OutRef o = make_out<Op::kBytes >= 4 ? 16 : kStNT>(out, vec ? nvec : 0);
+  const OutRef o = make_out<Op::kBytes >= 4 ? 16 : kStNT>(static_cast<char*>(out) + hb, vec ? nvec : 0);
+  const size_t ncol = ilp_begin - head;
   if (local == 0) {
     if (full * kTile < nvec) {  // the partial tile, block map (bounds-checked)
       using PT = CmShape<SH::VPT, false, SH::RF>;
-      if (vec) cm_tile<Op, A, PT, LV, true, true>(a, m, o, full * kTile + threadIdx.x, nvec, ilp_begin, div);
-      else cm_tile<Op, A, PT, LV, false, true>(a, m, o, full * kTile + threadIdx.x, nvec, ilp_begin, div);
+      if (vec) cm_tile<Op, ShiftArgs<A>, PT, LV, true, true>(sa, m, o, full * kTile + threadIdx.x, nvec, ncol, div);
+      else cm_tile<Op, ShiftArgs<A>, PT, LV, false, true>(sa, m, o, full * kTile + threadIdx.x, nvec, ncol, div);
     }
-    const size_t c0 = nvec * Op::E;
+    if (head > 0) cm_scalar_cols<Op, A>(a, m, out, 0, head, ilp_begin, false, div);
+    const size_t c0 = head + nvec * Op::E;
     if (c0 < n) cm_scalar_cols<Op, A>(a, m, out, c0, n, ilp_begin, (flags & kCmInner) != 0, div);
     return;
   }
   const size_t v0 = static_cast<size_t>(local - 1) * kTile + SH::lane_off();
-  if (vec) cm_tile<Op, A, SH, LV, true, false>(a, m, o, v0, nvec, ilp_begin, div);
-  else cm_tile<Op, A, SH, LV, false, false>(a, m, o, v0, nvec, ilp_begin, div);
+  if (vec) cm_tile<Op, ShiftArgs<A>, SH, LV, true, false>(sa, m, o, v0, nvec, ncol, div);
+  else cm_tile<Op, ShiftArgs<A>, SH, LV, false, false>(sa, m, o, v0, nvec, ncol, div);
 }
 
 // Kernel-argument batch: up to kCmMaxTasks tasks, kCmMaxPtrs inputs (so
@@ -376,7 +396,7 @@ __global__ __launch_bounds__(kBlock) void k_chunk_mean_batch(const ChunkMeanSlot
   while (t + 1 < s.ntasks && bid >= s.block_start[t + 1]) ++t;  // wave-uniform scan
   const PtrArgs a{s.p + s.ptr_off[t]};
   cm_task<Op, PtrArgs, SH, 2>(a, s.m[t], s.out[t], s.nelem[t], s.ilp_begin[t], s.flags[t],
-                               bid - s.block_start[t]);
+                               bid - s.block_start[t], s.head[t]);
 }
 
 // One task whose input pointers live in device memory (any m).
@@ -385,7 +405,7 @@ __global__ __launch_bounds__(kBlock) void k_chunk_mean_table(const void* const* 
                                                              void* out, size_t n, size_t ilp_begin,
                                                              uint8_t flags) {
   const PtrArgs a{ptrs};
-  cm_task<Op, PtrArgs, SH, 4>(a, m, out, n, ilp_begin, flags, blockIdx.x);
+  cm_task<Op, PtrArgs, SH, 4>(a, m, out, n, ilp_begin, flags, blockIdx.x, 0);
 }
 
 }  // namespace dlsim

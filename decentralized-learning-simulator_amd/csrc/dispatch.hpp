@@ -594,7 +594,21 @@ int run_chunk_mean(int b, const int* fan_in, const void* const* in, void* const*
     if (nelem[t] == 1 && fan_in[t] >= dlsim::cm_lanes<Op>()) f |= dlsim::kCmInner;
     return f;
   };
-  auto task_blocks = [&](int t, size_t ib) { return ib / Op::E / tile + 1; };
+  // Leading columns block 0 folds so the tiles start on a 128-B line (cm_task):
+  // only when every input and the output share one misalignment (chunks cut
+  // at the same offset of equally aligned rows, ChunkManager's layout) and the
+  // task has whole tiles to align.
+  auto task_head = [&](int t, size_t ib, uint8_t flags) -> uint32_t {
+    if (!(flags & dlsim::kCmVec)) return 0;
+    const uintptr_t mis = reinterpret_cast<uintptr_t>(outs[t]) & 127u;
+    if (mis == 0) return 0;
+    for (int i = 0; i < fan_in[t]; ++i)
+      if ((reinterpret_cast<uintptr_t>(in[off[t] + i]) & 127u) != mis) return 0;
+    const size_t h = (128u - mis) / Op::kBytes;  // mis is a multiple of 16: whole elements
+    return ib >= h + 2 * tile * Op::E ? static_cast<uint32_t>(h) : 0u;
+  };
+  static_assert(128 / 2 <= dlsim::kCmTailCols, "a head fits block 0's scalar columns");
+  auto task_blocks = [&](size_t ib, uint32_t head) { return (ib - head) / Op::E / tile + 1; };
   // RF by the call's largest contributor count (both shapes use VPT 4, so the
   // block layout is the same)
   int mmax = 0;
@@ -628,7 +642,8 @@ int run_chunk_mean(int b, const int* fan_in, const void* const* in, void* const*
     const int m = fan_in[t];
     const size_t ib = chunk_mean_ilp_begin(m, n, threads, Op::kBytes == 8 ? 8 : 4, dlsim::cm_lanes<Op>());
     const uint8_t flags = task_flags(t);
-    const size_t tb = task_blocks(t, ib);
+    const uint32_t head = m > dlsim::kCmMaxPtrs ? 0u : task_head(t, ib, flags);
+    const size_t tb = task_blocks(ib, head);
     if (m > dlsim::kCmMaxPtrs) {
       // input pointers through a stream-ordered device array (any m)
       void* d = nullptr;
@@ -659,6 +674,7 @@ int run_chunk_mean(int b, const int* fan_in, const void* const* in, void* const*
     s.nelem[nt] = n;
     s.ilp_begin[nt] = ib;
     s.flags[nt] = flags;
+    s.head[nt] = static_cast<uint8_t>(head);
     for (int i = 0; i < m; ++i) s.p[np + i] = in[off[t] + i];
     np += m;
     blocks += tb;

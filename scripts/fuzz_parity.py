@@ -86,8 +86,8 @@ def to_host(rows, dtype):
     """Host tensors of the rows, every other one at an odd element offset."""
     out = []
     for i, r in enumerate(rows):
-        h = torch.from_numpy(np.ascontiguousarray(r).view(np.int16).copy()).view(DT[dtype]) if dtype != "f32" \
-            else torch.from_numpy(np.ascontiguousarray(r).copy())
+        h = torch.from_numpy(np.ascontiguousarray(r).view(np.int16).copy()).view(DT[dtype]) \
+            if dtype in ("bf16", "f16") else torch.from_numpy(np.ascontiguousarray(r).copy())
         if i % 2:
             buf = torch.empty(h.numel() + 1, dtype=h.dtype)
             buf[1:].copy_(h)

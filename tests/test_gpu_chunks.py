@@ -201,6 +201,41 @@ def test_chunk_mean_unaligned_and_aliased(dtype):
         assert orc.same_bits(_bits(ts[0]), e)
 
 
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16", "f64"])
+def test_chunk_mean_line_misaligned_heads(dtype):
+    """Chunks that start off a 128-B line (slices of equally aligned rows, as
+    chunk_model cuts a flat model): block 0 folds the leading columns and the
+    tiles start on the line. Every 16-B misalignment, sizes around the point
+    where the head is taken, one input (or the output) misaligned differently
+    (no head), in one batch: each task bit-identical to the oracle."""
+    rng = np.random.default_rng(77 + ["f32", "bf16", "f16", "f64"].index(dtype))
+    esz = {"f32": 4, "bf16": 2, "f16": 2, "f64": 8}[dtype]
+    tdt = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16, "f64": torch.float64}[dtype]
+    for threads in (1, 4):
+        tasks, exp = [], []
+        for k, mis in enumerate(range(16, 128, 16)):
+            off = mis // esz
+            for m, n in ((2, 8192 + 64), (4, 3 * 4096 + 5), (7, 40001), (17, 70_000 + k)):
+                rows, _ = _rows_t(rng, m, n, dtype)
+                ts = []
+                odd = int(rng.integers(0, m + 1)) if k % 3 == 2 else -1  # that one elsewhere
+                for i, r in enumerate(rows):
+                    h = torch.from_numpy(r.view(np.int16).copy()).view(tdt) if dtype in ("bf16", "f16") \
+                        else torch.from_numpy(r.copy())
+                    o = off + (16 // esz if i == odd else 0)
+                    buf = torch.empty(64 + n + 64, dtype=tdt, device=dev())  # caching allocator: 512-B aligned
+                    buf[o:o + n].copy_(h)
+                    ts.append(buf[o:o + n])
+                ob = torch.empty(64 + n + 64, dtype=tdt, device=dev())
+                out = ob[off + (16 // esz if odd == m else 0):][:n]
+                assert out.data_ptr() % 128 == (mis if odd != m else (mis + 16) % 128)
+                tasks.append((ts, out))
+                exp.append(orc.chunk_mean(list(rows), dtype, threads))
+        _native.chunk_mean_batched(tasks, threads=threads)
+        for (ts, out), e in zip(tasks, exp):
+            assert orc.same_bits(_bits(out), e), (len(ts), out.numel(), ts[0].data_ptr() % 128)
+
+
 @pytest.mark.parametrize("dtype", ["f32", "f64"])
 @pytest.mark.parametrize("m", [193, 256, 300])
 def test_chunk_mean_large_fan_in(m, dtype):
