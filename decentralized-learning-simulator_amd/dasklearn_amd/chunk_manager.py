@@ -197,7 +197,10 @@ class ChunkManager:
         # into every state_dict tensor (parameters and buffers, with the
         # dtype conversion of copy_). The copies go out as one
         # torch._foreach_copy_ (a few multi-tensor launches for a device
-        # model instead of one per tensor).
+        # model instead of one per tensor) unless two destinations share
+        # memory: a tied parameter is in state_dict() under each of its names,
+        # and the reference's copies run in order (the later one wins), which
+        # a multi-tensor launch does not guarantee.
         dsts, srcs = [], []
         pointer = 0
         for param in model.state_dict().values():
@@ -206,12 +209,18 @@ class ChunkManager:
             srcs.append(flat_params[pointer:pointer + numel].view(param.data.shape))
             pointer += numel
         with torch.no_grad():
-            if dsts and all(d.device == flat_params.device for d in dsts):
+            if dsts and all(d.device == flat_params.device for d in dsts) and not _overlapping(dsts):
                 torch._foreach_copy_(dsts, srcs)
             else:
                 for d, src in zip(dsts, srcs):
                     d.copy_(src)
         return model
+
+
+def _overlapping(ts: List[torch.Tensor]) -> bool:
+    """Whether any two of the tensors (on one device) share bytes."""
+    spans = sorted((t.data_ptr(), t.data_ptr() + t.numel() * t.element_size()) for t in ts if t.numel())
+    return any(b0 < a1 for (_, a1), (b0, _) in zip(spans, spans[1:]))
 
 
 def _span(ts: List[torch.Tensor]):

@@ -140,6 +140,7 @@ def rand_module(rng, seed):
     n_leaf = int(rng.integers(1, 6))
     dts = [DT[str(d)] for d in rng.choice(["f32", "f32", "bf16", "f16", "f64"], size=n_leaf)]
     shapes = [tuple(int(v) for v in rng.integers(1, 40, size=int(rng.integers(1, 4)))) for _ in range(n_leaf)]
+    share = bool(rng.random() < 0.3)  # a tied parameter and a shared submodule
 
     class Leaf(nn.Module):
         def __init__(self, shape, dt):
@@ -152,6 +153,10 @@ def rand_module(rng, seed):
             self.leaves = nn.ModuleList([Leaf(sh, dt) for sh, dt in zip(shapes, dts)])
             self.bn = nn.BatchNorm1d(7)
             self.frozen = nn.Parameter(torch.randn(5, generator=g), requires_grad=False)
+            if share:
+                self.tied = Leaf(shapes[0], dts[0])
+                self.tied.w = self.leaves[0].w  # one parameter, two attributes
+                self.alias = self.leaves  # a shared submodule
 
     return Tree()
 
@@ -343,6 +348,8 @@ def main():
                         ok = ok and orc.same_bits(bits(got), orc.wreduce(rows, w, code))
                 ok = ok and all(torch.equal(a.cpu(), b.cpu()) for a, b in zip(out.buffers(), models[0].buffers()))
                 ok = ok and [p.requires_grad for p in out.parameters()] == [p.requires_grad for p in models[0].parameters()]
+                if hasattr(models[0], "tied"):  # deepcopy(models[0]) keeps the sharing (fedavg.py:20)
+                    ok = ok and out.tied.w is out.leaves[0].w and out.alias is out.leaves
                 counts["modules"] += 1
                 case = dict(kind="modules", n=n, device=on_dev, weighted=weights is not None)
             elif which == "reconstruct":
@@ -364,7 +371,17 @@ def main():
                 prev = torch.get_num_threads()
                 torch.set_num_threads(threads)
                 try:
-                    expect = torch.cat([torch.mean(torch.stack(cs), dim=0) for cs in by_index])
+                    # the reference's reconstruct_model (chunk_manager.py:34-53) on a CPU
+                    # target: means, cat, copied in state_dict() order (a tied tensor
+                    # appears there twice: the later copy wins), then get_flat_params
+                    flat = torch.cat([torch.mean(torch.stack(cs), dim=0) for cs in by_index])
+                    ref_target = rand_module(np.random.default_rng(base), base).float()
+                    ptr = 0
+                    with torch.no_grad():
+                        for prm in ref_target.state_dict().values():
+                            prm.data.copy_(flat[ptr:ptr + prm.numel()].view(prm.shape))
+                            ptr += prm.numel()
+                    expect = torch.cat([t.data.view(-1) for t in ref_target.state_dict().values()])
                     on_dev = bool(rng.random() < 0.5)
                     chunks = [[c.to("cuda") for c in cs] if on_dev else list(cs) for cs in by_index]
                     target = rand_module(np.random.default_rng(base), base).float()

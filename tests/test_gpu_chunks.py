@@ -394,3 +394,44 @@ def test_reconstruct_f64_matches_reference(path, where):
     got = ChunkManager.get_flat_params(out).cpu().numpy()
     assert got.dtype == np.float64
     assert np.array_equal(got.view(np.int64), d["expected"].view(np.int64)), counts
+
+
+class _TiedNet(torch.nn.Module):
+    """A tied weight (in state_dict() under two names) and a shared
+    submodule (once: named_modules() de-duplicates it)."""
+
+    def __init__(self):
+        super().__init__()
+        self.a = torch.nn.Linear(40, 30)
+        self.b = torch.nn.Linear(40, 30)
+        self.b.weight = self.a.weight
+        self.seq = torch.nn.Sequential(torch.nn.Linear(30, 7))
+        self.again = self.seq
+
+
+@pytest.mark.parametrize("where", ["host", "device"])
+@pytest.mark.parametrize("k", [3, 7])
+def test_reconstruct_tied_parameters_follows_copy_order(where, k):
+    """chunk_manager.py:45-52 copies the flat means into the state_dict
+    tensors one after another, so a tied tensor (two entries) ends with the
+    means at its SECOND position; the device path's multi-tensor copy must not
+    race them. Compared with the reference's sequence run on the CPU."""
+    torch.manual_seed(5)
+    peers = [_TiedNet() for _ in range(4)]
+    chunked = [ChunkManager.chunk_model(m, k) for m in peers]
+    by_index = [[chunked[i][c] for i in range(4) if (i + c) % 3 != 0] or [chunked[0][c]] for c in range(k)]
+    ref = _TiedNet()
+    flat = torch.cat([torch.mean(torch.stack(cs), dim=0) for cs in by_index])
+    ptr = 0
+    with torch.no_grad():
+        for t in ref.state_dict().values():
+            t.copy_(flat[ptr:ptr + t.numel()].view(t.shape))
+            ptr += t.numel()
+    target = _TiedNet()
+    chunks = [[c.to(dev()) for c in cs] for cs in by_index] if where == "device" else [list(cs) for cs in by_index]
+    if where == "device":
+        target = target.to(dev())
+    out = ChunkManager.reconstruct_model(chunks, target)
+    assert out.b.weight is out.a.weight and out.again is out.seq
+    for (na, ta), (nb, tb) in zip(out.state_dict().items(), ref.state_dict().items()):
+        assert na == nb and orc.same_bits(ta.cpu().numpy(), tb.numpy()), na

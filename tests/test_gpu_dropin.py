@@ -310,3 +310,48 @@ def test_host_pipeline_resnet18_shapes_multi_chunk():
         out = FedAvg.aggregate(models, w)
         assert all(p.is_pinned() for p in out.parameters())
         assert orc.same_bits(flat_of(out), exp)
+
+
+class _Tied(nn.Module):
+    """Weight tying and a shared submodule: parameters() yields each tensor
+    once, and deepcopy(models[0]) (fedavg.py:20) keeps the sharing."""
+
+    def __init__(self):
+        super().__init__()
+        self.a = nn.Linear(3, 4)
+        self.tied = nn.Linear(3, 4)
+        self.tied.weight = self.a.weight  # tied: one parameter, two attributes
+        self.seq = nn.Sequential(nn.Linear(4, 4), nn.ReLU())
+        self.again = self.seq  # shared submodule
+        self.bn = nn.BatchNorm1d(4)
+        self.register_parameter("none_slot", None)
+
+
+@pytest.mark.parametrize("where", ["host", "device"])
+def test_tied_parameters_and_shared_submodules(where):
+    """FedAvg.aggregate on modules with a tied weight and a shared submodule:
+    each shared tensor is aggregated once, the output keeps the sharing
+    (out.tied.weight IS out.a.weight, out.again IS out.seq) as the reference's
+    deepcopy does, and every parameter is bit-identical to the reference's op
+    sequence (oracle/fedavg_torch.py); buffers come from models[0]."""
+    models = []
+    for i in range(5):
+        torch.manual_seed(100 + i)
+        m = _Tied()
+        with torch.no_grad():
+            m.bn.running_mean.copy_(torch.randn(4))
+            m.bn.num_batches_tracked.fill_(i + 3)
+        models.append(m)
+    w = [float(v) for v in np.random.default_rng(11).dirichlet(np.ones(5))]
+    ref = fedavg_torch.aggregate_modules([copy.deepcopy(m) for m in models], w)
+    ins = [m.to("cuda") for m in models] if where == "device" else models
+    out = FedAvg.aggregate(ins, w)
+    assert type(out) is _Tied
+    assert out.tied.weight is out.a.weight and out.again is out.seq
+    assert len(list(out.parameters())) == len(list(ref.parameters())) == 7
+    for (na, pa), (nb, pb) in zip(out.named_parameters(), ref.named_parameters()):
+        assert na == nb and pa.is_cuda == (where == "device")
+        assert orc.same_bits(pa.detach().cpu().numpy(), pb.detach().numpy()), na
+    assert torch.equal(out.bn.running_mean.cpu(), models[0].bn.running_mean.cpu())
+    assert int(out.bn.num_batches_tracked) == 3
+    assert out.none_slot is None
