@@ -131,16 +131,20 @@ def rand_weights(rng, n, dtype="f32"):
     return orc.reference_weights_f64(n, raw) if dtype == "f64" else orc.reference_weights(n, raw)
 
 
-def rand_module(rng, seed):
+def rand_module(rng, seed, odd=False):
     """A random nn.Module tree: nested submodules, parameters of random shapes
     and dtypes, a BatchNorm (buffers incl. an int64 counter), a frozen
-    parameter."""
+    parameter; sometimes a tied parameter and a shared submodule; with `odd`,
+    sometimes a transposed (non-contiguous) parameter and a submodule without
+    parameters."""
     from torch import nn
     g = torch.Generator().manual_seed(int(seed))
     n_leaf = int(rng.integers(1, 6))
     dts = [DT[str(d)] for d in rng.choice(["f32", "f32", "bf16", "f16", "f64"], size=n_leaf)]
     shapes = [tuple(int(v) for v in rng.integers(1, 40, size=int(rng.integers(1, 4)))) for _ in range(n_leaf)]
     share = bool(rng.random() < 0.3)  # a tied parameter and a shared submodule
+    strided = odd and bool(rng.random() < 0.3)
+    tshape = (int(rng.integers(1, 9)), int(rng.integers(2, 9)))
 
     class Leaf(nn.Module):
         def __init__(self, shape, dt):
@@ -157,6 +161,9 @@ def rand_module(rng, seed):
                 self.tied = Leaf(shapes[0], dts[0])
                 self.tied.w = self.leaves[0].w  # one parameter, two attributes
                 self.alias = self.leaves  # a shared submodule
+            if strided:
+                self.tw = nn.Parameter(torch.randn(tshape, generator=g).t())  # non-contiguous
+                self.act = nn.ReLU()  # no parameters
 
     return Tree()
 
@@ -326,7 +333,7 @@ def main():
                 from dasklearn_amd.gradient_aggregation.fedavg import FedAvg
                 n = int(rng.choice([1, 2, 3, 8, 17]))
                 base = int(rng.integers(0, 1 << 30))
-                models = [rand_module(np.random.default_rng(base), base + i) for i in range(n)]
+                models = [rand_module(np.random.default_rng(base), base + i, odd=True) for i in range(n)]
                 on_dev = bool(rng.random() < 0.5)
                 if on_dev:
                     models = [m.to("cuda") for m in models]
