@@ -179,7 +179,7 @@ def executor_case(rng):
     n = int(rng.integers(2, 7))
     rounds = int(rng.integers(1, 3))
     base = int(rng.integers(0, 1 << 30))
-    init = rand_module(np.random.default_rng(base), base)
+    init = rand_module(np.random.default_rng(base), base, odd=True)
     place = {(p, r): str(rng.choice(["cuda", "cpu"])) for p in range(n) for r in range(1, rounds + 1)}
     tasks = []
     for r in range(1, rounds + 1):
