@@ -389,10 +389,13 @@ def main():
                             prm.data.copy_(flat[ptr:ptr + prm.numel()].view(prm.shape))
                             ptr += prm.numel()
                     expect = torch.cat([t.data.view(-1) for t in ref_target.state_dict().values()])
-                    on_dev = bool(rng.random() < 0.5)
-                    chunks = [[c.to("cuda") for c in cs] if on_dev else list(cs) for cs in by_index]
+                    # every chunk on the device or every chunk on the host (the
+                    # reference's stack and cat need one device), the target model
+                    # on either (its copy_ crosses devices)
+                    place = str(rng.choice(["device", "host"]))
+                    chunks = [[c.to("cuda") if place == "device" else c for c in cs] for cs in by_index]
                     target = rand_module(np.random.default_rng(base), base).float()
-                    if on_dev:
+                    if rng.random() < 0.5:
                         target = target.to("cuda")
                     ChunkManager.reconstruct_model(chunks, target)
                 finally:
@@ -400,7 +403,8 @@ def main():
                 got = ChunkManager.get_flat_params(target).cpu()
                 ok = orc.same_bits(got.numpy(), expect.numpy())
                 counts["reconstruct"] += 1
-                case = dict(kind="reconstruct", k=k, peers=n_peers, threads=threads, device=on_dev)
+                case = dict(kind="reconstruct", k=k, peers=n_peers, threads=threads, place=place,
+                            target=str(next(target.parameters()).device))
             elif which == "host_reduce":
                 from dasklearn_amd.arena import _side_streams
                 n = int(rng.choice([1, 2, 3, 8, 9, 17]))
