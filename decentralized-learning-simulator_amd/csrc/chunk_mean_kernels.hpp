@@ -55,7 +55,7 @@ struct ChunkMeanSlots {
   void* out[kCmMaxTasks];
   size_t nelem[kCmMaxTasks];
   size_t ilp_begin[kCmMaxTasks];
-  uint32_t block_start[kCmMaxTasks + 1];
+  uint32_t block_start[kCmMaxTasks + 1];  // first full tile of each task (k_chunk_mean_batch)
   uint16_t ptr_off[kCmMaxTasks];
   uint16_t m[kCmMaxTasks];
   uint8_t flags[kCmMaxTasks];
@@ -388,15 +388,25 @@ __device__ __forceinline__ void cm_task(const A& a, int m, void* out, size_t n, 
 }
 
 // Kernel-argument batch: up to kCmMaxTasks tasks, kCmMaxPtrs inputs (so
-// m < 256 and two accumulator levels suffice).
+// m < 256 and two accumulator levels suffice). Blocks 0 .. ntasks-1 are the
+// tasks' ragged-end blocks (local block 0: a few dependent round trips), so
+// all of them are dispatched first and finish under the full tiles instead of
+// one of them trailing the grid; block ntasks + f is full tile f of the
+// concatenated tasks (block_start: each task's first full tile).
 template <class Op, class SH>
 __global__ __launch_bounds__(kBlock) void k_chunk_mean_batch(const ChunkMeanSlots s) {
   const uint32_t bid = blockIdx.x;
   int t = 0;
-  while (t + 1 < s.ntasks && bid >= s.block_start[t + 1]) ++t;  // wave-uniform scan
+  uint32_t local = 0;
+  if (bid < static_cast<uint32_t>(s.ntasks)) {
+    t = static_cast<int>(bid);
+  } else {
+    const uint32_t f = bid - static_cast<uint32_t>(s.ntasks);
+    while (t + 1 < s.ntasks && f >= s.block_start[t + 1]) ++t;  // wave-uniform scan
+    local = f - s.block_start[t] + 1;
+  }
   const PtrArgs a{s.p + s.ptr_off[t]};
-  cm_task<Op, PtrArgs, SH, 2>(a, s.m[t], s.out[t], s.nelem[t], s.ilp_begin[t], s.flags[t],
-                               bid - s.block_start[t], s.head[t]);
+  cm_task<Op, PtrArgs, SH, 2>(a, s.m[t], s.out[t], s.nelem[t], s.ilp_begin[t], s.flags[t], local, s.head[t]);
 }
 
 // One task whose input pointers live in device memory (any m).

@@ -618,11 +618,11 @@ int run_chunk_mean(int b, const int* fan_in, const void* const* in, void* const*
   dlsim::ChunkMeanSlots s;
   std::memset(&s, 0, sizeof(s));
   int nt = 0, np = 0;
-  size_t blocks = 0;
+  size_t blocks = 0;  // the launch's grid: one ragged-end block per task + the full tiles
   auto flush = [&]() -> int {
     if (nt == 0) return DLSIM_OK;
     s.ntasks = nt;
-    s.block_start[nt] = static_cast<uint32_t>(blocks);
+    s.block_start[nt] = static_cast<uint32_t>(blocks - static_cast<size_t>(nt));
     if (few_rows)
       hipLaunchKernelGGL((dlsim::k_chunk_mean_batch<Op, CmFewRows>), dim3(static_cast<unsigned>(blocks)),
                          dim3(dlsim::kBlock), 0, st, s);
@@ -667,7 +667,7 @@ int run_chunk_mean(int b, const int* fan_in, const void* const* in, void* const*
       int rc = flush();
       if (rc != DLSIM_OK) return rc;
     }
-    s.block_start[nt] = static_cast<uint32_t>(blocks);
+    s.block_start[nt] = static_cast<uint32_t>(blocks - static_cast<size_t>(nt));  // full tiles before task nt
     s.ptr_off[nt] = static_cast<uint16_t>(np);
     s.m[nt] = static_cast<uint16_t>(m);
     s.out[nt] = outs[t];

@@ -845,10 +845,10 @@ int run_chunk(int m, size_t n, int tasks, int reps) {
       const size_t ib = cm_ilp_begin(m, n, 4);
       s.ilp_begin[t] = ib;
       s.flags[t] = (n * 4) % 16 == 0 ? kCmVec : 0;
-      s.block_start[t] = (uint32_t)blocks;
+      s.block_start[t] = (uint32_t)(blocks - t);  // full tiles before task t (ragged ends first)
       blocks += ib / 4 / tile + 1;
     }
-    s.block_start[tasks] = (uint32_t)blocks;
+    s.block_start[tasks] = (uint32_t)(blocks - tasks);
     s.ntasks = tasks;
     return std::make_pair(s, (unsigned)blocks);
   };
