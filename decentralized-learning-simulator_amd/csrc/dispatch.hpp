@@ -282,6 +282,14 @@ inline bool cross_task_overlap(int nt, const int* fan_in, const void* const* in,
 }
 
 // ---- batched launches ---------------------------------------------------------
+// Lane map of the table batches' full tiles: the wave map (each wave sweeps
+// VPT contiguous KiB per stream) where the single-task kernels use it, VPT 4
+// tiles of 4/8-byte elements: 8 x 11.2 M fp32 cut into 8 / 32 tasks 64.47 ->
+// 63.67 / 65.43 -> 64.46 us; the kernel-argument batches measured the same or
+// 0.5 % slower with it and keep the block map
+// (scripts/probes/probe_batch_vs_single.py, profiles/r03s3_batch_vs_single/).
+template <class Op, int VPT> constexpr bool kBatchWave = VPT == 4 && wave_map<Op>();
+
 template <class Op, int NF, int VPT>
 hipError_t launch_batch_nf(const dlsim::BatchSlots& s, unsigned blocks, hipStream_t st) {
   hipLaunchKernelGGL((dlsim::k_wreduce_batch<Op, NF, group_size<Op>(), VPT, kNT, store_policy<Op>()>), dim3(blocks),
@@ -318,7 +326,7 @@ hipError_t launch_batch(const int* fan_in, const size_t* in_off, const void* con
     s.out[k] = outs[t];
     s.nvec[k] = nvec;
     s.nelem[k] = nelem[t];
-    s.block_start[k] = blocks;
+    s.block_start[k] = blocks - static_cast<uint32_t>(k);  // full tiles before task k (ragged ends first)
     s.ptr_off[k] = static_cast<uint16_t>(ptrs);
     s.fan_in[k] = static_cast<uint16_t>(fan_in[t]);
     s.div[k] = divs ? divs[t] : 1.0f;
@@ -331,7 +339,7 @@ hipError_t launch_batch(const int* fan_in, const size_t* in_off, const void* con
     uniform = uniform && fan_in[t] == fan_in[t0];
   }
   s.ntasks = t1 - t0;
-  s.block_start[t1 - t0] = blocks;
+  s.block_start[t1 - t0] = blocks - static_cast<uint32_t>(t1 - t0);
   if (vpt == 1) {
     if (uniform) return launch_batch_fixed<Op, 1, 1>(s, fan_in[t0], blocks, st);
     return launch_batch_nf<Op, 0, 1>(s, blocks, st);
@@ -468,7 +476,9 @@ int table_fill(int b, const int* fan_in, const void* const* in, const float* w, 
   h->map_off = L.map_off;
   h->ptrs_off = L.ptrs_off;
   h->w_off = L.w_off;
-  uint32_t blk = 0, off = 0;
+  // block order (k_wreduce_batch_table): the b ragged-end blocks, then every
+  // task's full tiles; a task's block_start is one before its first full tile
+  uint32_t blk = static_cast<uint32_t>(b), off = 0;
   bool uniform = true;
   for (int t = 0; t < b; ++t) {
     const size_t total = nelem[t] * Op::kBytes;
@@ -479,17 +489,18 @@ int table_fill(int b, const int* fan_in, const void* const* in, const float* w, 
     tasks[t].out = outs[t];
     tasks[t].nvec = nelem[t] / Op::E;
     tasks[t].nelem = nelem[t];
-    tasks[t].block_start = blk;
+    tasks[t].block_start = blk - 1;
     tasks[t].ptr_off = off;
     tasks[t].fan_in = static_cast<uint32_t>(fan_in[t]);
-    for (uint32_t k = 0; k < nb; ++k) map[blk + k] = static_cast<uint32_t>(t);
+    map[t] = static_cast<uint32_t>(t);  // its ragged end
+    for (uint32_t k = 0; k + 1 < nb; ++k) map[blk + k] = static_cast<uint32_t>(t);
     for (int i = 0; i < fan_in[t]; ++i) {
       if (!aligned16(in[off + i]))
         return fail(DLSIM_E_ARG, "task %d input %d is not 16-byte aligned", t, i);
       ptrs[off + i] = in[off + i];
       ws[off + i] = w[off + i];
     }
-    blk += nb;
+    blk += nb - 1;
     off += static_cast<uint32_t>(fan_in[t]);
     uniform = uniform && fan_in[t] == fan_in[0];
   }
@@ -499,7 +510,8 @@ int table_fill(int b, const int* fan_in, const void* const* in, const float* w, 
 
 template <class Op, int NF, int VPT>
 hipError_t launch_table_nf(const void* d_table, uint32_t blocks, hipStream_t st) {
-  hipLaunchKernelGGL((dlsim::k_wreduce_batch_table<Op, NF, group_size<Op>(), VPT, kNT, store_policy<Op>()>),
+  hipLaunchKernelGGL((dlsim::k_wreduce_batch_table<Op, NF, group_size<Op>(), VPT, kNT, store_policy<Op>(),
+                                                    kBatchWave<Op, VPT>>),
                      dim3(blocks), dim3(dlsim::kBlock), 0, st, static_cast<const unsigned char*>(d_table));
   return hipGetLastError();
 }

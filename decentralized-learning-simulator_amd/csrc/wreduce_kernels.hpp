@@ -637,10 +637,13 @@ __global__ __launch_bounds__(kBlock) void k_wreduce_tiles(const S s, int n, void
 // ---- batched launch: many independent aggregates in one grid -----------------
 // The aggregate tasks of one simulated round (every peer's neighbour mix) are
 // independent; small models (GNLeNet: 3 MB per task) are launch-bound when
-// each is its own kernel. One grid covers every task: task t owns blocks
-// [block_start[t], block_start[t+1]); its first block folds the task's ragged
-// end, the others one full tile each. Descriptors travel as kernel arguments
-// (read with scalar loads); the host splits larger batches.
+// each is its own kernel. One grid covers every task: blocks 0 .. ntasks-1
+// fold the tasks' ragged ends (the partial tile, then the scalar tail: two
+// dependent phases), so they are all dispatched first and finish under the
+// full tiles instead of the last task's trailing the grid; block ntasks + f is
+// full tile f of the concatenated tasks (task t's full tiles start at
+// block_start[t]). Descriptors travel as kernel arguments (read with scalar
+// loads); the host splits larger batches.
 constexpr int kBatchMaxTasks = 32;
 constexpr int kBatchMaxPtrs = 192;
 
@@ -651,7 +654,7 @@ struct BatchSlots {
   size_t nvec[kBatchMaxTasks];
   size_t nelem[kBatchMaxTasks];
   float div[kBatchMaxTasks];  // final divisor per task (mean policies; 1 for the reduce)
-  uint32_t block_start[kBatchMaxTasks + 1];
+  uint32_t block_start[kBatchMaxTasks + 1];  // first full tile of each task
   uint16_t ptr_off[kBatchMaxTasks];
   uint16_t fan_in[kBatchMaxTasks];
   int ntasks;
@@ -667,18 +670,24 @@ struct TaskArgs {
   __device__ float divisor() const { return d; }
 };
 
-template <class Op, int NF, int G, int VPT, int NT, int STP>
+template <class Op, int NF, int G, int VPT, int NT, int STP, bool WAVEMAP = false>
 __global__ __launch_bounds__(kBlock) void k_wreduce_batch(const BatchSlots s) {
   const uint32_t bid = blockIdx.x;
   int t = 0;
-  while (t + 1 < s.ntasks && bid >= s.block_start[t + 1]) ++t;  // wave-uniform scan
+  uint32_t local = 0;
+  if (bid < static_cast<uint32_t>(s.ntasks)) {
+    t = static_cast<int>(bid);
+  } else {
+    const uint32_t f = bid - static_cast<uint32_t>(s.ntasks);
+    while (t + 1 < s.ntasks && f >= s.block_start[t + 1]) ++t;  // wave-uniform scan
+    local = f - s.block_start[t] + 1;
+  }
   const TaskArgs a{s, s.ptr_off[t], s.div[t]};
   const int n = NF > 0 ? NF : s.fan_in[t];
   const size_t nvec = s.nvec[t];
   constexpr size_t kTile = static_cast<size_t>(kBlock) * VPT;
   const size_t full = nvec / kTile;
   const OutRef o = make_out<STP>(s.out[t], nvec);
-  const uint32_t local = bid - s.block_start[t];
   if (local == 0) {
     if (full * kTile < nvec)
       reduce_tile<Op, TaskArgs, NF, G, VPT, NT, true, STP>(a, n, o, full * kTile + threadIdx.x, nvec);
@@ -686,14 +695,21 @@ __global__ __launch_bounds__(kBlock) void k_wreduce_batch(const BatchSlots s) {
     if (j < s.nelem[t]) fold_scalar<Op, TaskArgs>(a, n, s.out[t], j);
     return;
   }
-  reduce_tile<Op, TaskArgs, NF, G, VPT, NT, false, STP>(a, n, o, (local - 1) * kTile + threadIdx.x, nvec);
+  if constexpr (WAVEMAP) {
+    const size_t lane_off = (threadIdx.x >> 6) * 64 * VPT + (threadIdx.x & 63);
+    reduce_tile<Op, TaskArgs, NF, G, VPT, NT, false, STP, 64>(a, n, o, (local - 1) * kTile + lane_off, nvec);
+  } else {
+    reduce_tile<Op, TaskArgs, NF, G, VPT, NT, false, STP>(a, n, o, (local - 1) * kTile + threadIdx.x, nvec);
+  }
 }
 
 // ---- batched launch from a device descriptor table ----------------------------
 // Same work as k_wreduce_batch for any number of tasks: the descriptors live
 // in a device buffer the caller uploads (dlsim_batch_table_*), each block
 // finds its task with one read of a block -> task map (scalar loads, the
-// index is wave-uniform).
+// index is wave-uniform). The same block order: the ntasks ragged-end blocks
+// first, then every task's full tiles (a task's block_start is one before its
+// first full-tile block, so local = blockIdx.x - block_start >= 1 there).
 struct BatchTableHeader {
   uint32_t ntasks;
   uint32_t nblocks;
@@ -723,7 +739,7 @@ struct TableArgs {
   __device__ float divisor() const { return 1.0f; }
 };
 
-template <class Op, int NF, int G, int VPT, int NT, int STP>
+template <class Op, int NF, int G, int VPT, int NT, int STP, bool WAVEMAP = false>
 __global__ __launch_bounds__(kBlock) void k_wreduce_batch_table(const unsigned char* __restrict__ table) {
   const BatchTableHeader* h = reinterpret_cast<const BatchTableHeader*>(table);
   const uint32_t* map = reinterpret_cast<const uint32_t*>(table + h->map_off);
@@ -736,7 +752,7 @@ __global__ __launch_bounds__(kBlock) void k_wreduce_batch_table(const unsigned c
   constexpr size_t kTile = static_cast<size_t>(kBlock) * VPT;
   const size_t full = nvec / kTile;
   const OutRef o = make_out<STP>(d.out, nvec);
-  const uint32_t local = blockIdx.x - d.block_start;
+  const uint32_t local = blockIdx.x < h->ntasks ? 0u : blockIdx.x - d.block_start;
   if (local == 0) {
     if (full * kTile < nvec)
       reduce_tile<Op, TableArgs, NF, G, VPT, NT, true, STP>(a, n, o, full * kTile + threadIdx.x, nvec);
@@ -744,7 +760,12 @@ __global__ __launch_bounds__(kBlock) void k_wreduce_batch_table(const unsigned c
     if (j < d.nelem) fold_scalar<Op, TableArgs>(a, n, d.out, j);
     return;
   }
-  reduce_tile<Op, TableArgs, NF, G, VPT, NT, false, STP>(a, n, o, (local - 1) * kTile + threadIdx.x, nvec);
+  if constexpr (WAVEMAP) {
+    const size_t lane_off = (threadIdx.x >> 6) * 64 * VPT + (threadIdx.x & 63);
+    reduce_tile<Op, TableArgs, NF, G, VPT, NT, false, STP, 64>(a, n, o, (local - 1) * kTile + lane_off, nvec);
+  } else {
+    reduce_tile<Op, TableArgs, NF, G, VPT, NT, false, STP>(a, n, o, (local - 1) * kTile + threadIdx.x, nvec);
+  }
 }
 
 // Memory-only probe (dlsim_probe_pattern): the element policy of the reduce
