@@ -13,6 +13,7 @@
 #include <cstring>
 #include <string>
 #include <type_traits>
+#include <map>
 #include <vector>
 
 #include "wreduce_kernels.hpp"
@@ -290,6 +291,40 @@ void launch_ts(const Slots<128>& s, int n, void* out, size_t nvec, size_t nelem,
                      st, s, n, out, nvec, nelem);
 }
 
+// The same kernel with the library's argument carriers (round 3, session 3:
+// is the harness/bench gap the kernel-argument size?): Slots<16> as
+// dlsim_wreduce passes n <= 16, and DevSlots (pointers and weights read from a
+// device buffer, uploaded once per slot set).
+template <class Op, int NF, int G, int VPT, int NT, int NTS, bool WM = false>
+void launch_ts16(const Slots<128>& s, int n, void* out, size_t nvec, size_t nelem, hipStream_t st, int) {
+  Slots<16> s16;
+  memset(&s16, 0, sizeof(s16));
+  for (int i = 0; i < n && i < 16; ++i) {
+    s16.p[i] = s.p[i];
+    s16.w[i] = s.w[i];
+  }
+  const size_t grid = nvec / ((size_t)kBlock * VPT) + 1;
+  hipLaunchKernelGGL((k_wreduce_tiles<Op, Slots<16>, NF, G, VPT, NT, NTS, WM>), dim3((unsigned)grid), dim3(kBlock), 0,
+                     st, s16, n, out, nvec, nelem);
+}
+template <class Op, int NF, int G, int VPT, int NT, int NTS, bool WM = false>
+void launch_tsdev(const Slots<128>& s, int n, void* out, size_t nvec, size_t nelem, hipStream_t st, int) {
+  static std::map<const void*, void*> dev;  // slot set -> its device copy (pointers, then weights)
+  void*& d = dev[&s];
+  if (!d) {
+    std::vector<char> h(128 * sizeof(void*) + 128 * sizeof(float));
+    memcpy(h.data(), s.p, 128 * sizeof(void*));
+    memcpy(h.data() + 128 * sizeof(void*), s.w, 128 * sizeof(float));
+    CK(hipMalloc(&d, h.size()));
+    CK(hipMemcpy(d, h.data(), h.size(), hipMemcpyHostToDevice));
+  }
+  DevSlots<float> ds{static_cast<const void* const*>(d),
+                     reinterpret_cast<const float*>(static_cast<char*>(d) + 128 * sizeof(void*)), 1.0f};
+  const size_t grid = nvec / ((size_t)kBlock * VPT) + 1;
+  hipLaunchKernelGGL((k_wreduce_tiles<Op, DevSlots<float>, NF, G, VPT, NT, NTS, WM>), dim3((unsigned)grid),
+                     dim3(kBlock), 0, st, ds, n, out, nvec, nelem);
+}
+
 // LDS-DMA body over full tiles; ragged end by the tiled kernel's last block
 // (only exact for inputs whose nvec is a multiple of the tile: the harness
 // flags any mismatch through `same`).
@@ -431,6 +466,12 @@ void add_r03(std::vector<Variant>& vs, int n) {
   const std::string p = "NF" + std::to_string(NF);
   const double rd = (double)NF / (NF + 1), wr = 1.0 / (NF + 1);
   vs.push_back({p + "_V4_sc1_wave", launch_ts<Op, NF, 8, 4, 1, 16, true>, 0});
+  if (getenv("DLSIM_TUNE_ARGS")) {  // kernel-argument carriers only
+    vs.push_back({p + "_V4_sc1_wave_S16", launch_ts16<Op, NF, 8, 4, 1, 16, true>, 0});
+    vs.push_back({p + "_V4_sc1_wave_dev", launch_tsdev<Op, NF, 8, 4, 1, 16, true>, 0});
+    vs.push_back({p + "_V4_sc1_wave_b", launch_ts<Op, NF, 8, 4, 1, 16, true>, 0});
+    return;
+  }
   vs.push_back({p + "_xorprobe", launch_probe<Op, NF>, 0});
   vs.push_back({p + "_rdonly_V4w", launch_rdonly<NF, 4>, 0, rd});
   vs.push_back({p + "_rdonly_V2w", launch_rdonly<NF, 2>, 0, rd});
