@@ -26,7 +26,7 @@ print((n + 1) * (e - b) * bench.ELEM_BYTES[dt])")
   step "$NAME fetch";  timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -f csv -d $O/fetch_$NAME -o run -- python3 $R/bench.py $ARGS --steps 50 --warmup 5 > $O/fetch_$NAME.log 2>&1 || return 1
   step "$NAME write";  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -f csv -d $O/write_$NAME -o run -- python3 $R/bench.py $ARGS --steps 50 --warmup 5 > $O/write_$NAME.log 2>&1 || return 1
   python3 scripts/pmc_summary.py --trace $O/trace_$NAME --fetch $O/fetch_$NAME --write $O/write_$NAME \
-    --config $KEY --mode exact --bytes-per-launch $BYTES --out $O/r03_pmc_traffic.json > /dev/null || return 1
+    --config $KEY --mode exact --bytes-per-launch $BYTES --out $O/${PMC_NAME:-r03_pmc_traffic.json} > /dev/null || return 1
 }
 if [ $# -ge 2 ]; then  # a chosen list: "name:config:slice ..."
   for spec in $2; do
