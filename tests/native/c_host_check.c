@@ -9,8 +9,9 @@
  * (n = 2), dlsim_wreduce_f64, dlsim_wreduce_tensors (7 models x 3 tensors),
  * dlsim_wreduce_batched (tasks of several fan-ins), dlsim_chunk_mean_batched
  * (k = 10 chunks of a flat model, chunks off 128-B lines), dlsim_host_wreduce
- * (host models, pinned staging, pipelined chunks), the error codes, and
- * dlsim_version / dlsim_shard_range.
+ * (host models, pinned staging, pipelined chunks), a descriptor-table batch
+ * (dlsim_batch_table_*), dlsim_host_chunk_mean (host chunks), the error
+ * codes, and dlsim_version / dlsim_shard_range.
  *
  * Built by __graft_entry__.build(); run by tests/test_gpu_c_host.py. Prints
  * one line per case and "c_host_check OK"; exits non-zero on the first
@@ -349,6 +350,111 @@ static void case_host_wreduce(hipStream_t st) {
   HIPCK(hipStreamDestroy(d2h));
 }
 
+static void case_table_batch(hipStream_t st) {
+  /* a prepared round: 5 tasks of several sizes and fan-ins in one caller-owned
+   * descriptor table, launched twice (graph-capturable: no allocation) */
+  enum { B = 5 };
+  const int fan[B] = {2, 7, 3, 7, 1};
+  const size_t ns[B] = {85354, 4096, 333333, 17, 70000};
+  int tot = 0;
+  for (int t = 0; t < B; ++t) tot += fan[t];
+  float* h[2 + 7 + 3 + 7 + 1];
+  const void* din[2 + 7 + 3 + 7 + 1];
+  float w[2 + 7 + 3 + 7 + 1];
+  void* douts[B];
+  int o = 0;
+  for (int t = 0; t < B; ++t) {
+    weights(w + o, fan[t]);
+    for (int i = 0; i < fan[t]; ++i, ++o) {
+      h[o] = (float*)malloc(ns[t] * 4);
+      fill_f32(h[o], ns[t]);
+      din[o] = dev_copy(h[o], ns[t] * 4);
+    }
+    HIPCK(hipMalloc(&douts[t], ns[t] * 4));
+  }
+  size_t bytes = 0;
+  DLCK(dlsim_batch_table_bytes(B, fan, ns, DLSIM_F32, &bytes));
+  void *htab = NULL, *dtab = NULL;
+  HIPCK(hipHostMalloc(&htab, bytes, 0));
+  HIPCK(hipMalloc(&dtab, bytes));
+  DLCK(dlsim_batch_table_fill(B, fan, din, w, douts, ns, DLSIM_F32, htab, bytes));
+  HIPCK(hipMemcpyAsync(dtab, htab, bytes, hipMemcpyHostToDevice, st));
+  for (int rep = 0; rep < 2; ++rep) DLCK(dlsim_batch_table_launch(htab, dtab, DLSIM_F32, DLSIM_EXACT, st));
+  HIPCK(hipStreamSynchronize(st));
+  o = 0;
+  for (int t = 0; t < B; ++t) {
+    float* exp = (float*)malloc(ns[t] * 4);
+    float* got = (float*)malloc(ns[t] * 4);
+    oracle_wreduce_f32((const float* const*)(h + o), fan[t], w + o, exp, ns[t]);
+    HIPCK(hipMemcpy(got, douts[t], ns[t] * 4, hipMemcpyDeviceToHost));
+    char what[64];
+    snprintf(what, sizeof what, "dlsim_batch_table task %d (fan-in %d, %zu)", t, fan[t], ns[t]);
+    expect_same(what, got, exp, ns[t] * 4);
+    free(exp);
+    free(got);
+    o += fan[t];
+  }
+  for (int j = 0; j < tot; ++j) {
+    free(h[j]);
+    HIPCK(hipFree((void*)din[j]));
+  }
+  for (int t = 0; t < B; ++t) HIPCK(hipFree(douts[t]));
+  HIPCK(hipHostFree(htab));
+  HIPCK(hipFree(dtab));
+}
+
+static void case_host_chunk_mean(hipStream_t st) {
+  /* Conflux from host chunks: k = 6 indices, 3-5 contributors each, pinned
+   * staging, means back on the device and in page-locked host memory */
+  enum { K = 6 };
+  const int fan[K] = {3, 4, 5, 3, 4, 5};
+  const size_t ns[K] = {14226, 14226, 14226, 14226, 14226, 14224};
+  float* h[3 + 4 + 5 + 3 + 4 + 5];
+  const void* hin[3 + 4 + 5 + 3 + 4 + 5];
+  void *douts[K], *houts[K];
+  size_t need = 0;
+  int o = 0;
+  for (int t = 0; t < K; ++t) {
+    for (int i = 0; i < fan[t]; ++i, ++o) {
+      h[o] = (float*)malloc(ns[t] * 4 + 4);
+      fill_f32(h[o], ns[t]);
+      hin[o] = h[o];
+    }
+    need += (size_t)fan[t] * ((ns[t] + 63) / 64 * 64);
+    HIPCK(hipMalloc(&douts[t], ns[t] * 4));
+    HIPCK(hipHostMalloc(&houts[t], ns[t] * 4, 0));
+  }
+  void *stage = NULL, *dstage = NULL;
+  HIPCK(hipHostMalloc(&stage, need * 4, 0));
+  HIPCK(hipMalloc(&dstage, need * 4));
+  DLCK(dlsim_host_chunk_mean(K, fan, hin, ns, stage, dstage, need, douts, houts, DLSIM_F32, 4, 2, st, NULL, NULL));
+  HIPCK(hipStreamSynchronize(st));
+  o = 0;
+  for (int t = 0; t < K; ++t) {
+    float* exp = (float*)malloc(ns[t] * 4);
+    float* got = (float*)malloc(ns[t] * 4);
+    oracle_chunk_mean_f32((const float* const*)(h + o), fan[t], exp, ns[t], 4);
+    HIPCK(hipMemcpy(got, douts[t], ns[t] * 4, hipMemcpyDeviceToHost));
+    char what[64];
+    snprintf(what, sizeof what, "dlsim_host_chunk_mean index %d (m=%d)", t, fan[t]);
+    expect_same(what, got, exp, ns[t] * 4);
+    if (memcmp(houts[t], exp, ns[t] * 4) != 0) {
+      fprintf(stderr, "dlsim_host_chunk_mean index %d: host copy differs\n", t);
+      exit(1);
+    }
+    free(exp);
+    free(got);
+    o += fan[t];
+  }
+  for (int j = 0; j < o; ++j) free(h[j]);
+  for (int t = 0; t < K; ++t) {
+    HIPCK(hipFree(douts[t]));
+    HIPCK(hipHostFree(houts[t]));
+  }
+  HIPCK(hipHostFree(stage));
+  HIPCK(hipFree(dstage));
+}
+
 static void case_errors(hipStream_t st) {
   void* d = NULL;
   HIPCK(hipMalloc(&d, 256));
@@ -396,6 +502,8 @@ int main(void) {
   case_tensors_and_batched(st);
   case_chunk_means(st);
   case_host_wreduce(st);
+  case_table_batch(st);
+  case_host_chunk_mean(st);
   case_errors(st);
   HIPCK(hipStreamDestroy(st));
   printf("c_host_check OK\n");
