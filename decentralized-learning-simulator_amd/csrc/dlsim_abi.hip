@@ -14,6 +14,7 @@
 #include <string>
 #include <thread>
 #include <type_traits>
+#include <type_traits>
 #include <vector>
 
 #include "dlsim.h"
@@ -119,7 +120,7 @@ struct Rccl {
   const char* (*err)(rccl_result_t) = nullptr;
 };
 Rccl g_rccl;
-constexpr int kRcclFloat16 = 6, kRcclFloat32 = 7, kRcclBfloat16 = 9;  // ncclDataType_t (rccl.h)
+constexpr int kRcclFloat16 = 6, kRcclFloat32 = 7, kRcclFloat64 = 8, kRcclBfloat16 = 9;  // ncclDataType_t (rccl.h)
 constexpr int kRcclInt64 = 4, kRcclMax = 2;                           // ncclInt64, ncclMax
 
 int rccl_fail(rccl_result_t r, const char* what) {
@@ -427,9 +428,13 @@ int sharded_agree(void* comm, int world, int rank, bool local_fail, size_t n_ele
   return DLSIM_OK;
 }
 
-int dlsim_wreduce_sharded(const void* const* d_slices, size_t slice_elems, int n, const float* h_weights,
-                          void* d_out, size_t n_elems, int dtype, int mode, void* rccl_comm, int gather,
-                          void* stream) {
+// The body of dlsim_wreduce_sharded / _f64 (float or double weights): C++
+// linkage, internal to the library.
+extern "C++" {
+namespace {
+template <class W>
+int wreduce_sharded(const void* const* d_slices, size_t slice_elems, int n, const W* h_weights, void* d_out,
+                    size_t n_elems, int dtype, int mode, void* rccl_comm, int gather, void* stream) {
   g_err.clear();
   if (!g_rccl.lib) return fail(DLSIM_E_RCCL, "RCCL not bound (call dlsim_rccl_bind first)");
   if (!rccl_comm) return fail(DLSIM_E_ARG, "null RCCL communicator");
@@ -449,12 +454,19 @@ int dlsim_wreduce_sharded(const void* const* d_slices, size_t slice_elems, int n
   if (rc == DLSIM_OK && slice_elems != e - b)
     rc = fail(DLSIM_E_ARG, "rank %d of %d: slices have %zu elements, its shard [%zu, %zu) has %zu", rank, world,
               slice_elems, b, e, e - b);
-  const size_t esz = known_dtype(dtype) ? elem_bytes(dtype) : 0;
+  constexpr bool kF64 = std::is_same<W, double>::value;
+  const bool dtype_ok = kF64 ? dtype == DLSIM_F64 : known_dtype(dtype);
+  const size_t esz = dtype_ok ? elem_bytes(dtype) : 0;
   char* out = static_cast<char*>(d_out);
   if (rc == DLSIM_OK) {
     // this rank's slice of every model -> this rank's slice of the output
-    if (e > b) rc = dlsim_wreduce(d_slices, n, h_weights, out + b * esz, e - b, dtype, mode, stream);
-    else rc = check_args(d_slices, n, h_weights, nullptr, 0, dtype, mode);
+    if constexpr (kF64) {
+      if (e > b) rc = dlsim_wreduce_f64(d_slices, n, h_weights, out + b * esz, e - b, mode, stream);
+      else rc = check_args(d_slices, n, h_weights, nullptr, 0, dtype, mode, true, true);
+    } else {
+      if (e > b) rc = dlsim_wreduce(d_slices, n, h_weights, out + b * esz, e - b, dtype, mode, stream);
+      else rc = check_args(d_slices, n, h_weights, nullptr, 0, dtype, mode);
+    }
   }
   if (world > 1) {
     const std::string local_err = g_err;
@@ -480,7 +492,10 @@ int dlsim_wreduce_sharded(const void* const* d_slices, size_t slice_elems, int n
   }
   if (!gather || world == 1 || n_elems == 0) return DLSIM_OK;
   // variable-size all-gather: every rank broadcasts its slice in place
-  const int dt = dtype == DLSIM_BF16 ? kRcclBfloat16 : dtype == DLSIM_F16 ? kRcclFloat16 : kRcclFloat32;
+  const int dt = dtype == DLSIM_BF16 ? kRcclBfloat16
+                 : dtype == DLSIM_F16  ? kRcclFloat16
+                 : dtype == DLSIM_F64  ? kRcclFloat64
+                                       : kRcclFloat32;
   rr = g_rccl.group_start();
   if (rr != 0) return rccl_fail(rr, "ncclGroupStart");
   for (int r = 0; r < world; ++r) {
@@ -496,6 +511,21 @@ int dlsim_wreduce_sharded(const void* const* d_slices, size_t slice_elems, int n
   rr = g_rccl.group_end();
   if (rr != 0) return rccl_fail(rr, "ncclGroupEnd");
   return DLSIM_OK;
+}
+}  // namespace
+}  // extern "C++"
+
+int dlsim_wreduce_sharded(const void* const* d_slices, size_t slice_elems, int n, const float* h_weights,
+                          void* d_out, size_t n_elems, int dtype, int mode, void* rccl_comm, int gather,
+                          void* stream) {
+  return wreduce_sharded(d_slices, slice_elems, n, h_weights, d_out, n_elems, dtype, mode, rccl_comm, gather,
+                         stream);
+}
+
+int dlsim_wreduce_sharded_f64(const void* const* d_slices, size_t slice_elems, int n, const double* h_weights,
+                              void* d_out, size_t n_elems, int mode, void* rccl_comm, int gather, void* stream) {
+  return wreduce_sharded(d_slices, slice_elems, n, h_weights, d_out, n_elems, DLSIM_F64, mode, rccl_comm, gather,
+                         stream);
 }
 
 int dlsim_host_wreduce(int n, int t, const void* const* h_srcs, const size_t* numels,

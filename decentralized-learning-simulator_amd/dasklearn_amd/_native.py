@@ -42,6 +42,7 @@ EXPORTS = (
     "dlsim_chunk_mean_ilp_begin",
     "dlsim_rccl_bind",
     "dlsim_wreduce_sharded",
+    "dlsim_wreduce_sharded_f64",
     "dlsim_host_wreduce",
     "dlsim_host_chunk_mean",
     "dlsim_host_pack",
@@ -114,6 +115,9 @@ def load() -> ctypes.CDLL:
         lib.dlsim_wreduce_sharded.argtypes = [ctypes.POINTER(vp), sz, i, ctypes.POINTER(ctypes.c_float), vp, sz, i,
                                               i, vp, i, vp]
         lib.dlsim_wreduce_sharded.restype = i
+        lib.dlsim_wreduce_sharded_f64.argtypes = [ctypes.POINTER(vp), sz, i, ctypes.POINTER(ctypes.c_double), vp,
+                                                  sz, i, vp, i, vp]
+        lib.dlsim_wreduce_sharded_f64.restype = i
         lib.dlsim_host_wreduce.argtypes = [i, i, ctypes.POINTER(vp), ctypes.POINTER(sz),
                                            ctypes.POINTER(ctypes.c_float), vp, vp, sz, vp, vp, i, i, sz, i,
                                            vp, vp, vp]
@@ -513,7 +517,9 @@ def wreduce_sharded(slices, weights_f32, out, comm_ptr: int, gather: bool = True
                     mode: int = DLSIM_EXACT, stream=None):
     """dlsim_wreduce_sharded: `slices[i]` is this rank's slice of model i,
     `out` the full-size output; `comm_ptr` an RCCL communicator (e.g.
-    ProcessGroupNCCL._comm_ptr())."""
+    ProcessGroupNCCL._comm_ptr()). fp64 tensors go to
+    dlsim_wreduce_sharded_f64 and take exact double weights (pass
+    weights_for_dtype(weights, torch.float64))."""
     lib = load()
     if _RCCL_BOUND is None:  # the caller may have bound another RCCL (tests bind a stub)
         rccl_bind()
@@ -527,10 +533,21 @@ def wreduce_sharded(slices, weights_f32, out, comm_ptr: int, gather: bool = True
                              "and device")
     if not out.is_cuda or not out.is_contiguous():
         raise ValueError("out must be a contiguous device tensor")
+    import torch
+    ptrs = (ctypes.c_void_p * n)(*[x.data_ptr() for x in slices])
+    if out.dtype == torch.float64:
+        wd = np.ascontiguousarray(weights_f32, dtype=np.float64)
+        if wd.size != n:
+            raise AssertionError("weights/models length mismatch")
+        _check("dlsim_wreduce_sharded_f64",
+               lib.dlsim_wreduce_sharded_f64(ptrs, slices[0].numel(), n,
+                                             wd.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), out.data_ptr(),
+                                             out.numel(), mode, ctypes.c_void_p(comm_ptr), 1 if gather else 0,
+                                             _stream_handle(out.device, stream)))
+        return out
     w = np.ascontiguousarray(weights_f32, dtype=np.float32)
     if w.size != n:
         raise AssertionError("weights/models length mismatch")
-    ptrs = (ctypes.c_void_p * n)(*[x.data_ptr() for x in slices])
     _check("dlsim_wreduce_sharded",
            lib.dlsim_wreduce_sharded(ptrs, slices[0].numel(), n, w.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
                                      out.data_ptr(),

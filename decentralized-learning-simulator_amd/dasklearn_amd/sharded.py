@@ -111,9 +111,10 @@ class ShardedAggregator:
         try:
             if not shard_inputs:
                 raise IndexError("list index out of range")  # models[0] of fedavg.py:20
-            w32 = _resolve(len(shard_inputs), weights)
-            b, e = self.bounds(n_elems)
             x0 = shard_inputs[0]
+            # fp32-rounded weights, or exact doubles for a double model (fedavg.py:25)
+            w32 = _resolve(len(shard_inputs), weights, x0.dtype)
+            b, e = self.bounds(n_elems)
             for x in shard_inputs:
                 if x.numel() != e - b:
                     raise ValueError(f"rank {self.rank}: shard has {x.numel()} elements, expected {e - b}")
@@ -141,7 +142,8 @@ class ShardedAggregator:
                 if failed is not None:
                     self._raise_collectively(failed)
                 return full if gather else full[b:e]
-        self._agree(local, [n_elems, 1 if gather else 0, _native.dtype_code(x0.dtype) if local is None else 0])
+        self._agree(local, [n_elems, 1 if gather else 0,
+                            _native.dtype_code(x0.dtype, single_task=True) if local is None else 0])
         out = torch.empty(e - b, dtype=x0.dtype, device=x0.device)
         if e > b:
             self.local_reduce(list(shard_inputs), w32, out, mode)
@@ -195,15 +197,16 @@ class ShardedAggregator:
             local = ex
         ref = local_models[0] if local_models and local is None else None
         # every rank checks its arguments before the first collective; the
-        # agreement also tells ranks without models the model size
-        n_elems = _agree_numel(ref, self.group, self, local)
-        dtype = ref.dtype if ref is not None else torch.float32
+        # agreement also tells ranks without models the model size and dtype
+        n_elems, dtype = _agree_numel(ref, self.group, self, local, with_dtype=True)
+        w32 = _resolve(n_total, weights, dtype)  # exact doubles for a double model (fedavg.py:25)
         device = ref.device if ref is not None else _default_device()
         first = sum(counts[:self.rank])
         if exact:
             return self._model_sharded_exact(local_models, counts, w32, n_elems, dtype, device)
         # FAST: partial sums of local models, then sum over ranks
-        partial = torch.zeros(n_elems, dtype=torch.float32, device=device)
+        acc_dt = torch.float64 if dtype == torch.float64 else torch.float32
+        partial = torch.zeros(n_elems, dtype=acc_dt, device=device)
         if local_models:
             lw = w32[first:first + len(local_models)]
             acc = torch.empty(n_elems, dtype=dtype, device=device)
@@ -211,10 +214,10 @@ class ShardedAggregator:
             partial.copy_(acc)
         bnds = self.all_bounds(n_elems)
         width = max(e - b for b, e in bnds)
-        padded = torch.zeros(width * self.world, dtype=torch.float32, device=device)
+        padded = torch.zeros(width * self.world, dtype=acc_dt, device=device)
         for r, (b, e) in enumerate(bnds):
             padded[r * width:r * width + (e - b)].copy_(partial[b:e])
-        mine = torch.empty(width, dtype=torch.float32, device=device)
+        mine = torch.empty(width, dtype=acc_dt, device=device)
         dist.reduce_scatter_tensor(mine, padded, op=dist.ReduceOp.SUM, group=self.group)
         b, e = bnds[self.rank]
         return self.all_gather(mine[:e - b].to(dtype).contiguous(), n_elems)
@@ -244,13 +247,14 @@ class ShardedAggregator:
         return self.all_gather(out, n_elems)
 
 
-def _resolve(n: int, weights) -> np.ndarray:
-    # fedavg.py:14-17 rules, then the fp32 rounding of `w * p1` (fedavg.py:25)
+def _resolve(n: int, weights, dtype=None) -> np.ndarray:
+    # fedavg.py:14-17 rules, then the weight as `w * p1` sees it (fedavg.py:25):
+    # rounded to fp32, or an exact double for a double tensor
     if not weights:
         weights = [float(1. / n) for _ in range(n)]
     else:
         assert len(weights) == n
-    return _native.fp32_weights(weights)
+    return _native.weights_for_dtype(weights, dtype) if dtype is not None else _native.fp32_weights(weights)
 
 
 def _default_device():
@@ -279,19 +283,32 @@ def _max_allreduce(group, world: int, rank: int, failed: bool, args: Sequence[in
     return t.tolist()
 
 
+_DTYPES = {0: torch.float32, 1: torch.bfloat16, 2: torch.float16, 3: torch.float64}  # enum dlsim_dtype
+
+
 def _agree_numel(ref: Optional[torch.Tensor], group, agg: Optional["ShardedAggregator"] = None,
-                 local: Optional[BaseException] = None) -> int:
-    """Every rank must see the same model size; ranks without models learn
-    it. With `agg`, rank-local argument errors are agreed in the same
-    all-reduce (a failure slot per rank) and raised on every rank; a size
-    disagreement is raised on every rank too."""
+                 local: Optional[BaseException] = None, with_dtype: bool = False):
+    """Every rank must see the same model size (and, with_dtype, element
+    type); ranks without models learn them. With `agg`, rank-local argument
+    errors are agreed in the same all-reduce (a failure slot per rank) and
+    raised on every rank; a size or dtype disagreement is raised on every rank
+    too. Returns n, or (n, dtype) with_dtype (fp32 when no rank holds a
+    model)."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
+    none = -2 ** 62
     # ranks without models contribute (-1, -2^62): neutral for both maxima
-    hi, neg_lo = (ref.numel(), -ref.numel()) if ref is not None else (-1, -2 ** 62)
-    t = torch.zeros(world + 2, dtype=torch.int64, device=_coll_device(group))
+    hi, neg_lo = (ref.numel(), -ref.numel()) if ref is not None else (-1, none)
+    code = None
+    if ref is not None and local is None:
+        try:
+            code = _native.dtype_code(ref.dtype, single_task=True)
+        except TypeError as ex:  # an unsupported dtype fails this rank, collectively
+            local = ex
+    t = torch.zeros(world + 4, dtype=torch.int64, device=_coll_device(group))
     t[rank] = 1 if local is not None else 0
     t[world], t[world + 1] = hi, neg_lo
+    t[world + 2], t[world + 3] = (code, -code) if code is not None else (-1, none)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     w = t.tolist()
     if any(w[:world]):
@@ -299,6 +316,10 @@ def _agree_numel(ref: Optional[torch.Tensor], group, agg: Optional["ShardedAggre
             raise RuntimeError("a rank failed its checks")
         agg._raise_collectively(local)
     n = int(w[world])
-    if w[world + 1] != -2 ** 62 and n != -w[world + 1]:
+    if w[world + 1] != none and n != -w[world + 1]:
         raise ValueError("models differ in size across ranks")
-    return n
+    if w[world + 3] != none and w[world + 2] != -w[world + 3]:
+        raise ValueError("models differ in dtype across ranks")
+    if not with_dtype:
+        return n
+    return n, _DTYPES.get(int(w[world + 2]), torch.float32)

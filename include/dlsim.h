@@ -274,6 +274,17 @@ int dlsim_wreduce_sharded(const void* const* d_slices, size_t slice_elems, int n
                           void* stream);
 
 /*
+ * dlsim_wreduce_sharded_f64 — dlsim_wreduce_sharded for fp64 (double)
+ * parameters: double weights and the arithmetic of dlsim_wreduce_f64 (a
+ * double model's `w * p1` keeps the Python float exact, fedavg.py:25), the
+ * gather as ncclFloat64 broadcasts. The agreement step is the same one, with
+ * dtype DLSIM_F64, so ranks that call the fp32/bf16/fp16 entry with the same
+ * communicator are told of the disagreement instead of left waiting.
+ */
+int dlsim_wreduce_sharded_f64(const void* const* d_slices, size_t slice_elems, int n, const double* h_weights,
+                              void* d_out, size_t n_elems, int mode, void* rccl_comm, int gather, void* stream);
+
+/*
  * dlsim_host_wreduce — the aggregate of N *host* models (the reference's own
  * case: CPU modules, fedavg.py:20-25 run by functions.py:89-106), staged
  * through pinned memory and reduced on the device, as one pipeline.

@@ -39,6 +39,8 @@ def rccl_world1():
 
 def _expect(xs, w32, dtype):
     from oracle import oracle as orc
+    if dtype == torch.float64:
+        return torch.from_numpy(orc.wreduce([x.cpu().numpy() for x in xs], np.asarray(w32, np.float64), "f64"))
     if dtype in (torch.bfloat16, torch.float16):
         code = "bf16" if dtype == torch.bfloat16 else "f16"
         rows = [x.cpu().view(torch.int16).numpy().view(np.uint16) for x in xs]
@@ -50,11 +52,14 @@ def _same(a, b):
     a, b = a.cpu(), b.cpu()
     if a.dtype in (torch.bfloat16, torch.float16):
         return torch.equal(a.view(torch.int16), b.view(torch.int16))
-    return torch.equal(a.view(torch.int32), b.view(torch.int32))
+    if a.dtype != b.dtype:
+        return False
+    return torch.equal(a.view(torch.int64 if a.dtype == torch.float64 else torch.int32),
+                       b.view(torch.int64 if b.dtype == torch.float64 else torch.int32))
 
 
 @pytest.mark.parametrize("n,p,dtype", [(5, 100_003, torch.float32), (8, 1_048_577, torch.float32),
-                                       (3, 50_001, torch.bfloat16)])
+                                       (3, 50_001, torch.bfloat16), (4, 40_003, torch.float64)])
 def test_sharded_entry_points_rccl(rccl_world1, n, p, dtype):
     from dasklearn_amd.sharded import ShardedAggregator
     from oracle import oracle as orc
@@ -64,7 +69,8 @@ def test_sharded_entry_points_rccl(rccl_world1, n, p, dtype):
     g = torch.Generator(device=dev).manual_seed(11 + n)
     xs = [(torch.randn(p, generator=g, device=dev) * 0.05).to(dtype) for _ in range(n)]
     weights = [float(w) for w in np.random.default_rng(n).dirichlet(np.ones(n))]
-    w32 = orc.reference_weights(n, weights)
+    f64 = dtype == torch.float64  # the Python floats stay exact (fedavg.py:25)
+    w32 = orc.reference_weights_f64(n, weights) if f64 else orc.reference_weights(n, weights)
     expect = _expect(xs, w32, dtype)
 
     agg = ShardedAggregator()  # HIP kernel as the local reduce
@@ -75,16 +81,17 @@ def test_sharded_entry_points_rccl(rccl_world1, n, p, dtype):
     # whole models on "different ranks" (all on rank 0 here): all-to-all, exact fold, all-gather
     assert _same(agg.aggregate_model_sharded(xs, [n], weights, exact=True), expect)
     # FAST: partial sums + reduce-scatter + all-gather, tolerance only
-    fast = agg.aggregate_model_sharded(xs, [n], weights, exact=False).cpu().float()
-    scale = sum(abs(float(w)) * x.cpu().float().abs() for w, x in zip(w32, xs))
-    ulp = 2.0 ** -8 if dtype == torch.bfloat16 else 2.0 ** -23
-    assert torch.all((fast - expect.float()).abs() <= (n + 2) * ulp * scale + 1e-30)
+    fast = agg.aggregate_model_sharded(xs, [n], weights, exact=False).cpu().double()
+    scale = sum(abs(float(w)) * x.cpu().double().abs() for w, x in zip(w32, xs))
+    ulp = {torch.bfloat16: 2.0 ** -8, torch.float64: 2.0 ** -52}.get(dtype, 2.0 ** -23)
+    assert torch.all((fast - expect.double()).abs() <= (n + 2) * ulp * scale + 1e-300)
     # uniform weights (fedavg.py:14-15)
-    assert _same(agg.aggregate_param_sharded(xs, None, p), _expect(xs, orc.reference_weights(n, None), dtype))
+    wu = orc.reference_weights_f64(n, None) if f64 else orc.reference_weights(n, None)
+    assert _same(agg.aggregate_param_sharded(xs, None, p), _expect(xs, wu, dtype))
 
 
 @pytest.mark.parametrize("n,p,dtype", [(4, 70_001, torch.float32), (3, 50_001, torch.bfloat16),
-                                       (5, 30_003, torch.float16)])
+                                       (5, 30_003, torch.float16), (3, 20_001, torch.float64)])
 def test_c_abi_sharded_entry_on_torch_rccl_comm(rccl_world1, n, p, dtype):
     """dlsim_wreduce_sharded driven directly on the process group's own RCCL
     communicator (ProcessGroupNCCL._comm_ptr, RCCL bound from torch/lib):
@@ -96,7 +103,7 @@ def test_c_abi_sharded_entry_on_torch_rccl_comm(rccl_world1, n, p, dtype):
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(5 + n)
     xs = [(torch.randn(p, generator=g, device=dev) * 0.05).to(dtype) for _ in range(n)]
-    w32 = orc.reference_weights(n, None)
+    w32 = orc.reference_weights_f64(n, None) if dtype == torch.float64 else orc.reference_weights(n, None)
     expect = _expect(xs, w32, dtype)
     agg = ShardedAggregator()
     comm = agg._rccl_comm(dev)

@@ -57,13 +57,16 @@ def _nan_like(t):
     return torch.full_like(t, float("nan"))
 
 
-@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16"])
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16", "f64"])
 @pytest.mark.parametrize("world,p", [(2, 64 * 37 * 2 + 13), (3, 64 * 41 * 3 + 50), (8, 64 * 29 * 8 + 63),
                                      (8, 100), (3, 64)])
 def test_sharded_gather_assembles_the_whole_output(stub, world, p, dtype):
+    """fp64 goes through dlsim_wreduce_sharded_f64 (exact double weights,
+    ncclFloat64 broadcasts)."""
     n = 5
     rows = make_rows(n, p, world * 1000 + p, dtype)
-    w = orc.reference_weights(n, list(np.random.default_rng(world).dirichlet(np.ones(n))))
+    ws = [float(v) for v in np.random.default_rng(world).dirichlet(np.ones(n))]
+    w = orc.reference_weights_f64(n, ws) if dtype == "f64" else orc.reference_weights(n, ws)
     xs = to_dev(list(rows), dtype)
     full = torch.empty_like(xs[0])
     _native.wreduce(xs, w, full)

@@ -30,7 +30,11 @@ def _free_port():
 def oracle_reduce(inputs, w32, out, mode):
     from oracle import oracle as orc
     bf16 = inputs[0].dtype == torch.bfloat16
-    if bf16:
+    if inputs[0].dtype == torch.float64:  # exact double weights (weights_for_dtype)
+        rows = [t.contiguous().numpy() for t in inputs]
+        out.copy_(torch.from_numpy(orc.wreduce(rows, np.asarray(w32, np.float64), "f64",
+                                               "exact" if mode == 0 else "fast")))
+    elif bf16:
         rows = [t.contiguous().view(torch.int16).numpy().view(np.uint16) for t in inputs]
         res = orc.wreduce(rows, w32, "bf16", "exact" if mode == 0 else "fast")
         out.copy_(torch.from_numpy(res.view(np.int16).copy()).view(torch.bfloat16))
@@ -45,7 +49,7 @@ def models(n, p, dtype):
     return [x.to(dtype) for x in xs]
 
 
-def _worker(rank, world, port, p, dtype_name, q):
+def _worker(rank, world, port, p, dtype_name, q, n=5):
     for path in PATHS:
         sys.path.insert(0, path)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -53,22 +57,27 @@ def _worker(rank, world, port, p, dtype_name, q):
     try:
         from dasklearn_amd.sharded import ShardedAggregator
         from oracle import oracle as orc
-        dtype = torch.bfloat16 if dtype_name == "bf16" else torch.float32
+        dtype = {"bf16": torch.bfloat16, "f64": torch.float64}.get(dtype_name, torch.float32)
         agg = ShardedAggregator(local_reduce=oracle_reduce)
-        n = 5
         xs = models(n, p, dtype)
-        weights = [0.1, 0.3, 0.2, 0.15, 0.25]
+        weights = [0.1, 0.3, 0.2, 0.15, 0.25][:n]
         w32 = orc.reference_weights(n, weights)
         if dtype == torch.bfloat16:
             rows = [x.view(torch.int16).numpy().view(np.uint16) for x in xs]
             expect = torch.from_numpy(orc.wreduce(rows, w32, "bf16").view(np.int16).copy()).view(torch.bfloat16)
+        elif dtype == torch.float64:  # the Python floats kept exact (fedavg.py:25)
+            w32 = orc.reference_weights_f64(n, weights)
+            expect = torch.from_numpy(orc.wreduce([x.numpy() for x in xs], w32, "f64"))
         else:
             expect = torch.from_numpy(orc.wreduce([x.numpy() for x in xs], w32, "f32"))
 
         def same(a, b):
+            if a.dtype != b.dtype:
+                return False
             if a.dtype == torch.bfloat16:
                 return torch.equal(a.view(torch.int16), b.view(torch.int16))
-            return torch.equal(a.view(torch.int32), b.view(torch.int32))
+            return torch.equal(a.view(torch.int64 if a.dtype == torch.float64 else torch.int32),
+                               b.view(torch.int64 if b.dtype == torch.float64 else torch.int32))
 
         res = {}
         # 1) parameter-sharded: each rank holds its slice of every model
@@ -86,15 +95,17 @@ def _worker(rank, world, port, p, dtype_name, q):
         res["model_sharded_exact"] = same(full2, expect)
         # 3) model-sharded, fast (partial sums + reduce-scatter): tolerance only
         full3 = agg.aggregate_model_sharded(mine, counts, weights, exact=False)
-        scale = sum(abs(w) * x.float().abs() for w, x in zip(w32, xs))
-        ulp = 2.0 ** -8 if dtype == torch.bfloat16 else 2.0 ** -23
+        scale = sum(abs(w) * x.double().abs() for w, x in zip(w32, xs))
+        ulp = {torch.bfloat16: 2.0 ** -8, torch.float64: 2.0 ** -52}.get(dtype, 2.0 ** -23)
         res["model_sharded_fast_tol"] = bool(torch.all(
-            (full3.float() - expect.float()).abs() <= (n + 2) * ulp * scale + 1e-30))
+            (full3.double() - expect.double()).abs() <= (n + 2) * ulp * scale + 1e-300))
         # 4) uniform weights (None) path
         full4 = agg.aggregate_param_sharded([x[b:e].contiguous() for x in xs], None, p)
         w_u = orc.reference_weights(n, None)
         if dtype == torch.bfloat16:
             exp4 = torch.from_numpy(orc.wreduce(rows, w_u, "bf16").view(np.int16).copy()).view(torch.bfloat16)
+        elif dtype == torch.float64:
+            exp4 = torch.from_numpy(orc.wreduce([x.numpy() for x in xs], orc.reference_weights_f64(n, None), "f64"))
         else:
             exp4 = torch.from_numpy(orc.wreduce([x.numpy() for x in xs], w_u, "f32"))
         res["param_sharded_uniform"] = same(full4, exp4)
@@ -106,13 +117,14 @@ def _worker(rank, world, port, p, dtype_name, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,p,dtype", [(2, 10_003, "f32"), (3, 4_097, "f32"), (2, 5_001, "bf16"),
-                                           (3, 130, "f32")])
-def test_sharded_paths_gloo(world, p, dtype):
+@pytest.mark.parametrize("world,p,dtype,n", [(2, 10_003, "f32", 5), (3, 4_097, "f32", 5), (2, 5_001, "bf16", 5),
+                                             (3, 130, "f32", 5), (2, 3_001, "f64", 5),
+                                             (3, 1_000, "bf16", 2)])  # rank 2 holds no model
+def test_sharded_paths_gloo(world, p, dtype, n):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, p, dtype, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, p, dtype, q, n)) for r in range(world)]
     for pr in procs:
         pr.start()
     results = {}
