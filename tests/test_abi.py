@@ -141,3 +141,27 @@ def test_host_chunk_mean_argument_errors_need_no_gpu():
     assert call([2, 3], [100, 7], staging_elems=2 * 128 + 3 * 64 - 1) == -1
     assert call([2], [10], staging=4100) == -1 and b"aligned" in lib.dlsim_last_error()
     assert call([2], [10], outs=[0]) == -1 and b"null output" in lib.dlsim_last_error()
+
+
+def test_library_errors_stay_on_the_calling_thread():
+    """dlsim_last_error is thread-local: a failing call on one thread does not
+    clobber the message another thread reads (argument errors, no GPU)."""
+    import threading
+    lib = _native.load()
+    for _ in range(20):
+        barrier = threading.Barrier(2)
+        seen = {}
+
+        def fail_with(tag, n):
+            barrier.wait()
+            rc = lib.dlsim_wreduce(None, n, None, None, 16, 0, 0, None)
+            seen[tag] = (rc, lib.dlsim_last_error().decode())
+
+        ts = [threading.Thread(target=fail_with, args=("zero", 0)),
+              threading.Thread(target=fail_with, args=("neg", -3))]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        assert seen["zero"][0] == -1 and "got 0)" in seen["zero"][1], seen
+        assert seen["neg"][0] == -1 and "got -3)" in seen["neg"][1], seen
