@@ -441,8 +441,9 @@ def _host_pipeline(all_params, idx, layout, dt, dev, out, weights_f32, mode, str
     stream (PCIe is full duplex). Bytes and results are those of the
     unchunked reduce (elements are independent). One-chunk models use the
     caller's stream for everything (the side-stream events cost more than
-    they hide there). Returns the pinned host result (want_host; complete
-    once `stream` is) or None (the result is in `out`, queued on `stream`)."""
+    they hide there). Returns (the pinned host result (want_host; complete
+    once `stream` is) or None (the result is in `out`, queued on `stream`),
+    whether a non-contiguous tensor was copied)."""
     n = len(all_params)
     total = layout.totals[dt]
     esz = out.element_size()
@@ -467,7 +468,7 @@ def _host_pipeline(all_params, idx, layout, dt, dev, out, weights_f32, mode, str
             synced = True
     finally:
         STAGING.release(dev, dt, stream, synced)
-    return host
+    return host, bool(keep)
 
 
 def _data_ptrs(all_params, idx):
@@ -506,7 +507,8 @@ def _staged_reduce(all_params, idx, dt, dev, out, weights, mode, stream):
 def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, mode: int,
                              device=None, timing: Optional[dict] = None, host_out: Optional[bool] = False,
                              weights_f64: Optional[np.ndarray] = None
-                             ) -> Tuple[ParamLayout, Dict[torch.dtype, torch.Tensor], torch.device, bool, bool]:
+                             ) -> Tuple[ParamLayout, Dict[torch.dtype, torch.Tensor], torch.device, bool, bool,
+                                        bool]:
     """Reduce the parameters of `models` into one fresh arena per dtype.
 
     weights_f32: the fp32-rounded weights (fp32/bf16/fp16 groups);
@@ -514,7 +516,9 @@ def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, m
     group (fedavg.py:25 keeps the Python float exact for a double tensor);
     default: widened fp32.
     host_out None: as the reference's output, iff models[0]'s parameters are on
-    the host. Returns (layout, arenas, device, on_host, host_out). With
+    the host. Returns (layout, arenas, device, on_host, host_out, staged):
+    staged = some group went through a path that also takes non-contiguous
+    tensors (the caller then gives such parameters models[0]'s strides). With
     host_out, host models take the chunked pipeline and come back already in
     host memory (on_host True, copies complete); otherwise the arenas are on
     the device."""
@@ -537,6 +541,7 @@ def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, m
     host_models = all(not all_params[i][idx[0]].is_cuda
                       for idx in layout.groups.values() for i in range(n))
     piped = host_out and host_models and len(layout.groups) > 0
+    staged = False
     with torch.no_grad():
         for dt, idx in layout.groups.items():
             total = layout.totals[dt]
@@ -560,6 +565,7 @@ def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, m
                     continue
                 if f64:  # one task through dlsim_wreduce_f64
                     _staged_reduce(all_params, idx, dt, dev, out, w, mode, get_stream())
+                    staged = True
                     st.mark("kernel")
                     continue
                 # separate device tensors, read in place: the layout checked
@@ -571,13 +577,16 @@ def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, m
                     # a tensor is not contiguous, or (in a model whose first
                     # tensor is here) on another device: stage them all
                     _staged_reduce(all_params, idx, dt, dev, out, w, mode, get_stream())
+                    staged = True
                 st.mark("kernel")
                 continue
             if not f64 and not any(all_params[i][idx[0]].is_cuda for i in range(n)):
                 # host models (the reference's case): chunked pack / H2D /
                 # reduce (/ D2H) pipeline
                 st.mark("layout")
-                h = _host_pipeline(all_params, idx, layout, dt, dev, out, weights_f32, mode, get_stream(), piped)
+                h, copied = _host_pipeline(all_params, idx, layout, dt, dev, out, weights_f32, mode, get_stream(),
+                                           piped)
+                staged = staged or copied
                 if h is not None:
                     outs[dt] = h
                 st.mark("pipeline")
@@ -586,6 +595,7 @@ def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, m
             # one, then reduce
             st.mark("layout")
             _staged_reduce(all_params, idx, dt, dev, out, w, mode, get_stream())
+            staged = True
             st.mark("kernel")
     if piped:
         left = {dt: a for dt, a in outs.items() if a.is_cuda}
@@ -594,7 +604,7 @@ def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, m
             st.mark("d2h")
         else:
             get_stream().synchronize()
-    return layout, outs, dev, piped, host_out
+    return layout, outs, dev, piped, host_out, staged
 
 
 def arenas_to_host(arenas: Dict[torch.dtype, torch.Tensor], stream) -> Dict[torch.dtype, torch.Tensor]:
@@ -831,17 +841,36 @@ def aggregate_modules(models: List[nn.Module], weights: Optional[Sequence[float]
         assert len(weights) == len(models)
     model0 = models[0]  # IndexError for an empty list, as the reference
     w32 = _native.fp32_weights(weights)
-    layout, arenas, dev, on_host, host_out = reduce_modules_to_arenas(models, w32, mode, device, timing, to_host,
-                                                                      weights_f64=weights)
+    layout, arenas, dev, on_host, host_out, staged = reduce_modules_to_arenas(models, w32, mode, device, timing,
+                                                                              to_host, weights_f64=weights)
     if timing is None and not (host_out and not on_host):
-        return module_from_arenas(model0, layout, arenas)
+        out = module_from_arenas(model0, layout, arenas)
+        return _restride(out, layout) if staged else out
     stream = torch.cuda.current_stream(dev)
     st = _Stages(timing, stream)
     if host_out and not on_host:
         arenas = arenas_to_host(arenas, stream)
         st.mark("d2h")
     out = module_from_arenas(model0, layout, arenas)
+    if staged:
+        _restride(out, layout)
     st.mark("module")
+    return out
+
+
+def _restride(out: nn.Module, layout: ParamLayout) -> nn.Module:
+    """Give every output parameter whose models[0] counterpart is not
+    contiguous the layout deepcopy(models[0]) gives it (fedavg.py:20:
+    Parameter.__deepcopy__ clones with preserve_format, e.g. a transposed
+    weight stays transposed); the values are the reduce's, element for
+    element. Such parameters leave the result arena (the next aggregate reads
+    them as separate tensors)."""
+    with torch.no_grad():
+        for q, p0 in zip(module_params(out), layout.params):
+            if not p0.is_contiguous():
+                fresh = torch.empty_like(p0, memory_format=torch.preserve_format, device=q.device)
+                fresh.copy_(q.detach())
+                q.data = fresh
     return out
 
 

@@ -97,7 +97,7 @@ def main():
         total = hlayout.totals[dt]
 
         def pipeline():
-            arena._host_pipeline(hall, hidx, hlayout, dt, dev, out, w32, _native.DLSIM_EXACT, stream, True)
+            arena._host_pipeline(hall, hidx, hlayout, dt, dev, out, w32, _native.DLSIM_EXACT, stream, True)[0]
 
         def stage_cycle():
             arena.STAGING.acquire(dev, dt, 7, total, stream)

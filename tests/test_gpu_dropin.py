@@ -355,3 +355,28 @@ def test_tied_parameters_and_shared_submodules(where):
     assert torch.equal(out.bn.running_mean.cpu(), models[0].bn.running_mean.cpu())
     assert int(out.bn.num_batches_tracked) == 3
     assert out.none_slot is None
+
+
+class _Strided(nn.Module):
+    def __init__(self, seed):
+        super().__init__()
+        g = torch.Generator().manual_seed(seed)
+        self.w = nn.Parameter(torch.randn(5, 9, generator=g).t())  # transposed: strides (1, 9)
+        self.b = nn.Parameter(torch.randn(9, generator=g))
+        self.c = nn.Parameter(torch.randn(2, 3, 4, generator=g).permute(2, 0, 1))
+
+
+@pytest.mark.parametrize("where", ["host", "device"])
+def test_non_contiguous_parameters_keep_models0_strides(where):
+    """deepcopy(models[0]) (fedavg.py:20) clones a non-contiguous parameter with
+    its strides (preserve_format) and add_ works on logical elements: the
+    output has models[0]'s strides and the reference's values bit for bit."""
+    models = [_Strided(7 + i) for i in range(4)]
+    w = [0.1, 0.2, 0.3, 0.4]
+    ref = fedavg_torch.aggregate_modules([copy.deepcopy(m) for m in models], w)
+    ins = [copy.deepcopy(m).to("cuda") for m in models] if where == "device" else models
+    out = FedAvg.aggregate(ins, w)
+    for (na, pa), (nb, pb) in zip(out.named_parameters(), ref.named_parameters()):
+        assert pa.shape == pb.shape and pa.stride() == pb.stride(), (na, pa.stride(), pb.stride())
+        assert pa.is_cuda == (where == "device")
+        assert torch.equal(pa.detach().cpu().contiguous().view(torch.int32), pb.detach().contiguous().view(torch.int32)), na
