@@ -355,9 +355,13 @@ def main():
                         ok = ok and orc.same_bits(bits(got), orc.wreduce(rows, w, code))
                 ok = ok and all(torch.equal(a.cpu(), b.cpu()) for a, b in zip(out.buffers(), models[0].buffers()))
                 ok = ok and [p.requires_grad for p in out.parameters()] == [p.requires_grad for p in models[0].parameters()]
-                # deepcopy(models[0])'s layouts (preserve_format: a transposed weight stays transposed)
-                ok = ok and [q.stride() for q in out.parameters()] == \
-                    [torch.empty_like(q0, memory_format=torch.preserve_format).stride() for q0 in models[0].parameters()]
+                # deepcopy(models[0])'s layouts (preserve_format: a transposed weight stays
+                # transposed); strides of size-1 dimensions carry no layout
+                ok = ok and all(
+                    all(sa == sb for sa, sb, k in zip(q.stride(), q0.stride(), q.shape) if k > 1)
+                    for q, q0 in zip(out.parameters(),
+                                     (torch.empty_like(t, memory_format=torch.preserve_format)
+                                      for t in models[0].parameters())))
                 if hasattr(models[0], "tied"):  # deepcopy(models[0]) keeps the sharing (fedavg.py:20)
                     ok = ok and out.tied.w is out.leaves[0].w and out.alias is out.leaves
                 counts["modules"] += 1
