@@ -20,7 +20,8 @@ rank's HIP-event time around its K launches; the barriers that line the ranks
 up sit outside that window. The line carries the speed-up over the same
 config on one GPU (rank 0 times it alone, same K, same timing) and, in their
 own fields, the RCCL all-gather that would materialise the full output and
-the C ABI's sharded entry point (local reduce + grouped in-place broadcasts).
+the C ABI's sharded entry points (local reduce + grouped in-place broadcasts
+or a padded all-gather, agreed per call or once through a plan).
 --weak instead gives every rank the config's full parameter count.
 
 Bytes per step per rank = (N_models + 1) * P_rank * sizeof(dtype) (read N,
@@ -122,6 +123,9 @@ def parse(argv=None):
                     help="process-group backend: nccl (= RCCL over xGMI, the real path); gloo only "
                          "to rehearse the multi-process flow on a box with fewer GPUs than ranks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-gate", action="store_true",
+                    help="start the timing window on an idle GPU (the start event then also times the host's "
+                         "enqueue of the first launch); default: a short GPU spin before the start event")
     ap.add_argument("--two-streams", action="store_true",
                     help="diagnostic: also time the K steps alternating over two streams (field two_streams); "
                          "off by default because those overlapping dispatches would enter a rocprof average "
@@ -173,15 +177,25 @@ def spawn_ranks(n: int, argv, script: str = None) -> int:
 
 # ---- timing ----------------------------------------------------------------------
 
-def time_steps(launch, k_steps: int, sync, barrier, new_event):
+def time_steps(launch, k_steps: int, sync, barrier, new_event, gate=None):
     """Time exactly k_steps launches. The barrier that lines the ranks up and
     a device sync come BEFORE the window; the window is two events on the
     launch stream around the launches (plus a host clock from the first
     launch to the sync after the last); the closing barrier comes AFTER the
-    window is read. Returns (event_ms, wall_ms) for all k_steps."""
+    window is read. Returns (event_ms, wall_ms) for all k_steps.
+
+    gate: enqueued after the sync and before the start event, a short GPU
+    spin (no step, no data) that keeps the stream busy while the host
+    enqueues the start event and the first launches. Without it the start
+    event is stamped on an idle GPU and the window also holds the host's
+    enqueue of launch 0 (~5 us through ctypes: 0.4 % of a 20-step window);
+    with it the window is the K steps' GPU time, as rocprof's per-dispatch
+    durations see them."""
     barrier()
     sync()
     e0, e1 = new_event(), new_event()
+    if gate is not None:
+        gate()
     t0 = time.perf_counter()
     e0.record()
     for k in range(k_steps):
@@ -260,14 +274,14 @@ class ReduceWorkload:
         self.probe_plans[k % self.sets].launch(self.stream)
 
 
-def pattern_ceiling(wl, k_steps: int, sync, new_event, achieved_gbps: float):
+def pattern_ceiling(wl, k_steps: int, sync, new_event, achieved_gbps: float, gate=None):
     """dlsim_probe_pattern over the same rotating sets: the reduce's own
     dispatch (kernel, launch shape, nt loads, store policy) with the weighted
     fold replaced by a bitwise XOR — what the memory system allows for exactly
     this read/write mix, measured in the same run."""
     for k in range(10):
         wl.launch_probe(k)
-    ev_ms, _ = time_steps(wl.launch_probe, k_steps, sync, lambda: None, new_event)
+    ev_ms, _ = time_steps(wl.launch_probe, k_steps, sync, lambda: None, new_event, gate)
     us = ev_ms * 1e3 / k_steps
     gbps = wl.bytes_per_step / (us * 1e-6) / 1e9
     return {"GBps": round(gbps, 1), "frac": round(gbps / HBM_PEAK_GBPS, 4), "us_per_launch": round(us, 3),
@@ -512,11 +526,13 @@ def run_rank(args, rank: int, world: int, local: int):
     new_event = lambda: _StreamEvent(stream)  # noqa: E731
     sync = lambda: torch.cuda.synchronize(dev)  # noqa: E731
 
+    gate = None if args.no_gate else (lambda: _gpu_gate(stream))
+
     wl = ReduceWorkload(n, p, dtype, w32, mode, B, dev, 1234 + rank, stream)
     for k in range(args.warmup):
         wl.launch(k)
     K = args.steps
-    ev_ms, wall_ms = time_steps(wl.launch, K, sync, barrier, new_event)
+    ev_ms, wall_ms = time_steps(wl.launch, K, sync, barrier, new_event, gate)
 
     stats = torch.tensor([ev_ms, wall_ms, float(wl.bytes_per_step) * K], dtype=torch.float64, device=cdev)
     per_rank_us = torch.tensor([ev_ms / K * 1e3], dtype=torch.float64, device=cdev)
@@ -547,7 +563,7 @@ def run_rank(args, rank: int, world: int, local: int):
             full = ReduceWorkload(n, p_cfg, dtype, w32, mode, B, dev, 99, stream)
             for k in range(args.warmup):
                 full.launch(k)
-            t1_ms, _ = time_steps(full.launch, K, sync, lambda: None, new_event)
+            t1_ms, _ = time_steps(full.launch, K, sync, lambda: None, new_event, gate)
             single = {"ms_per_step": round(t1_ms / K, 6),
                       "speedup": round((t1_ms / K) / (max_ev / K), 3),
                       "note": f"T1 = the whole {args.config} aggregate on rank 0's GPU alone, {K} launches, "
@@ -560,7 +576,7 @@ def run_rank(args, rank: int, world: int, local: int):
         achieved = wl.bytes_per_step / (ev_ms / K * 1e-3) / 1e9
         traffic, traffic_src = (pmc_traffic(args.config, args.mode, split) if B == 1
                                 else (None, "no committed PMC summary for batched launches"))
-        probe = pattern_ceiling(wl, K, sync, new_event, achieved) if B == 1 else None
+        probe = pattern_ceiling(wl, K, sync, new_event, achieved, gate) if B == 1 else None
         floor = launch_floor(wl, n, dtype, w32, mode, dev, K, sync, new_event, ev_ms / K * 1e3) \
             if B == 1 else None
         # opt-in: its concurrent launches share the reduce's kernel name, so
@@ -598,6 +614,9 @@ def run_rank(args, rank: int, world: int, local: int):
                        "bytes_per_step_rank0": wl.bytes_per_step},
             "timing": {"value_from": "HIP events around the K launches on each rank's launch stream; "
                                      "value = all ranks' bytes / max over ranks; barriers outside the window",
+                       "gate": None if args.no_gate else
+                       f"torch.cuda._sleep({GATE_CYCLES}) on the launch stream after the sync, before the start "
+                       "event (the window holds the K steps' GPU time, not the host's enqueue of launch 0)",
                        "kernel_avg_us_per_rank": rank_us,
                        "wall_ms_per_step_max": round(max_wall / K, 6)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
@@ -635,6 +654,16 @@ def run_rank(args, rank: int, world: int, local: int):
     if world > 1:
         dist.destroy_process_group()
     return 0
+
+
+GATE_CYCLES = 200_000  # GPU clock cycles (~80-100 us): covers the host's enqueue of the start event + launch 0
+
+
+def _gpu_gate(stream):
+    """The timing gate (time_steps): torch's spin kernel on the launch
+    stream, bounded by its cycle count; it touches no data."""
+    with torch.cuda.stream(stream):
+        torch.cuda._sleep(GATE_CYCLES)
 
 
 class _StreamEvent:
@@ -692,37 +721,63 @@ SHARDED_TIMEOUT_S = 90.0
 
 
 def _time_sharded(wl, n, p_cfg, w32, mode, dtype, dev, cdev, stream, barrier, reps: int = 20):
-    """The C ABI's dlsim_wreduce_sharded end to end on the group's own RCCL
-    communicator: this rank's reduce into the full buffer + grouped in-place
-    ncclBroadcast of every rank's slice (a variable-size all-gather), HIP
-    events on the launch stream, max over ranks."""
+    """The C ABI's sharded aggregate end to end on the group's own RCCL
+    communicator, four ways, HIP events on the launch stream, max over ranks:
+    dlsim_wreduce_sharded (agreement all-reduce + host wait every call) and a
+    dlsim_sharded_plan (agreed once), each with the grouped in-place
+    ncclBroadcast gather and with the padded ncclAllGather + unpad kernel."""
     from dasklearn_amd import _native
-    out = {}
-    try:
-        pg = dist.distributed_c10d._get_default_group()
-        comm = int(pg._get_backend(dev)._comm_ptr())
-        slices = [wl.plans[0]._keep[0][i] for i in range(n)]
-        fullout = torch.empty(p_cfg, dtype=TORCH_DTYPE[dtype], device=dev)
-        for _ in range(3):
-            _native.wreduce_sharded(slices, w32, fullout, comm, True, mode, stream)
-        torch.cuda.synchronize(dev)
-        barrier()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        for _ in range(reps):
-            _native.wreduce_sharded(slices, w32, fullout, comm, True, mode, stream)
-        e1.record(stream)
-        torch.cuda.synchronize(dev)
-        ms = e0.elapsed_time(e1) / reps
-        out["sharded_note"] = ("dlsim_wreduce_sharded(gather=1) on the group's RCCL communicator: local reduce "
-                               "+ grouped in-place ncclBroadcast, HIP events on the launch stream, max over ranks")
-    except Exception as e:  # report, do not fail the bench line
-        ms = -1.0
-        out["dlsim_wreduce_sharded_error"] = f"{type(e).__name__}: {e}"[:300]
-    t = torch.tensor([ms], dtype=torch.float64, device=cdev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    if ms >= 0:
-        out["dlsim_wreduce_sharded_gather_ms"] = round(float(t[0]), 4)
+    out = {"sharded_note": "this rank's reduce + the gather on the group's RCCL communicator; agreed = "
+                           "dlsim_wreduce_sharded (agreement all-reduce and host wait per call), plan = "
+                           "dlsim_sharded_plan_run (agreed once); HIP events on the launch stream, max over ranks"}
+    pg = dist.distributed_c10d._get_default_group()
+    comm = int(pg._get_backend(dev)._comm_ptr())
+    slices = [wl.plans[0]._keep[0][i] for i in range(n)]
+    fullout = torch.empty(p_cfg, dtype=TORCH_DTYPE[dtype], device=dev)
+    plans = {}
+    for gather in ("bcast", "allgather"):
+        try:  # collective: the agreement makes a failure every rank's
+            plans[gather] = _native.ShardedPlan(comm, p_cfg, n, TORCH_DTYPE[dtype], gather, device=dev,
+                                                stream=stream)
+        except Exception as e:  # noqa: BLE001 - reported in the line
+            plans[gather] = None
+            out[f"plan_{gather}_create_error"] = f"{type(e).__name__}: {e}"[:300]
+
+    def run_plan(gather):
+        if plans[gather] is None:
+            raise RuntimeError("no plan")
+        plans[gather].run(slices, w32, fullout, mode, stream)
+    runs = {
+        "dlsim_wreduce_sharded_gather_ms": lambda: _native.wreduce_sharded(slices, w32, fullout, comm, "bcast",
+                                                                         mode, stream),
+        "dlsim_wreduce_sharded_allgather_ms": lambda: _native.wreduce_sharded(slices, w32, fullout, comm,
+                                                                            "allgather", mode, stream),
+        "plan_bcast_ms": lambda: run_plan("bcast"),
+        "plan_allgather_ms": lambda: run_plan("allgather"),
+    }
+    for key, fn in runs.items():
+        try:
+            for _ in range(3):
+                fn()
+            torch.cuda.synchronize(dev)
+            barrier()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(reps):
+                fn()
+            e1.record(stream)
+            torch.cuda.synchronize(dev)
+            ms = e0.elapsed_time(e1) / reps
+        except Exception as e:  # report, do not fail the bench line
+            ms = -1.0
+            out[key.replace("_ms", "_error")] = f"{type(e).__name__}: {e}"[:300]
+        t = torch.tensor([ms], dtype=torch.float64, device=cdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        if ms >= 0:
+            out[key] = round(float(t[0]), 4)
+    for pl in plans.values():
+        if pl is not None:
+            pl.close()
     return out
 
 

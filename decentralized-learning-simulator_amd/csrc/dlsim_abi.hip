@@ -1,8 +1,8 @@
 // dlsim_abi.hip — the C ABI of include/dlsim.h over the gfx950 kernels of
 // wreduce_kernels.hpp. Host-side dispatch only: argument checks, choice of
 // vector vs scalar kernel, launch shape, kernarg or device-table fan-in, batching
-// and its hazard checks, host staging pipelines.
-#include <dlfcn.h>
+// and its hazard checks, host staging pipelines. The RCCL entry points are in
+// sharded_abi.hip.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -13,43 +13,13 @@
 #include <mutex>
 #include <string>
 #include <thread>
-#include <type_traits>
-#include <type_traits>
 #include <vector>
 
-#include "dlsim.h"
+#include "abi_common.hpp"
 #include "dispatch.hpp"
 #include "host_pack.hpp"
 
 namespace dlsim_host __attribute__((visibility("hidden"))) {
-
-thread_local std::string g_err;
-
-int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
-int fail(int code, const char* fmt, ...) {
-  char buf[512];
-  va_list ap;
-  va_start(ap, fmt);
-  vsnprintf(buf, sizeof(buf), fmt, ap);
-  va_end(ap);
-  g_err = buf;
-  return code;
-}
-
-int hip_fail(hipError_t e, const char* what) {
-  return fail(DLSIM_E_HIP - static_cast<int>(e), "%s: %s", what, hipGetErrorString(e));
-}
-
-size_t elem_bytes(int dtype) { return dtype == DLSIM_F64 ? 8 : dtype == DLSIM_F32 ? 4 : 2; }
-
-// dtypes of the float-weight entry points (fp64 buffers take dlsim_wreduce_f64)
-bool known_dtype(int dtype) { return dtype == DLSIM_F32 || dtype == DLSIM_BF16 || dtype == DLSIM_F16; }
-
-int dtype_fail(int dtype) {
-  if (dtype == DLSIM_F64)
-    return fail(DLSIM_E_DTYPE, "DLSIM_F64 buffers go through dlsim_wreduce_f64 (double weights)");
-  return fail(DLSIM_E_DTYPE, "unsupported dtype %d", dtype);
-}
 
 // f(Op{}) with the element policy of (dtype, mode). Callers check both first.
 template <class F>
@@ -75,56 +45,9 @@ int with_chunk_policy(int dtype, F&& f) {
   return with_mean_policy(dtype, f);
 }
 
-int check_args(const void* const* in, int n, const void* w, const void* out, size_t nelem,
-               int dtype, int mode, bool need_w = true, bool f64_ok = false) {
-  if (!known_dtype(dtype) && !(f64_ok && dtype == DLSIM_F64)) return dtype_fail(dtype);
-  if (mode != DLSIM_EXACT && mode != DLSIM_FAST) return fail(DLSIM_E_MODE, "unsupported mode %d", mode);
-  if (n < 1) return fail(DLSIM_E_ARG, "n must be >= 1 (got %d)", n);
-  if (!in || (need_w && !w)) return fail(DLSIM_E_ARG, "null inputs or weights array");
-  if (nelem == 0) return DLSIM_OK;
-  if (!out) return fail(DLSIM_E_ARG, "null output pointer");
-  const size_t bytes = nelem * elem_bytes(dtype);
-  const uintptr_t o0 = reinterpret_cast<uintptr_t>(out), o1 = o0 + bytes;
-  for (int i = 0; i < n; ++i) {
-    if (!in[i]) return fail(DLSIM_E_ARG, "null input pointer at index %d", i);
-    const uintptr_t a0 = reinterpret_cast<uintptr_t>(in[i]), a1 = a0 + bytes;
-    // Exact aliasing (out == in[i]) is safe for every i: the reduce is one
-    // pass, and a lane reads all n terms of an element before writing it.
-    // Partial overlap is not.
-    if (a0 != o0 && a0 < o1 && o0 < a1)
-      return fail(DLSIM_E_ARG, "output partially overlaps input %d", i);
-  }
-  return DLSIM_OK;
-}
-
 int dispatch(const void* const* in, int n, const float* w, void* out, size_t nelem, int dtype,
              int mode, hipStream_t st) {
   return with_policy(dtype, mode, [&](auto op) { return run<decltype(op)>(in, n, w, out, nelem, st); });
-}
-
-// ---- RCCL, bound at run time --------------------------------------------------
-// The sharded entry point drives collectives on a caller's RCCL communicator.
-// The library does not link RCCL: dlsim_rccl_bind() dlopens the copy the
-// caller already uses (for a PyTorch process, the librccl.so next to
-// libtorch_hip.so, whose communicator ProcessGroupNCCL._comm_ptr() returns),
-// so one RCCL instance owns the communicator and its calls.
-typedef int rccl_result_t;  // ncclResult_t
-struct Rccl {
-  void* lib = nullptr;
-  rccl_result_t (*bcast)(const void*, void*, size_t, int, int, void*, hipStream_t) = nullptr;
-  rccl_result_t (*allreduce)(const void*, void*, size_t, int, int, void*, hipStream_t) = nullptr;
-  rccl_result_t (*group_start)() = nullptr;
-  rccl_result_t (*group_end)() = nullptr;
-  rccl_result_t (*count)(void*, int*) = nullptr;
-  rccl_result_t (*user_rank)(void*, int*) = nullptr;
-  const char* (*err)(rccl_result_t) = nullptr;
-};
-Rccl g_rccl;
-constexpr int kRcclFloat16 = 6, kRcclFloat32 = 7, kRcclFloat64 = 8, kRcclBfloat16 = 9;  // ncclDataType_t (rccl.h)
-constexpr int kRcclInt64 = 4, kRcclMax = 2;                           // ncclInt64, ncclMax
-
-int rccl_fail(rccl_result_t r, const char* what) {
-  return fail(DLSIM_E_RCCL, "%s: %s (ncclResult %d)", what, g_rccl.err ? g_rccl.err(r) : "?", r);
 }
 
 // ---- host staging pipelines (dlsim_host_wreduce, dlsim_host_chunk_mean) -------
@@ -185,6 +108,38 @@ constexpr size_t kSmallHostJobBytes = size_t{4} << 20;
 size_t staged_row_elems(size_t n, size_t esz) {
   const size_t al = 256 / esz;
   return (n + al - 1) / al * al;
+}
+
+// The results of a small host chunk job in ONE D2H, when that is exact: the
+// non-empty outputs, sorted by device address, lie back to back (each starts
+// where the previous one ends) and every host output sits at the same offset
+// from the first as its device output. Returns DLSIM_OK after queueing the
+// one copy, 1 when the layout does not qualify (the caller copies per task),
+// or a HIP error code.
+int d2h_one_span(int b, void* const* d_outs, void* const* h_outs, const size_t* n_elems, size_t esz,
+                 hipStream_t st) {
+  struct Part {
+    uintptr_t d, h;
+    size_t bytes;
+  };
+  std::vector<Part> parts;
+  for (int t = 0; t < b; ++t) {
+    if (n_elems[t] == 0) continue;
+    if (!h_outs[t]) return 1;
+    parts.push_back({reinterpret_cast<uintptr_t>(d_outs[t]), reinterpret_cast<uintptr_t>(h_outs[t]),
+                     n_elems[t] * esz});
+  }
+  if (parts.empty()) return DLSIM_OK;
+  std::sort(parts.begin(), parts.end(), [](const Part& x, const Part& y) { return x.d < y.d; });
+  const uintptr_t d0 = parts[0].d, h0 = parts[0].h;
+  size_t span = 0;
+  for (const Part& q : parts) {
+    if (q.d - d0 != span || q.h - h0 != span) return 1;  // a gap, an overlap or a different host offset
+    span += q.bytes;
+  }
+  const hipError_t e = hipMemcpyAsync(reinterpret_cast<void*>(h0), reinterpret_cast<const void*>(d0), span,
+                                      hipMemcpyDeviceToHost, st);
+  return e == hipSuccess ? DLSIM_OK : hip_fail(e, "result D2H");
 }
 
 }  // namespace dlsim_host
@@ -365,169 +320,6 @@ int dlsim_chunk_mean_batched(int b, const int* fan_in, const void* const* d_inpu
   });
 }
 
-int dlsim_rccl_bind(const char* librccl_path) {
-  g_err.clear();
-  if (!librccl_path || !*librccl_path) return fail(DLSIM_E_ARG, "null/empty librccl path");
-  void* h = dlopen(librccl_path, RTLD_NOW | RTLD_LOCAL);
-  if (!h) return fail(DLSIM_E_RCCL, "dlopen(%s): %s", librccl_path, dlerror());
-  Rccl r;
-  r.lib = h;
-  r.bcast = reinterpret_cast<decltype(r.bcast)>(dlsym(h, "ncclBroadcast"));
-  r.allreduce = reinterpret_cast<decltype(r.allreduce)>(dlsym(h, "ncclAllReduce"));
-  r.group_start = reinterpret_cast<decltype(r.group_start)>(dlsym(h, "ncclGroupStart"));
-  r.group_end = reinterpret_cast<decltype(r.group_end)>(dlsym(h, "ncclGroupEnd"));
-  r.count = reinterpret_cast<decltype(r.count)>(dlsym(h, "ncclCommCount"));
-  r.user_rank = reinterpret_cast<decltype(r.user_rank)>(dlsym(h, "ncclCommUserRank"));
-  r.err = reinterpret_cast<decltype(r.err)>(dlsym(h, "ncclGetErrorString"));
-  if (!r.bcast || !r.allreduce || !r.group_start || !r.group_end || !r.count || !r.user_rank || !r.err)
-    return fail(DLSIM_E_RCCL, "%s lacks an RCCL symbol", librccl_path);
-  g_rccl = r;
-  return DLSIM_OK;
-}
-
-// The agreement step of dlsim_wreduce_sharded: one
-// int64 MAX all-reduce of [a failure slot per rank | n_elems, -n_elems,
-// dtype, -dtype, gather, -gather] on the caller's stream, read back by the
-// host. Every rank learns which ranks failed their local checks (or their
-// local reduce launch) and whether all ranks agree on the arguments that
-// shape the broadcast group, so either every rank enters the group or none
-// does. Sets *failed to the failing ranks and *mismatch to the disagreement.
-int sharded_agree(void* comm, int world, int rank, bool local_fail, size_t n_elems, int dtype, int gather,
-                  hipStream_t st, std::vector<int>* failed, bool* mismatch) {
-  const int nw = world + 6;
-  std::vector<int64_t> w(static_cast<size_t>(nw), 0);
-  w[rank] = local_fail ? 1 : 0;
-  const int64_t args[3] = {static_cast<int64_t>(n_elems), dtype, gather ? 1 : 0};
-  for (int k = 0; k < 3; ++k) {
-    w[world + 2 * k] = args[k];
-    w[world + 2 * k + 1] = -args[k];
-  }
-  void* d = nullptr;
-  const size_t bytes = sizeof(int64_t) * static_cast<size_t>(nw);
-  hipError_t e = hipMallocAsync(&d, bytes, st);
-  if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(agreement)");
-  int rc = DLSIM_OK;
-  e = hipMemcpyAsync(d, w.data(), bytes, hipMemcpyHostToDevice, st);
-  if (e != hipSuccess) rc = hip_fail(e, "hipMemcpyAsync(agreement H2D)");
-  if (rc == DLSIM_OK) {
-    const rccl_result_t rr = g_rccl.allreduce(d, d, static_cast<size_t>(nw), kRcclInt64, kRcclMax, comm, st);
-    if (rr != 0) rc = rccl_fail(rr, "ncclAllReduce(agreement)");
-  }
-  if (rc == DLSIM_OK) {
-    e = hipMemcpyAsync(w.data(), d, bytes, hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
-    if (e != hipSuccess) rc = hip_fail(e, "agreement D2H");
-  }
-  (void)hipFreeAsync(d, st);
-  if (rc != DLSIM_OK) return rc;
-  failed->clear();
-  for (int r = 0; r < world; ++r)
-    if (w[r] != 0) failed->push_back(r);
-  *mismatch = false;
-  for (int k = 0; k < 3; ++k) *mismatch |= w[world + 2 * k] != -w[world + 2 * k + 1];
-  return DLSIM_OK;
-}
-
-// The body of dlsim_wreduce_sharded / _f64 (float or double weights): C++
-// linkage, internal to the library.
-extern "C++" {
-namespace {
-template <class W>
-int wreduce_sharded(const void* const* d_slices, size_t slice_elems, int n, const W* h_weights, void* d_out,
-                    size_t n_elems, int dtype, int mode, void* rccl_comm, int gather, void* stream) {
-  g_err.clear();
-  if (!g_rccl.lib) return fail(DLSIM_E_RCCL, "RCCL not bound (call dlsim_rccl_bind first)");
-  if (!rccl_comm) return fail(DLSIM_E_ARG, "null RCCL communicator");
-  int world = 0, rank = 0;
-  rccl_result_t rr = g_rccl.count(rccl_comm, &world);
-  if (rr != 0) return rccl_fail(rr, "ncclCommCount");
-  rr = g_rccl.user_rank(rccl_comm, &rank);
-  if (rr != 0) return rccl_fail(rr, "ncclCommUserRank");
-  hipStream_t st = static_cast<hipStream_t>(stream);
-  // Rank-local checks and the local reduce: a failure here is not returned
-  // before the other ranks have heard of it (sharded_agree), so no rank is
-  // left waiting inside the broadcast group.
-  size_t b = 0, e = 0;
-  int rc = DLSIM_OK;
-  if (n_elems > 0 && !d_out) rc = fail(DLSIM_E_ARG, "null output pointer");
-  if (rc == DLSIM_OK) rc = dlsim_shard_range(n_elems, world, rank, 64, &b, &e);
-  if (rc == DLSIM_OK && slice_elems != e - b)
-    rc = fail(DLSIM_E_ARG, "rank %d of %d: slices have %zu elements, its shard [%zu, %zu) has %zu", rank, world,
-              slice_elems, b, e, e - b);
-  constexpr bool kF64 = std::is_same<W, double>::value;
-  const bool dtype_ok = kF64 ? dtype == DLSIM_F64 : known_dtype(dtype);
-  const size_t esz = dtype_ok ? elem_bytes(dtype) : 0;
-  char* out = static_cast<char*>(d_out);
-  if (rc == DLSIM_OK) {
-    // this rank's slice of every model -> this rank's slice of the output
-    if constexpr (kF64) {
-      if (e > b) rc = dlsim_wreduce_f64(d_slices, n, h_weights, out + b * esz, e - b, mode, stream);
-      else rc = check_args(d_slices, n, h_weights, nullptr, 0, dtype, mode, true, true);
-    } else {
-      if (e > b) rc = dlsim_wreduce(d_slices, n, h_weights, out + b * esz, e - b, dtype, mode, stream);
-      else rc = check_args(d_slices, n, h_weights, nullptr, 0, dtype, mode);
-    }
-  }
-  if (world > 1) {
-    const std::string local_err = g_err;
-    std::vector<int> failed;
-    bool mismatch = false;
-    const int arc = sharded_agree(rccl_comm, world, rank, rc != DLSIM_OK, n_elems, dtype, gather, st, &failed,
-                                  &mismatch);
-    if (arc != DLSIM_OK) return arc;
-    if (rc != DLSIM_OK) {
-      g_err = local_err;
-      return rc;
-    }
-    if (!failed.empty()) {
-      std::string who;
-      for (int r : failed) who += (who.empty() ? "" : ",") + std::to_string(r);
-      return fail(DLSIM_E_PEER, "rank(s) %s of %d failed their checks; no rank entered the broadcast group",
-                  who.c_str(), world);
-    }
-    if (mismatch)
-      return fail(DLSIM_E_ARG, "ranks disagree on n_elems, dtype or gather; no rank entered the broadcast group");
-  } else if (rc != DLSIM_OK) {
-    return rc;
-  }
-  if (!gather || world == 1 || n_elems == 0) return DLSIM_OK;
-  // variable-size all-gather: every rank broadcasts its slice in place
-  const int dt = dtype == DLSIM_BF16 ? kRcclBfloat16
-                 : dtype == DLSIM_F16  ? kRcclFloat16
-                 : dtype == DLSIM_F64  ? kRcclFloat64
-                                       : kRcclFloat32;
-  rr = g_rccl.group_start();
-  if (rr != 0) return rccl_fail(rr, "ncclGroupStart");
-  for (int r = 0; r < world; ++r) {
-    size_t rb = 0, re = 0;
-    dlsim_shard_range(n_elems, world, r, 64, &rb, &re);
-    if (re == rb) continue;
-    rr = g_rccl.bcast(out + rb * esz, out + rb * esz, re - rb, dt, r, rccl_comm, st);
-    if (rr != 0) {
-      g_rccl.group_end();
-      return rccl_fail(rr, "ncclBroadcast");
-    }
-  }
-  rr = g_rccl.group_end();
-  if (rr != 0) return rccl_fail(rr, "ncclGroupEnd");
-  return DLSIM_OK;
-}
-}  // namespace
-}  // extern "C++"
-
-int dlsim_wreduce_sharded(const void* const* d_slices, size_t slice_elems, int n, const float* h_weights,
-                          void* d_out, size_t n_elems, int dtype, int mode, void* rccl_comm, int gather,
-                          void* stream) {
-  return wreduce_sharded(d_slices, slice_elems, n, h_weights, d_out, n_elems, dtype, mode, rccl_comm, gather,
-                         stream);
-}
-
-int dlsim_wreduce_sharded_f64(const void* const* d_slices, size_t slice_elems, int n, const double* h_weights,
-                              void* d_out, size_t n_elems, int mode, void* rccl_comm, int gather, void* stream) {
-  return wreduce_sharded(d_slices, slice_elems, n, h_weights, d_out, n_elems, DLSIM_F64, mode, rccl_comm, gather,
-                         stream);
-}
-
 int dlsim_host_wreduce(int n, int t, const void* const* h_srcs, const size_t* numels,
                        const float* h_weights, void* h_staging, void* d_rows, size_t row_stride,
                        void* d_out, void* h_out, int dtype, int mode, size_t chunk_elems, int threads,
@@ -689,9 +481,8 @@ int dlsim_host_chunk_mean(int b, const int* fan_in, const void* const* h_inputs,
     // Small job (GNLeNet's Conflux reconstruct: ~1.4 MB):
     // a DMA costs ~15 us of copy-engine time whatever its size, so pack every
     // row first, then ONE H2D of the staging, ONE batched launch of every
-    // task's mean and, when the outputs sit at the same offsets on both
-    // sides (the ChunkManager's back-to-back layout), ONE D2H; all on
-    // `stream`.
+    // task's mean and, when the outputs lie back to back at the same offsets
+    // on both sides (the ChunkManager's layout), ONE D2H; all on `stream`.
     pack_and_dispatch(job, threads, need * esz, [](size_t, size_t) {});
     hipError_t e = hipMemcpyAsync(ds, hs, need * esz, hipMemcpyHostToDevice, st);
     if (e != hipSuccess) return hip_fail(e, "staging H2D");
@@ -701,23 +492,12 @@ int dlsim_host_chunk_mean(int b, const int* fan_in, const void* const* h_inputs,
       return run_chunk_mean<decltype(op)>(b, fan_in, ins_all.data(), d_outs, n_elems, cpu_threads, st);
     });
     if (rc != DLSIM_OK || !h_outs) return rc;
-    // one D2H if every task's output keeps its offset from task 0's on both
-    // sides; else one per task
-    const char* d0 = static_cast<const char*>(d_outs[0]);
-    char* h0 = static_cast<char*>(h_outs[0]);
-    bool one = h0 != nullptr;
-    size_t span = 0;
-    for (int t = 0; t < b && one; ++t) {
-      if (n_elems[t] == 0) continue;
-      const ptrdiff_t dd = static_cast<const char*>(d_outs[t]) - d0;
-      one = h_outs[t] && dd >= 0 && static_cast<char*>(h_outs[t]) - h0 == dd;
-      span = std::max(span, static_cast<size_t>(dd) + n_elems[t] * esz);
-    }
-    if (one) {
-      if (span > 0 && (e = hipMemcpyAsync(h0, d0, span, hipMemcpyDeviceToHost, st)) != hipSuccess)
-        return hip_fail(e, "result D2H");
-      return DLSIM_OK;
-    }
+    // One D2H when the non-empty outputs tile one span back to back (sorted
+    // by offset, each starting where the previous one ends) at the same
+    // offsets on both sides; else one per task. Equal offsets alone are not
+    // enough: host bytes between outputs must not be overwritten, and the
+    // copy must not read past the device outputs.
+    if (const int rc1 = d2h_one_span(b, d_outs, h_outs, n_elems, esz, st); rc1 != 1) return rc1;
     for (int t = 0; t < b; ++t) {
       if (n_elems[t] == 0 || !h_outs[t]) continue;
       e = hipMemcpyAsync(h_outs[t], d_outs[t], n_elems[t] * esz, hipMemcpyDeviceToHost, st);
@@ -822,6 +602,6 @@ int dlsim_probe_pattern(const void* const* d_inputs, int n, void* d_out, size_t 
 
 const char* dlsim_last_error(void) { return g_err.c_str(); }
 
-int dlsim_version(void) { return (1 << 16) | 0; }
+int dlsim_version(void) { return (1 << 16) | 1; }
 
 }  // extern "C"

@@ -25,6 +25,10 @@ MAX_FUSED_INPUTS = 128
 DLSIM_E_ARG = -1
 DLSIM_E_RCCL = -4
 DLSIM_E_PEER = -5  # another rank failed (dlsim_wreduce_sharded's agreement step)
+DLSIM_E_DISAGREE = -6  # the ranks passed different n_elems / fan-in / dtype / gather
+DLSIM_GATHER_NONE = 0
+DLSIM_GATHER_BCAST = 1
+DLSIM_GATHER_ALLGATHER = 2
 
 # Every symbol include/dlsim.h declares (tests/test_abi.py checks the header
 # against this list and the library's exports).
@@ -43,6 +47,10 @@ EXPORTS = (
     "dlsim_rccl_bind",
     "dlsim_wreduce_sharded",
     "dlsim_wreduce_sharded_f64",
+    "dlsim_sharded_plan_create",
+    "dlsim_sharded_plan_run",
+    "dlsim_sharded_plan_run_f64",
+    "dlsim_sharded_plan_destroy",
     "dlsim_host_wreduce",
     "dlsim_host_chunk_mean",
     "dlsim_host_pack",
@@ -118,6 +126,15 @@ def load() -> ctypes.CDLL:
         lib.dlsim_wreduce_sharded_f64.argtypes = [ctypes.POINTER(vp), sz, i, ctypes.POINTER(ctypes.c_double), vp,
                                                   sz, i, vp, i, vp]
         lib.dlsim_wreduce_sharded_f64.restype = i
+        lib.dlsim_sharded_plan_create.argtypes = [vp, sz, i, i, i, vp, ctypes.POINTER(vp)]
+        lib.dlsim_sharded_plan_create.restype = i
+        lib.dlsim_sharded_plan_run.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_float), vp, i, vp]
+        lib.dlsim_sharded_plan_run.restype = i
+        lib.dlsim_sharded_plan_run_f64.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_double), vp, i,
+                                                   vp]
+        lib.dlsim_sharded_plan_run_f64.restype = i
+        lib.dlsim_sharded_plan_destroy.argtypes = [vp]
+        lib.dlsim_sharded_plan_destroy.restype = i
         lib.dlsim_host_wreduce.argtypes = [i, i, ctypes.POINTER(vp), ctypes.POINTER(sz),
                                            ctypes.POINTER(ctypes.c_float), vp, vp, sz, vp, vp, i, i, sz, i,
                                            vp, vp, vp]
@@ -513,16 +530,21 @@ def rccl_bind(path: Optional[str] = None) -> str:
     return path
 
 
-def wreduce_sharded(slices, weights_f32, out, comm_ptr: int, gather: bool = True,
-                    mode: int = DLSIM_EXACT, stream=None):
-    """dlsim_wreduce_sharded: `slices[i]` is this rank's slice of model i,
-    `out` the full-size output; `comm_ptr` an RCCL communicator (e.g.
-    ProcessGroupNCCL._comm_ptr()). fp64 tensors go to
-    dlsim_wreduce_sharded_f64 and take exact double weights (pass
-    weights_for_dtype(weights, torch.float64))."""
-    lib = load()
-    if _RCCL_BOUND is None:  # the caller may have bound another RCCL (tests bind a stub)
-        rccl_bind()
+def gather_code(gather) -> int:
+    """enum dlsim_gather of a `gather` argument: False/True (no gather / the
+    grouped broadcasts), an enum value, or "none" / "bcast" / "allgather"."""
+    if isinstance(gather, str):
+        codes = {"none": DLSIM_GATHER_NONE, "bcast": DLSIM_GATHER_BCAST, "allgather": DLSIM_GATHER_ALLGATHER}
+        if gather not in codes:
+            raise ValueError(f"gather must be one of {sorted(codes)}, got {gather!r}")
+        return codes[gather]
+    g = int(gather)
+    if g not in (DLSIM_GATHER_NONE, DLSIM_GATHER_BCAST, DLSIM_GATHER_ALLGATHER):
+        raise ValueError(f"gather must be 0, 1 or 2 (enum dlsim_gather), got {gather!r}")
+    return g
+
+
+def _check_slices(slices, out):
     n = len(slices)
     if n < 1:
         raise IndexError("list index out of range")
@@ -533,41 +555,118 @@ def wreduce_sharded(slices, weights_f32, out, comm_ptr: int, gather: bool = True
                              "and device")
     if not out.is_cuda or not out.is_contiguous():
         raise ValueError("out must be a contiguous device tensor")
-    import torch
-    ptrs = (ctypes.c_void_p * n)(*[x.data_ptr() for x in slices])
-    if out.dtype == torch.float64:
-        wd = np.ascontiguousarray(weights_f32, dtype=np.float64)
-        if wd.size != n:
-            raise AssertionError("weights/models length mismatch")
-        _check("dlsim_wreduce_sharded_f64",
-               lib.dlsim_wreduce_sharded_f64(ptrs, slices[0].numel(), n,
-                                             wd.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), out.data_ptr(),
-                                             out.numel(), mode, ctypes.c_void_p(comm_ptr), 1 if gather else 0,
-                                             _stream_handle(out.device, stream)))
-        return out
-    w = np.ascontiguousarray(weights_f32, dtype=np.float32)
+    return (ctypes.c_void_p * n)(*[x.data_ptr() for x in slices])
+
+
+def _weights_arg(weights, n, f64):
+    w = np.ascontiguousarray(weights, dtype=np.float64 if f64 else np.float32)
     if w.size != n:
         raise AssertionError("weights/models length mismatch")
+    return w, w.ctypes.data_as(ctypes.POINTER(ctypes.c_double if f64 else ctypes.c_float))
+
+
+def wreduce_sharded(slices, weights_f32, out, comm_ptr: int, gather=True,
+                    mode: int = DLSIM_EXACT, stream=None):
+    """dlsim_wreduce_sharded: `slices[i]` is this rank's slice of model i,
+    `out` the full-size output; `comm_ptr` an RCCL communicator (e.g.
+    ProcessGroupNCCL._comm_ptr()); `gather` as gather_code. fp64 tensors go to
+    dlsim_wreduce_sharded_f64 and take exact double weights (pass
+    weights_for_dtype(weights, torch.float64))."""
+    import torch
+    lib = load()
+    if _RCCL_BOUND is None:  # the caller may have bound another RCCL (tests bind a stub)
+        rccl_bind()
+    g = gather_code(gather)
+    ptrs = _check_slices(slices, out)
+    n = len(slices)
+    f64 = out.dtype == torch.float64
+    w, wp = _weights_arg(weights_f32, n, f64)
+    st = _stream_handle(out.device, stream)
+    if f64:
+        _check("dlsim_wreduce_sharded_f64",
+               lib.dlsim_wreduce_sharded_f64(ptrs, slices[0].numel(), n, wp, out.data_ptr(), out.numel(), mode,
+                                             ctypes.c_void_p(comm_ptr), g, st))
+        return out
     _check("dlsim_wreduce_sharded",
-           lib.dlsim_wreduce_sharded(ptrs, slices[0].numel(), n, w.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
-                                     out.data_ptr(),
-                                     out.numel(), dtype_code(out.dtype), mode, ctypes.c_void_p(comm_ptr),
-                                     1 if gather else 0, _stream_handle(out.device, stream)))
+           lib.dlsim_wreduce_sharded(ptrs, slices[0].numel(), n, wp, out.data_ptr(), out.numel(),
+                                     dtype_code(out.dtype), mode, ctypes.c_void_p(comm_ptr), g, st))
     return out
 
 
-def wreduce_sharded_failed(comm_ptr: int, n_elems: int, gather: bool, device, stream=None) -> None:
+def wreduce_sharded_failed(comm_ptr: int, n_elems: int, gather, device, stream=None) -> None:
     """Join dlsim_wreduce_sharded's agreement step as a rank whose arguments
     already failed the caller's own checks (no slices, no output): the library
-    tells every other rank, so none enters the broadcast group, and this call
-    returns the library's own argument error (raised as DlsimError)."""
+    tells every other rank, so none enters the gather, and this call returns
+    the library's own argument error (raised as DlsimError)."""
     lib = load()
     if _RCCL_BOUND is None:
         rccl_bind()
     _check("dlsim_wreduce_sharded",
            lib.dlsim_wreduce_sharded(None, ctypes.c_size_t(-1 & 0xFFFFFFFFFFFFFFFF), 0, None, None, n_elems,
-                                     DLSIM_F32, DLSIM_EXACT, ctypes.c_void_p(comm_ptr), 1 if gather else 0,
+                                     DLSIM_F32, DLSIM_EXACT, ctypes.c_void_p(comm_ptr), gather_code(gather),
                                      _stream_handle(device, stream)))
+
+
+class ShardedPlan:
+    """dlsim_sharded_plan: the sharded aggregate of one shape (n_elems, n
+    models, dtype, gather) on one RCCL communicator, agreed ONCE by every
+    rank at construction (a collective call), then run any number of times
+    with no agreement and no host wait (`run`). A rank whose run fails its
+    local checks still enters the gather and raises afterwards; its peers are
+    not told (include/dlsim.h)."""
+
+    def __init__(self, comm_ptr: int, n_elems: int, n: int, dtype, gather=True, device=None, stream=None):
+        import torch
+        lib = load()
+        if _RCCL_BOUND is None:
+            rccl_bind()
+        self._lib = lib
+        self.n_elems, self.n, self.dtype = int(n_elems), int(n), dtype
+        self.gather = gather_code(gather)
+        self.f64 = dtype == torch.float64
+        code = dtype_code(dtype, single_task=True)
+        h = ctypes.c_void_p()
+        _check("dlsim_sharded_plan_create",
+               lib.dlsim_sharded_plan_create(ctypes.c_void_p(comm_ptr), self.n_elems, self.n, code, self.gather,
+                                             _stream_handle(device, stream), ctypes.byref(h)))
+        self._h = h
+
+    def run(self, slices, weights, out, mode: int = DLSIM_EXACT, stream=None):
+        if self._h is None:
+            raise ValueError("plan destroyed")
+        try:
+            ptrs = _check_slices(slices, out)
+            w, wp = _weights_arg(weights, len(slices), self.f64)
+        except (AssertionError, ValueError, IndexError, TypeError):
+            # still enter the gather, so no peer is left waiting in it
+            try:
+                self.run_failed(getattr(out, "device", None))
+            except DlsimError:
+                pass
+            raise
+        fn = "dlsim_sharded_plan_run_f64" if self.f64 else "dlsim_sharded_plan_run"
+        _check(fn, getattr(self._lib, fn)(self._h, ptrs, wp, out.data_ptr(), mode, _stream_handle(out.device, stream)))
+        return out
+
+    def run_failed(self, device, stream=None) -> None:
+        """Enter the plan's gather as a rank whose own arguments failed the
+        caller's checks (no slices, no output): peers are not left waiting;
+        raises the library's argument error."""
+        if self._h is None:
+            raise ValueError("plan destroyed")
+        fn = "dlsim_sharded_plan_run_f64" if self.f64 else "dlsim_sharded_plan_run"
+        _check(fn, getattr(self._lib, fn)(self._h, None, None, None, DLSIM_EXACT, _stream_handle(device, stream)))
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None:
+            h, self._h = self._h, None
+            _check("dlsim_sharded_plan_destroy", self._lib.dlsim_sharded_plan_destroy(h))
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def chunk_mean_ilp_begin(m: int, n: int, threads: int) -> int:

@@ -79,39 +79,51 @@ class ShardedAggregator:
         return int(ptr) or None
 
     # ---- collectives ------------------------------------------------------------
+    def _via_host(self, t: torch.Tensor) -> bool:
+        """gloo moves host tensors: device tensors are staged through host
+        memory around each gloo collective (a gloo control plane on GPUs,
+        e.g. several ranks sharing one GPU); RCCL takes them in place."""
+        return t.is_cuda and dist.get_backend(self.group) == "gloo"
+
     def all_gather(self, shard: torch.Tensor, n_elems: int) -> torch.Tensor:
         """Concatenate every rank's slice into the full vector (ragged last
         slice handled by padding to the largest slice)."""
         bnds = self.all_bounds(n_elems)
         width = max(e - b for b, e in bnds)
-        padded = shard
-        if shard.numel() != width:
-            padded = torch.zeros(width, dtype=shard.dtype, device=shard.device)
-            padded[:shard.numel()].copy_(shard)
-        gathered = torch.empty(width * self.world, dtype=shard.dtype, device=shard.device)
+        dev = shard.device
+        cdev = torch.device("cpu") if self._via_host(shard) else dev
+        padded = torch.zeros(width, dtype=shard.dtype, device=cdev)
+        padded[:shard.numel()].copy_(shard)
+        gathered = torch.empty(width * self.world, dtype=shard.dtype, device=cdev)
         dist.all_gather_into_tensor(gathered, padded, group=self.group)
         if all(e - b == width for b, e in bnds):
-            return gathered
-        full = torch.empty(n_elems, dtype=shard.dtype, device=shard.device)
+            return gathered.to(dev)
+        full = torch.empty(n_elems, dtype=shard.dtype, device=dev)
         for r, (b, e) in enumerate(bnds):
             full[b:e].copy_(gathered[r * width:r * width + (e - b)])
         return full
 
     # ---- entry points -----------------------------------------------------------
     def aggregate_param_sharded(self, shard_inputs: Sequence[torch.Tensor], weights,
-                                n_elems: int, gather: bool = True,
+                                n_elems: int, gather=True,
                                 mode: int = _native.DLSIM_EXACT) -> torch.Tensor:
         """shard_inputs[i] = this rank's slice (self.bounds(n_elems)) of model i.
+        gather: False (keep this rank's slice), True / "bcast" (grouped
+        in-place broadcasts) or "allgather" (one padded all-gather); on gloo
+        both gathers are torch's all_gather_into_tensor.
 
         Errors are collective: a rank whose arguments fail its checks does not
         raise before the other ranks know, so none of them is left inside a
         collective; every rank then raises the same error (the failing ranks'
         messages, in rank order)."""
-        local = None
+        local, code, b, e = None, 0, 0, 0
+        g = _native.gather_code(gather)
+        c_abi = self._uses_c_abi()
         try:
             if not shard_inputs:
                 raise IndexError("list index out of range")  # models[0] of fedavg.py:20
             x0 = shard_inputs[0]
+            code = _native.dtype_code(x0.dtype, single_task=True)
             # fp32-rounded weights, or exact doubles for a double model (fedavg.py:25)
             w32 = _resolve(len(shard_inputs), weights, x0.dtype)
             b, e = self.bounds(n_elems)
@@ -120,34 +132,38 @@ class ShardedAggregator:
                     raise ValueError(f"rank {self.rank}: shard has {x.numel()} elements, expected {e - b}")
                 if x.dtype != x0.dtype or x.device != x0.device or not x.is_contiguous():
                     raise ValueError(f"rank {self.rank}: shards must be contiguous tensors of one dtype and device")
+                if c_abi and not x.is_cuda:
+                    raise ValueError(f"rank {self.rank}: the RCCL path takes device shards")
         except (AssertionError, ValueError, IndexError, TypeError) as ex:
             local = ex
-        if self._uses_c_abi():
+        if c_abi:
             dev = shard_inputs[0].device if local is None else _default_device()
             comm = self._rccl_comm(dev)
             if comm is not None:
                 # the C ABI end to end: local reduce into the full buffer, the
-                # library's agreement step, then the grouped in-place broadcasts
-                # on the caller's RCCL communicator
-                failed = local
+                # library's agreement step, then the gather on the caller's
+                # RCCL communicator
                 full = None
                 try:
                     if local is None:
                         full = torch.empty(n_elems, dtype=x0.dtype, device=x0.device)
-                        _native.wreduce_sharded(list(shard_inputs), w32, full, comm, gather, mode)
+                        _native.wreduce_sharded(list(shard_inputs), w32, full, comm, g, mode)
                     else:  # join the library's agreement as a failed rank
-                        _native.wreduce_sharded_failed(comm, n_elems, gather, dev)
+                        _native.wreduce_sharded_failed(comm, n_elems, g, dev)
                 except _native.DlsimError as ex:
-                    failed = failed or ex
-                if failed is not None:
-                    self._raise_collectively(failed)
-                return full if gather else full[b:e]
-        self._agree(local, [n_elems, 1 if gather else 0,
-                            _native.dtype_code(x0.dtype, single_task=True) if local is None else 0])
+                    self._library_failure(local, ex)
+                return full if g else full[b:e]
+        self._agree(local, [n_elems, 1 if g else 0, code if local is None else 0])
         out = torch.empty(e - b, dtype=x0.dtype, device=x0.device)
         if e > b:
             self.local_reduce(list(shard_inputs), w32, out, mode)
-        return self.all_gather(out, n_elems) if gather else out
+        return self.all_gather(out, n_elems) if g else out
+
+    def plan(self, n_elems: int, n_models: int, dtype: torch.dtype, gather=True) -> "ParamShardPlan":
+        """A collective call: every rank agrees ONCE on (n_elems, n_models,
+        dtype, gather); the plan's run() then skips the per-call agreement
+        and, on RCCL, its host wait (VERDICT r03 next #2)."""
+        return ParamShardPlan(self, n_elems, n_models, dtype, gather)
 
     # ---- collective error handling ------------------------------------------------
     def _uses_c_abi(self) -> bool:
@@ -180,6 +196,18 @@ class ShardedAggregator:
         kinds = {"ValueError": ValueError, "AssertionError": AssertionError, "IndexError": IndexError,
                  "TypeError": TypeError}
         raise kinds.get(failed[0][1][0] if failed else "", RuntimeError)(msg or "a rank failed")
+
+    def _library_failure(self, local: Optional[BaseException], ex: "_native.DlsimError") -> None:
+        """After the library's agreement failed on this rank: the ranks that
+        failed their own checks raise collectively with their errors; a rank
+        whose only failure is a peer's (DLSIM_E_PEER) joins with none, so the
+        type and message come from the failing ranks (the gloo path's rule);
+        a disagreement is known to every rank and raised without a gather."""
+        if local is None and ex.rc == _native.DLSIM_E_DISAGREE:
+            raise ValueError("ranks disagree on the model size, gather or dtype; no collective was entered")
+        if local is None and ex.rc == _native.DLSIM_E_PEER:
+            self._raise_collectively(None)
+        self._raise_collectively(local or ex)
 
     def aggregate_model_sharded(self, local_models: Sequence[torch.Tensor], counts: Sequence[int],
                                 weights, exact: bool = True) -> torch.Tensor:
@@ -217,8 +245,12 @@ class ShardedAggregator:
         padded = torch.zeros(width * self.world, dtype=acc_dt, device=device)
         for r, (b, e) in enumerate(bnds):
             padded[r * width:r * width + (e - b)].copy_(partial[b:e])
-        mine = torch.empty(width, dtype=acc_dt, device=device)
+        host = self._via_host(padded)
+        if host:
+            padded = padded.cpu()
+        mine = torch.empty(width, dtype=acc_dt, device=padded.device)
         dist.reduce_scatter_tensor(mine, padded, op=dist.ReduceOp.SUM, group=self.group)
+        mine = mine.to(device)
         b, e = bnds[self.rank]
         return self.all_gather(mine[:e - b].to(dtype).contiguous(), n_elems)
 
@@ -237,14 +269,95 @@ class ShardedAggregator:
             in_splits.append(k * (e - b))
         my_len = lens[self.rank]
         out_splits = [counts[r] * my_len for r in range(self.world)]
-        recv = torch.empty(sum(out_splits), dtype=dtype, device=device)
+        if self._via_host(send):
+            send = send.cpu()
+        recv = torch.empty(sum(out_splits), dtype=dtype, device=send.device)
         dist.all_to_all_single(recv, send, output_split_sizes=out_splits,
                                input_split_sizes=in_splits, group=self.group)
+        recv = recv.to(device)
         rows = [recv[i * my_len:(i + 1) * my_len] for i in range(sum(counts))]
         out = torch.empty(my_len, dtype=dtype, device=device)
         if my_len > 0:
             self.local_reduce(rows, w32, out, _native.DLSIM_EXACT)
         return self.all_gather(out, n_elems)
+
+
+class ParamShardPlan:
+    """aggregate_param_sharded for one shape, agreed once (ShardedAggregator.plan).
+
+    On an RCCL group with the HIP reduce this is the C ABI's
+    dlsim_sharded_plan; elsewhere (gloo, injected reduces) the agreement runs
+    once here and each run is the local reduce plus the all-gather. Every
+    rank must run the same sequence of plans. A run whose local checks fail
+    still enters the gather (so no peer waits forever) and raises on that
+    rank only; its peers' copy of its slice is undefined."""
+
+    def __init__(self, agg: ShardedAggregator, n_elems: int, n_models: int, dtype: torch.dtype, gather=True):
+        self.agg, self.n_elems, self.n, self.dtype = agg, int(n_elems), int(n_models), dtype
+        self.gather = _native.gather_code(gather)
+        self.bounds = agg.bounds(self.n_elems)
+        self._c = None
+        local, code = None, 0
+        try:
+            code = _native.dtype_code(dtype, single_task=True)
+            if self.n < 1:
+                raise ValueError("a plan needs n_models >= 1")
+        except (ValueError, TypeError) as ex:
+            local = ex
+        comm = agg._rccl_comm(_default_device()) if agg._uses_c_abi() else None
+        if comm is not None:
+            try:
+                if local is None:
+                    self._c = _native.ShardedPlan(comm, self.n_elems, self.n, dtype, self.gather,
+                                                  device=_default_device())
+                else:  # join the agreement as a failed rank
+                    _native.wreduce_sharded_failed(comm, self.n_elems, self.gather, _default_device())
+            except _native.DlsimError as ex:
+                agg._library_failure(local, ex)
+            return
+        agg._agree(local, [self.n_elems, self.n, code, 1 if self.gather else 0])
+
+    def run(self, shard_inputs: Sequence[torch.Tensor], weights, mode: int = _native.DLSIM_EXACT,
+            out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """The full output (gather) or this rank's slice, as
+        aggregate_param_sharded; `out` (full size, gather on RCCL) is reused
+        when given."""
+        b, e = self.bounds
+        local = None
+        try:
+            if len(shard_inputs) != self.n:
+                raise ValueError(f"rank {self.agg.rank}: plan has {self.n} models, got {len(shard_inputs)}")
+            w = _resolve(self.n, weights, self.dtype)
+            for x in shard_inputs:
+                if x.numel() != e - b or x.dtype != self.dtype or not x.is_contiguous():
+                    raise ValueError(f"rank {self.agg.rank}: shards must be contiguous {self.dtype} slices of "
+                                     f"{e - b} elements")
+        except (AssertionError, ValueError, TypeError) as ex:
+            local = ex
+        dev = shard_inputs[0].device if local is None else _default_device()
+        if self._c is not None:
+            if local is not None:
+                try:
+                    self._c.run_failed(dev)  # enters the gather; raises the library's error
+                except _native.DlsimError:
+                    pass
+                raise local
+            if out is None:
+                out = torch.empty(self.n_elems, dtype=self.dtype, device=dev)
+            self._c.run(list(shard_inputs), w, out, mode)
+            return out if self.gather else out[b:e]
+        part = torch.zeros(e - b, dtype=self.dtype, device=dev)
+        if local is None and e > b:
+            self.agg.local_reduce(list(shard_inputs), w, part, mode)
+        res = self.agg.all_gather(part, self.n_elems) if self.gather else part
+        if local is not None:
+            raise local
+        return res
+
+    def close(self) -> None:
+        if self._c is not None:
+            self._c.close()
+            self._c = None
 
 
 def _resolve(n: int, weights, dtype=None) -> np.ndarray:

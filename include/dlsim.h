@@ -66,6 +66,19 @@ enum dlsim_mode {
 #define DLSIM_E_RCCL (-4)     /* RCCL not bound, or an RCCL call failed       */
 #define DLSIM_E_PEER (-5)     /* another rank of the communicator failed its
                                  checks (dlsim_wreduce_sharded's agreement)   */
+#define DLSIM_E_DISAGREE (-6) /* the ranks of a communicator passed different
+                                 n_elems / fan-in / dtype / gather (agreement) */
+
+/* How the sharded entry points materialise the whole output on every rank. */
+enum dlsim_gather {
+  DLSIM_GATHER_NONE = 0,      /* each rank keeps its own slice only            */
+  DLSIM_GATHER_BCAST = 1,     /* every rank broadcasts its slice in place in
+                                 d_out: W ncclBroadcast in one group            */
+  DLSIM_GATHER_ALLGATHER = 2  /* one in-place ncclAllGather of equal-width
+                                 (padded) segments in a scratch buffer, then one
+                                 kernel moves them to their offsets in d_out;
+                                 at most 64 ranks                               */
+};
 #define DLSIM_E_HIP (-100)    /* a HIP call failed: code = -100 - hipError_t  */
 
 /* Fan-in carried in kernel arguments. Larger n (any n >= 1) reads its
@@ -252,22 +265,25 @@ int dlsim_rccl_bind(const char* librccl_path);
  *   dlsim_shard_range(n_elems, W, r, 64); d_slices[i] points at that slice of
  *   model i (slice_elems elements, which must equal e_r - b_r, else
  *   DLSIM_E_ARG); d_out is a full n_elems buffer, and the
- *   exact reduce of the slices lands at d_out + b_r. gather != 0: every
- *   rank's slice is then broadcast in place (a variable-size all-gather,
- *   grouped ncclBroadcast on `stream`), so every rank ends with the whole
- *   output. Each element's N terms stay on one GPU in input order: results
- *   are bit-identical to dlsim_wreduce on one GPU.
+ *   exact reduce of the slices lands at d_out + b_r. gather (enum
+ *   dlsim_gather; 1 = DLSIM_GATHER_BCAST for callers that pass a bool):
+ *   every rank ends with the whole output, through grouped in-place
+ *   broadcasts or one padded all-gather plus an unpad kernel, on `stream`.
+ *   Each element's N terms stay on one GPU in input order: results are
+ *   bit-identical to dlsim_wreduce on one GPU, with either gather.
  *   Errors are collective when W > 1: the rank-local checks (slice length,
- *   pointers, dtype, fan-in, weights) and the local reduce's launch run
- *   first, then every rank joins one agreement all-reduce (int64 MAX of a
+ *   pointers, dtype, fan-in, weights, gather) and the local reduce's launch
+ *   run first, then every rank joins one agreement all-reduce (int64 MAX of a
  *   failure slot per rank plus n_elems, dtype and gather, on `stream`, read
  *   back by the host: the call waits for the stream once). A rank whose own
  *   checks failed returns its own error; every other rank returns
- *   DLSIM_E_PEER naming the failed ranks, or DLSIM_E_ARG if the ranks
+ *   DLSIM_E_PEER naming the failed ranks, or DLSIM_E_DISAGREE if the ranks
  *   disagree on n_elems, dtype or gather; in both cases no rank enters the
- *   broadcast group, so none is left waiting in it. Only a failure before the
+ *   gather, so none is left waiting in it. Only a failure before the
  *   communicator can be queried (RCCL not bound, null communicator) is
- *   rank-local.
+ *   rank-local. For repeated aggregates of one shape, a plan
+ *   (dlsim_sharded_plan_create) agrees once and skips the per-call
+ *   agreement and its host wait.
  */
 int dlsim_wreduce_sharded(const void* const* d_slices, size_t slice_elems, int n, const float* h_weights,
                           void* d_out, size_t n_elems, int dtype, int mode, void* rccl_comm, int gather,
@@ -277,12 +293,49 @@ int dlsim_wreduce_sharded(const void* const* d_slices, size_t slice_elems, int n
  * dlsim_wreduce_sharded_f64 — dlsim_wreduce_sharded for fp64 (double)
  * parameters: double weights and the arithmetic of dlsim_wreduce_f64 (a
  * double model's `w * p1` keeps the Python float exact, fedavg.py:25), the
- * gather as ncclFloat64 broadcasts. The agreement step is the same one, with
+ * gather in ncclFloat64. The agreement step is the same one, with
  * dtype DLSIM_F64, so ranks that call the fp32/bf16/fp16 entry with the same
  * communicator are told of the disagreement instead of left waiting.
  */
 int dlsim_wreduce_sharded_f64(const void* const* d_slices, size_t slice_elems, int n, const double* h_weights,
                               void* d_out, size_t n_elems, int mode, void* rccl_comm, int gather, void* stream);
+
+/*
+ * dlsim_sharded_plan — dlsim_wreduce_sharded for a repeated shape, without
+ * the per-call agreement.
+ *
+ * dlsim_sharded_plan_create is COLLECTIVE: every rank of the communicator
+ * calls it with its own arguments; the ranks agree once on n_elems, the
+ * fan-in n, dtype (DLSIM_F32/BF16/F16/F64) and gather (enum dlsim_gather), in
+ * one int64 MAX all-reduce read back by the host, as dlsim_wreduce_sharded
+ * does. A rank whose own checks failed gets its error, the others
+ * DLSIM_E_PEER or DLSIM_E_DISAGREE, and *plan stays NULL on every rank.
+ * DLSIM_GATHER_ALLGATHER plans own their padded segment buffer
+ * (W x ceil64(max slice) elements, hipMalloc).
+ *
+ * dlsim_sharded_plan_run[_f64] reduces this rank's slices (dlsim_shard_range
+ * of the plan's n_elems, n models) into d_out + b_r and runs the plan's
+ * gather: stream-ordered, no host wait, no agreement. Every rank must run
+ * the same sequence of plans, as with any collective. A rank whose local
+ * checks or launch fail (null or overlapping pointers, mode, the f64 entry
+ * on a non-f64 plan) still enters the plan's gather with whatever its slice
+ * holds (a stand-in buffer when d_out is NULL), so no peer is left waiting,
+ * and returns its error; its peers are not told (their copy of that slice is
+ * undefined). Agree again (dlsim_wreduce_sharded, or a new plan) when that
+ * matters.
+ *
+ * dlsim_sharded_plan_destroy frees the plan (rank-local; NULL is a no-op).
+ * Plans are not thread-safe: one caller per plan at a time.
+ */
+typedef struct dlsim_sharded_plan dlsim_sharded_plan;
+
+int dlsim_sharded_plan_create(void* rccl_comm, size_t n_elems, int n, int dtype, int gather, void* stream,
+                              dlsim_sharded_plan** plan);
+int dlsim_sharded_plan_run(dlsim_sharded_plan* plan, const void* const* d_slices, const float* h_weights,
+                           void* d_out, int mode, void* stream);
+int dlsim_sharded_plan_run_f64(dlsim_sharded_plan* plan, const void* const* d_slices, const double* h_weights,
+                               void* d_out, int mode, void* stream);
+int dlsim_sharded_plan_destroy(dlsim_sharded_plan* plan);
 
 /*
  * dlsim_host_wreduce — the aggregate of N *host* models (the reference's own

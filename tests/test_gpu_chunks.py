@@ -327,36 +327,46 @@ def test_host_chunk_mean_rejects_small_staging():
 
 
 @pytest.mark.parametrize("dtype", ["f32", "bf16", "f64"])
-@pytest.mark.parametrize("tight", [True, False])
-def test_host_chunk_mean_small_job_one_dma(dtype, tight):
+@pytest.mark.parametrize("layout", ["tight", "padded", "gaps", "reversed"])
+def test_host_chunk_mean_small_job_one_dma(dtype, layout):
     """a job under 4 MiB (GNLeNet's Conflux reconstruct:
     k = 10 chunk indices of ~8.5 K elements, m = 4) packs every row, sends ONE
-    H2D, runs ONE batched launch and, when the outputs keep the same offsets
-    on the device and the host (ChunkManager's back-to-back layout), ONE D2H;
-    every mean bit-identical to the order-exact oracle, with outputs back to
-    back and at padded device offsets."""
+    H2D, runs ONE batched launch and, when the outputs lie back to back at the
+    same offsets on the device and the host (ChunkManager's layout), ONE D2H;
+    every mean bit-identical to the order-exact oracle. Layouts: back to back
+    (tight), padded device offsets, equal offsets on both sides with gaps
+    between the outputs (the host bytes in the gaps must survive),
+    and back to back in reverse task order."""
     rng = np.random.default_rng(17)
     k, m, size = 10, 4, 85_354 // 10
     sizes = [size] * (k - 1) + [85_354 - size * (k - 1)]
     tdt = {"f32": torch.float32, "bf16": torch.bfloat16, "f64": torch.float64}[dtype]
     esz = torch.empty((), dtype=tdt).element_size()
     al = 256 // esz
+    gap = 37 if layout == "gaps" else 0
+    padded = layout == "padded"
+    dev_len = [((n + al - 1) // al * al if padded else n) + gap for n in sizes]
+    host_len = [n + gap for n in sizes]
+    d_out = torch.empty(sum(dev_len), dtype=tdt, device=dev())
+    host = torch.empty(sum(host_len), dtype=tdt, pin_memory=True)
+    host.view(torch.uint8).fill_(0xA5)  # the sentinel the gaps must keep
+    order = list(range(k))[::-1] if layout == "reversed" else list(range(k))
+    doff, hoff = {}, {}
+    o = h = 0
+    for t in order:
+        doff[t], hoff[t] = o, h
+        o += dev_len[t]
+        h += host_len[t]
     tasks, exp, hosts = [], [], []
-    total = sum(sizes) if tight else sum((n + al - 1) // al * al for n in sizes)
-    d_out = torch.empty(total, dtype=tdt, device=dev())
-    host = torch.empty(sum(sizes), dtype=tdt, pin_memory=True)
-    off = hoff = 0
-    for n in sizes:
+    for t, n in enumerate(sizes):
         x = rng.standard_normal((m, n)) * 0.1
         x = x if dtype == "f64" else x.astype(np.float32)
         rows = orc.f32_to_bf16_bits(x) if dtype == "bf16" else x
         ts = [torch.from_numpy(r.view(np.int16).copy()).view(tdt) if dtype == "bf16" else torch.from_numpy(r.copy())
               for r in rows]
-        tasks.append((ts, d_out[off:off + n]))
-        hosts.append(host[hoff:hoff + n])
+        tasks.append((ts, d_out[doff[t]:doff[t] + n]))
+        hosts.append(host[hoff[t]:hoff[t] + n])
         exp.append(orc.chunk_mean(list(rows), dtype, 4))
-        off += n if tight else (n + al - 1) // al * al
-        hoff += n
     need = _native.staged_rows_elems(sizes, [m] * k, esz)
     assert need * esz < 4 << 20
     stage = torch.empty(need, dtype=tdt, pin_memory=True)
@@ -364,9 +374,14 @@ def test_host_chunk_mean_small_job_one_dma(dtype, tight):
     stream = torch.cuda.current_stream(dev())
     _native.host_chunk_mean(tasks, stage, d_in, host_outs=hosts, threads=4, cpu_threads=4, stream=stream)
     stream.synchronize()
-    for (ts, out), h, e in zip(tasks, hosts, exp):
+    for (ts, out), hh, e in zip(tasks, hosts, exp):
         assert orc.same_bits(_bits(out), e)
-        assert orc.same_bits(_bits(h), e)
+        assert orc.same_bits(_bits(hh), e)
+    if gap:
+        raw = host.view(torch.uint8).numpy()
+        for t, n in enumerate(sizes):
+            g0 = (hoff[t] + n) * esz
+            assert (raw[g0:g0 + gap * esz] == 0xA5).all(), f"gap after task {t} overwritten"
 
 
 CHUNK_FIXTURES_F64 = sorted(__import__("glob").glob(os.path.join(os.path.dirname(CHUNK_FIXTURES[0]), "..",

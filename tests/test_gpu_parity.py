@@ -233,6 +233,23 @@ def test_cfg3_17way_11M_f32_bit_exact():
     assert orc.same_bits(got, orc.wreduce_rows_f32(x, w))
 
 
+def test_cfg5_100way_11M_f32_bit_exact():
+    """BASELINE.json configs[4] at full size: the FedAvg-style 100-client
+    Dirichlet(1)-weighted fp32 reduce of 11,181,642 params (4.5 GB of inputs,
+    the device-table fan-in path), every element against the oracle's ordered
+    fold (fedavg.py:23-25)."""
+    n, p = 100, 11_181_642
+    g = torch.Generator(device="cpu").manual_seed(100)
+    x = np.empty((n, p), dtype=np.float32)
+    for i in range(n):  # row by row: no second 4.5 GB temporary
+        x[i] = (torch.randn(p, generator=g) * 0.05).numpy()
+    w = orc.reference_weights(n, list(np.random.default_rng(7).dirichlet(np.ones(n))))
+    got = hip_reduce(list(x), w, "f32")
+    assert orc.same_bits(got, orc.wreduce_rows_f32(x, w))
+    del x
+    torch.cuda.empty_cache()
+
+
 def test_cfg4_2way_125M_bf16_properties():
     """2-way bf16 gossip merge of 125 M params with age weights [3/8, 5/8]:
     size-independent properties at full size, bit-exact on a strided sample."""

@@ -1,0 +1,56 @@
+"""The sharded path with the HIP kernel as the local reduce in more than one
+process (GPU).
+
+Two fresh rank processes (tests/_sharded_hip_child.py) share the one
+MI355X of the box with a gloo control plane: each runs
+aggregate_param_sharded (gathered and not), a plan's repeated runs and
+aggregate_model_sharded(exact=True) with ShardedAggregator's default local
+reduce, the HIP kernel, on fp32 and bf16 models; the gathers go through host
+tensors (gloo). Every rank's assembled output must be bit-identical to the
+oracle's single fold ("results are bit-identical to 1 GPU").
+The ranks are started as fresh interpreters, as bench.py starts its ranks:
+this pytest process has used the GPU and forks nothing that uses it."""
+from __future__ import annotations
+
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_two_processes_hip_local_reduce_bit_exact():
+    world, port = 2, _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "_sharded_hip_child.py")], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = []
+    try:
+        for pr in procs:
+            out, err = pr.communicate(timeout=180)
+            outs.append((pr.returncode, out, err))
+    finally:
+        for pr in procs:
+            if pr.poll() is None:
+                pr.kill()
+                pr.wait()
+    for r, (rc, out, err) in enumerate(outs):
+        lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+        assert rc == 0 and lines, f"rank {r}: rc={rc}\n{out[-2000:]}\n{err[-3000:]}"
+        res = json.loads(lines[-1])
+        assert res["rank"] == r and res["world"] == world
+        assert res["checks"] and all(res["checks"].values()), (r, res["checks"])

@@ -108,10 +108,23 @@ def test_c_abi_sharded_entry_on_torch_rccl_comm(rccl_world1, n, p, dtype):
     agg = ShardedAggregator()
     comm = agg._rccl_comm(dev)
     assert comm is not None  # the ABI path is the one aggregate_param_sharded takes here
-    for gather in (True, False):
+    for gather in (True, False, "allgather"):
         out = torch.full((p,), float("nan"), dtype=dtype, device=dev)
         _native.wreduce_sharded(xs, w32, out, comm, gather=gather)
         assert _same(out, expect)
+    # a plan on the real communicator (agreed once; world 1 runs no gather)
+    for gather in ("bcast", "allgather"):
+        plan = _native.ShardedPlan(comm, p, n, dtype, gather, device=dev)
+        for _ in range(3):
+            out = torch.full((p,), float("nan"), dtype=dtype, device=dev)
+            plan.run(xs, w32, out)
+            assert _same(out, expect)
+        plan.close()
+    # through ShardedAggregator.plan (the C plan on this group's communicator)
+    pl = agg.plan(p, n, dtype)
+    assert pl._c is not None
+    assert _same(pl.run(xs, None), expect)  # uniform weights, as w32
+    pl.close()
     # a null communicator and a slice length that is not this rank's shard are
     # argument errors, not launches
     assert _native.load().dlsim_wreduce_sharded(None, 0, 0, None, None, 0, 0, 0, None, 0, None) == -1

@@ -109,6 +109,12 @@ def _worker(rank, world, port, p, dtype_name, q, n=5):
         else:
             exp4 = torch.from_numpy(orc.wreduce([x.numpy() for x in xs], w_u, "f32"))
         res["param_sharded_uniform"] = same(full4, exp4)
+        # 5) a plan (agreed once): repeated runs, gathered and not
+        plan = agg.plan(p, n, dtype)
+        res["plan_run_1"] = same(plan.run([x[b:e].contiguous() for x in xs], weights), expect)
+        res["plan_run_2"] = same(plan.run([x[b:e].contiguous() for x in xs], weights), expect)
+        plan_s = agg.plan(p, n, dtype, gather=False)
+        res["plan_shard_only"] = same(plan_s.run([x[b:e].contiguous() for x in xs], weights), expect[b:e])
         q.put((rank, res))
     except Exception as exc:  # surface worker failures to the parent
         import traceback
@@ -170,6 +176,10 @@ def _err_worker(rank, world, port, case, q):
                 agg.aggregate_model_sharded(mine, counts if rank != 1 else counts[::-1] + [0], None)
             elif case == "size_mismatch":
                 agg.aggregate_model_sharded([m[:-64] for m in mine] if rank == 1 else mine, counts, None)
+            elif case == "int64_shard":  # a dtype error joins the agreement too
+                agg.aggregate_param_sharded(shards if rank != 1 else [s.to(torch.int64) for s in shards], None, p)
+            elif case == "plan_mismatch":
+                agg.plan(p, n if rank == 0 else n + 1, torch.float32)
         except Exception as ex:  # noqa: BLE001 - the error is the result
             err = (type(ex).__name__, str(ex))
         secs = time.perf_counter() - t0
@@ -189,6 +199,8 @@ def _err_worker(rank, world, port, case, q):
     ("gather_mismatch", "ValueError", "disagree"),
     ("bad_counts", "ValueError", "rank 1 of 2: counts must list"),
     ("size_mismatch", "ValueError", "differ in size"),
+    ("int64_shard", "TypeError", "rank 1 of 2: aggregation supports"),
+    ("plan_mismatch", "ValueError", "disagree"),
 ])
 def test_sharded_errors_are_collective_gloo(case, kind, text):
     """a rank-local argument error (a wrong-length shard,
@@ -214,3 +226,57 @@ def test_sharded_errors_are_collective_gloo(case, kind, text):
         assert results[r]["secs"] < 20, (r, results[r]["secs"])
         assert results[r]["after_ok"]
     assert results[0]["err"] == results[1]["err"]  # the same error on every rank
+
+
+def _plan_fail_worker(rank, world, port, q):
+    """A plan run whose local checks fail on rank 1 (wrong-length shards):
+    rank 1 raises after entering the gather, rank 0 completes (its copy of
+    rank 1's slice is undefined), nobody hangs, and the plan keeps working."""
+    import datetime
+    import time
+    for path in PATHS:
+        sys.path.insert(0, path)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
+    try:
+        from dasklearn_amd.sharded import ShardedAggregator
+        from oracle import oracle as orc
+        agg = ShardedAggregator(local_reduce=oracle_reduce)
+        n, p = 3, 1000
+        xs = models(n, p, torch.float32)
+        b, e = agg.bounds(p)
+        shards = [x[b:e].contiguous() for x in xs]
+        plan = agg.plan(p, n, torch.float32)
+        t0 = time.perf_counter()
+        err = None
+        try:
+            plan.run(shards if rank != 1 else [s[:-1] for s in shards], None)
+        except Exception as ex:  # noqa: BLE001
+            err = type(ex).__name__
+        secs = time.perf_counter() - t0
+        again = plan.run(shards, None)
+        expect = torch.from_numpy(orc.wreduce([x.numpy() for x in xs], orc.reference_weights(n, None), "f32"))
+        q.put((rank, {"err": err, "secs": secs, "again": torch.equal(again.view(torch.int32),
+                                                                      expect.view(torch.int32))}))
+    except Exception:
+        import traceback
+        q.put((rank, {"error": traceback.format_exc()}))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_plan_run_failure_does_not_hang_gloo():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_plan_fail_worker, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    results = dict(q.get(timeout=120) for _ in range(world))
+    for pr in procs:
+        pr.join(timeout=60)
+    for r in range(world):
+        assert "error" not in results[r], results[r].get("error")
+        assert results[r]["secs"] < 20 and results[r]["again"], (r, results[r])
+    assert results[0]["err"] is None and results[1]["err"] == "ValueError"
