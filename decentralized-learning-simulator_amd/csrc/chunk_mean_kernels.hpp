@@ -297,13 +297,17 @@ __device__ __forceinline__ void cm_tile(const A& a, int m, const OutRef& o, size
 
 // Block 0 of a task: the scalar columns [c0, n) — cascade order below
 // ilp_begin, ilp order from it (or the inner order for a one-element chunk) —
-// staged through LDS kCmTailRows rows at a time.
+// staged through LDS TR rows at a time (kCmTailRows, halved for 8-byte
+// elements so the stage is 16 KiB for every policy: the static LDS of this
+// function is reserved by every block of k_chunk_mean_batch).
 template <class Op, class A>
 __device__ __forceinline__ void cm_scalar_cols(const A& a, int m, void* out, size_t c0, size_t n,
                                                size_t ilp_begin, bool inner, float div) {
   using T = acc_t<Op>;
   constexpr int VW = cm_lanes<Op>();
-  __shared__ T st[kCmTailRows][kCmTailCols];
+  constexpr int TR = kCmTailRows * 4 / static_cast<int>(sizeof(T));
+  static_assert(TR * kCmTailCols * sizeof(T) == 16384, "16 KiB tail stage");
+  __shared__ T st[TR][kCmTailCols];
   const int W = static_cast<int>(n - c0);  // block-uniform, <= kCmTailCols
   const int tid = threadIdx.x;
   const size_t col = c0 + static_cast<size_t>(tid);
@@ -314,8 +318,8 @@ __device__ __forceinline__ void cm_scalar_cols(const A& a, int m, void* out, siz
   cs.init();
   il.init(inner ? vs : m);
   T fin = T(0);  // inner: the m mod VW trailing rows, from +0
-  for (int r0 = 0; r0 < m; r0 += kCmTailRows) {
-    const int rc = m - r0 < kCmTailRows ? m - r0 : kCmTailRows;
+  for (int r0 = 0; r0 < m; r0 += TR) {
+    const int rc = m - r0 < TR ? m - r0 : TR;
     for (int idx = tid; idx < rc * W; idx += kBlock) {
       const int row = idx / W, c = idx - row * W;
       st[row][c] = load_elem<Op>(a.ptr(r0 + row), c0 + static_cast<size_t>(c));

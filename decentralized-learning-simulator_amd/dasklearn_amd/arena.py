@@ -319,7 +319,8 @@ class _Staging:
             stride = row_stride(numel, esz)
             need = max(1, n * stride)
             al = base_align(numel * esz, esz)
-            flat = self._grow(self.dev, key, need, lambda k: aligned_empty(k, dt, device, ROW_ALIGN), align=al)
+            # aligned as this call needs (a later call that needs 2 MiB rows regrows the buffer)
+            flat = self._grow(self.dev, key, need, lambda k: aligned_empty(k, dt, device, al), align=al)
             hflat = self._grow(self.host, key, need, lambda k: torch.empty(k, dtype=dt, pin_memory=True)) \
                 if pinned else None
             last = self._views.get(key)
