@@ -552,6 +552,13 @@ int dlsim_host_chunk_mean(int b, const int* fan_in, const void* const* h_inputs,
   return ln.rc;
 }
 
+int dlsim_host_prewarm(int threads) {
+  g_err.clear();
+  if (threads < 1) return fail(DLSIM_E_ARG, "threads must be >= 1 (got %d)", threads);
+  dlsim::PackPool::get().prewarm(std::min(threads, 64) - 1);
+  return DLSIM_OK;
+}
+
 int dlsim_host_pack(int t, const void* const* h_srcs, const size_t* nbytes, const size_t* dst_off, void* h_dst,
                     int threads) {
   g_err.clear();

@@ -10,8 +10,11 @@
 // one pipeline chunk): the dispatching thread starts a unit's DMA as soon as
 // the unit is packed, while the other threads already pack the next ones.
 //
-// Plain C++ (no device code). The pool's threads are created once and sleep
-// between calls; a process that forks gets a fresh pool in the child.
+// Plain C++ (no device code). The pool's threads are created once; between
+// calls they spin for a short while (DLSIM_PACK_SPIN_US, default 200 us) so
+// that back-to-back host tasks find them awake, then sleep. A caller can wake
+// them ahead of a job (prewarm). A process that forks gets a fresh pool in the
+// child.
 #pragma once
 
 #include <emmintrin.h>
@@ -19,6 +22,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdlib>
 #include <condition_variable>
 #include <cstdint>
@@ -115,6 +119,8 @@ struct PackJob {
 };
 
 // Helper threads for PackJobs. One job at a time (callers hold call_mutex()).
+// A helper joins a job only while it is open; join() closes it, so a helper
+// that wakes late skips the job instead of holding up the caller.
 class PackPool {
  public:
   static PackPool& get() {
@@ -142,23 +148,54 @@ class PackPool {
     std::lock_guard<std::mutex> lk(mu_);
     job_ = job;
     helpers_ = helpers;
+    joined_ = 0;
     finished_.store(0, std::memory_order_relaxed);
-    ++gen_;
+    bump();
     cv_.notify_all();
   }
-  // Wait until every helper of the current job has left it (the job may be
-  // destroyed after this returns).
+  // Close the job to helpers that have not joined it, then wait until every
+  // helper that did has left it (the job may be destroyed after this returns).
   void join() {
-    while (finished_.load(std::memory_order_acquire) < helpers_) std::this_thread::yield();
+    int joined;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      job_ = nullptr;
+      joined = joined_;
+    }
+    while (finished_.load(std::memory_order_acquire) < joined) std::this_thread::yield();
+  }
+  // Wake `helpers` threads without a job: they spin for the next one (a
+  // caller that knows a host job is coming calls this first). Skipped while
+  // a job runs.
+  void prewarm(int helpers) {
+    std::unique_lock<std::mutex> call(call_mu_, std::try_to_lock);
+    if (!call.owns_lock() || helpers < 1) return;
+    grow(helpers);
+    std::lock_guard<std::mutex> lk(mu_);
+    job_ = nullptr;
+    helpers_ = helpers;
+    bump();
+    cv_.notify_all();
   }
 
  private:
-  PackPool() : pid_(getpid()) {}
+  PackPool() : pid_(getpid()), spin_ns_(spin_ns_from_env()) {}
+
+  static int64_t spin_ns_from_env() {
+    const char* e = std::getenv("DLSIM_PACK_SPIN_US");
+    const long us = e ? std::strtol(e, nullptr, 10) : 200;
+    return us > 0 ? static_cast<int64_t>(us) * 1000 : 0;
+  }
+
+  void bump() {  // with mu_ held
+    ++gen_;
+    gen_seen_.store(gen_, std::memory_order_release);
+  }
 
   void grow(int helpers) {
     while (static_cast<int>(threads_) < helpers) {
-      // gen_ changes only in start(), after this: the new thread takes
-      // part from the coming job on
+      // gen_ changes only in start()/prewarm(), after this: the new thread
+      // takes part from the coming job on
       const int id = static_cast<int>(threads_++);
       const uint64_t seen = gen_;
       std::thread([this, id, seen] { loop(id, seen); }).detach();
@@ -167,13 +204,22 @@ class PackPool {
 
   void loop(int id, uint64_t seen) {
     for (;;) {
+      // spin a while for the next generation before sleeping on the condvar
+      if (spin_ns_ > 0) {
+        const auto t0 = std::chrono::steady_clock::now();
+        while (gen_seen_.load(std::memory_order_acquire) == seen &&
+               std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count() <
+                   spin_ns_)
+          _mm_pause();
+      }
       PackJob* job;
       {
         std::unique_lock<std::mutex> lk(mu_);
         cv_.wait(lk, [&] { return gen_ != seen; });
         seen = gen_;
-        if (id >= helpers_) continue;
+        if (id >= helpers_ || job_ == nullptr) continue;  // not asked, a prewarm, or already closed
         job = job_;
+        ++joined_;
       }
       while (job->run_one()) {
       }
@@ -182,13 +228,16 @@ class PackPool {
   }
 
   const pid_t pid_;
+  const int64_t spin_ns_;
   std::mutex call_mu_;
   std::mutex mu_;
   std::condition_variable cv_;
   size_t threads_ = 0;
   PackJob* job_ = nullptr;
   int helpers_ = 0;
+  int joined_ = 0;
   uint64_t gen_ = 0;
+  std::atomic<uint64_t> gen_seen_{0};
   std::atomic<int> finished_{0};
 };
 

@@ -24,6 +24,7 @@ the reduced arena, keeping each original's requires_grad.
 from __future__ import annotations
 
 import copy
+import os
 import threading
 import time
 import weakref
@@ -424,15 +425,21 @@ def pipeline_chunk_elems(total: int, esz: int) -> int:
     return 0 if k == 1 else -(-total // k)
 
 
-# Host results below this many bytes come back into pageable memory (the
-# runtime stages the copy): a fresh page-locked block costs far more than the
-# staged copy of a small model (hipHostMalloc ~0.2 ms against ~0.05 ms for a
-# GNLeNet result, scripts/probe_result_alloc.py), and a result the caller
-# keeps would hold the pinned block for its lifetime.
+# Host results come back into page-locked memory from torch's caching host
+# allocator: the D2H is then asynchronous, so the output module is built while
+# the pipeline still runs (round 4), and once the simulation's results turn
+# over, a result reuses a freed block (a fresh hipHostMalloc costs ~0.2 ms,
+# scripts/probes/probe_result_alloc.py). DLSIM_HOST_RESULT=pageable restores
+# round 3's rule for A/B runs: results below PAGEABLE_RESULT_BYTES in pageable
+# memory (the runtime stages that copy, and the library call waits for it).
 PAGEABLE_RESULT_BYTES = 4 << 20
+HOST_RESULT_PINNED = os.environ.get("DLSIM_HOST_RESULT", "pinned") != "pageable"
+# Wake the library's pack threads when a task's models are on the host, before
+# the task's own host work (DLSIM_HOST_PREWARM=0 disables it, for A/B runs).
+HOST_PREWARM = os.environ.get("DLSIM_HOST_PREWARM", "1") != "0"
 
 
-def _host_pipeline(all_params, idx, layout, dt, dev, out, weights_f32, mode, stream, want_host):
+def _host_pipeline(all_params, idx, layout, dt, dev, out, weights_f32, mode, stream, want_host, defer=False):
     """Host models -> device reduce (-> host result) in one dlsim_host_wreduce
     call: the parameters are packed into pinned staging rows by the library's
     thread pool (torch's intra-op thread count), chunk by chunk of the
@@ -442,17 +449,20 @@ def _host_pipeline(all_params, idx, layout, dt, dev, out, weights_f32, mode, str
     stream (PCIe is full duplex). Bytes and results are those of the
     unchunked reduce (elements are independent). One-chunk models use the
     caller's stream for everything (the side-stream events cost more than
-    they hide there). Returns (the pinned host result (want_host; complete
-    once `stream` is) or None (the result is in `out`, queued on `stream`),
-    whether a non-contiguous tensor was copied)."""
+    they hide there). Returns (the host result (want_host; complete once
+    `stream` is) or None (the result is in `out`, queued on `stream`),
+    whether a non-contiguous tensor was copied, whether the caller must still
+    wait for `stream` before reading the host result: defer and a page-locked
+    result; otherwise this call has waited)."""
     n = len(all_params)
     total = layout.totals[dt]
     esz = out.element_size()
     chunk = pipeline_chunk_elems(total, esz)
     h2d, d2h = _side_streams(dev) if chunk else (None, None)
     host = None
+    pinned_result = want_host and (HOST_RESULT_PINNED or total * esz >= PAGEABLE_RESULT_BYTES)
     if want_host:
-        host = torch.empty(total, dtype=dt, pin_memory=total * esz >= PAGEABLE_RESULT_BYTES)
+        host = torch.empty(total, dtype=dt, pin_memory=pinned_result)
     # the layout checked every tensor's shape and dtype against models[0];
     # the library reads data pointers, so only non-contiguous ones are copied
     keep, ptrs = _data_ptrs(all_params, idx)
@@ -462,14 +472,14 @@ def _host_pipeline(all_params, idx, layout, dt, dev, out, weights_f32, mode, str
         _native.host_wreduce_raw(ptrs, n, layout.split_sizes[dt], weights_f32, pinned, dev_rows, out, host,
                                  _native.dtype_code(dt), mode, chunk, torch.get_num_threads(), stream.cuda_stream,
                                  h2d, d2h)
-        if want_host:
-            # the host result is complete once `stream` is, and the caller
-            # waits for it anyway: wait here, and hand the rows back free
+        if want_host and not (defer and pinned_result):
+            # the host result is complete once `stream` is: wait here, and
+            # hand the rows back free
             stream.synchronize()
             synced = True
     finally:
         STAGING.release(dev, dt, stream, synced)
-    return host, bool(keep)
+    return host, bool(keep), want_host and not synced
 
 
 def _data_ptrs(all_params, idx):
@@ -507,9 +517,9 @@ def _staged_reduce(all_params, idx, dt, dev, out, weights, mode, stream):
 
 def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, mode: int,
                              device=None, timing: Optional[dict] = None, host_out: Optional[bool] = False,
-                             weights_f64: Optional[np.ndarray] = None
+                             weights_f64: Optional[np.ndarray] = None, defer_host_sync: bool = False
                              ) -> Tuple[ParamLayout, Dict[torch.dtype, torch.Tensor], torch.device, bool, bool,
-                                        bool]:
+                                        bool, bool]:
     """Reduce the parameters of `models` into one fresh arena per dtype.
 
     weights_f32: the fp32-rounded weights (fp32/bf16/fp16 groups);
@@ -517,11 +527,13 @@ def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, m
     group (fedavg.py:25 keeps the Python float exact for a double tensor);
     default: widened fp32.
     host_out None: as the reference's output, iff models[0]'s parameters are on
-    the host. Returns (layout, arenas, device, on_host, host_out, staged):
-    staged = some group went through a path that also takes non-contiguous
-    tensors (the caller then gives such parameters models[0]'s strides). With
-    host_out, host models take the chunked pipeline and come back already in
-    host memory (on_host True, copies complete); otherwise the arenas are on
+    the host. Returns (layout, arenas, device, on_host, host_out, staged,
+    pending): staged = some group went through a path that also takes
+    non-contiguous tensors (the caller then gives such parameters models[0]'s
+    strides). With host_out, host models take the chunked pipeline and come
+    back in host memory (on_host True): complete, or with defer_host_sync
+    still in flight on the device's current stream (pending True: the caller
+    waits for that stream before reading them). Otherwise the arenas are on
     the device."""
     layout, all_params, in_views = input_arenas(models)
     if host_out is None:
@@ -542,7 +554,7 @@ def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, m
     host_models = all(not all_params[i][idx[0]].is_cuda
                       for idx in layout.groups.values() for i in range(n))
     piped = host_out and host_models and len(layout.groups) > 0
-    staged = False
+    staged = pending = False
     with torch.no_grad():
         for dt, idx in layout.groups.items():
             total = layout.totals[dt]
@@ -585,9 +597,10 @@ def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, m
                 # host models (the reference's case): chunked pack / H2D /
                 # reduce (/ D2H) pipeline
                 st.mark("layout")
-                h, copied = _host_pipeline(all_params, idx, layout, dt, dev, out, weights_f32, mode, get_stream(),
-                                           piped)
+                h, copied, waits = _host_pipeline(all_params, idx, layout, dt, dev, out, weights_f32, mode,
+                                                  get_stream(), piped, defer_host_sync)
                 staged = staged or copied
+                pending = pending or waits
                 if h is not None:
                     outs[dt] = h
                 st.mark("pipeline")
@@ -600,12 +613,13 @@ def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, m
             st.mark("kernel")
     if piped:
         left = {dt: a for dt, a in outs.items() if a.is_cuda}
-        if left:  # single-chunk groups: their D2H now
+        if left:  # single-chunk groups: their D2H now (and the wait)
             outs.update(arenas_to_host(left, get_stream()))
+            pending = False
             st.mark("d2h")
-        else:
+        elif not pending:
             get_stream().synchronize()
-    return layout, outs, dev, piped, host_out, staged
+    return layout, outs, dev, piped, host_out, staged, pending
 
 
 def arenas_to_host(arenas: Dict[torch.dtype, torch.Tensor], stream) -> Dict[torch.dtype, torch.Tensor]:
@@ -841,11 +855,17 @@ def aggregate_modules(models: List[nn.Module], weights: Optional[Sequence[float]
     else:
         assert len(weights) == len(models)
     model0 = models[0]  # IndexError for an empty list, as the reference
+    if HOST_PREWARM:
+        _prewarm_if_host(model0)
     w32 = _native.fp32_weights(weights)
-    layout, arenas, dev, on_host, host_out, staged = reduce_modules_to_arenas(models, w32, mode, device, timing,
-                                                                              to_host, weights_f64=weights)
+    layout, arenas, dev, on_host, host_out, staged, pending = reduce_modules_to_arenas(
+        models, w32, mode, device, timing, to_host, weights_f64=weights, defer_host_sync=timing is None)
     if timing is None and not (host_out and not on_host):
+        # the output module is built while a host result's copies may still
+        # run (pending); it only makes views of the result
         out = module_from_arenas(model0, layout, arenas)
+        if pending:
+            torch.cuda.current_stream(dev).synchronize()
         return _restride(out, layout) if staged else out
     stream = torch.cuda.current_stream(dev)
     st = _Stages(timing, stream)
@@ -857,6 +877,15 @@ def aggregate_modules(models: List[nn.Module], weights: Optional[Sequence[float]
         _restride(out, layout)
     st.mark("module")
     return out
+
+
+def _prewarm_if_host(model0: nn.Module) -> None:
+    """models[0]'s first parameter on the host: the task is a host pipeline
+    (or a copy), so wake the library's pack threads now; they are awake by
+    the time the task's own host work reaches the pack."""
+    ps = module_params(model0)
+    if ps and not ps[0].is_cuda:
+        _native.host_prewarm(torch.get_num_threads())
 
 
 def _restride(out: nn.Module, layout: ParamLayout) -> nn.Module:

@@ -17,6 +17,11 @@ every aggregate reads host models: the executor uploads each wave's models
 once, the sequential worker loop stages them per task.
 
     python scripts/bench_rounds.py [--peers 100] [--rounds 4] [--host] [--model gnlenet|flat|resnet18]
+
+BASELINE.json configs[0] (cfg1: the 2-peer D-PSGD average of the default
+CIFAR-10 model, tests/test_dpsgd.py:26-35) is `--peers 2 --host`: every
+aggregate is functions.aggregate of 2 host GNLeNet modules, the reference's
+own worker path (functions.py:89-106), against its op sequence at 4 threads.
 """
 from __future__ import annotations
 
@@ -340,8 +345,10 @@ def main():
                                              * 1e6, 1),
                 "gc_collections_by_generation": gc_n[kind]}
 
+    from bench import box_info
+    box = box_info()
     for kind in samples:
-        print(json.dumps(line(kind)), flush=True)
+        print(json.dumps(dict(line(kind), box=box)), flush=True)
 
 
 if __name__ == "__main__":

@@ -28,3 +28,13 @@ for f in $O/bench_*.json; do
   python3 -c "import json,sys; d=json.load(open('$f')); print('$(basename $f)', d['ms_per_step'], d['roofline']['frac'], d['pattern_ceiling']['frac'])"
 done
 step done
+step host_task_parts
+timeout -k 10 300 python3 -u scripts/probes/probe_host_task_parts.py 400 > $O/host_task_parts.json 2> $O/host_task_parts.err || exit $?
+cat $O/host_task_parts.json
+step cfg1
+timeout -k 10 400 python3 -u scripts/bench_rounds.py --peers 2 --host --rounds 300 --cpu-rounds 300 > $O/cfg1.jsonl 2> $O/cfg1.err || exit $?
+cut -c1-300 $O/cfg1.jsonl
+step rounds_host_100
+timeout -k 10 400 python3 -u scripts/bench_rounds.py --peers 100 --host > $O/rounds_host_100.jsonl 2> $O/rounds_host_100.err || exit $?
+cut -c1-300 $O/rounds_host_100.jsonl
+step done2

@@ -1,0 +1,127 @@
+"""Probe (round 4): where one host-model aggregate task's
+time goes outside the library pipeline.
+
+7 x GNLeNet (the reference's module tree, fan-in 7 = its 100-peer D-PSGD
+default), host tensors in, host module out, at the worker's 4 torch threads
+(broker.py:31). The task's steps are replayed one by one as
+FedAvg.aggregate -> arena.aggregate_modules runs them (input_arenas, the
+device output arena, the host result, the data pointers, the staging rows,
+dlsim_host_wreduce, the wait, the release, the output module), each timed
+with perf_counter and NO extra synchronisation (the one wait is the path's
+own), medians over REPS tasks; then the whole FedAvg.aggregate call alone.
+Prints one JSON line.
+
+    python scripts/probes/probe_host_task_parts.py [reps]
+"""
+from __future__ import annotations
+
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+for p in (ROOT, os.path.join(ROOT, "scripts"), os.path.join(ROOT, "decentralized-learning-simulator_amd")):
+    sys.path.insert(0, p)
+
+import torch  # noqa: E402
+
+from bench_rounds import GNLeNetTree  # noqa: E402
+from dasklearn_amd import _native, arena  # noqa: E402
+from dasklearn_amd.gradient_aggregation.fedavg import FedAvg  # noqa: E402
+
+
+def parts_once(models, dev, stream):
+    n = len(models)
+    marks = []
+    t0 = time.perf_counter()
+
+    def mark(name):
+        nonlocal t0
+        now = time.perf_counter()
+        marks.append((name, now - t0))
+        t0 = now
+
+    weights = [float(1. / n) for _ in range(n)]
+    w32 = _native.fp32_weights(weights)
+    mark("weights")
+    layout, all_params, _ = arena.input_arenas(models)
+    mark("input_arenas")
+    (dt, idx), = layout.groups.items()
+    total = layout.totals[dt]
+    out = arena.arena_empty(total, dt, dev)
+    mark("device_out_alloc")
+    pinned_result = arena.HOST_RESULT_PINNED or total * 4 >= arena.PAGEABLE_RESULT_BYTES
+    host = torch.empty(total, dtype=dt, pin_memory=pinned_result)
+    mark("host_result_alloc")
+    keep, ptrs = arena._data_ptrs(all_params, idx)
+    mark("data_ptrs")
+    rows, pinned = arena.STAGING.acquire(dev, dt, n, total, stream)
+    mark("staging_acquire")
+    _native.host_wreduce_raw(ptrs, n, layout.split_sizes[dt], w32, pinned, rows, out, host, _native.dtype_code(dt),
+                             _native.DLSIM_EXACT, 0, torch.get_num_threads(), stream.cuda_stream, None, None)
+    mark("native_call")
+    if not pinned_result:  # round 3: wait, then build the module
+        stream.synchronize()
+        mark("stream_wait")
+    arena.STAGING.release(dev, dt, stream, not pinned_result)
+    mark("staging_release")
+    res = arena.module_from_arenas(models[0], layout, {dt: host})
+    mark("output_module")
+    if pinned_result:  # round 4: the module is built while the copies run
+        stream.synchronize()
+        mark("stream_wait")
+    return marks, res
+
+
+def fedavg_us(models, reps):
+    for _ in range(20):
+        FedAvg.aggregate(models, None)
+    ts = []
+    for _ in range(reps):
+        t = time.perf_counter()
+        FedAvg.aggregate(models, None)
+        ts.append(time.perf_counter() - t)
+    ts.sort()
+    return round(statistics.median(ts) * 1e6, 1), [round(ts[len(ts) // 10] * 1e6, 1), round(ts[len(ts) * 9 // 10] * 1e6, 1)]
+
+
+def main():
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 400
+    torch.set_num_threads(4)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    stream = torch.cuda.current_stream(dev)
+    torch.manual_seed(0)
+    models = [GNLeNetTree() for _ in range(7)]
+    res = {"model": "gnlenet_tree", "n": 7, "threads": torch.get_num_threads(), "reps": reps,
+           "pack_spin_us": os.environ.get("DLSIM_PACK_SPIN_US", "200 (default)")}
+    for pinned in (False, True):
+        arena.HOST_RESULT_PINNED = pinned
+        for _ in range(20):
+            parts_once(models, dev, stream)
+        acc, totals = {}, []
+        for _ in range(reps):
+            t = time.perf_counter()
+            marks, _ = parts_once(models, dev, stream)
+            totals.append(time.perf_counter() - t)
+            for k, v in marks:
+                acc.setdefault(k, []).append(v)
+        key = "pinned_deferred" if pinned else "pageable_r03"
+        res[f"parts_us_median_{key}"] = {k: round(statistics.median(v) * 1e6, 1) for k, v in acc.items()}
+        res[f"parts_sum_us_median_{key}"] = round(statistics.median(totals) * 1e6, 1)
+    # the whole call, interleaved variants: result memory x prewarm
+    for rnd in range(2):
+        for pinned in (False, True):
+            for prewarm in (False, True):
+                arena.HOST_RESULT_PINNED, arena.HOST_PREWARM = pinned, prewarm
+                med, p1090 = fedavg_us(models, reps)
+                k = f"fedavg_us_{'pinned' if pinned else 'pageable'}_{'prewarm' if prewarm else 'noprewarm'}"
+                res.setdefault(k, []).append(med)
+                res.setdefault(k + "_p10_p90", []).append(p1090)
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

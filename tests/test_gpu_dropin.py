@@ -189,9 +189,11 @@ def test_device_resident_option_keeps_result_on_gpu():
 
 
 def test_host_result_placement_and_stage_timing_works():
-    """Host models -> host result: a small result comes back in pageable
-    memory (arena.PAGEABLE_RESULT_BYTES), a large one in page-locked memory;
-    both exact."""
+    """Host models -> host result: in page-locked memory (round 4: the D2H is
+    asynchronous and the output module is built meanwhile; the call returns a
+    complete result), small and large; under DLSIM_HOST_RESULT=pageable's
+    rule (arena.HOST_RESULT_PINNED False) a small result comes back in
+    pageable memory. All exact, the timed variant too."""
     from dasklearn_amd import _native, arena
     from dasklearn_amd.arena import aggregate_modules
     g = load_golden(os.path.join(GOLDEN, "cfg1_gnlenet_f32_n2_none.npz"))
@@ -199,9 +201,20 @@ def test_host_result_placement_and_stage_timing_works():
     stages = {}
     out = aggregate_modules(models, None, _native.DLSIM_EXACT, timing=stages)
     assert set(stages) >= {"layout", "pipeline", "module"}  # the D2H is part of the pipeline
-    p0 = next(out.parameters())
-    assert not p0.is_cuda and not p0.is_pinned()  # 341 KB < PAGEABLE_RESULT_BYTES
     assert orc.same_bits(flat_of(out), g["expected"])
+    for _ in range(3):  # the deferred wait: read right after the call returns
+        out = aggregate_modules(models, None, _native.DLSIM_EXACT)
+        p0 = next(out.parameters())
+        assert not p0.is_cuda and p0.is_pinned()
+        assert orc.same_bits(flat_of(out), g["expected"])
+    saved = arena.HOST_RESULT_PINNED
+    arena.HOST_RESULT_PINNED = False
+    try:
+        out = aggregate_modules(models, None, _native.DLSIM_EXACT)
+        assert not next(out.parameters()).is_pinned()  # 341 KB < PAGEABLE_RESULT_BYTES
+        assert orc.same_bits(flat_of(out), g["expected"])
+    finally:
+        arena.HOST_RESULT_PINNED = saved
     torch.manual_seed(9)
     big = [Ragged([(arena.PAGEABLE_RESULT_BYTES // 4 + 1000,), (77,)]) for _ in range(3)]
     with torch.no_grad():
