@@ -9,6 +9,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -97,6 +98,14 @@ void pack_and_dispatch(dlsim::PackJob& job, int threads, size_t in_bytes, F&& on
     }
   }
   if (helpers > 0) pool.join();
+}
+
+// Smallest H2D run of a one-chunk dlsim_host_wreduce (DLSIM_H2D_MIN_KB, read
+// per call: A/B probes; default 1 MiB).
+size_t h2d_min_bytes() {
+  const char* e = std::getenv("DLSIM_H2D_MIN_KB");
+  const long kb = e ? std::strtol(e, nullptr, 10) : 1024;
+  return static_cast<size_t>(kb > 0 ? kb : 0) << 10;
 }
 
 // dlsim_host_chunk_mean jobs below this many staged bytes take the one-DMA
@@ -400,23 +409,41 @@ int dlsim_host_wreduce(int n, int t, const void* const* h_srcs, const size_t* nu
                                         hipMemcpyDeviceToHost, d2h);
     if (e != hipSuccess) ln.rc = hip_fail(e, "result D2H");
   };
+  // One chunk: packed rows go H2D in runs of at least min_dma bytes (the last
+  // run whatever is left). A DMA costs ~8 us of copy-engine time beyond its
+  // bytes, so one per 341 KB GNLeNet row made the copies, not the pack, the
+  // task's critical path (7 rows: ~105 us against 50 us for one 2.4 MB DMA);
+  // two runs overlap the first one's copy with the rest of the pack
+  // (DLSIM_H2D_MIN_KB overrides the 1 MiB, for A/B runs).
+  const size_t min_dma = h2d_min_bytes();
+  size_t pending = 0;  // first row not yet sent (one chunk)
   pack_and_dispatch(job, threads, total * esz * n, [&](size_t u0, size_t u1) {
-    for (size_t u = u0; u < u1 && ln.rc == DLSIM_OK;) {
-      const size_t c = u / n, i = u % n;
-      const size_t c0 = c * chunk, c1 = std::min(total, c0 + chunk);
-      // units of one chunk in the run: rows [i, j) of chunk c. With one chunk
-      // they are consecutive whole rows, one DMA (latency, not bandwidth,
-      // bounds small models: one copy per model was 7 DMAs for a GNLeNet task)
-      const size_t j = n_chunks == 1 ? std::min(static_cast<size_t>(n), i + (u1 - u)) : i + 1;
-      const size_t o = i * row_bytes + c0 * esz;
-      const size_t bytes = (j - i - 1) * row_bytes + (c1 - c0) * esz;
+    if (n_chunks == 1) {
+      if (ln.rc != DLSIM_OK) return;
+      const size_t j = u1;  // rows [pending, j) are packed
+      if (j < static_cast<size_t>(n) && (j - pending) * row_bytes < min_dma) return;
+      const size_t o = pending * row_bytes;
+      const size_t bytes = (j - pending - 1) * row_bytes + total * esz;
       const hipError_t e = hipMemcpyAsync(rows + o, stage + o, bytes, hipMemcpyHostToDevice, h2d);
       if (e != hipSuccess) {
         ln.rc = hip_fail(e, "staging H2D");
         return;
       }
-      u += j - i;
-      if (j == static_cast<size_t>(n)) finish_chunk(c);
+      pending = j;
+      if (j == static_cast<size_t>(n)) finish_chunk(0);
+      return;
+    }
+    for (size_t u = u0; u < u1 && ln.rc == DLSIM_OK; ++u) {
+      // several chunks: one DMA per unit (model i's share of chunk c, ~8 MiB)
+      const size_t c = u / n, i = u % n;
+      const size_t c0 = c * chunk, c1 = std::min(total, c0 + chunk);
+      const size_t o = i * row_bytes + c0 * esz;
+      const hipError_t e = hipMemcpyAsync(rows + o, stage + o, (c1 - c0) * esz, hipMemcpyHostToDevice, h2d);
+      if (e != hipSuccess) {
+        ln.rc = hip_fail(e, "staging H2D");
+        return;
+      }
+      if (i + 1 == static_cast<size_t>(n)) finish_chunk(c);
     }
   });
   if (h_out) ln.link(d2h, st, "order stream after D2H");
@@ -550,13 +577,6 @@ int dlsim_host_chunk_mean(int b, const int* fan_in, const void* const* h_inputs,
   });
   if (h_outs) ln.link(d2h, st, "order stream after D2H");
   return ln.rc;
-}
-
-int dlsim_host_prewarm(int threads) {
-  g_err.clear();
-  if (threads < 1) return fail(DLSIM_E_ARG, "threads must be >= 1 (got %d)", threads);
-  dlsim::PackPool::get().prewarm(std::min(threads, 64) - 1);
-  return DLSIM_OK;
 }
 
 int dlsim_host_pack(int t, const void* const* h_srcs, const size_t* nbytes, const size_t* dst_off, void* h_dst,

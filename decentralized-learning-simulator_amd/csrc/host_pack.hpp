@@ -10,11 +10,11 @@
 // one pipeline chunk): the dispatching thread starts a unit's DMA as soon as
 // the unit is packed, while the other threads already pack the next ones.
 //
-// Plain C++ (no device code). The pool's threads are created once; between
-// calls they spin for a short while (DLSIM_PACK_SPIN_US, default 200 us) so
-// that back-to-back host tasks find them awake, then sleep. A caller can wake
-// them ahead of a job (prewarm). A process that forks gets a fresh pool in the
-// child.
+// Plain C++ (no device code). The pool's threads are created once and sleep
+// between calls; a process that forks gets a fresh pool in the child. (Round
+// 4 measured helpers that spin between calls, and a wake-up ahead of the
+// job: no gain on a GNLeNet host task, whose pack is not its critical path;
+// DESIGN.md §6.)
 #pragma once
 
 #include <emmintrin.h>
@@ -22,7 +22,6 @@
 
 #include <algorithm>
 #include <atomic>
-#include <chrono>
 #include <cstdlib>
 #include <condition_variable>
 #include <cstdint>
@@ -150,7 +149,7 @@ class PackPool {
     helpers_ = helpers;
     joined_ = 0;
     finished_.store(0, std::memory_order_relaxed);
-    bump();
+    ++gen_;
     cv_.notify_all();
   }
   // Close the job to helpers that have not joined it, then wait until every
@@ -164,38 +163,14 @@ class PackPool {
     }
     while (finished_.load(std::memory_order_acquire) < joined) std::this_thread::yield();
   }
-  // Wake `helpers` threads without a job: they spin for the next one (a
-  // caller that knows a host job is coming calls this first). Skipped while
-  // a job runs.
-  void prewarm(int helpers) {
-    std::unique_lock<std::mutex> call(call_mu_, std::try_to_lock);
-    if (!call.owns_lock() || helpers < 1) return;
-    grow(helpers);
-    std::lock_guard<std::mutex> lk(mu_);
-    job_ = nullptr;
-    helpers_ = helpers;
-    bump();
-    cv_.notify_all();
-  }
 
  private:
-  PackPool() : pid_(getpid()), spin_ns_(spin_ns_from_env()) {}
-
-  static int64_t spin_ns_from_env() {
-    const char* e = std::getenv("DLSIM_PACK_SPIN_US");
-    const long us = e ? std::strtol(e, nullptr, 10) : 200;
-    return us > 0 ? static_cast<int64_t>(us) * 1000 : 0;
-  }
-
-  void bump() {  // with mu_ held
-    ++gen_;
-    gen_seen_.store(gen_, std::memory_order_release);
-  }
+  PackPool() : pid_(getpid()) {}
 
   void grow(int helpers) {
     while (static_cast<int>(threads_) < helpers) {
-      // gen_ changes only in start()/prewarm(), after this: the new thread
-      // takes part from the coming job on
+      // gen_ changes only in start(), after this: the new thread takes
+      // part from the coming job on
       const int id = static_cast<int>(threads_++);
       const uint64_t seen = gen_;
       std::thread([this, id, seen] { loop(id, seen); }).detach();
@@ -204,20 +179,12 @@ class PackPool {
 
   void loop(int id, uint64_t seen) {
     for (;;) {
-      // spin a while for the next generation before sleeping on the condvar
-      if (spin_ns_ > 0) {
-        const auto t0 = std::chrono::steady_clock::now();
-        while (gen_seen_.load(std::memory_order_acquire) == seen &&
-               std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count() <
-                   spin_ns_)
-          _mm_pause();
-      }
       PackJob* job;
       {
         std::unique_lock<std::mutex> lk(mu_);
         cv_.wait(lk, [&] { return gen_ != seen; });
         seen = gen_;
-        if (id >= helpers_ || job_ == nullptr) continue;  // not asked, a prewarm, or already closed
+        if (id >= helpers_ || job_ == nullptr) continue;  // not asked, or the job is already closed
         job = job_;
         ++joined_;
       }
@@ -228,7 +195,6 @@ class PackPool {
   }
 
   const pid_t pid_;
-  const int64_t spin_ns_;
   std::mutex call_mu_;
   std::mutex mu_;
   std::condition_variable cv_;
@@ -237,7 +203,6 @@ class PackPool {
   int helpers_ = 0;
   int joined_ = 0;
   uint64_t gen_ = 0;
-  std::atomic<uint64_t> gen_seen_{0};
   std::atomic<int> finished_{0};
 };
 

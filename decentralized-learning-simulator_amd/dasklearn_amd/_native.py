@@ -54,7 +54,6 @@ EXPORTS = (
     "dlsim_host_wreduce",
     "dlsim_host_chunk_mean",
     "dlsim_host_pack",
-    "dlsim_host_prewarm",
     "dlsim_shard_range",
     "dlsim_probe_pattern",
     "dlsim_last_error",
@@ -145,8 +144,6 @@ def load() -> ctypes.CDLL:
         lib.dlsim_host_chunk_mean.restype = i
         lib.dlsim_host_pack.argtypes = [i, ctypes.POINTER(vp), ctypes.POINTER(sz), ctypes.POINTER(sz), vp, i]
         lib.dlsim_host_pack.restype = i
-        lib.dlsim_host_prewarm.argtypes = [i]
-        lib.dlsim_host_prewarm.restype = i
         lib.dlsim_shard_range.argtypes = [sz, i, i, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)]
         lib.dlsim_shard_range.restype = i
         lib.dlsim_probe_pattern.argtypes = [ctypes.POINTER(vp), i, vp, sz, i, vp]
@@ -843,11 +840,6 @@ def host_wreduce(inputs_by_model, weights_f32, staging, rows, out, host_out=None
         None if d2h_stream is None else d2h_stream.cuda_stream)
     _check("dlsim_host_wreduce", rc)
     return out
-
-
-def host_prewarm(threads: int) -> None:
-    """dlsim_host_prewarm: wake the pack threads ahead of a host call."""
-    _check("dlsim_host_prewarm", load().dlsim_host_prewarm(max(1, int(threads))))
 
 
 def host_pack(srcs, dst_offsets, dst, threads: Optional[int] = None):

@@ -434,9 +434,6 @@ def pipeline_chunk_elems(total: int, esz: int) -> int:
 # memory (the runtime stages that copy, and the library call waits for it).
 PAGEABLE_RESULT_BYTES = 4 << 20
 HOST_RESULT_PINNED = os.environ.get("DLSIM_HOST_RESULT", "pinned") != "pageable"
-# Wake the library's pack threads when a task's models are on the host, before
-# the task's own host work (DLSIM_HOST_PREWARM=0 disables it, for A/B runs).
-HOST_PREWARM = os.environ.get("DLSIM_HOST_PREWARM", "1") != "0"
 
 
 def _host_pipeline(all_params, idx, layout, dt, dev, out, weights_f32, mode, stream, want_host, defer=False):
@@ -855,8 +852,6 @@ def aggregate_modules(models: List[nn.Module], weights: Optional[Sequence[float]
     else:
         assert len(weights) == len(models)
     model0 = models[0]  # IndexError for an empty list, as the reference
-    if HOST_PREWARM:
-        _prewarm_if_host(model0)
     w32 = _native.fp32_weights(weights)
     layout, arenas, dev, on_host, host_out, staged, pending = reduce_modules_to_arenas(
         models, w32, mode, device, timing, to_host, weights_f64=weights, defer_host_sync=timing is None)
@@ -877,15 +872,6 @@ def aggregate_modules(models: List[nn.Module], weights: Optional[Sequence[float]
         _restride(out, layout)
     st.mark("module")
     return out
-
-
-def _prewarm_if_host(model0: nn.Module) -> None:
-    """models[0]'s first parameter on the host: the task is a host pipeline
-    (or a copy), so wake the library's pack threads now; they are awake by
-    the time the task's own host work reaches the pack."""
-    ps = module_params(model0)
-    if ps and not ps[0].is_cuda:
-        _native.host_prewarm(torch.get_num_threads())
 
 
 def _restride(out: nn.Module, layout: ParamLayout) -> nn.Module:

@@ -410,16 +410,6 @@ int dlsim_host_pack(int t, const void* const* h_srcs, const size_t* nbytes, cons
                     int threads);
 
 /*
- * dlsim_host_prewarm — wake the host entry points' pack threads ahead of a
- * call (threads - 1 helpers, as the call's `threads` will ask for): they spin
- * for the job instead of being woken by it. A caller that knows a host
- * aggregate is coming (it has seen host models) calls this first; between
- * calls the helpers spin for DLSIM_PACK_SPIN_US (default 200) microseconds,
- * then sleep. No effect while another thread's host call runs. Host-only.
- */
-int dlsim_host_prewarm(int threads);
-
-/*
  * dlsim_shard_range — parameter-axis partition used by the sharded path.
  *
  * Splits [0, n_elems) into `world` contiguous slices whose boundaries are

@@ -95,10 +95,10 @@ def main():
     stream = torch.cuda.current_stream(dev)
     torch.manual_seed(0)
     models = [GNLeNetTree() for _ in range(7)]
-    res = {"model": "gnlenet_tree", "n": 7, "threads": torch.get_num_threads(), "reps": reps,
-           "pack_spin_us": os.environ.get("DLSIM_PACK_SPIN_US", "200 (default)")}
+    res = {"model": "gnlenet_tree", "n": 7, "threads": torch.get_num_threads(), "reps": reps}
     for pinned in (False, True):
         arena.HOST_RESULT_PINNED = pinned
+        os.environ["DLSIM_H2D_MIN_KB"] = "1024" if pinned else "0"  # round 4's path / round 3's
         for _ in range(20):
             parts_once(models, dev, stream)
         acc, totals = {}, []
@@ -111,15 +111,19 @@ def main():
         key = "pinned_deferred" if pinned else "pageable_r03"
         res[f"parts_us_median_{key}"] = {k: round(statistics.median(v) * 1e6, 1) for k, v in acc.items()}
         res[f"parts_sum_us_median_{key}"] = round(statistics.median(totals) * 1e6, 1)
-    # the whole call, interleaved variants: result memory x prewarm
+    # the whole call, interleaved variants: result memory x smallest H2D run
+    # (DLSIM_H2D_MIN_KB, read per call by the library: 0 = every packed run at
+    # once, as round 3; 4096 = one DMA for the task's 2.4 MB)
     for rnd in range(2):
         for pinned in (False, True):
-            for prewarm in (False, True):
-                arena.HOST_RESULT_PINNED, arena.HOST_PREWARM = pinned, prewarm
+            for kb in ("0", "512", "1024", "4096"):
+                arena.HOST_RESULT_PINNED = pinned
+                os.environ["DLSIM_H2D_MIN_KB"] = kb
                 med, p1090 = fedavg_us(models, reps)
-                k = f"fedavg_us_{'pinned' if pinned else 'pageable'}_{'prewarm' if prewarm else 'noprewarm'}"
+                k = f"fedavg_us_{'pinned' if pinned else 'pageable'}_h2dmin{kb}k"
                 res.setdefault(k, []).append(med)
                 res.setdefault(k + "_p10_p90", []).append(p1090)
+    os.environ.pop("DLSIM_H2D_MIN_KB")
     print(json.dumps(res), flush=True)
 
 
