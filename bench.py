@@ -123,9 +123,6 @@ def parse(argv=None):
                     help="process-group backend: nccl (= RCCL over xGMI, the real path); gloo only "
                          "to rehearse the multi-process flow on a box with fewer GPUs than ranks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-gate", action="store_true",
-                    help="start the timing window on an idle GPU (the start event then also times the host's "
-                         "enqueue of the first launch); default: a short GPU spin before the start event")
     ap.add_argument("--two-streams", action="store_true",
                     help="diagnostic: also time the K steps alternating over two streams (field two_streams); "
                          "off by default because those overlapping dispatches would enter a rocprof average "
@@ -177,25 +174,18 @@ def spawn_ranks(n: int, argv, script: str = None) -> int:
 
 # ---- timing ----------------------------------------------------------------------
 
-def time_steps(launch, k_steps: int, sync, barrier, new_event, gate=None):
+def time_steps(launch, k_steps: int, sync, barrier, new_event):
     """Time exactly k_steps launches. The barrier that lines the ranks up and
     a device sync come BEFORE the window; the window is two events on the
     launch stream around the launches (plus a host clock from the first
     launch to the sync after the last); the closing barrier comes AFTER the
-    window is read. Returns (event_ms, wall_ms) for all k_steps.
-
-    gate: enqueued after the sync and before the start event, a short GPU
-    spin (no step, no data) that keeps the stream busy while the host
-    enqueues the start event and the first launches. Without it the start
-    event is stamped on an idle GPU and the window also holds the host's
-    enqueue of launch 0 (~5 us through ctypes: 0.4 % of a 20-step window);
-    with it the window is the K steps' GPU time, as rocprof's per-dispatch
-    durations see them."""
+    window is read. Returns (event_ms, wall_ms) for all k_steps. (Round 4
+    measured a GPU-side gate before the start event, so the window would not
+    hold the host's enqueue of launch 0: no difference at K = 20 or 400,
+    profiles/r04a/placement.jsonl; not kept.)"""
     barrier()
     sync()
     e0, e1 = new_event(), new_event()
-    if gate is not None:
-        gate()
     t0 = time.perf_counter()
     e0.record()
     for k in range(k_steps):
@@ -274,14 +264,14 @@ class ReduceWorkload:
         self.probe_plans[k % self.sets].launch(self.stream)
 
 
-def pattern_ceiling(wl, k_steps: int, sync, new_event, achieved_gbps: float, gate=None):
+def pattern_ceiling(wl, k_steps: int, sync, new_event, achieved_gbps: float):
     """dlsim_probe_pattern over the same rotating sets: the reduce's own
     dispatch (kernel, launch shape, nt loads, store policy) with the weighted
     fold replaced by a bitwise XOR — what the memory system allows for exactly
     this read/write mix, measured in the same run."""
     for k in range(10):
         wl.launch_probe(k)
-    ev_ms, _ = time_steps(wl.launch_probe, k_steps, sync, lambda: None, new_event, gate)
+    ev_ms, _ = time_steps(wl.launch_probe, k_steps, sync, lambda: None, new_event)
     us = ev_ms * 1e3 / k_steps
     gbps = wl.bytes_per_step / (us * 1e-6) / 1e9
     return {"GBps": round(gbps, 1), "frac": round(gbps / HBM_PEAK_GBPS, 4), "us_per_launch": round(us, 3),
@@ -526,13 +516,11 @@ def run_rank(args, rank: int, world: int, local: int):
     new_event = lambda: _StreamEvent(stream)  # noqa: E731
     sync = lambda: torch.cuda.synchronize(dev)  # noqa: E731
 
-    gate = None if args.no_gate else (lambda: _gpu_gate(stream))
-
     wl = ReduceWorkload(n, p, dtype, w32, mode, B, dev, 1234 + rank, stream)
     for k in range(args.warmup):
         wl.launch(k)
     K = args.steps
-    ev_ms, wall_ms = time_steps(wl.launch, K, sync, barrier, new_event, gate)
+    ev_ms, wall_ms = time_steps(wl.launch, K, sync, barrier, new_event)
 
     stats = torch.tensor([ev_ms, wall_ms, float(wl.bytes_per_step) * K], dtype=torch.float64, device=cdev)
     per_rank_us = torch.tensor([ev_ms / K * 1e3], dtype=torch.float64, device=cdev)
@@ -563,7 +551,7 @@ def run_rank(args, rank: int, world: int, local: int):
             full = ReduceWorkload(n, p_cfg, dtype, w32, mode, B, dev, 99, stream)
             for k in range(args.warmup):
                 full.launch(k)
-            t1_ms, _ = time_steps(full.launch, K, sync, lambda: None, new_event, gate)
+            t1_ms, _ = time_steps(full.launch, K, sync, lambda: None, new_event)
             single = {"ms_per_step": round(t1_ms / K, 6),
                       "speedup": round((t1_ms / K) / (max_ev / K), 3),
                       "note": f"T1 = the whole {args.config} aggregate on rank 0's GPU alone, {K} launches, "
@@ -576,7 +564,7 @@ def run_rank(args, rank: int, world: int, local: int):
         achieved = wl.bytes_per_step / (ev_ms / K * 1e-3) / 1e9
         traffic, traffic_src = (pmc_traffic(args.config, args.mode, split) if B == 1
                                 else (None, "no committed PMC summary for batched launches"))
-        probe = pattern_ceiling(wl, K, sync, new_event, achieved, gate) if B == 1 else None
+        probe = pattern_ceiling(wl, K, sync, new_event, achieved) if B == 1 else None
         floor = launch_floor(wl, n, dtype, w32, mode, dev, K, sync, new_event, ev_ms / K * 1e3) \
             if B == 1 else None
         # opt-in: its concurrent launches share the reduce's kernel name, so
@@ -614,9 +602,6 @@ def run_rank(args, rank: int, world: int, local: int):
                        "bytes_per_step_rank0": wl.bytes_per_step},
             "timing": {"value_from": "HIP events around the K launches on each rank's launch stream; "
                                      "value = all ranks' bytes / max over ranks; barriers outside the window",
-                       "gate": None if args.no_gate else
-                       f"torch.cuda._sleep({GATE_CYCLES}) on the launch stream after the sync, before the start "
-                       "event (the window holds the K steps' GPU time, not the host's enqueue of launch 0)",
                        "kernel_avg_us_per_rank": rank_us,
                        "wall_ms_per_step_max": round(max_wall / K, 6)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
@@ -654,16 +639,6 @@ def run_rank(args, rank: int, world: int, local: int):
     if world > 1:
         dist.destroy_process_group()
     return 0
-
-
-GATE_CYCLES = 200_000  # GPU clock cycles (~80-100 us): covers the host's enqueue of the start event + launch 0
-
-
-def _gpu_gate(stream):
-    """The timing gate (time_steps): torch's spin kernel on the launch
-    stream, bounded by its cycle count; it touches no data."""
-    with torch.cuda.stream(stream):
-        torch.cuda._sleep(GATE_CYCLES)
 
 
 class _StreamEvent:

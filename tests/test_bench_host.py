@@ -44,21 +44,6 @@ def test_barriers_are_outside_the_timed_window():
     assert calls[1:-1] == ["sync", 0, 1, 2, 3, 4, "sync"]
 
 
-def test_gate_runs_after_the_sync_and_before_the_window():
-    """The GPU gate is enqueued after the pre-window sync and before the start
-    event; the window still holds exactly the K launches."""
-    calls = []
-
-    class Ev(_ClockEvent):
-        def record(self):
-            calls.append("event")
-            super().record()
-
-    bench.time_steps(lambda k: calls.append(k), 3, lambda: calls.append("sync"), lambda: calls.append("barrier"),
-                     Ev, gate=lambda: calls.append("gate"))
-    assert calls == ["barrier", "sync", "gate", "event", 0, 1, 2, "event", "sync", "barrier"]
-
-
 def test_input_sets_cover_the_infinity_cache():
     # the north star (402.5 MB a step): 3 sets; its 8-rank slice (50.3 MB): 22
     assert bench.n_sets(402_539_112) == 3
