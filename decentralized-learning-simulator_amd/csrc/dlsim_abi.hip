@@ -450,6 +450,90 @@ int dlsim_host_wreduce(int n, int t, const void* const* h_srcs, const size_t* nu
   return ln.rc;
 }
 
+int dlsim_host_wreduce_resident(int n, int t, const void* const* h_srcs, const size_t* numels,
+                                const float* h_weights, const int* resident, void* const* d_rows, void* h_staging,
+                                size_t staging_stride, void* d_out, void* h_out, int dtype, int mode, int threads,
+                                void* stream) {
+  g_err.clear();
+  if (!known_dtype(dtype)) return dtype_fail(dtype);
+  if (mode != DLSIM_EXACT && mode != DLSIM_FAST) return fail(DLSIM_E_MODE, "unsupported mode %d", mode);
+  if (n < 1 || t < 0) return fail(DLSIM_E_ARG, "need n >= 1 and t >= 0 (got %d, %d)", n, t);
+  if (!h_weights || !resident || !d_rows || (t > 0 && (!h_srcs || !numels)))
+    return fail(DLSIM_E_ARG, "null array argument");
+  const size_t esz = elem_bytes(dtype);
+  size_t total = 0;
+  for (int k = 0; k < t; ++k) total += numels[k];
+  if (total == 0) return DLSIM_OK;
+  if (!d_out) return fail(DLSIM_E_ARG, "null output");
+  int misses = 0;
+  for (int i = 0; i < n; ++i) {
+    if (!d_rows[i]) return fail(DLSIM_E_ARG, "null device row %d", i);
+    if (!aligned16(d_rows[i])) return fail(DLSIM_E_ARG, "device row %d is not 16-B aligned", i);
+    const uintptr_t r0 = reinterpret_cast<uintptr_t>(d_rows[i]), r1 = r0 + total * esz;
+    const uintptr_t o0 = reinterpret_cast<uintptr_t>(d_out), o1 = o0 + total * esz;
+    if (o0 < r1 && r0 < o1) return fail(DLSIM_E_ARG, "d_out overlaps device row %d", i);
+    if (resident[i]) continue;
+    ++misses;
+    for (int k = 0; k < t; ++k)
+      if (!h_srcs[static_cast<size_t>(i) * t + k] && numels[k] > 0)
+        return fail(DLSIM_E_ARG, "null source pointer (model %d, tensor %d)", i, k);
+  }
+  if (misses > 0) {
+    if (!h_staging || !aligned16(h_staging) || staging_stride % 8 != 0 || staging_stride < total)
+      return fail(DLSIM_E_ARG, "staging: 16-B aligned rows of >= %zu elements, stride a multiple of 8", total);
+  }
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  char* stage = static_cast<char*>(h_staging);
+  const size_t row_bytes = staging_stride * esz;
+  // The models not resident: model miss[j] is packed into staging row j, then
+  // sent to d_rows[miss[j]]; consecutive misses whose device rows are one
+  // staging stride apart go in one DMA (a cache fills them that way).
+  std::vector<int> miss;
+  dlsim::PackJob job;
+  for (int i = 0; i < n; ++i) {
+    if (resident[i]) continue;
+    const uint32_t j = static_cast<uint32_t>(miss.size());
+    miss.push_back(i);
+    size_t o = 0;
+    for (int k = 0; k < t; ++k) {
+      if (numels[k] > 0)
+        job.add(j, static_cast<const char*>(h_srcs[static_cast<size_t>(i) * t + k]), stage + j * row_bytes + o * esz,
+                numels[k] * esz);
+      o += numels[k];
+    }
+  }
+  job.seal(miss.size());
+  int rc = DLSIM_OK;
+  size_t sent = 0;  // first packed row not yet sent
+  auto send = [&](size_t j1) {  // rows [sent, j1) are packed: DMA them in device-contiguous runs
+    while (sent < j1 && rc == DLSIM_OK) {
+      size_t e = sent + 1;
+      while (e < j1 && static_cast<const char*>(d_rows[miss[e]]) ==
+                           static_cast<const char*>(d_rows[miss[e - 1]]) + row_bytes)
+        ++e;
+      const size_t bytes = (e - sent - 1) * row_bytes + total * esz;
+      const hipError_t err = hipMemcpyAsync(d_rows[miss[sent]], stage + sent * row_bytes, bytes,
+                                            hipMemcpyHostToDevice, st);
+      if (err != hipSuccess) rc = hip_fail(err, "staging H2D");
+      sent = e;
+    }
+  };
+  if (!miss.empty()) {
+    const size_t min_dma = h2d_min_bytes();
+    pack_and_dispatch(job, threads, total * esz * miss.size(), [&](size_t, size_t u1) {
+      if (u1 < miss.size() && (u1 - sent) * row_bytes < min_dma) return;
+      send(u1);
+    });
+    send(miss.size());
+    if (rc != DLSIM_OK) return rc;
+  }
+  std::vector<const void*> ins(d_rows, d_rows + n);
+  rc = dispatch(ins.data(), n, h_weights, d_out, total, dtype, mode, st);
+  if (rc != DLSIM_OK || !h_out) return rc;
+  const hipError_t e = hipMemcpyAsync(h_out, d_out, total * esz, hipMemcpyDeviceToHost, st);
+  return e == hipSuccess ? DLSIM_OK : hip_fail(e, "result D2H");
+}
+
 int dlsim_host_chunk_mean(int b, const int* fan_in, const void* const* h_inputs, const size_t* n_elems,
                           void* h_staging, void* d_staging, size_t staging_elems, void* const* d_outs,
                           void* const* h_outs, int dtype, int cpu_threads, int threads, void* stream,

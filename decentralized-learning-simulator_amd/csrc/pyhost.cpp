@@ -28,6 +28,9 @@
 //                                      dlsim_wreduce_tensors call
 //   wreduce_rows_multi(...)        the same for many tasks, one
 //                                      dlsim_wreduce_batched call
+//   shm_keys(rows, idx)            per model, the identity of its tensors'
+//                                      torch.multiprocessing file_system
+//                                      storages (device_cache.py), or None
 //
 // Tensor fields (shape, dtype, contiguity, device, data pointer) are read from
 // the at::Tensor itself (libtorch headers; the extension links torch's
@@ -37,10 +40,12 @@
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
 
+#include <libshm.h>
 #include <torch/csrc/Dtype.h>
 #include <torch/csrc/autograd/python_variable.h>
 
 #include <cstdint>
+#include <cstring>
 #include <unordered_set>
 #include <vector>
 
@@ -314,6 +319,63 @@ PyObject* py_data_ptrs(PyObject*, PyObject* args) {
       return nullptr;
     }
     PyList_SET_ITEM(out, static_cast<Py_ssize_t>(q), p);
+  }
+  return out;
+}
+
+// shm_keys(rows, idx) -> [key_i or None]: for model i, the identity of
+// tensors rows[i][k] (k in idx) when every one is a CPU tensor whose storage
+// is a torch.multiprocessing file_system shared-memory file (what a worker of
+// the reference receives, worker.py:6): (the first tensor's shm file name,
+// a 64-bit FNV-1a hash over every tensor's file name, storage offset, numel
+// and dtype). A file name names one storage allocation for the run, so a key
+// seen again by this process is the same model's memory (device_cache.py);
+// None for a model with any tensor elsewhere. No Python attribute calls.
+PyObject* py_shm_keys(PyObject*, PyObject* args) {
+  PyObject *rows, *idx;
+  if (!PyArg_ParseTuple(args, "OO", &rows, &idx)) return nullptr;
+  std::vector<const at::Tensor*> ts;
+  Py_ssize_t n, t;
+  if (!row_tensors(rows, idx, ts, &n, &t)) return nullptr;
+  PyObject* out = PyList_New(n);
+  if (!out) return nullptr;
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&h](const void* p, size_t len) {
+      const unsigned char* c = static_cast<const unsigned char*>(p);
+      for (size_t q = 0; q < len; ++q) h = (h ^ c[q]) * 1099511628211ull;
+    };
+    const char* first = nullptr;
+    bool ok = t > 0;
+    for (Py_ssize_t j = 0; ok && j < t; ++j) {
+      const at::Tensor* x = ts[static_cast<size_t>(i * t + j)];
+      if (x->device().type() != c10::DeviceType::CPU || !x->has_storage()) {
+        ok = false;
+        break;
+      }
+      THManagedMapAllocator* ctx = THManagedMapAllocator::fromDataPtr(x->storage().data_ptr());
+      if (!ctx) {
+        ok = false;
+        break;
+      }
+      const char* fn = ctx->filename();
+      if (!first) first = fn;
+      mix(fn, std::strlen(fn) + 1);
+      const int64_t meta[3] = {x->storage_offset(), x->numel(), static_cast<int64_t>(x->scalar_type())};
+      mix(meta, sizeof(meta));
+    }
+    PyObject* key;
+    if (ok) {
+      key = Py_BuildValue("(yK)", first, static_cast<unsigned long long>(h));
+      if (!key) {
+        Py_DECREF(out);
+        return nullptr;
+      }
+    } else {
+      key = Py_None;
+      Py_INCREF(key);
+    }
+    PyList_SET_ITEM(out, i, key);
   }
   return out;
 }
@@ -974,6 +1036,7 @@ PyMethodDef kMethods[] = {
     {"module_params", py_module_params, METH_O, "list(module.parameters()), in C"},
     {"matches", py_matches, METH_VARARGS, "params match a [(shape, dtype)] signature"},
     {"data_ptrs", py_data_ptrs, METH_VARARGS, "data pointers of rows[i][k] for k in idx, None if not contiguous"},
+    {"shm_keys", py_shm_keys, METH_VARARGS, "per model, the identity of its file_system shm storages, or None"},
     {"clone_init", py_clone_init, METH_VARARGS,
      "clone_init(plain_cache, plain_fn, atomic_types, setstate_keys, deepcopy, OrderedDict)"},
     {"clone_module", py_clone_module, METH_VARARGS, "clone_module(module, memo): arena._clone_module in C"},

@@ -52,6 +52,7 @@ EXPORTS = (
     "dlsim_sharded_plan_run_f64",
     "dlsim_sharded_plan_destroy",
     "dlsim_host_wreduce",
+    "dlsim_host_wreduce_resident",
     "dlsim_host_chunk_mean",
     "dlsim_host_pack",
     "dlsim_shard_range",
@@ -139,6 +140,10 @@ def load() -> ctypes.CDLL:
                                            ctypes.POINTER(ctypes.c_float), vp, vp, sz, vp, vp, i, i, sz, i,
                                            vp, vp, vp]
         lib.dlsim_host_wreduce.restype = i
+        lib.dlsim_host_wreduce_resident.argtypes = [i, i, ctypes.POINTER(vp), ctypes.POINTER(sz),
+                                                    ctypes.POINTER(ctypes.c_float), ctypes.POINTER(i),
+                                                    ctypes.POINTER(vp), vp, sz, vp, vp, i, i, i, vp]
+        lib.dlsim_host_wreduce_resident.restype = i
         lib.dlsim_host_chunk_mean.argtypes = [i, ctypes.POINTER(i), ctypes.POINTER(vp), ctypes.POINTER(sz), vp, vp,
                                               sz, ctypes.POINTER(vp), ctypes.POINTER(vp), i, i, i, vp, vp, vp]
         lib.dlsim_host_chunk_mean.restype = i
@@ -787,6 +792,24 @@ def host_wreduce_raw(src_ptrs: Sequence[int], n: int, numels: Sequence[int], wei
         stream_handle, None if h2d_stream is None else h2d_stream.cuda_stream,
         None if d2h_stream is None else d2h_stream.cuda_stream)
     _check("dlsim_host_wreduce", rc)
+
+
+def host_wreduce_resident_raw(src_ptrs: Sequence[int], n: int, numels: Sequence[int], weights_f32,
+                              resident: Sequence[bool], row_ptrs: Sequence[int], staging, out, host_out, dtype: int,
+                              mode: int, threads: int, stream_handle) -> None:
+    """dlsim_host_wreduce_resident on pointers the caller has validated (the
+    arena path with a device cache): src_ptrs model-major, n * len(numels)
+    entries (0 for a resident model's tensors); row_ptrs the n device rows;
+    staging a pinned [m, stride] buffer for the m non-resident models."""
+    t = len(numels)
+    w = np.ascontiguousarray(weights_f32, dtype=np.float32)
+    stride = staging.stride(0) if staging is not None and staging.dim() == 2 else 0
+    rc = load().dlsim_host_wreduce_resident(
+        n, t, (ctypes.c_void_p * max(1, len(src_ptrs)))(*[p or None for p in src_ptrs]), (ctypes.c_size_t * t)(*numels),
+        w.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), (ctypes.c_int * n)(*[1 if r else 0 for r in resident]),
+        (ctypes.c_void_p * n)(*row_ptrs), None if staging is None else staging.data_ptr(), stride, out.data_ptr(),
+        None if host_out is None else host_out.data_ptr(), dtype, mode, threads, stream_handle)
+    _check("dlsim_host_wreduce_resident", rc)
 
 
 def host_wreduce(inputs_by_model, weights_f32, staging, rows, out, host_out=None, mode: int = DLSIM_EXACT,

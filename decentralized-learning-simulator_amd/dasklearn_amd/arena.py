@@ -35,7 +35,7 @@ import numpy as np
 import torch
 from torch import nn
 
-from . import _native
+from . import _native, device_cache
 from . import _pyhost  # csrc/pyhost.cpp (built with the library by __graft_entry__.build())
 
 
@@ -479,6 +479,62 @@ def _host_pipeline(all_params, idx, layout, dt, dev, out, weights_f32, mode, str
     return host, bool(keep), want_host and not synced
 
 
+def _cached_host_reduce(cache, all_params, idx, layout, dt, dev, out, weights_f32, mode, stream, defer):
+    """Host models with a device cache (device_cache.py): the models whose
+    file_system shm storages this process uploaded before are read from their
+    cached device rows; the others are packed, sent to fresh device rows (one
+    block, rows one stride apart: one DMA run) and cached; then the reduce and
+    the D2H, one dlsim_host_wreduce_resident call. None when no model is in
+    shared memory (the normal pipeline then runs). Returns as _host_pipeline."""
+    keys = _pyhost.shm_keys(all_params, idx)
+    if all(k is None for k in keys):
+        return None
+    n = len(all_params)
+    total = layout.totals[dt]
+    esz = _elem_size(dt)
+    stride = row_stride(total, esz)
+    full = [None if k is None else (k, dev.index, dt, total) for k in keys]
+    with cache.lock:
+        rows = [None if k is None else cache.get(k) for k in full]
+        miss = [i for i in range(n) if rows[i] is None]
+        resident = [r is not None for r in rows]
+        keep, src = [], [0] * (n * len(idx))
+        if miss:
+            block = aligned_empty(len(miss) * stride, dt, dev, base_align(total * esz, esz)).view(len(miss), stride)
+            for j, i in enumerate(miss):
+                rows[i] = block[j, :total]
+            keep, ptrs = _data_ptrs([all_params[i] for i in miss], idx)
+            t = len(idx)
+            for j, i in enumerate(miss):
+                src[i * t:(i + 1) * t] = ptrs[j * t:(j + 1) * t]
+        pinned_result = HOST_RESULT_PINNED or total * esz >= PAGEABLE_RESULT_BYTES
+        host = torch.empty(total, dtype=dt, pin_memory=pinned_result)
+        pinned = None
+        if miss:
+            _, pinned = STAGING.acquire(dev, dt, len(miss), total, stream)
+        synced = False
+        try:
+            _native.host_wreduce_resident_raw(src, n, layout.split_sizes[dt], weights_f32, resident,
+                                              [r.data_ptr() for r in rows], pinned, out, host,
+                                              _native.dtype_code(dt), mode, torch.get_num_threads(),
+                                              stream.cuda_stream)
+            if not (defer and pinned_result):
+                stream.synchronize()
+                synced = True
+        finally:
+            if miss:
+                STAGING.release(dev, dt, stream, synced)
+        for i in miss:
+            if full[i] is not None:
+                cache.put(full[i], rows[i], stride * esz)
+        st = cache.stats
+        st["hits"] += n - len(miss)
+        st["misses"] += sum(1 for i in miss if full[i] is not None)
+        st["uncacheable"] += sum(1 for i in miss if full[i] is None)
+        st["bytes_not_sent"] += (n - len(miss)) * total * esz
+    return host, bool(keep), not synced
+
+
 def _data_ptrs(all_params, idx):
     """(keep-alive list, data pointers of tensor k of every model for k in
     idx, model-major). Non-contiguous tensors are copied (and kept alive until
@@ -592,10 +648,14 @@ def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, m
                 continue
             if not f64 and not any(all_params[i][idx[0]].is_cuda for i in range(n)):
                 # host models (the reference's case): chunked pack / H2D /
-                # reduce (/ D2H) pipeline
+                # reduce (/ D2H) pipeline, or with a device cache the models
+                # this process has uploaded before are read in place
                 st.mark("layout")
-                h, copied, waits = _host_pipeline(all_params, idx, layout, dt, dev, out, weights_f32, mode,
-                                                  get_stream(), piped, defer_host_sync)
+                cache = device_cache.active()
+                r = _cached_host_reduce(cache, all_params, idx, layout, dt, dev, out, weights_f32, mode,
+                                        get_stream(), defer_host_sync) if cache is not None and piped else None
+                h, copied, waits = r if r is not None else _host_pipeline(
+                    all_params, idx, layout, dt, dev, out, weights_f32, mode, get_stream(), piped, defer_host_sync)
                 staged = staged or copied
                 pending = pending or waits
                 if h is not None:

@@ -374,6 +374,26 @@ int dlsim_host_wreduce(int n, int t, const void* const* h_srcs, const size_t* nu
                        void* stream, void* h2d_stream, void* d2h_stream);
 
 /*
+ * dlsim_host_wreduce_resident — dlsim_host_wreduce when some models are
+ * already on the device (a per-worker cache of host models it has uploaded
+ * before, dasklearn_amd/device_cache.py).
+ *   resident[i] != 0  d_rows[i] already holds model i (sum(numels) elements)
+ *   resident[i] == 0  model i's tensors h_srcs[i * t + k] are packed into
+ *                     staging row j (the j-th such model; rows of
+ *                     staging_stride elements, page-locked, 16-B aligned)
+ *                     and sent to d_rows[i], which keeps them for later calls
+ * then the reduce of d_rows[0..n) into d_out (dlsim_wreduce rules, input
+ * order i) and, if h_out, the D2H of the result; one chunk, all on `stream`,
+ * asynchronous (h_out page-locked). Device rows must not overlap d_out.
+ * Consecutive non-resident models whose device rows lie one staging stride
+ * apart go H2D in runs of >= 1 MiB (DLSIM_H2D_MIN_KB).
+ */
+int dlsim_host_wreduce_resident(int n, int t, const void* const* h_srcs, const size_t* numels,
+                                const float* h_weights, const int* resident, void* const* d_rows, void* h_staging,
+                                size_t staging_stride, void* d_out, void* h_out, int dtype, int mode, int threads,
+                                void* stream);
+
+/*
  * dlsim_host_chunk_mean — dlsim_chunk_mean_batched for *host* chunks (the
  * reference's case: ChunkManager.reconstruct_model over chunks received from
  * peers, chunk_manager.py:38-40), staged and pipelined like

@@ -131,7 +131,12 @@ def train_host(settings, params):
     with torch.no_grad():
         for p in out.parameters():
             p.add_(1e-3 * (params["peer"] + 1))
+    if SHM:  # as the worker's result crosses to the broker: file_system shared memory (worker.py:6)
+        out.share_memory()
     return [out]
+
+
+SHM = False
 
 
 def resolve(results, v):
@@ -227,12 +232,19 @@ def main():
                     help="RoundExecutor drops a wave's inputs after the wave (release_early=False)")
     ap.add_argument("--flatten", action="store_true",
                     help="RoundExecutor copies device-trained models into arenas first (tensors_in_place=False)")
+    ap.add_argument("--shm", action="store_true",
+                    help="with --host: trained models move to torch.multiprocessing file_system shared memory, as a "
+                         "reference worker's results do (the device model cache keys on it; DLSIM_DEVICE_CACHE_MB)")
     ap.add_argument("--profile", default=None, help="cProfile the batched run into this file")
     ap.add_argument("--profile-seq", default=None, help="cProfile the sequential run into this file")
     ap.add_argument("--reps", type=int, default=3,
                     help="repetitions of each way, interleaved; the line reports the median and the best "
                          "(Python's collector runs at times set by the objects the whole run keeps alive)")
     a = ap.parse_args()
+    global SHM
+    SHM = a.shm
+    if a.shm:
+        torch.multiprocessing.set_sharing_strategy("file_system")
     from dasklearn_amd.functions import aggregate
     from dasklearn_amd.rounds import RoundExecutor
     from oracle import fedavg_torch
@@ -346,9 +358,13 @@ def main():
                 "gc_collections_by_generation": gc_n[kind]}
 
     from bench import box_info
+    from dasklearn_amd import device_cache
     box = box_info()
+    extra = {"shm_models": a.shm}
+    if device_cache.active() is not None:
+        extra["device_cache"] = dict(device_cache.active().stats, capacity=device_cache.active().capacity)
     for kind in samples:
-        print(json.dumps(dict(line(kind), box=box)), flush=True)
+        print(json.dumps(dict(line(kind), box=box, **extra)), flush=True)
 
 
 if __name__ == "__main__":

@@ -17,6 +17,9 @@ import json
 import os
 import sys
 
+if "cache" in sys.argv[2:]:  # the worker's device model cache, before the package is imported
+    os.environ["DLSIM_DEVICE_CACHE_MB"] = "256"
+
 import torch
 import torch.multiprocessing as multiprocessing
 
@@ -87,6 +90,31 @@ def main():
                                 and orc.same_bits(flat(m), exp)
                                 and torch.equal(m.bn.running_mean, ms[0].bn.running_mean))
         checks["error_protocol"] = got.get("error", (None,))[0] == "agg_bad"
+        if "cache" in sys.argv[2:]:
+            # the worker died on agg_bad (the reference's protocol): a second
+            # worker runs the same three tasks, then reports its cache: the
+            # models it received before are read from the device
+            proc.join(timeout=60)
+            proc2 = ctx.Process(target=worker_main, args=(shared, results, 0))
+            proc2.start()
+            for name, ms, ws in tasks:
+                data = {"models": ms, "round": 3, "peer": 1}
+                if ws is not None:
+                    data["weights"] = ws
+                shared.put((name, "aggregate", data))
+            shared.put(("stats", "cache_stats", {}))
+            shared.put(None)
+            got2 = {}
+            for _ in range(4):
+                name, res, info = results.get(timeout=120)
+                got2[name] = res
+            for name, ms, ws in tasks:
+                exp = orc.wreduce([flat(x) for x in ms], orc.reference_weights(len(ms), ws), "f32")
+                checks[name + "_cached"] = orc.same_bits(flat(got2[name][0]), exp)
+            out["cache_stats"] = got2["stats"][0]
+            # agg_0 sends models 0-1, agg_1 0-6 (0-1 resident), agg_2 2-4 (all resident)
+            checks["cache_hits"] = out["cache_stats"] == dict(out["cache_stats"], hits=5, misses=7, uncacheable=0)
+            proc2.join(timeout=60)
         out["checks"] = checks
         ok = all(checks.values())
         proc.join(timeout=60)

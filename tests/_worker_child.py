@@ -15,6 +15,14 @@ torch.multiprocessing.set_sharing_strategy("file_system")  # worker.py:6
 from dasklearn_amd.functions import *  # noqa: E402,F401,F403
 
 
+def cache_stats(settings, data):
+    """A task of this test worker only: the device cache's counters
+    (dasklearn_amd/device_cache.py), or None when it is off."""
+    from dasklearn_amd import device_cache
+    c = device_cache.active()
+    return [None if c is None else dict(c.stats, entries=len(c))]
+
+
 class Settings:
     gradient_aggregation = 1  # GradientAggregationMethod.FEDAVG
     torch_threads = 4

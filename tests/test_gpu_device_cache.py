@@ -1,0 +1,124 @@
+"""The per-worker device model cache (dasklearn_amd/device_cache.py; SURVEY.md
+§8f row 1) on MI355X.
+
+Host models whose parameters live in torch.multiprocessing file_system shared
+memory (what a reference worker receives, worker.py:6) are uploaded once per
+process and read from the device on later aggregates; every result stays
+bit-identical to the oracle's fold (fedavg.py:20-25), hits or not. In one
+process here, and through the reference's broker/worker process model
+(tests/_broker_child.py in cache mode: a forked worker that receives the same
+models in several tasks)."""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+import torch.multiprocessing as tmp
+from torch import nn
+
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+class Net(nn.Module):
+    def __init__(self, seed):
+        super().__init__()
+        g = torch.Generator().manual_seed(seed)
+        self.conv = nn.Conv2d(3, 16, 5)
+        self.fc = nn.Linear(400, 10)
+        with torch.no_grad():
+            for q in self.parameters():
+                q.copy_(torch.randn(q.shape, generator=g) * 0.05)
+
+
+def flat(m):
+    return torch.cat([q.detach().reshape(-1) for q in m.parameters()]).numpy()
+
+
+@pytest.fixture()
+def shm_models():
+    prev = tmp.get_sharing_strategy()
+    tmp.set_sharing_strategy("file_system")
+    try:
+        ms = [Net(s) for s in range(9)]
+        for m in ms:
+            m.share_memory()
+        yield ms
+    finally:
+        tmp.set_sharing_strategy(prev)
+
+
+@pytest.fixture()
+def cache():
+    from dasklearn_amd import device_cache
+    prev = device_cache.active()
+    c = device_cache.enable(64 << 20)
+    yield c
+    if prev is None:
+        device_cache.disable()
+    else:
+        device_cache._CACHE = prev
+
+
+def _check(models, weights):
+    from dasklearn_amd.gradient_aggregation.fedavg import FedAvg
+    out = FedAvg.aggregate(models, weights)
+    assert not any(q.is_cuda for q in out.parameters())
+    exp = orc.wreduce([flat(m) for m in models], orc.reference_weights(len(models), weights), "f32")
+    assert orc.same_bits(flat(out), exp)
+
+
+def test_cache_hits_are_bit_exact(shm_models, cache):
+    ms = shm_models
+    _check(ms[:7], None)
+    assert cache.stats["misses"] == 7 and cache.stats["hits"] == 0 and len(cache) == 7
+    _check(ms[:7], [0.1, 0.2, 0.1, 0.2, 0.1, 0.2, 0.1])
+    assert cache.stats["hits"] == 7
+    _check([ms[8], ms[0], ms[7], ms[3]], None)  # two new, two resident, in another order
+    assert cache.stats["hits"] == 9 and cache.stats["misses"] == 9
+    row_bytes = sum(q.numel() for q in ms[0].parameters()) * 4
+    assert cache.stats["bytes_not_sent"] == 9 * row_bytes
+
+
+def test_non_shared_models_take_the_normal_pipeline(cache):
+    ms = [Net(s) for s in range(3)]  # private host memory: no identity across tasks
+    _check(ms, None)
+    _check(ms, None)
+    assert cache.stats["hits"] == 0 and len(cache) == 0
+
+
+def test_eviction_keeps_results_exact(shm_models):
+    from dasklearn_amd import arena, device_cache
+    ms = shm_models
+    row = arena.row_stride(sum(q.numel() for q in ms[0].parameters()), 4) * 4
+    c = device_cache.enable(3 * row)  # room for three models
+    try:
+        _check(ms[:5], None)
+        assert len(c) == 3 and c.stats["evictions"] == 2
+        _check(ms[:5], None)  # models 2-4 resident, 0-1 sent again
+        assert c.stats["hits"] == 3
+        _check(ms[4:9], [0.3, 0.2, 0.2, 0.2, 0.1])
+    finally:
+        device_cache.disable()
+
+
+@pytest.mark.parametrize("method", ["fork", "spawn"])
+def test_worker_process_cache(method):
+    """The broker/worker process model with the cache on in the worker: the
+    second worker's three tasks send 7 models and read 5 from its cache, all
+    results exact."""
+    r = subprocess.run([sys.executable, os.path.join(HERE, "_broker_child.py"), method, "cache"],
+                       capture_output=True, text=True, timeout=240)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert lines, r.stdout[-2000:] + r.stderr[-3000:]
+    out = json.loads(lines[-1])
+    assert all(out["checks"].values()), out
+    assert out["cache_stats"]["hits"] == 5 and out["cache_stats"]["misses"] == 7, out["cache_stats"]
+    assert out["ok"] and r.returncode == 0, out
