@@ -42,26 +42,27 @@ class DeviceModelCache:
 
     def __init__(self, capacity_bytes: int):
         self.capacity = int(capacity_bytes)
-        self._rows: "OrderedDict[tuple, torch.Tensor]" = OrderedDict()
+        self._rows: "OrderedDict[tuple, tuple]" = OrderedDict()  # key -> (row, bytes it is charged)
         self.bytes = 0
         self.lock = threading.Lock()
         self.stats: Dict[str, int] = {"hits": 0, "misses": 0, "uncacheable": 0, "evictions": 0,
                                       "bytes_not_sent": 0}
 
     def get(self, key) -> Optional[torch.Tensor]:
-        row = self._rows.get(key)
-        if row is not None:
-            self._rows.move_to_end(key)
-        return row
+        e = self._rows.get(key)
+        if e is None:
+            return None
+        self._rows.move_to_end(key)
+        return e[0]
 
     def put(self, key, row: torch.Tensor, nbytes: int) -> None:
         if key in self._rows or nbytes > self.capacity:
             return
-        self._rows[key] = row
+        self._rows[key] = (row, nbytes)
         self.bytes += nbytes
         while self.bytes > self.capacity and self._rows:
-            _, old = self._rows.popitem(last=False)
-            self.bytes -= old.numel() * old.element_size()
+            _, (_, old_bytes) = self._rows.popitem(last=False)
+            self.bytes -= old_bytes
             self.stats["evictions"] += 1
 
     def __len__(self) -> int:

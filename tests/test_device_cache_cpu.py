@@ -26,10 +26,13 @@ def test_lru_evicts_the_least_recently_used():
     c.put("d", rows["d"], 400)      # evicts b
     assert c.get("b") is None and c.get("c") is rows["c"] and c.get("d") is rows["d"]
     assert len(c) == 3 and c.bytes == 1200 and c.stats["evictions"] == 1
+    c.put("e", torch.zeros(10), 800)  # charged by the bytes given (a row's stride), not its view
+    assert c.get("c") is None and c.get("a") is None and c.get("e") is not None and c.bytes == 1200
     c.put("big", torch.zeros(1000), 4000)  # larger than the whole cache: not kept
     assert c.get("big") is None
     c.clear()
     assert len(c) == 0 and c.bytes == 0
+    assert c.stats["evictions"] == 3
 
 
 def test_enable_from_env(monkeypatch):
