@@ -1,0 +1,21 @@
+# Round 4: row layouts of the north star averaged over physical placements
+# (probe_layout_placements.py), then five fresh bench processes at the
+# driver's shape; a cProfile of the 100-peer host round, one call per task.
+set -u
+export TMPDIR=/tmp
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/r04e
+mkdir -p $O
+step() { echo "[$(date +%T)] $*"; }
+step layouts
+timeout -k 10 400 python3 -u scripts/probes/probe_layout_placements.py 4 200 > $O/layout_placements.jsonl 2> $O/layout_placements.err || exit $?
+grep summary $O/layout_placements.jsonl
+step bench
+for i in 1 2 3 4 5; do
+  timeout -k 10 120 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_$i.json 2> $O/bench_$i.err || exit $?
+  python3 -c "import json; d=json.load(open('$O/bench_$i.json')); print($i, d['ms_per_step'], d['roofline']['frac'])"
+done
+step profile_seq_host
+timeout -k 10 400 python3 -u scripts/bench_rounds.py --peers 100 --host --reps 1 --profile-seq $O/seq_host_prof.txt > $O/seq_host.jsonl 2> $O/seq_host.err || exit $?
+head -60 $O/seq_host_prof.txt
+step done

@@ -9,7 +9,8 @@
  * (n = 2), dlsim_wreduce_f64, dlsim_wreduce_tensors (7 models x 3 tensors),
  * dlsim_wreduce_batched (tasks of several fan-ins), dlsim_chunk_mean_batched
  * (k = 10 chunks of a flat model, chunks off 128-B lines), dlsim_host_wreduce
- * (host models, pinned staging, pipelined chunks), a descriptor-table batch
+ * (host models, pinned staging, pipelined chunks), dlsim_host_wreduce_resident
+ * (some models already on the device), a descriptor-table batch
  * (dlsim_batch_table_*), dlsim_host_chunk_mean (host chunks), the error
  * codes, and dlsim_version / dlsim_shard_range.
  *
@@ -350,6 +351,60 @@ static void case_host_wreduce(hipStream_t st) {
   HIPCK(hipStreamDestroy(d2h));
 }
 
+static void case_host_wreduce_resident(hipStream_t st) {
+  /* 5 host models of 2 tensors; models 1 and 3 already on the device (a
+   * worker's cache), the other three packed and sent to their device rows,
+   * which keep them: a second call with every model resident gives the same */
+  enum { N = 5, T = 2 };
+  const size_t numels[T] = {70001, 33};
+  const size_t total = numels[0] + numels[1];
+  const size_t stride = (total + 63) / 64 * 64;
+  float* h[N * T];
+  float w[N];
+  weights(w, N);
+  float* cat[N];
+  for (int i = 0; i < N; ++i) {
+    cat[i] = (float*)malloc(total * 4);
+    for (int k = 0; k < T; ++k) {
+      h[i * T + k] = (float*)malloc(numels[k] * 4);
+      fill_f32(h[i * T + k], numels[k]);
+    }
+    memcpy(cat[i], h[i * T], numels[0] * 4);
+    memcpy(cat[i] + numels[0], h[i * T + 1], numels[1] * 4);
+  }
+  void *staging = NULL, *block = NULL, *dout = NULL, *hout = NULL;
+  HIPCK(hipHostMalloc(&staging, N * stride * 4, 0));
+  HIPCK(hipHostMalloc(&hout, total * 4, 0));
+  HIPCK(hipMalloc(&block, N * stride * 4));
+  HIPCK(hipMalloc(&dout, total * 4));
+  void* rows[N];
+  for (int i = 0; i < N; ++i) rows[i] = (char*)block + (size_t)i * stride * 4;
+  int resident[N] = {0, 1, 0, 1, 0};
+  HIPCK(hipMemcpy(rows[1], cat[1], total * 4, hipMemcpyHostToDevice));
+  HIPCK(hipMemcpy(rows[3], cat[3], total * 4, hipMemcpyHostToDevice));
+  const void* srcs[N * T];
+  for (int j = 0; j < N * T; ++j) srcs[j] = resident[j / T] ? NULL : h[j];
+  float* exp = (float*)malloc(total * 4);
+  oracle_wreduce_f32((const float* const*)cat, N, w, exp, total);
+  DLCK(dlsim_host_wreduce_resident(N, T, srcs, numels, w, resident, rows, staging, stride, dout, hout, DLSIM_F32,
+                                   DLSIM_EXACT, 4, st));
+  HIPCK(hipStreamSynchronize(st));
+  expect_same("dlsim_host_wreduce_resident 2 of 5 resident", hout, exp, total * 4);
+  int all[N] = {1, 1, 1, 1, 1};
+  memset(hout, 0, total * 4);
+  DLCK(dlsim_host_wreduce_resident(N, T, srcs, numels, w, all, rows, NULL, 0, dout, hout, DLSIM_F32, DLSIM_EXACT, 4,
+                                   st));
+  HIPCK(hipStreamSynchronize(st));
+  expect_same("dlsim_host_wreduce_resident all resident (rows kept)", hout, exp, total * 4);
+  for (int i = 0; i < N; ++i) free(cat[i]);
+  for (int j = 0; j < N * T; ++j) free(h[j]);
+  free(exp);
+  HIPCK(hipHostFree(staging));
+  HIPCK(hipHostFree(hout));
+  HIPCK(hipFree(block));
+  HIPCK(hipFree(dout));
+}
+
 static void case_table_batch(hipStream_t st) {
   /* a prepared round: 5 tasks of several sizes and fan-ins in one caller-owned
    * descriptor table, launched twice (graph-capturable: no allocation) */
@@ -502,6 +557,7 @@ int main(void) {
   case_tensors_and_batched(st);
   case_chunk_means(st);
   case_host_wreduce(st);
+  case_host_wreduce_resident(st);
   case_table_batch(st);
   case_host_chunk_mean(st);
   case_errors(st);
