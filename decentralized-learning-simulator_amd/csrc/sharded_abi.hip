@@ -276,8 +276,8 @@ int wreduce_sharded(const void* const* d_slices, size_t slice_elems, int n, cons
 // local checks or launch fail still enters the plan's gather (so no peer is
 // left waiting in it) and then returns its error; its peers are not told.
 template <class W>
-int plan_run(dlsim_sharded_plan* p, const void* const* d_slices, const W* h_weights, void* d_out, int mode,
-             void* stream) {
+int plan_run(dlsim_sharded_plan* p, const void* const* d_slices, size_t slice_elems, const W* h_weights, void* d_out,
+             int mode, void* stream) {
   g_err.clear();
   if (!p) return fail(DLSIM_E_ARG, "null plan");
   constexpr bool kF64 = std::is_same<W, double>::value;
@@ -290,6 +290,9 @@ int plan_run(dlsim_sharded_plan* p, const void* const* d_slices, const W* h_weig
     rc = fail(DLSIM_E_DTYPE, kF64 ? "plan is not DLSIM_F64: use dlsim_sharded_plan_run"
                                   : "DLSIM_F64 plan: use dlsim_sharded_plan_run_f64");
   if (rc == DLSIM_OK && p->n_elems > 0 && !d_out) rc = fail(DLSIM_E_ARG, "null output pointer");
+  if (rc == DLSIM_OK && slice_elems != p->e - p->b)
+    rc = fail(DLSIM_E_ARG, "rank %d of %d: slices have %zu elements, the plan's shard [%zu, %zu) has %zu", p->rank,
+              p->world, slice_elems, p->b, p->e, p->e - p->b);
   if (rc == DLSIM_OK) {
     void* target = padded ? static_cast<void*>(static_cast<char*>(p->scratch) + static_cast<size_t>(p->rank) * p->width * esz)
                           : static_cast<void*>(out + p->b * esz);
@@ -399,14 +402,14 @@ int dlsim_sharded_plan_create(void* rccl_comm, size_t n_elems, int n, int dtype,
   return DLSIM_OK;
 }
 
-int dlsim_sharded_plan_run(dlsim_sharded_plan* plan, const void* const* d_slices, const float* h_weights, void* d_out,
-                           int mode, void* stream) {
-  return plan_run(plan, d_slices, h_weights, d_out, mode, stream);
+int dlsim_sharded_plan_run(dlsim_sharded_plan* plan, const void* const* d_slices, size_t slice_elems,
+                           const float* h_weights, void* d_out, int mode, void* stream) {
+  return plan_run(plan, d_slices, slice_elems, h_weights, d_out, mode, stream);
 }
 
-int dlsim_sharded_plan_run_f64(dlsim_sharded_plan* plan, const void* const* d_slices, const double* h_weights,
-                               void* d_out, int mode, void* stream) {
-  return plan_run(plan, d_slices, h_weights, d_out, mode, stream);
+int dlsim_sharded_plan_run_f64(dlsim_sharded_plan* plan, const void* const* d_slices, size_t slice_elems,
+                               const double* h_weights, void* d_out, int mode, void* stream) {
+  return plan_run(plan, d_slices, slice_elems, h_weights, d_out, mode, stream);
 }
 
 int dlsim_sharded_plan_destroy(dlsim_sharded_plan* plan) {

@@ -129,10 +129,10 @@ def load() -> ctypes.CDLL:
         lib.dlsim_wreduce_sharded_f64.restype = i
         lib.dlsim_sharded_plan_create.argtypes = [vp, sz, i, i, i, vp, ctypes.POINTER(vp)]
         lib.dlsim_sharded_plan_create.restype = i
-        lib.dlsim_sharded_plan_run.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_float), vp, i, vp]
+        lib.dlsim_sharded_plan_run.argtypes = [vp, ctypes.POINTER(vp), sz, ctypes.POINTER(ctypes.c_float), vp, i, vp]
         lib.dlsim_sharded_plan_run.restype = i
-        lib.dlsim_sharded_plan_run_f64.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_double), vp, i,
-                                                   vp]
+        lib.dlsim_sharded_plan_run_f64.argtypes = [vp, ctypes.POINTER(vp), sz, ctypes.POINTER(ctypes.c_double), vp,
+                                                   i, vp]
         lib.dlsim_sharded_plan_run_f64.restype = i
         lib.dlsim_sharded_plan_destroy.argtypes = [vp]
         lib.dlsim_sharded_plan_destroy.restype = i
@@ -641,6 +641,8 @@ class ShardedPlan:
             raise ValueError("plan destroyed")
         try:
             ptrs = _check_slices(slices, out)
+            if out.numel() != self.n_elems or out.dtype != self.dtype:
+                raise ValueError(f"out must be a full {self.n_elems}-element {self.dtype} buffer")
             w, wp = _weights_arg(weights, len(slices), self.f64)
         except (AssertionError, ValueError, IndexError, TypeError):
             # still enter the gather, so no peer is left waiting in it
@@ -650,7 +652,8 @@ class ShardedPlan:
                 pass
             raise
         fn = "dlsim_sharded_plan_run_f64" if self.f64 else "dlsim_sharded_plan_run"
-        _check(fn, getattr(self._lib, fn)(self._h, ptrs, wp, out.data_ptr(), mode, _stream_handle(out.device, stream)))
+        _check(fn, getattr(self._lib, fn)(self._h, ptrs, slices[0].numel(), wp, out.data_ptr(), mode,
+                                          _stream_handle(out.device, stream)))
         return out
 
     def run_failed(self, device, stream=None) -> None:
@@ -660,7 +663,7 @@ class ShardedPlan:
         if self._h is None:
             raise ValueError("plan destroyed")
         fn = "dlsim_sharded_plan_run_f64" if self.f64 else "dlsim_sharded_plan_run"
-        _check(fn, getattr(self._lib, fn)(self._h, None, None, None, DLSIM_EXACT, _stream_handle(device, stream)))
+        _check(fn, getattr(self._lib, fn)(self._h, None, 0, None, None, DLSIM_EXACT, _stream_handle(device, stream)))
 
     def close(self) -> None:
         if getattr(self, "_h", None) is not None:

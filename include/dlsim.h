@@ -314,8 +314,9 @@ int dlsim_wreduce_sharded_f64(const void* const* d_slices, size_t slice_elems, i
  * (W x ceil64(max slice) elements, hipMalloc).
  *
  * dlsim_sharded_plan_run[_f64] reduces this rank's slices (dlsim_shard_range
- * of the plan's n_elems, n models) into d_out + b_r and runs the plan's
- * gather: stream-ordered, no host wait, no agreement. Every rank must run
+ * of the plan's n_elems, n models; slice_elems must equal e_r - b_r) into
+ * d_out + b_r (a full n_elems buffer) and runs the plan's gather:
+ * stream-ordered, no host wait, no agreement. Every rank must run
  * the same sequence of plans, as with any collective. A rank whose local
  * checks or launch fail (null or overlapping pointers, mode, the f64 entry
  * on a non-f64 plan) still enters the plan's gather with whatever its slice
@@ -331,10 +332,10 @@ typedef struct dlsim_sharded_plan dlsim_sharded_plan;
 
 int dlsim_sharded_plan_create(void* rccl_comm, size_t n_elems, int n, int dtype, int gather, void* stream,
                               dlsim_sharded_plan** plan);
-int dlsim_sharded_plan_run(dlsim_sharded_plan* plan, const void* const* d_slices, const float* h_weights,
-                           void* d_out, int mode, void* stream);
-int dlsim_sharded_plan_run_f64(dlsim_sharded_plan* plan, const void* const* d_slices, const double* h_weights,
-                               void* d_out, int mode, void* stream);
+int dlsim_sharded_plan_run(dlsim_sharded_plan* plan, const void* const* d_slices, size_t slice_elems,
+                           const float* h_weights, void* d_out, int mode, void* stream);
+int dlsim_sharded_plan_run_f64(dlsim_sharded_plan* plan, const void* const* d_slices, size_t slice_elems,
+                               const double* h_weights, void* d_out, int mode, void* stream);
 int dlsim_sharded_plan_destroy(dlsim_sharded_plan* plan);
 
 /*

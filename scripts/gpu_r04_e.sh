@@ -18,4 +18,7 @@ done
 step profile_seq_host
 timeout -k 10 400 python3 -u scripts/bench_rounds.py --peers 100 --host --reps 1 --profile-seq $O/seq_host_prof.txt > $O/seq_host.jsonl 2> $O/seq_host.err || exit $?
 head -60 $O/seq_host_prof.txt
+step c_host
+timeout -k 10 120 ./tests/native/_build/c_host_check > $O/c_host.txt 2>&1 || exit $?
+tail -4 $O/c_host.txt
 step done

@@ -332,9 +332,11 @@ def test_plan_run_failure_still_enters_the_gather(stub, gather):
         bad = np.concatenate([w, w[:1]])
         with pytest.raises(AssertionError):  # caught in Python, which still enters the gather
             plan.run([x[b:e] for x in xs], bad, out)
+        with pytest.raises(_native.DlsimError, match="slices have"):  # the library checks the length
+            plan.run([x[b:e - 1] for x in xs], w, out)
         entered = stub.stub_comm_calls(comm, None, None, None, 0) if gather == "bcast" \
             else stub.stub_comm_gathers(comm, None, None)
-        assert entered == (2 * world if gather == "bcast" else 2)
+        assert entered == (3 * world if gather == "bcast" else 3)
         assert stub.stub_comm_allreduces(comm) == 1
         # the plan still works after a failed run
         plan.run([x[b:e] for x in xs], w, out)
