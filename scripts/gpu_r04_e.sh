@@ -7,6 +7,11 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/r04e
 mkdir -p $O
 step() { echo "[$(date +%T)] $*"; }
+step pytest
+timeout -k 10 300 python3 -u -m pytest -p no:cacheprovider -x -q --timeout 180 --timeout-method thread \
+  tests/test_gpu_sharded_stub.py tests/test_gpu_sharded_rccl.py tests/test_gpu_c_host.py tests/test_gpu_device_cache.py > $O/pytest.log 2>&1
+rc=$?; tail -2 $O/pytest.log
+if [ $rc -ne 0 ]; then exit $rc; fi
 step layouts
 timeout -k 10 400 python3 -u scripts/probes/probe_layout_placements.py 4 200 > $O/layout_placements.jsonl 2> $O/layout_placements.err || exit $?
 grep summary $O/layout_placements.jsonl
