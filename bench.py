@@ -221,7 +221,10 @@ class ReduceWorkload:
         esz = ELEM_BYTES[dtype]
         self.stream = stream
         self.bytes_per_step = (n + 1) * p * esz * batch
-        self.sets = n_sets(self.bytes_per_step)
+        # DLSIM_BENCH_MIN_SETS / DLSIM_BENCH_SET_ALLOC=per_set: A/B knobs for
+        # the placement study, not for bench lines
+        self.sets = max(n_sets(self.bytes_per_step), int(os.environ.get("DLSIM_BENCH_MIN_SETS", "0")))
+        per_set = os.environ.get("DLSIM_BENCH_SET_ALLOC") == "per_set"
         g = torch.Generator(device=dev).manual_seed(seed)
         # the models are rows of one arena laid out as the product's staging
         # and round uploads lay them out (arena.row_stride / base_align: 256 B
@@ -234,11 +237,14 @@ class ReduceWorkload:
         # call's rows: rows in separate per-set allocations measured 0.5-2.5 %
         # slower and varied with where the driver placed them
         # (profiles/r03_bench_gap.jsonl)
-        rows = aligned_empty(self.sets * batch * n * p_pad, tdt, dev, al).view(self.sets, batch, n, p_pad)
+        if per_set:
+            rows = [aligned_empty(batch * n * p_pad, tdt, dev, al).view(batch, n, p_pad) for _ in range(self.sets)]
+        else:
+            rows = aligned_empty(self.sets * batch * n * p_pad, tdt, dev, al).view(self.sets, batch, n, p_pad)
         self._keep.append(rows)
         for s in range(self.sets):
             if batch == 1:
-                x = rows[s, 0]
+                x = rows[s][0]
                 x[:, :p].copy_((torch.randn((n, p), generator=g, device=dev) * 0.05).to(tdt))
                 out = arena_empty(p, tdt, dev)
                 plan = _native.ReducePlan([x[i, :p] for i in range(n)], w32, out, mode)

@@ -18,7 +18,8 @@ grep summary $O/layout_placements.jsonl
 step bench
 for i in 1 2 3 4 5; do
   timeout -k 10 120 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_$i.json 2> $O/bench_$i.err || exit $?
-  python3 -c "import json; d=json.load(open('$O/bench_$i.json')); print($i, d['ms_per_step'], d['roofline']['frac'])"
+  DLSIM_BENCH_SET_ALLOC=per_set DLSIM_BENCH_MIN_SETS=6 timeout -k 10 120 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_perset6_$i.json 2> $O/bench_perset6_$i.err || exit $?
+  python3 -c "import json; d=json.load(open('$O/bench_$i.json')); e=json.load(open('$O/bench_perset6_$i.json')); print($i, 'arena', d['ms_per_step'], d['roofline']['frac'], 'per_set x6', e['ms_per_step'], e['roofline']['frac'])"
 done
 step profile_seq_host
 timeout -k 10 400 python3 -u scripts/bench_rounds.py --peers 100 --host --reps 1 --profile-seq $O/seq_host_prof.txt > $O/seq_host.jsonl 2> $O/seq_host.err || exit $?
