@@ -24,6 +24,10 @@ done
 step profile_seq_host
 timeout -k 10 400 python3 -u scripts/bench_rounds.py --peers 100 --host --reps 1 --profile-seq $O/seq_host_prof.txt > $O/seq_host.jsonl 2> $O/seq_host.err || exit $?
 head -60 $O/seq_host_prof.txt
+step workers
+timeout -k 10 500 python3 -u scripts/bench_workers.py --peers 100 --workers 4 --rounds 6 > $O/workers_gnlenet.jsonl 2> $O/workers_gnlenet.err || exit $?
+timeout -k 10 500 python3 -u scripts/bench_workers.py --peers 16 --workers 4 --rounds 4 --model resnet18 > $O/workers_resnet18.jsonl 2> $O/workers_resnet18.err || exit $?
+cut -c1-400 $O/workers_gnlenet.jsonl $O/workers_resnet18.jsonl
 step c_host
 timeout -k 10 120 ./tests/native/_build/c_host_check > $O/c_host.txt 2>&1 || exit $?
 tail -4 $O/c_host.txt
