@@ -92,8 +92,6 @@ def run(way, peers, workers, rounds, model):
     import torch
     import torch.multiprocessing as mp
     from bench_rounds import dag, make_model
-    torch.manual_seed(0)
-    init = make_model(model)
     tasks, fan = dag(peers, rounds)
     by_name = {n: (f, d) for n, f, d in tasks}
     deps, consumers = {}, {}
@@ -106,6 +104,11 @@ def run(way, peers, workers, rounds, model):
     procs = [mp.Process(target=worker_proc, args=(way, shared, results, i)) for i in range(workers)]
     for pr in procs:
         pr.start()
+    # the initial model is made after the fork: a parallel torch op in the
+    # broker before it would leave the forked workers' OpenMP runtime locked
+    # (the reference's broker makes no model either)
+    torch.manual_seed(0)
+    init = make_model(model)
     data = {"init": init}
     waiting = {n: sum(1 for r in deps[n] if r != "init") for n in deps}
     left = {r: len(c) for r, c in consumers.items()}
