@@ -242,11 +242,15 @@ class ReduceWorkload:
         else:
             rows = aligned_empty(self.sets * batch * n * p_pad, tdt, dev, al).view(self.sets, batch, n, p_pad)
         self._keep.append(rows)
+        # DLSIM_BENCH_OUTS_FIRST: every output allocated before any fill (A/B
+        # knob of scripts/probes/probe_bench_setup.py)
+        outs_first = [arena_empty(p, tdt, dev) for _ in range(self.sets)] \
+            if batch == 1 and os.environ.get("DLSIM_BENCH_OUTS_FIRST") else None
         for s in range(self.sets):
             if batch == 1:
                 x = rows[s][0]
                 x[:, :p].copy_((torch.randn((n, p), generator=g, device=dev) * 0.05).to(tdt))
-                out = arena_empty(p, tdt, dev)
+                out = outs_first[s] if outs_first else arena_empty(p, tdt, dev)
                 plan = _native.ReducePlan([x[i, :p] for i in range(n)], w32, out, mode)
                 assert all(t.data_ptr() % 16 == 0 for t in plan._keep[0]), "arena rows must be 16-B aligned"
                 self.outs.append(out)

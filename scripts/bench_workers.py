@@ -167,14 +167,28 @@ def main():
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--ways", nargs="+", default=["cpu_ref", "hip", "hip_cache"])
     ap.add_argument("--model", choices=("gnlenet", "resnet18"), default="gnlenet")
+    ap.add_argument("--one", action="store_true", help=argparse.SUPPRESS)
     a = ap.parse_args()
+    if not a.one:
+        # one fresh broker process per way: a broker that has run parallel
+        # torch ops (the previous way's models) would fork workers whose
+        # OpenMP runtime is left locked
+        import subprocess
+        rc = 0
+        for way in a.ways:
+            r = subprocess.run([sys.executable, os.path.abspath(__file__), "--one", "--ways", way, "--peers",
+                                str(a.peers), "--workers", str(a.workers), "--rounds", str(a.rounds), "--model",
+                                a.model], timeout=900)
+            rc = rc or r.returncode
+        return rc
     import torch.multiprocessing as mp
     mp.set_sharing_strategy("file_system")  # broker.py:26
     from bench import box_info
     box = box_info()
     for way in a.ways:
         print(json.dumps(dict(run(way, a.peers, a.workers, a.rounds, a.model), box=box)), flush=True)
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())
