@@ -482,10 +482,11 @@ def _host_pipeline(all_params, idx, layout, dt, dev, out, weights_f32, mode, str
 def _cached_host_reduce(cache, all_params, idx, layout, dt, dev, out, weights_f32, mode, stream, defer):
     """Host models with a device cache (device_cache.py): the models whose
     file_system shm storages this process uploaded before are read from their
-    cached device rows; the others are packed, sent to fresh device rows (one
-    block, rows one stride apart: one DMA run) and cached; then the reduce and
-    the D2H, one dlsim_host_wreduce_resident call. None when no model is in
-    shared memory (the normal pipeline then runs). Returns as _host_pipeline."""
+    cached device rows; the others are packed and sent to free cache slots
+    (or to transient rows past the capacity, or for models not in shared
+    memory) and cached; then the reduce and the D2H, one
+    dlsim_host_wreduce_resident call. None when no model is in shared memory
+    (the normal pipeline then runs). Returns as _host_pipeline."""
     keys = _pyhost.shm_keys(all_params, idx)
     if all(k is None for k in keys):
         return None
@@ -496,13 +497,26 @@ def _cached_host_reduce(cache, all_params, idx, layout, dt, dev, out, weights_f3
     full = [None if k is None else (k, dev.index, dt, total) for k in keys]
     with cache.lock:
         rows = [None if k is None else cache.get(k) for k in full]
-        miss = [i for i in range(n) if rows[i] is None]
         resident = [r is not None for r in rows]
+        miss = [i for i in range(n) if rows[i] is None]
+        # cache slots for the keyed misses (one per distinct key), never
+        # evicting the rows this task reads; the rest get transient rows
+        want = []
+        for i in miss:
+            if full[i] is not None and full[i] not in [full[j] for j in want]:
+                want.append(i)
+        taken = cache.take_rows(dev, dt, stride, total, len(want), protected=sum(resident)) if want else []
+        slot_of = {}
+        for i, t in zip(want, taken):
+            slot_of[i] = t
+            rows[i] = t[2]
+        rest = [i for i in miss if i not in slot_of]
+        if rest:
+            block = aligned_empty(len(rest) * stride, dt, dev, base_align(total * esz, esz)).view(len(rest), stride)
+            for j, i in enumerate(rest):
+                rows[i] = block[j, :total]
         keep, src = [], [0] * (n * len(idx))
         if miss:
-            block = aligned_empty(len(miss) * stride, dt, dev, base_align(total * esz, esz)).view(len(miss), stride)
-            for j, i in enumerate(miss):
-                rows[i] = block[j, :total]
             keep, ptrs = _data_ptrs([all_params[i] for i in miss], idx)
             t = len(idx)
             for j, i in enumerate(miss):
@@ -521,12 +535,15 @@ def _cached_host_reduce(cache, all_params, idx, layout, dt, dev, out, weights_f3
             if not (defer and pinned_result):
                 stream.synchronize()
                 synced = True
+        except BaseException:
+            for t in slot_of.values():
+                cache.give_back(t)
+            raise
         finally:
             if miss:
                 STAGING.release(dev, dt, stream, synced)
-        for i in miss:
-            if full[i] is not None:
-                cache.put(full[i], rows[i], stride * esz)
+        for i, t in slot_of.items():
+            cache.put(full[i], t)
         st = cache.stats
         st["hits"] += n - len(miss)
         st["misses"] += sum(1 for i in miss if full[i] is not None)

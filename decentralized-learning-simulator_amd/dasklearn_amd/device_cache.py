@@ -16,6 +16,12 @@ is one allocation for the whole run), so a later aggregate in the same
 worker reads it in place and packs and sends only the models it has not seen
 (dlsim_host_wreduce_resident).
 
+Rows live in slabs the cache allocates once and reuses (one per device,
+dtype and row stride, grown in blocks of about 64 MB up to the capacity):
+an evicted row's slot takes the next upload, so a worker does not allocate
+device memory per task. Every use is on the caller's current stream, which
+orders a slot's reuse after the reads of its previous model.
+
 Contract (why it is opt-in): a cached model's shared storages must not be
 written while the cache holds them. The reference's aggregate inputs are the
 train task's freshly serialised outputs (functions.py:70-77), which nothing
@@ -32,9 +38,38 @@ from __future__ import annotations
 import os
 import threading
 from collections import OrderedDict
-from typing import Dict, Optional
+from typing import Dict, List, Optional, Tuple
 
 import torch
+
+BLOCK_BYTES = 64 << 20  # slab growth unit (at least one row)
+
+
+class _Slab:
+    """Row slots of one (device, dtype, stride): blocks of rows allocated
+    once, a sorted free list (lowest slots first, so a fresh run of rows is
+    contiguous and goes H2D in one DMA)."""
+
+    def __init__(self, dev, dt, stride: int, row_bytes: int, capacity: int):
+        self.dev, self.dt, self.stride, self.row_bytes = dev, dt, stride, row_bytes
+        self.per_block = max(1, min(BLOCK_BYTES, capacity) // row_bytes)
+        self.blocks: List[torch.Tensor] = []
+        self.free: List[int] = []
+
+    def grow(self) -> int:
+        """One more block; returns the bytes it took."""
+        from .arena import aligned_empty, base_align
+        esz = torch.empty((), dtype=self.dt).element_size()
+        al = base_align(self.stride * esz, esz)
+        blk = aligned_empty(self.per_block * self.stride, self.dt, self.dev, al).view(self.per_block, self.stride)
+        b = len(self.blocks)
+        self.blocks.append(blk)
+        self.free.extend(range(b * self.per_block, (b + 1) * self.per_block))
+        self.free.sort()
+        return self.per_block * self.row_bytes
+
+    def row(self, slot: int, total: int) -> torch.Tensor:
+        return self.blocks[slot // self.per_block][slot % self.per_block, :total]
 
 
 class DeviceModelCache:
@@ -42,8 +77,11 @@ class DeviceModelCache:
 
     def __init__(self, capacity_bytes: int):
         self.capacity = int(capacity_bytes)
-        self._rows: "OrderedDict[tuple, tuple]" = OrderedDict()  # key -> (row, bytes it is charged)
-        self.bytes = 0
+        # key -> (slab key, slot, row view)
+        self._rows: "OrderedDict[tuple, Tuple[tuple, int, torch.Tensor]]" = OrderedDict()
+        self._slabs: Dict[tuple, _Slab] = {}
+        self.bytes = 0          # bytes of rows held by entries
+        self.slab_bytes = 0     # device memory the slabs took
         self.lock = threading.Lock()
         self.stats: Dict[str, int] = {"hits": 0, "misses": 0, "uncacheable": 0, "evictions": 0,
                                       "bytes_not_sent": 0}
@@ -53,17 +91,62 @@ class DeviceModelCache:
         if e is None:
             return None
         self._rows.move_to_end(key)
-        return e[0]
+        return e[2]
 
-    def put(self, key, row: torch.Tensor, nbytes: int) -> None:
-        if key in self._rows or nbytes > self.capacity:
+    def _evict_one(self) -> None:
+        _, (sk, slot, _row) = self._rows.popitem(last=False)
+        slab = self._slabs[sk]
+        slab.free.append(slot)
+        slab.free.sort()
+        self.bytes -= slab.row_bytes
+        self.stats["evictions"] += 1
+
+    def take_rows(self, dev, dt, stride: int, total: int, k: int,
+                  protected: int = 0) -> List[Tuple[tuple, int, torch.Tensor]]:
+        """Up to k free row slots (fewer when the capacity does not allow
+        them), lowest first, evicting least recently used entries as needed
+        but never the `protected` most recently used ones (the rows the
+        calling task reads: get() made them the most recent). The caller
+        fills the slots on the current stream, then put()s them."""
+        esz = torch.empty((), dtype=dt).element_size()
+        row_bytes = stride * esz
+        sk = (dev.index, dt, stride)
+        slab = self._slabs.get(sk)
+        if slab is None:
+            slab = self._slabs[sk] = _Slab(dev, dt, stride, row_bytes, self.capacity)
+        out = []
+        while len(out) < k:
+            if not slab.free:
+                need = slab.per_block * row_bytes
+                if self.slab_bytes + need > self.capacity:
+                    if self.bytes + row_bytes > self.capacity and len(self._rows) > protected:
+                        self._evict_one()
+                        continue
+                    break  # no room for another block: the rest go uncached
+                self.slab_bytes += slab.grow()
+                continue
+            if self.bytes + row_bytes > self.capacity:
+                if len(self._rows) <= protected:
+                    break
+                self._evict_one()
+                continue
+            slot = slab.free.pop(0)
+            self.bytes += row_bytes  # charged now; put() or give_back() settles it
+            out.append((sk, slot, slab.row(slot, total)))
+        return out
+
+    def put(self, key, taken: Tuple[tuple, int, torch.Tensor]) -> None:
+        if key in self._rows:  # the same model twice in one task: keep the first
+            self.give_back(taken)
             return
-        self._rows[key] = (row, nbytes)
-        self.bytes += nbytes
-        while self.bytes > self.capacity and self._rows:
-            _, (_, old_bytes) = self._rows.popitem(last=False)
-            self.bytes -= old_bytes
-            self.stats["evictions"] += 1
+        self._rows[key] = taken
+
+    def give_back(self, taken: Tuple[tuple, int, torch.Tensor]) -> None:
+        sk, slot, _ = taken
+        slab = self._slabs[sk]
+        slab.free.append(slot)
+        slab.free.sort()
+        self.bytes -= slab.row_bytes
 
     def __len__(self) -> int:
         return len(self._rows)
@@ -71,7 +154,8 @@ class DeviceModelCache:
     def clear(self) -> None:
         with self.lock:
             self._rows.clear()
-            self.bytes = 0
+            self._slabs.clear()
+            self.bytes = self.slab_bytes = 0
 
 
 _CACHE: Optional[DeviceModelCache] = None

@@ -36,7 +36,7 @@ for p in (ROOT, os.path.join(ROOT, "scripts"), os.path.join(ROOT, "decentralized
         sys.path.insert(0, p)
 
 
-def worker_proc(way, shared, results, index):
+def worker_proc(way, shared, results, index, model_kind="gnlenet"):
     import copy
 
     import torch
@@ -69,6 +69,14 @@ def worker_proc(way, shared, results, index):
 
     funcs = {"aggregate": aggregate, "train": train}
     settings = Settings()
+    # one untimed aggregate first: the worker's one-time start-up (HIP
+    # context, library and kernel loads, staging buffers) is not a task cost
+    from bench_rounds import make_model
+    warm = make_model(model_kind)
+    for _ in range(2):
+        aggregate(settings, {"models": [warm, warm], "round": 0, "peer": 0})
+    del warm
+    results.put(("__ready__", index))
     stats = []
     while True:
         item = shared.get()
@@ -101,9 +109,12 @@ def run(way, peers, workers, rounds, model):
         for r in refs:
             consumers.setdefault(r, []).append(n)
     shared, results = mp.Queue(), mp.Queue()
-    procs = [mp.Process(target=worker_proc, args=(way, shared, results, i)) for i in range(workers)]
+    procs = [mp.Process(target=worker_proc, args=(way, shared, results, i, model)) for i in range(workers)]
     for pr in procs:
         pr.start()
+    for _ in procs:  # every worker has warmed up
+        tag, _i = results.get(timeout=300)
+        assert tag == "__ready__"
     # the initial model is made after the fork: a parallel torch op in the
     # broker before it would leave the forked workers' OpenMP runtime locked
     # (the reference's broker makes no model either)

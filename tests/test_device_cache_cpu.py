@@ -16,23 +16,34 @@ ROOT = os.path.dirname(HERE)
 PATHS = [ROOT, os.path.join(ROOT, "decentralized-learning-simulator_amd")]
 
 
-def test_lru_evicts_the_least_recently_used():
+def test_lru_slots_are_reused_and_protected():
+    """Rows come from slab slots allocated once: an evicted entry's slot takes
+    the next model; the rows the current task reads (the most recent,
+    `protected`) are never evicted; past the capacity the rest go uncached."""
     from dasklearn_amd.device_cache import DeviceModelCache
-    c = DeviceModelCache(3 * 400)
-    rows = {k: torch.zeros(100) for k in "abcd"}
-    for k in "abc":
-        c.put(k, rows[k], 400)
-    assert c.get("a") is rows["a"]  # a is now the most recent
-    c.put("d", rows["d"], 400)      # evicts b
-    assert c.get("b") is None and c.get("c") is rows["c"] and c.get("d") is rows["d"]
-    assert len(c) == 3 and c.bytes == 1200 and c.stats["evictions"] == 1
-    c.put("e", torch.zeros(10), 800)  # charged by the bytes given (a row's stride), not its view
-    assert c.get("c") is None and c.get("a") is None and c.get("e") is not None and c.bytes == 1200
-    c.put("big", torch.zeros(1000), 4000)  # larger than the whole cache: not kept
-    assert c.get("big") is None
+    dev = torch.device("cpu")
+    stride, total = 64, 50
+    c = DeviceModelCache(3 * stride * 4)       # room for three rows
+    t = c.take_rows(dev, torch.float32, stride, total, 3)
+    assert [x[1] for x in t] == [0, 1, 2] and all(x[2].numel() == total for x in t)
+    base = t[0][2].data_ptr()
+    assert t[1][2].data_ptr() == base + stride * 4  # consecutive slots: one DMA run
+    for key, x in zip("abc", t):
+        c.put(key, x)
+    assert c.get("a") is not None  # a is now the most recent
+    t2 = c.take_rows(dev, torch.float32, stride, total, 1)  # evicts b, reuses its slot
+    assert c.get("b") is None and t2[0][1] == 1 and c.stats["evictions"] == 1
+    c.put("d", t2[0])
+    assert c.slab_bytes == 3 * stride * 4     # no new memory
+    c.get("c"), c.get("a"), c.get("d")        # one task reads all three
+    assert c.take_rows(dev, torch.float32, stride, total, 2, protected=3) == []  # nothing evictable
+    t3 = c.take_rows(dev, torch.float32, stride, total, 2, protected=1)  # keeps d, the most recent
+    assert len(t3) == 2 and c.get("d") is not None and len(c) == 1
+    for x in t3:
+        c.give_back(x)
+    assert c.bytes == stride * 4
     c.clear()
     assert len(c) == 0 and c.bytes == 0
-    assert c.stats["evictions"] == 3
 
 
 def test_enable_from_env(monkeypatch):

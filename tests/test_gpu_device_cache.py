@@ -95,16 +95,21 @@ def test_non_shared_models_take_the_normal_pipeline(cache):
 
 
 def test_eviction_keeps_results_exact(shm_models):
+    """A cache with room for three rows: the first task caches three of five
+    models (the rest take transient rows), the next reads them and cannot
+    evict them, a task of new models evicts and reuses their slots; every
+    result exact."""
     from dasklearn_amd import arena, device_cache
     ms = shm_models
     row = arena.row_stride(sum(q.numel() for q in ms[0].parameters()), 4) * 4
     c = device_cache.enable(3 * row)  # room for three models
     try:
         _check(ms[:5], None)
-        assert len(c) == 3 and c.stats["evictions"] == 2
-        _check(ms[:5], None)  # models 2-4 resident, 0-1 sent again
-        assert c.stats["hits"] == 3
+        assert len(c) == 3 and c.stats["misses"] == 5 and c.slab_bytes == 3 * row
+        _check(ms[:5], None)  # three resident, two sent again (no slot may be taken from this task)
+        assert c.stats["hits"] == 3 and c.stats["evictions"] == 0
         _check(ms[4:9], [0.3, 0.2, 0.2, 0.2, 0.1])
+        assert c.stats["evictions"] == 3 and c.slab_bytes == 3 * row
     finally:
         device_cache.disable()
 
