@@ -68,6 +68,12 @@ def worker_proc(way, shared, results, index, model_kind="gnlenet"):
         gradient_aggregation = 1
 
     funcs = {"aggregate": aggregate, "train": train}
+
+    def cache_hits():
+        if way != "hip_cache":
+            return 0
+        from dasklearn_amd import device_cache
+        return device_cache.active().stats["hits"]
     settings = Settings()
     # one untimed aggregate first: the worker's one-time start-up (HIP
     # context, library and kernel loads, staging buffers) is not a task cost
@@ -83,9 +89,10 @@ def worker_proc(way, shared, results, index, model_kind="gnlenet"):
         if item is None:
             break
         name, fn, data = item
+        h0 = cache_hits()
         t0 = time.perf_counter()
         res = funcs[fn](settings, data)
-        stats.append((fn, time.perf_counter() - t0))
+        stats.append((fn, time.perf_counter() - t0, cache_hits() - h0))
         results.put((name, res))
         del data, res
     cache = None
@@ -154,16 +161,23 @@ def run(way, peers, workers, rounds, model):
     for _ in procs:
         name, (idx, stats, cache) = results.get(timeout=120)
         assert name == "__stats__"
-        agg += [t for f, t in stats if f == "aggregate"]
-        train += [t for f, t in stats if f == "train"]
+        agg += [(t, h) for f, t, h in stats if f == "aggregate"]
+        train += [t for f, t, _ in stats if f == "train"]
         if cache is not None:
             caches.append(cache)
     for pr in procs:
         pr.join(timeout=60)
+    times = [t for t, _ in agg]
     line = {"way": way, "model": model, "peers": peers, "workers": workers, "rounds": rounds, "fan_in": fan,
-            "aggregate_tasks": len(agg), "aggregate_us_median": round(statistics.median(agg) * 1e6, 1),
-            "aggregate_us_mean": round(statistics.mean(agg) * 1e6, 1),
+            "aggregate_tasks": len(agg), "aggregate_us_median": round(statistics.median(times) * 1e6, 1),
+            "aggregate_us_mean": round(statistics.mean(times) * 1e6, 1),
             "train_us_median": round(statistics.median(train) * 1e6, 1), "wall_s": round(wall, 3)}
+    if way == "hip_cache":  # median task time by the number of its inputs read from the cache
+        by = {}
+        for t, h in agg:
+            by.setdefault(h, []).append(t)
+        line["aggregate_us_median_by_hits"] = {str(h): [len(v), round(statistics.median(v) * 1e6, 1)]
+                                              for h, v in sorted(by.items())}
     if caches:
         tot = {k: sum(c[k] for c in caches) for k in ("hits", "misses", "uncacheable", "bytes_not_sent")}
         tot["hit_fraction"] = round(tot["hits"] / max(1, tot["hits"] + tot["misses"] + tot["uncacheable"]), 4)
