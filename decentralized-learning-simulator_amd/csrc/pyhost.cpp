@@ -45,6 +45,7 @@
 #include <torch/csrc/autograd/python_variable.h>
 
 #include <cstdint>
+#include <algorithm>
 #include <cstring>
 #include <unordered_set>
 #include <vector>
@@ -327,46 +328,55 @@ PyObject* py_data_ptrs(PyObject*, PyObject* args) {
 // tensors rows[i][k] (k in idx) when every one is a CPU tensor whose storage
 // is a torch.multiprocessing file_system shared-memory file (what a worker of
 // the reference receives, worker.py:6): (the first tensor's shm file name,
-// a 64-bit FNV-1a hash over every tensor's file name, storage offset, numel
-// and dtype). A file name names one storage allocation for the run, so a key
+// a 64-bit FNV-style hash over every tensor's file name, storage offset,
+// numel and dtype). A file name names one storage allocation for the run, so a key
 // seen again by this process is the same model's memory (device_cache.py);
 // None for a model with any tensor elsewhere. No Python attribute calls.
-PyObject* py_shm_keys(PyObject*, PyObject* args) {
-  PyObject *rows, *idx;
-  if (!PyArg_ParseTuple(args, "OO", &rows, &idx)) return nullptr;
-  std::vector<const at::Tensor*> ts;
-  Py_ssize_t n, t;
-  if (!row_tensors(rows, idx, ts, &n, &t)) return nullptr;
+// The storages of freshly received models are cold in the CPU caches, and
+// each tensor's file name sits four dependent loads away (tensor -> storage ->
+// allocator context -> name): the walk goes level by level over all tensors,
+// so the loads of one level overlap, and the hash mixes 8 bytes a step.
+PyObject* shm_keys_of(const std::vector<const at::Tensor*>& ts, Py_ssize_t n, Py_ssize_t t) {
+  const size_t m = ts.size();
+  std::vector<const c10::DataPtr*> dps(m, nullptr);
+  std::vector<const char*> names(m, nullptr);
+  std::vector<char> model_ok(static_cast<size_t>(n), t > 0);
+  for (size_t q = 0; q < m; ++q) {
+    const at::Tensor* x = ts[q];
+    if (x->device().type() == c10::DeviceType::CPU && x->has_storage()) dps[q] = &x->storage().data_ptr();
+  }
+  for (size_t q = 0; q < m; ++q) {
+    THManagedMapAllocator* ctx = dps[q] ? THManagedMapAllocator::fromDataPtr(*dps[q]) : nullptr;
+    if (ctx) names[q] = ctx->filename();
+  }
+  for (size_t q = 0; q < m; ++q)
+    if (!names[q]) model_ok[q / static_cast<size_t>(t)] = 0;
   PyObject* out = PyList_New(n);
   if (!out) return nullptr;
   for (Py_ssize_t i = 0; i < n; ++i) {
-    uint64_t h = 1469598103934665603ull;
-    auto mix = [&h](const void* p, size_t len) {
-      const unsigned char* c = static_cast<const unsigned char*>(p);
-      for (size_t q = 0; q < len; ++q) h = (h ^ c[q]) * 1099511628211ull;
-    };
-    const char* first = nullptr;
-    bool ok = t > 0;
-    for (Py_ssize_t j = 0; ok && j < t; ++j) {
-      const at::Tensor* x = ts[static_cast<size_t>(i * t + j)];
-      if (x->device().type() != c10::DeviceType::CPU || !x->has_storage()) {
-        ok = false;
-        break;
-      }
-      THManagedMapAllocator* ctx = THManagedMapAllocator::fromDataPtr(x->storage().data_ptr());
-      if (!ctx) {
-        ok = false;
-        break;
-      }
-      const char* fn = ctx->filename();
-      if (!first) first = fn;
-      mix(fn, std::strlen(fn) + 1);
-      const int64_t meta[3] = {x->storage_offset(), x->numel(), static_cast<int64_t>(x->scalar_type())};
-      mix(meta, sizeof(meta));
-    }
     PyObject* key;
-    if (ok) {
-      key = Py_BuildValue("(yK)", first, static_cast<unsigned long long>(h));
+    if (model_ok[static_cast<size_t>(i)]) {
+      uint64_t h = 1469598103934665603ull;
+      auto mix = [&h](uint64_t w) {
+        h = (h ^ w) * 1099511628211ull;
+        h ^= h >> 29;
+      };
+      for (Py_ssize_t j = 0; j < t; ++j) {
+        const size_t q = static_cast<size_t>(i * t + j);
+        const char* fn = names[q];
+        const size_t len = std::strlen(fn);
+        for (size_t o = 0; o < len; o += 8) {
+          uint64_t w = 0;
+          std::memcpy(&w, fn + o, std::min<size_t>(8, len - o));
+          mix(w);
+        }
+        mix(len);
+        const at::Tensor* x = ts[q];
+        mix(static_cast<uint64_t>(x->storage_offset()));
+        mix(static_cast<uint64_t>(x->numel()));
+        mix(static_cast<uint64_t>(x->scalar_type()));
+      }
+      key = Py_BuildValue("(yK)", names[static_cast<size_t>(i * t)], static_cast<unsigned long long>(h));
       if (!key) {
         Py_DECREF(out);
         return nullptr;
@@ -378,6 +388,53 @@ PyObject* py_shm_keys(PyObject*, PyObject* args) {
     PyList_SET_ITEM(out, i, key);
   }
   return out;
+}
+
+PyObject* py_shm_keys(PyObject*, PyObject* args) {
+  PyObject *rows, *idx;
+  if (!PyArg_ParseTuple(args, "OO", &rows, &idx)) return nullptr;
+  std::vector<const at::Tensor*> ts;
+  Py_ssize_t n, t;
+  if (!row_tensors(rows, idx, ts, &n, &t)) return nullptr;
+  return shm_keys_of(ts, n, t);
+}
+
+// shm_rows(rows, idx) -> (shm_keys(rows, idx), data_ptrs(rows, idx)): one
+// pass over the tensors of freshly received models, whose first touch is most
+// of the cost (device cache path, arena._cached_host_reduce)
+PyObject* py_shm_rows(PyObject*, PyObject* args) {
+  PyObject *rows, *idx;
+  if (!PyArg_ParseTuple(args, "OO", &rows, &idx)) return nullptr;
+  std::vector<const at::Tensor*> ts;
+  Py_ssize_t n, t;
+  if (!row_tensors(rows, idx, ts, &n, &t)) return nullptr;
+  PyObject* keys = shm_keys_of(ts, n, t);
+  if (!keys) return nullptr;
+  bool contiguous = true;
+  for (const at::Tensor* x : ts) contiguous = contiguous && x->is_contiguous();
+  PyObject* ptrs;
+  if (contiguous) {
+    ptrs = PyList_New(static_cast<Py_ssize_t>(ts.size()));
+    for (size_t q = 0; ptrs && q < ts.size(); ++q) {
+      PyObject* p = PyLong_FromVoidPtr(const_cast<void*>(ts[q]->const_data_ptr()));
+      if (!p) {
+        Py_CLEAR(ptrs);
+        break;
+      }
+      PyList_SET_ITEM(ptrs, static_cast<Py_ssize_t>(q), p);
+    }
+  } else {
+    ptrs = Py_None;
+    Py_INCREF(ptrs);
+  }
+  if (!ptrs) {
+    Py_DECREF(keys);
+    return nullptr;
+  }
+  PyObject* res = PyTuple_Pack(2, keys, ptrs);
+  Py_DECREF(keys);
+  Py_DECREF(ptrs);
+  return res;
 }
 
 // checked_params(module, signature) -> module_params(module) if it matches the
@@ -1037,6 +1094,7 @@ PyMethodDef kMethods[] = {
     {"matches", py_matches, METH_VARARGS, "params match a [(shape, dtype)] signature"},
     {"data_ptrs", py_data_ptrs, METH_VARARGS, "data pointers of rows[i][k] for k in idx, None if not contiguous"},
     {"shm_keys", py_shm_keys, METH_VARARGS, "per model, the identity of its file_system shm storages, or None"},
+    {"shm_rows", py_shm_rows, METH_VARARGS, "(shm_keys(rows, idx), data_ptrs(rows, idx)) in one pass"},
     {"clone_init", py_clone_init, METH_VARARGS,
      "clone_init(plain_cache, plain_fn, atomic_types, setstate_keys, deepcopy, OrderedDict)"},
     {"clone_module", py_clone_module, METH_VARARGS, "clone_module(module, memo): arena._clone_module in C"},

@@ -808,7 +808,7 @@ def host_wreduce_resident_raw(src_ptrs: Sequence[int], n: int, numels: Sequence[
     w = np.ascontiguousarray(weights_f32, dtype=np.float32)
     stride = staging.stride(0) if staging is not None and staging.dim() == 2 else 0
     rc = load().dlsim_host_wreduce_resident(
-        n, t, (ctypes.c_void_p * max(1, len(src_ptrs)))(*[p or None for p in src_ptrs]), (ctypes.c_size_t * t)(*numels),
+        n, t, (ctypes.c_void_p * max(1, len(src_ptrs)))(*src_ptrs), (ctypes.c_size_t * t)(*numels),
         w.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), (ctypes.c_int * n)(*[1 if r else 0 for r in resident]),
         (ctypes.c_void_p * n)(*row_ptrs), None if staging is None else staging.data_ptr(), stride, out.data_ptr(),
         None if host_out is None else host_out.data_ptr(), dtype, mode, threads, stream_handle)

@@ -487,7 +487,7 @@ def _cached_host_reduce(cache, all_params, idx, layout, dt, dev, out, weights_f3
     memory) and cached; then the reduce and the D2H, one
     dlsim_host_wreduce_resident call. None when no model is in shared memory
     (the normal pipeline then runs). Returns as _host_pipeline."""
-    keys = _pyhost.shm_keys(all_params, idx)
+    keys, ptrs = _pyhost.shm_rows(all_params, idx)
     if all(k is None for k in keys):
         return None
     n = len(all_params)
@@ -496,31 +496,34 @@ def _cached_host_reduce(cache, all_params, idx, layout, dt, dev, out, weights_f3
     stride = row_stride(total, esz)
     full = [None if k is None else (k, dev.index, dt, total) for k in keys]
     with cache.lock:
-        rows = [None if k is None else cache.get(k) for k in full]
+        rows = [None if k is None else cache.get(k) for k in full]  # device addresses of resident rows
         resident = [r is not None for r in rows]
         miss = [i for i in range(n) if rows[i] is None]
         # cache slots for the keyed misses (one per distinct key), never
         # evicting the rows this task reads; the rest get transient rows
-        want = []
+        want, seen = [], set()
         for i in miss:
-            if full[i] is not None and full[i] not in [full[j] for j in want]:
+            if full[i] is not None and full[i] not in seen:
+                seen.add(full[i])
                 want.append(i)
-        taken = cache.take_rows(dev, dt, stride, total, len(want), protected=sum(resident)) if want else []
-        slot_of = {}
-        for i, t in zip(want, taken):
-            slot_of[i] = t
+        taken = cache.take_rows(dev, dt, stride, total, len(want), protected=n - len(miss)) if want else []
+        slot_of = dict(zip(want, taken))
+        for i, t in slot_of.items():
             rows[i] = t[2]
         rest = [i for i in miss if i not in slot_of]
+        block = None
         if rest:
-            block = aligned_empty(len(rest) * stride, dt, dev, base_align(total * esz, esz)).view(len(rest), stride)
+            block = aligned_empty(len(rest) * stride, dt, dev, base_align(total * esz, esz))
+            b0 = block.data_ptr()
             for j, i in enumerate(rest):
-                rows[i] = block[j, :total]
-        keep, src = [], [0] * (n * len(idx))
-        if miss:
-            keep, ptrs = _data_ptrs([all_params[i] for i in miss], idx)
+                rows[i] = b0 + j * stride * esz
+        keep, src = [], ptrs  # resident models' pointers go unread
+        if miss and ptrs is None:  # a non-contiguous tensor: copies
+            keep, mp = _data_ptrs([all_params[i] for i in miss], idx)
             t = len(idx)
+            src = [0] * (n * t)
             for j, i in enumerate(miss):
-                src[i * t:(i + 1) * t] = ptrs[j * t:(j + 1) * t]
+                src[i * t:(i + 1) * t] = mp[j * t:(j + 1) * t]
         pinned_result = HOST_RESULT_PINNED or total * esz >= PAGEABLE_RESULT_BYTES
         host = torch.empty(total, dtype=dt, pin_memory=pinned_result)
         pinned = None
@@ -529,7 +532,7 @@ def _cached_host_reduce(cache, all_params, idx, layout, dt, dev, out, weights_f3
         synced = False
         try:
             _native.host_wreduce_resident_raw(src, n, layout.split_sizes[dt], weights_f32, resident,
-                                              [r.data_ptr() for r in rows], pinned, out, host,
+                                              rows, pinned, out, host,
                                               _native.dtype_code(dt), mode, torch.get_num_threads(),
                                               stream.cuda_stream)
             if not (defer and pinned_result):

@@ -54,31 +54,36 @@ class _Slab:
         self.dev, self.dt, self.stride, self.row_bytes = dev, dt, stride, row_bytes
         self.per_block = max(1, min(BLOCK_BYTES, capacity) // row_bytes)
         self.blocks: List[torch.Tensor] = []
+        self.bases: List[int] = []  # device address of each block
         self.free: List[int] = []
 
     def grow(self) -> int:
         """One more block; returns the bytes it took."""
-        from .arena import aligned_empty, base_align
-        esz = torch.empty((), dtype=self.dt).element_size()
+        from .arena import _elem_size, aligned_empty, base_align
+        esz = _elem_size(self.dt)
         al = base_align(self.stride * esz, esz)
-        blk = aligned_empty(self.per_block * self.stride, self.dt, self.dev, al).view(self.per_block, self.stride)
+        blk = aligned_empty(self.per_block * self.stride, self.dt, self.dev, al)
         b = len(self.blocks)
         self.blocks.append(blk)
+        self.bases.append(blk.data_ptr())
         self.free.extend(range(b * self.per_block, (b + 1) * self.per_block))
         self.free.sort()
         return self.per_block * self.row_bytes
 
-    def row(self, slot: int, total: int) -> torch.Tensor:
-        return self.blocks[slot // self.per_block][slot % self.per_block, :total]
+    def row_ptr(self, slot: int) -> int:
+        """Device address of a slot's row (plain ints: no tensor view per
+        row, the blocks keep the memory)."""
+        return self.bases[slot // self.per_block] + (slot % self.per_block) * self.row_bytes
 
 
 class DeviceModelCache:
-    """LRU of device rows keyed by (shm identity, device, dtype, elements)."""
+    """LRU of device rows keyed by (shm identity, device, dtype, elements);
+    a row is (slab key, slot, device address)."""
 
     def __init__(self, capacity_bytes: int):
         self.capacity = int(capacity_bytes)
-        # key -> (slab key, slot, row view)
-        self._rows: "OrderedDict[tuple, Tuple[tuple, int, torch.Tensor]]" = OrderedDict()
+        # key -> (slab key, slot, row address)
+        self._rows: "OrderedDict[tuple, Tuple[tuple, int, int]]" = OrderedDict()
         self._slabs: Dict[tuple, _Slab] = {}
         self.bytes = 0          # bytes of rows held by entries
         self.slab_bytes = 0     # device memory the slabs took
@@ -86,7 +91,7 @@ class DeviceModelCache:
         self.stats: Dict[str, int] = {"hits": 0, "misses": 0, "uncacheable": 0, "evictions": 0,
                                       "bytes_not_sent": 0}
 
-    def get(self, key) -> Optional[torch.Tensor]:
+    def get(self, key) -> Optional[int]:
         e = self._rows.get(key)
         if e is None:
             return None
@@ -102,19 +107,25 @@ class DeviceModelCache:
         self.stats["evictions"] += 1
 
     def take_rows(self, dev, dt, stride: int, total: int, k: int,
-                  protected: int = 0) -> List[Tuple[tuple, int, torch.Tensor]]:
+                  protected: int = 0) -> List[Tuple[tuple, int, int]]:
         """Up to k free row slots (fewer when the capacity does not allow
         them), lowest first, evicting least recently used entries as needed
         but never the `protected` most recently used ones (the rows the
         calling task reads: get() made them the most recent). The caller
         fills the slots on the current stream, then put()s them."""
-        esz = torch.empty((), dtype=dt).element_size()
-        row_bytes = stride * esz
+        from .arena import _elem_size
+        row_bytes = stride * _elem_size(dt)
         sk = (dev.index, dt, stride)
         slab = self._slabs.get(sk)
         if slab is None:
             slab = self._slabs[sk] = _Slab(dev, dt, stride, row_bytes, self.capacity)
         out = []
+        if len(slab.free) >= k and self.bytes + k * row_bytes <= self.capacity:  # the common case
+            for slot in slab.free[:k]:
+                out.append((sk, slot, slab.row_ptr(slot)))
+            del slab.free[:k]
+            self.bytes += k * row_bytes
+            return out
         while len(out) < k:
             if not slab.free:
                 need = slab.per_block * row_bytes
@@ -132,16 +143,16 @@ class DeviceModelCache:
                 continue
             slot = slab.free.pop(0)
             self.bytes += row_bytes  # charged now; put() or give_back() settles it
-            out.append((sk, slot, slab.row(slot, total)))
+            out.append((sk, slot, slab.row_ptr(slot)))
         return out
 
-    def put(self, key, taken: Tuple[tuple, int, torch.Tensor]) -> None:
+    def put(self, key, taken: Tuple[tuple, int, int]) -> None:
         if key in self._rows:  # the same model twice in one task: keep the first
             self.give_back(taken)
             return
         self._rows[key] = taken
 
-    def give_back(self, taken: Tuple[tuple, int, torch.Tensor]) -> None:
+    def give_back(self, taken: Tuple[tuple, int, int]) -> None:
         sk, slot, _ = taken
         slab = self._slabs[sk]
         slab.free.append(slot)

@@ -8,8 +8,15 @@ shared memory, fan-in 7, medians of FedAvg.aggregate: the normal pipeline
 (all miss), 7 resident models (all hit), and 3 resident + 4 new. New models
 are made and moved to shared memory before each timed call.
 
+Then, with cProfile, 100 calls each of the normal pipeline and the cache on
+7 new models (inputs built before profiling): the functions with the most
+own time, to place the cache path's extra cost (Python or the library call).
+
     python scripts/probes/probe_cache_path.py [reps]
 """
+import cProfile
+import io
+import pstats
 import json
 import os
 import statistics
@@ -65,8 +72,33 @@ def main():
         res.setdefault("cache_3_same_4_new", []).append(med(lambda: fixed[:3] + [shm_model() for _ in range(4)],
                                                             reps))
         res.setdefault("cache_stats", []).append(dict(c.stats, slab_bytes=c.slab_bytes))
+        # a cache of 32 rows: every miss reuses an evicted slot (device memory
+        # the cache has written before) instead of a never-used one
+        row = sum(q.numel() for q in fixed[0].parameters()) * 4
+        c = device_cache.enable(32 * (row + 4096))
+        res.setdefault("small_cache_7_new_all_miss", []).append(med(lambda: [shm_model() for _ in range(7)], reps))
+        res.setdefault("small_cache_stats", []).append(dict(c.stats, slab_bytes=c.slab_bytes))
     device_cache.disable()
     print(json.dumps(res), flush=True)
+    for name in ("normal", "cache"):
+        if name == "cache":
+            device_cache.enable(2 << 30)
+        else:
+            device_cache.disable()
+        for _ in range(10):
+            FedAvg.aggregate([shm_model() for _ in range(7)], None)
+        inputs = [[shm_model() for _ in range(7)] for _ in range(100)]
+        torch.cuda.synchronize()
+        pr = cProfile.Profile()
+        pr.enable()
+        for ms in inputs:
+            FedAvg.aggregate(ms, None)
+        pr.disable()
+        buf = io.StringIO()
+        pstats.Stats(pr, stream=buf).sort_stats("tottime").print_stats(14)
+        print("== profile", name, "(100 calls)\n" + buf.getvalue(), flush=True)
+        del inputs
+    device_cache.disable()
 
 
 if __name__ == "__main__":
