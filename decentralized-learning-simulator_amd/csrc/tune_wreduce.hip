@@ -231,6 +231,24 @@ __global__ __launch_bounds__(kBlock) void k_tiles_xcd(const Slots<128> s, int n,
   const size_t lane_off = (threadIdx.x >> 6) * 64 * VPT + (threadIdx.x & 63);
   reduce_tile<Op, Slots<128>, NF, 8, VPT, 1, false, 16, 64>(s, n, o, t * kT + lane_off, nvec);
 }
+// Translation-reach experiment (round 4, DLSIM_TUNE_TLB): the blocks that
+// share an XCD (blockIdx % 8) take runs of C consecutive tiles, the XCDs
+// advancing side by side through super-chunks of 8*C tiles, so one XCD's
+// translations cover ~1/8 of the pages in flight (C = 128 tiles of 16 KiB =
+// one 2 MiB page per stream). Full tiles only; block 0 idles.
+template <class Op, int NF, int VPT, int C>
+__global__ __launch_bounds__(kBlock) void k_tiles_xcdc(const Slots<128> s, int n, void* __restrict__ out,
+                                                       size_t nvec) {
+  constexpr size_t kT = static_cast<size_t>(kBlock) * VPT;
+  const OutRef o = make_out<16>(out, nvec);
+  if (blockIdx.x == 0) return;
+  const size_t k = blockIdx.x - 1;
+  const size_t j = k >> 3;
+  const size_t t = (j / C) * 8 * C + (k & 7) * C + (j % C);
+  if (t >= nvec / kT) return;
+  const size_t lane_off = (threadIdx.x >> 6) * 64 * VPT + (threadIdx.x & 63);
+  reduce_tile<Op, Slots<128>, NF, 8, VPT, 1, false, 16, 64>(s, n, o, t * kT + lane_off, nvec);
+}
 }  // namespace dlsim
 
 #define CK(x)                                                                          \
@@ -355,6 +373,14 @@ void launch_x(const Slots<128>& s, int n, void* out, size_t nvec, size_t, hipStr
                      nvec, per);
 }
 
+template <class Op, int NF, int VPT, int C>
+void launch_xc(const Slots<128>& s, int n, void* out, size_t nvec, size_t, hipStream_t st, int) {
+  const size_t full = nvec / ((size_t)kBlock * VPT);
+  const size_t super = 8 * (size_t)C;
+  const size_t grid = (full + super - 1) / super * super + 1;
+  hipLaunchKernelGGL((k_tiles_xcdc<Op, NF, VPT, C>), dim3((unsigned)grid), dim3(kBlock), 0, st, s, n, out, nvec);
+}
+
 // Memory-ceiling probe: the shipped fp32 access pattern (wave map, nt
 // loads, sc1 stores, same tiles) with the arithmetic replaced by a bitwise
 // XOR of the inputs. Its time is what the HBM allows for exactly this
@@ -470,6 +496,15 @@ void add_r03(std::vector<Variant>& vs, int n) {
     vs.push_back({p + "_V4_sc1_wave_S16", launch_ts16<Op, NF, 8, 4, 1, 16, true>, 0});
     vs.push_back({p + "_V4_sc1_wave_dev", launch_tsdev<Op, NF, 8, 4, 1, 16, true>, 0});
     vs.push_back({p + "_V4_sc1_wave_b", launch_ts<Op, NF, 8, 4, 1, 16, true>, 0});
+    return;
+  }
+  if (getenv("DLSIM_TUNE_TLB")) {  // tile orders against translation reach
+    vs.push_back({p + "_xorprobe", launch_probe<Op, NF>, 0});
+    vs.push_back({p + "_xcd_split", launch_x<Op, NF, 4>, 0});
+    vs.push_back({p + "_xcdc_16", launch_xc<Op, NF, 4, 16>, 0});
+    vs.push_back({p + "_xcdc_64", launch_xc<Op, NF, 4, 64>, 0});
+    vs.push_back({p + "_xcdc_128", launch_xc<Op, NF, 4, 128>, 0});
+    vs.push_back({p + "_xcdc_512", launch_xc<Op, NF, 4, 512>, 0});
     return;
   }
   vs.push_back({p + "_xorprobe", launch_probe<Op, NF>, 0});
@@ -605,7 +640,8 @@ int run(int n, size_t P, int reps, double peak_gbs) {
   // enough rotating input sets that their footprint is >= 1 GiB (4x the
   // 256 MiB Infinity Cache): small slices must not be served from it
   const double set_bytes = (double)(n + 1) * bytes;
-  const int sets = std::max(3, std::min(64, (int)((1ull << 30) / set_bytes) + 1));
+  int sets = std::max(3, std::min(64, (int)((1ull << 30) / set_bytes) + 1));
+  if (const char* ns = getenv("DLSIM_TUNE_SETS")) sets = std::max(1, atoi(ns));  // rotation length A/B
   printf("sets=%d footprint=%.0fMB\n", sets, sets * set_bytes / 1e6);
   const size_t nvec = P / Op::E;
   std::vector<void*> in((size_t)sets * n);
