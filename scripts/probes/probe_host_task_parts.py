@@ -12,8 +12,17 @@ own), medians over REPS tasks; then the whole FedAvg.aggregate call alone.
 Prints one JSON line.
 
     python scripts/probes/probe_host_task_parts.py [reps]
+    python scripts/probes/probe_host_task_parts.py [reps] --fresh
+
+--fresh: the shipped path's steps on the same 7 models every task against 7
+models made just before each task as a train task makes them (a deepcopy of
+the previous aggregate, updated in place: model_trainer.py's in-place
+optimiser steps), to place the ~100 us a task costs more in a round than
+isolated.
 """
 from __future__ import annotations
+
+import copy
 
 import json
 import os
@@ -87,12 +96,49 @@ def fedavg_us(models, reps):
     return round(statistics.median(ts) * 1e6, 1), [round(ts[len(ts) // 10] * 1e6, 1), round(ts[len(ts) * 9 // 10] * 1e6, 1)]
 
 
+def fresh_parts(reps, dev, stream):
+    torch.manual_seed(0)
+    base = GNLeNetTree()
+    same = [GNLeNetTree() for _ in range(7)]
+    arena.HOST_RESULT_PINNED = True
+    os.environ["DLSIM_H2D_MIN_KB"] = "1024"
+
+    def trained(m, i):
+        out = copy.deepcopy(m)
+        with torch.no_grad():
+            for q in out.parameters():
+                q.add_(1e-3 * (i + 1))
+        return out
+    res = {"model": "gnlenet_tree", "n": 7, "threads": torch.get_num_threads(), "reps": reps}
+    for rnd in range(2):
+        for kind in ("same", "fresh"):
+            acc, totals = {}, []
+            agg = base
+            for r in range(reps + 20):
+                models = same if kind == "same" else [trained(agg, i) for i in range(7)]
+                t = time.perf_counter()
+                marks, out = parts_once(models, dev, stream)
+                dt = time.perf_counter() - t
+                if kind == "fresh":
+                    agg = out  # the next task's models are trained from this result
+                if r >= 20:
+                    totals.append(dt)
+                    for k, v in marks:
+                        acc.setdefault(k, []).append(v)
+            res.setdefault(f"parts_us_median_{kind}", []).append(
+                {k: round(statistics.median(v) * 1e6, 1) for k, v in acc.items()})
+            res.setdefault(f"parts_sum_us_median_{kind}", []).append(round(statistics.median(totals) * 1e6, 1))
+    print(json.dumps(res), flush=True)
+
+
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 400
     torch.set_num_threads(4)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     stream = torch.cuda.current_stream(dev)
+    if "--fresh" in sys.argv:
+        return fresh_parts(reps, dev, stream)
     torch.manual_seed(0)
     models = [GNLeNetTree() for _ in range(7)]
     res = {"model": "gnlenet_tree", "n": 7, "threads": torch.get_num_threads(), "reps": reps}
