@@ -496,6 +496,7 @@ def _cached_host_reduce(cache, all_params, idx, layout, dt, dev, out, weights_f3
     stride = row_stride(total, esz)
     full = [None if k is None else (k, dev.index, dt, total) for k in keys]
     with cache.lock:
+        cache.order(stream)
         rows = [None if k is None else cache.get(k) for k in full]  # device addresses of resident rows
         resident = [r is not None for r in rows]
         miss = [i for i in range(n) if rows[i] is None]

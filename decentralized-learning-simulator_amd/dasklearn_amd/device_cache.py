@@ -20,7 +20,9 @@ Rows live in slabs the cache allocates once and reuses (one per device,
 dtype and row stride, grown in blocks of about 64 MB up to the capacity):
 an evicted row's slot takes the next upload, so a worker does not allocate
 device memory per task. Every use is on the caller's current stream, which
-orders a slot's reuse after the reads of its previous model.
+orders a slot's reuse after the reads of its previous model; a call on
+another stream than the previous call first waits for that stream's work
+(`order`), so threads with streams of their own stay ordered too.
 
 Contract (why it is opt-in): a cached model's shared storages must not be
 written while the cache holds them. The reference's aggregate inputs are the
@@ -88,8 +90,18 @@ class DeviceModelCache:
         self.bytes = 0          # bytes of rows held by entries
         self.slab_bytes = 0     # device memory the slabs took
         self.lock = threading.Lock()
+        self._stream = None     # the stream of the last call
         self.stats: Dict[str, int] = {"hits": 0, "misses": 0, "uncacheable": 0, "evictions": 0,
                                       "bytes_not_sent": 0}
+
+    def order(self, stream) -> None:
+        """Order this call's work on `stream` after every earlier call's: a
+        call on a new stream waits for the previous call's stream (whose
+        queued work includes every read and fill of the rows so far)."""
+        prev = self._stream
+        if prev is not None and prev != stream:
+            stream.wait_stream(prev)
+        self._stream = stream
 
     def get(self, key) -> Optional[int]:
         e = self._rows.get(key)
@@ -166,6 +178,7 @@ class DeviceModelCache:
         with self.lock:
             self._rows.clear()
             self._slabs.clear()
+            self._stream = None
             self.bytes = self.slab_bytes = 0
 
 

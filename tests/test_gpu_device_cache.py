@@ -127,3 +127,23 @@ def test_worker_process_cache(method):
     assert all(out["checks"].values()), out
     assert out["cache_stats"]["hits"] == 5 and out["cache_stats"]["misses"] == 7, out["cache_stats"]
     assert out["ok"] and r.returncode == 0, out
+
+
+def test_calls_on_two_streams_stay_ordered(shm_models):
+    """Two threads' streams taking turns on one cache: each call waits for the
+    other stream's reads and fills of the rows (DeviceModelCache.order); a
+    slot evicted on one stream is refilled on the other only after the first
+    stream's reads, so every result stays exact."""
+    from dasklearn_amd import arena, device_cache
+    ms = shm_models
+    row = arena.row_stride(sum(q.numel() for q in ms[0].parameters()), 4) * 4
+    c = device_cache.enable(4 * row)  # room for four rows: the alternation evicts
+    try:
+        streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+        sets = [ms[0:4], ms[4:8], ms[2:6], ms[5:9], ms[0:3] + [ms[8]]]
+        for k, group in enumerate(sets * 2):
+            with torch.cuda.stream(streams[k % 2]):
+                _check(group, None)
+        assert c.stats["evictions"] > 0 and c.stats["hits"] > 0
+    finally:
+        device_cache.disable()
