@@ -274,7 +274,10 @@ int wreduce_sharded(const void* const* d_slices, size_t slice_elems, int n, cons
 
 // The body of dlsim_sharded_plan_run / _f64: no agreement. A rank whose
 // local checks or launch fail still enters the plan's gather (so no peer is
-// left waiting in it) and then returns its error; its peers are not told.
+// left waiting in it) and then returns its error. Its peers get no error
+// code, but its slice arrives as NaN everywhere: the rank fills its share
+// with all-ones bytes, a NaN in every supported format, before the gather.
+// A stale or partial slice would otherwise reach them as plausible numbers.
 template <class W>
 int plan_run(dlsim_sharded_plan* p, const void* const* d_slices, size_t slice_elems, const W* h_weights, void* d_out,
              int mode, void* stream) {
@@ -303,7 +306,11 @@ int plan_run(dlsim_sharded_plan* p, const void* const* d_slices, size_t slice_el
   const Geometry g = geometry(p->n_elems, p->world, p->rank);
   const int dt = rccl_dtype(p->dtype);
   int crc;
+  const size_t share = (p->e - p->b) * esz;
   if (padded) {
+    if (rc != DLSIM_OK && share > 0)
+      (void)hipMemsetAsync(static_cast<char*>(p->scratch) + static_cast<size_t>(p->rank) * p->width * esz, 0xff,
+                           share, st);
     crc = gather_allgather(static_cast<char*>(p->scratch), out, g, p->world, p->rank, esz, dt, p->comm, st);
   } else {
     char* buf = out;
@@ -311,6 +318,7 @@ int plan_run(dlsim_sharded_plan* p, const void* const* d_slices, size_t slice_el
       const hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&buf), p->n_elems * esz, st);
       if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(stand-in output)");
     }
+    if (rc != DLSIM_OK && share > 0) (void)hipMemsetAsync(buf + p->b * esz, 0xff, share, st);
     crc = gather_bcast(buf, g, p->world, esz, dt, p->comm, st);
     if (buf != out) (void)hipFreeAsync(buf, st);
   }

@@ -617,8 +617,8 @@ class ShardedPlan:
     models, dtype, gather) on one RCCL communicator, agreed ONCE by every
     rank at construction (a collective call), then run any number of times
     with no agreement and no host wait (`run`). A rank whose run fails its
-    local checks still enters the gather and raises afterwards; its peers are
-    not told (include/dlsim.h)."""
+    local checks still enters the gather and raises afterwards; its peers get
+    no error, but its slice arrives as NaN (include/dlsim.h)."""
 
     def __init__(self, comm_ptr: int, n_elems: int, n: int, dtype, gather=True, device=None, stream=None):
         import torch

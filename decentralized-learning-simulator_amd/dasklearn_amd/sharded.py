@@ -288,9 +288,10 @@ class ParamShardPlan:
     On an RCCL group with the HIP reduce this is the C ABI's
     dlsim_sharded_plan; elsewhere (gloo, injected reduces) the agreement runs
     once here and each run is the local reduce plus the all-gather. Every
-    rank must run the same sequence of plans. A run whose local checks fail
-    still enters the gather (so no peer waits forever) and raises on that
-    rank only; its peers' copy of its slice is undefined."""
+    rank must run the same sequence of plans. A run whose local checks or
+    local reduce fail still enters the gather (so no peer waits forever) and
+    raises on that rank only; it sends its slice as NaN, so its peers' copy
+    of that slice is NaN rather than plausible numbers."""
 
     def __init__(self, agg: ShardedAggregator, n_elems: int, n_models: int, dtype: torch.dtype, gather=True):
         self.agg, self.n_elems, self.n, self.dtype = agg, int(n_elems), int(n_models), dtype
@@ -346,9 +347,14 @@ class ParamShardPlan:
                 out = torch.empty(self.n_elems, dtype=self.dtype, device=dev)
             self._c.run(list(shard_inputs), w, out, mode)
             return out if self.gather else out[b:e]
-        part = torch.zeros(e - b, dtype=self.dtype, device=dev)
+        part = torch.empty(e - b, dtype=self.dtype, device=dev)
         if local is None and e > b:
-            self.agg.local_reduce(list(shard_inputs), w, part, mode)
+            try:
+                self.agg.local_reduce(list(shard_inputs), w, part, mode)
+            except Exception as ex:  # noqa: BLE001 - raised after the gather
+                local = ex
+        if local is not None:
+            part.fill_(float("nan"))  # what the peers receive for this slice
         res = self.agg.all_gather(part, self.n_elems) if self.gather else part
         if local is not None:
             raise local

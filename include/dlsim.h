@@ -319,11 +319,12 @@ int dlsim_wreduce_sharded_f64(const void* const* d_slices, size_t slice_elems, i
  * stream-ordered, no host wait, no agreement. Every rank must run
  * the same sequence of plans, as with any collective. A rank whose local
  * checks or launch fail (null or overlapping pointers, mode, the f64 entry
- * on a non-f64 plan) still enters the plan's gather with whatever its slice
- * holds (a stand-in buffer when d_out is NULL), so no peer is left waiting,
- * and returns its error; its peers are not told (their copy of that slice is
- * undefined). Agree again (dlsim_wreduce_sharded, or a new plan) when that
- * matters.
+ * on a non-f64 plan) still enters the plan's gather, so no peer is left
+ * waiting, and returns its error. It sends its slice as all-ones bytes, a NaN
+ * in every supported format, through a stand-in buffer when d_out is NULL.
+ * Its peers get no error code, but that slice of their output is NaN, never
+ * stale numbers. Agree again (dlsim_wreduce_sharded, or a new plan) when a
+ * peer must learn of the failure.
  *
  * dlsim_sharded_plan_destroy frees the plan (rank-local; NULL is a no-op).
  * Plans are not thread-safe: one caller per plan at a time.

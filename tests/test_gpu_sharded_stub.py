@@ -316,7 +316,8 @@ def test_plan_agrees_once_over_ten_runs(stub, world, gather):
 def test_plan_run_failure_still_enters_the_gather(stub, gather):
     """A run whose local checks fail (null slices and output: run_failed, or
     a wrong weight count) still enters the plan's gather, so its peers are not
-    left waiting, and raises on this rank."""
+    left waiting, and raises on this rank. The slice it sends is all-ones
+    bytes (NaN), never the stale numbers its buffer held."""
     world, p = 3, 64 * 11 * 3 + 5
     xs, w, full, bounds = _case(world, p, "f32", 4242)
     peers = _peer_buffers(full, bounds)
@@ -332,8 +333,11 @@ def test_plan_run_failure_still_enters_the_gather(stub, gather):
         bad = np.concatenate([w, w[:1]])
         with pytest.raises(AssertionError):  # caught in Python, which still enters the gather
             plan.run([x[b:e] for x in xs], bad, out)
+        out[b:e].copy_(full[b:e])  # plausible numbers that must not be sent
         with pytest.raises(_native.DlsimError, match="slices have"):  # the library checks the length
             plan.run([x[b:e - 1] for x in xs], w, out)
+        torch.cuda.synchronize()
+        assert bool((out[b:e].view(torch.int32) == -1).all()), "a failed rank's slice goes out as NaN"
         entered = stub.stub_comm_calls(comm, None, None, None, 0) if gather == "bcast" \
             else stub.stub_comm_gathers(comm, None, None)
         assert entered == (3 * world if gather == "bcast" else 3)

@@ -230,8 +230,8 @@ def test_sharded_errors_are_collective_gloo(case, kind, text):
 
 def _plan_fail_worker(rank, world, port, q):
     """A plan run whose local checks fail on rank 1 (wrong-length shards):
-    rank 1 raises after entering the gather, rank 0 completes (its copy of
-    rank 1's slice is undefined), nobody hangs, and the plan keeps working."""
+    rank 1 raises after entering the gather, rank 0 completes with rank 1's
+    slice as NaN, nobody hangs, and the plan keeps working."""
     import datetime
     import time
     for path in PATHS:
@@ -248,16 +248,18 @@ def _plan_fail_worker(rank, world, port, q):
         shards = [x[b:e].contiguous() for x in xs]
         plan = agg.plan(p, n, torch.float32)
         t0 = time.perf_counter()
-        err = None
+        err, peer_nan = None, None
         try:
-            plan.run(shards if rank != 1 else [s[:-1] for s in shards], None)
+            got = plan.run(shards if rank != 1 else [s[:-1] for s in shards], None)
+            b1, e1 = agg.bounds(p, 1)
+            peer_nan = bool(torch.isnan(got[b1:e1]).all())
         except Exception as ex:  # noqa: BLE001
             err = type(ex).__name__
         secs = time.perf_counter() - t0
         again = plan.run(shards, None)
         expect = torch.from_numpy(orc.wreduce([x.numpy() for x in xs], orc.reference_weights(n, None), "f32"))
-        q.put((rank, {"err": err, "secs": secs, "again": torch.equal(again.view(torch.int32),
-                                                                      expect.view(torch.int32))}))
+        q.put((rank, {"err": err, "secs": secs, "peer_nan": peer_nan,
+                      "again": torch.equal(again.view(torch.int32), expect.view(torch.int32))}))
     except Exception:
         import traceback
         q.put((rank, {"error": traceback.format_exc()}))
@@ -280,3 +282,4 @@ def test_plan_run_failure_does_not_hang_gloo():
         assert "error" not in results[r], results[r].get("error")
         assert results[r]["secs"] < 20 and results[r]["again"], (r, results[r])
     assert results[0]["err"] is None and results[1]["err"] == "ValueError"
+    assert results[0]["peer_nan"] is True  # rank 1's slice arrived as NaN
