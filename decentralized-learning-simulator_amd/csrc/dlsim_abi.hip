@@ -79,11 +79,19 @@ struct StreamLinks {
 // on_units(u, v) on this thread for each run [u, v) of units that completed,
 // in order (u = 0 first; a run is every unit already packed when the
 // dispatcher looks, so a fast pack hands over long runs the caller can copy
-// with one DMA each). Below ~1 MiB of input the helpers stay asleep: their
-// wake-up costs more than they save.
+// with one DMA each). Below DLSIM_PACK_HELPERS_MIN_KB of input (read per
+// call, A/B probes) the helpers stay asleep: their wake-up costs more than
+// they save on sources already in the CPU caches.
+constexpr long kPackHelpersMinKB = 1024;
+size_t pack_helpers_min_bytes() {
+  const char* e = std::getenv("DLSIM_PACK_HELPERS_MIN_KB");
+  const long kb = e ? std::strtol(e, nullptr, 10) : kPackHelpersMinKB;
+  return static_cast<size_t>(kb > 0 ? kb : 0) << 10;
+}
+
 template <class F>
 void pack_and_dispatch(dlsim::PackJob& job, int threads, size_t in_bytes, F&& on_units) {
-  const int helpers = in_bytes < (size_t{1} << 20) ? 0 : std::min(std::max(threads, 1), 64) - 1;
+  const int helpers = in_bytes < pack_helpers_min_bytes() ? 0 : std::min(std::max(threads, 1), 64) - 1;
   dlsim::PackPool& pool = dlsim::PackPool::get();
   std::lock_guard<std::mutex> lk(pool.call_mutex());
   if (helpers > 0) pool.start(&job, helpers);

@@ -529,7 +529,10 @@ def _cached_host_reduce(cache, all_params, idx, layout, dt, dev, out, weights_f3
         host = torch.empty(total, dtype=dt, pin_memory=pinned_result)
         pinned = None
         if miss:
-            _, pinned = STAGING.acquire(dev, dt, len(miss), total, stream)
+            # rows for all n models, of which the misses use the first ones:
+            # the same shape every task, so acquire() reuses its views (a
+            # shape per miss count rebuilt them, ~30 us a task)
+            _, pinned = STAGING.acquire(dev, dt, n, total, stream)
         synced = False
         try:
             _native.host_wreduce_resident_raw(src, n, layout.split_sizes[dt], weights_f32, resident,

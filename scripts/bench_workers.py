@@ -36,7 +36,7 @@ for p in (ROOT, os.path.join(ROOT, "scripts"), os.path.join(ROOT, "decentralized
         sys.path.insert(0, p)
 
 
-def worker_proc(way, shared, results, index, model_kind="gnlenet"):
+def worker_proc(way, shared, results, index, model_kind="gnlenet", profile=False):
     import copy
 
     import torch
@@ -84,15 +84,23 @@ def worker_proc(way, shared, results, index, model_kind="gnlenet"):
     del warm
     results.put(("__ready__", index))
     stats = []
+    prof = None
+    if profile:  # --profile: cProfile around the aggregate calls only
+        import cProfile
+        prof = cProfile.Profile()
     while True:
         item = shared.get()
         if item is None:
             break
         name, fn, data = item
         h0 = cache_hits()
+        if prof is not None and fn == "aggregate":
+            prof.enable()
         t0 = time.perf_counter()
         res = funcs[fn](settings, data)
         stats.append((fn, time.perf_counter() - t0, cache_hits() - h0))
+        if prof is not None and fn == "aggregate":
+            prof.disable()
         results.put((name, res))
         del data, res
     cache = None
@@ -100,10 +108,17 @@ def worker_proc(way, shared, results, index, model_kind="gnlenet"):
         from dasklearn_amd import device_cache
         c = device_cache.active()
         cache = None if c is None else dict(c.stats, entries=len(c))
-    results.put(("__stats__", (index, stats, cache)))
+    top = None
+    if prof is not None:
+        import io
+        import pstats
+        buf = io.StringIO()
+        pstats.Stats(prof, stream=buf).sort_stats("tottime").print_stats(12)
+        top = buf.getvalue()
+    results.put(("__stats__", (index, stats, cache, top)))
 
 
-def run(way, peers, workers, rounds, model):
+def run(way, peers, workers, rounds, model, profile=False):
     import torch
     import torch.multiprocessing as mp
     from bench_rounds import dag, make_model
@@ -116,7 +131,8 @@ def run(way, peers, workers, rounds, model):
         for r in refs:
             consumers.setdefault(r, []).append(n)
     shared, results = mp.Queue(), mp.Queue()
-    procs = [mp.Process(target=worker_proc, args=(way, shared, results, i, model)) for i in range(workers)]
+    procs = [mp.Process(target=worker_proc, args=(way, shared, results, i, model, profile))
+             for i in range(workers)]
     for pr in procs:
         pr.start()
     for _ in procs:  # every worker has warmed up
@@ -159,8 +175,10 @@ def run(way, peers, workers, rounds, model):
         shared.put(None)
     agg, train, caches = [], [], []
     for _ in procs:
-        name, (idx, stats, cache) = results.get(timeout=120)
+        name, (idx, stats, cache, top) = results.get(timeout=120)
         assert name == "__stats__"
+        if top is not None and idx == 0:  # worker 0's profile
+            print(f"== {way}: worker 0 aggregate profile\n{top}", file=sys.stderr, flush=True)
         agg += [(t, h) for f, t, h in stats if f == "aggregate"]
         train += [t for f, t, _ in stats if f == "train"]
         if cache is not None:
@@ -192,6 +210,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--ways", nargs="+", default=["cpu_ref", "hip", "hip_cache"])
     ap.add_argument("--model", choices=("gnlenet", "resnet18"), default="gnlenet")
+    ap.add_argument("--profile", action="store_true", help="cProfile the aggregate calls (worker 0, stderr)")
     ap.add_argument("--one", action="store_true", help=argparse.SUPPRESS)
     a = ap.parse_args()
     if not a.one:
@@ -203,7 +222,7 @@ def main():
         for way in a.ways:
             r = subprocess.run([sys.executable, os.path.abspath(__file__), "--one", "--ways", way, "--peers",
                                 str(a.peers), "--workers", str(a.workers), "--rounds", str(a.rounds), "--model",
-                                a.model], timeout=900)
+                                a.model] + (["--profile"] if a.profile else []), timeout=900)
             rc = rc or r.returncode
         return rc
     import torch.multiprocessing as mp
@@ -211,7 +230,7 @@ def main():
     from bench import box_info
     box = box_info()
     for way in a.ways:
-        print(json.dumps(dict(run(way, a.peers, a.workers, a.rounds, a.model), box=box)), flush=True)
+        print(json.dumps(dict(run(way, a.peers, a.workers, a.rounds, a.model, a.profile), box=box)), flush=True)
     return 0
 
 
