@@ -84,6 +84,7 @@ class DeviceModelCache:
 
     def __init__(self, capacity_bytes: int):
         self.capacity = int(capacity_bytes)
+        self.pid = os.getpid()  # a forked child starts an empty cache of its own (active())
         # key -> (slab key, slot, row address)
         self._rows: "OrderedDict[tuple, Tuple[tuple, int, int]]" = OrderedDict()
         self._slabs: Dict[tuple, _Slab] = {}
@@ -198,7 +199,14 @@ def disable() -> None:
 
 
 def active() -> Optional[DeviceModelCache]:
-    return _CACHE
+    """The process's cache, or None. In a process forked from one that had a
+    cache, a new empty cache of the same capacity: the parent's device rows
+    and lock state mean nothing in the child."""
+    global _CACHE
+    c = _CACHE
+    if c is not None and c.pid != os.getpid():
+        c = _CACHE = DeviceModelCache(c.capacity)
+    return c
 
 
 def _from_env() -> None:

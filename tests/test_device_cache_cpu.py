@@ -121,3 +121,35 @@ def test_shm_keys_cover_every_tensor():
         assert _pyhost.shm_keys([[a, torch.randn(3)]], [0])[0] is not None
     finally:
         tmp.set_sharing_strategy(prev)
+
+
+def _child_cache(q):
+    from dasklearn_amd import device_cache
+    c = device_cache.active()
+    if c is None:
+        q.put((False, None, None, None))
+    else:
+        q.put((True, c.capacity, len(c), c.stats["hits"]))
+
+
+def test_forked_child_gets_an_empty_cache():
+    """A worker forked from a process that had a cache starts an empty one of
+    the same capacity (the parent's device rows mean nothing in the child)."""
+    import multiprocessing as mp
+    sys.path[:0] = [p for p in PATHS if p not in sys.path]
+    from dasklearn_amd import device_cache
+    prev = device_cache.active()
+    c = device_cache.enable(1 << 20)
+    try:
+        c._rows["k"] = (("x",), 0, 1234)  # a parent-side entry
+        c.stats["hits"] = 5
+        ctx = mp.get_context("fork")
+        q = ctx.Queue()
+        pr = ctx.Process(target=_child_cache, args=(q,))
+        pr.start()
+        got = q.get(timeout=60)
+        pr.join(timeout=60)
+        assert got == (True, 1 << 20, 0, 0)
+        assert device_cache.active() is c and len(c) == 1  # the parent's is untouched
+    finally:
+        device_cache._CACHE = prev
