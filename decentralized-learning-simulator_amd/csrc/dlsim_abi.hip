@@ -489,6 +489,19 @@ int dlsim_host_wreduce_resident(int n, int t, const void* const* h_srcs, const s
   if (misses > 0) {
     if (!h_staging || !aligned16(h_staging) || staging_stride % 8 != 0 || staging_stride < total)
       return fail(DLSIM_E_ARG, "staging: 16-B aligned rows of >= %zu elements, stride a multiple of 8", total);
+    // A row the call writes (a miss) must not overlap any other row; resident
+    // rows may alias each other (the same model twice in one task). Rows are
+    // all total*esz long, so sorted by address an overlap involving a miss
+    // shows between neighbours.
+    std::vector<std::pair<uintptr_t, int>> span(static_cast<size_t>(n));
+    for (int i = 0; i < n; ++i) span[i] = {reinterpret_cast<uintptr_t>(d_rows[i]), i};
+    std::sort(span.begin(), span.end());
+    for (size_t k = 1; k < span.size(); ++k) {
+      const int a = span[k - 1].second, b = span[k].second;
+      if (span[k].first < span[k - 1].first + total * esz && (!resident[a] || !resident[b]))
+        return fail(DLSIM_E_ARG, "device rows %d and %d overlap and one of them is written (not resident)",
+                    std::min(a, b), std::max(a, b));
+    }
   }
   hipStream_t st = static_cast<hipStream_t>(stream);
   char* stage = static_cast<char*>(h_staging);

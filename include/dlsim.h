@@ -386,8 +386,9 @@ int dlsim_host_wreduce(int n, int t, const void* const* h_srcs, const size_t* nu
  *                     and sent to d_rows[i], which keeps them for later calls
  * then the reduce of d_rows[0..n) into d_out (dlsim_wreduce rules, input
  * order i) and, if h_out, the D2H of the result; one chunk, all on `stream`,
- * asynchronous (h_out page-locked). Device rows must not overlap d_out.
- * Consecutive non-resident models whose device rows lie one staging stride
+ * asynchronous (h_out page-locked). Device rows must not overlap d_out; a
+ * non-resident model's row must not overlap any other row (resident rows may
+ * alias each other: the same model twice). Consecutive non-resident models whose device rows lie one staging stride
  * apart go H2D in runs of >= 1 MiB (DLSIM_H2D_MIN_KB).
  */
 int dlsim_host_wreduce_resident(int n, int t, const void* const* h_srcs, const size_t* numels,

@@ -104,3 +104,33 @@ def test_resident_all_and_none(dt, monkeypatch):
     rng = np.random.default_rng(7)
     _case(rng, dt, 1024, monkeypatch, all_resident=True)
     _case(rng, dt, 1024, monkeypatch, none_resident=True)
+
+
+def test_resident_rejects_overlapping_written_rows():
+    """A row the call writes (a model not resident) must not overlap another
+    row; resident rows may alias each other (the same model twice)."""
+    from dasklearn_amd import _native
+    dev = torch.device("cuda", 0)
+    total, n = 1000, 3
+    models = [[torch.randn(total)] for _ in range(n)]
+    rows = torch.zeros(4 * 1024, device=dev)
+    w32 = orc.reference_weights(n, None)
+    out = torch.empty(total, device=dev)
+    staging = torch.empty((n, 1024), pin_memory=True)
+    src = [m[0].data_ptr() for m in models]
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    base = rows.data_ptr()
+    # rows 0 and 1 overlap by half a row; row 1 is written
+    bad = [base, base + 500 * 4, base + 2048 * 4]
+    with pytest.raises(_native.DlsimError, match="overlap"):
+        _native.host_wreduce_resident_raw(src, n, [total], w32, [True, False, True], bad, staging, out, None,
+                                          _native.dtype_code(torch.float32), _native.DLSIM_EXACT, 1, stream)
+    # two resident rows that alias: allowed, and exact
+    r0 = rows[:total]
+    r0.copy_(models[0][0].to(dev))
+    same = [base, base, base + 2048 * 4]
+    _native.host_wreduce_resident_raw(src, n, [total], w32, [True, True, False], same, staging, out, None,
+                                      _native.dtype_code(torch.float32), _native.DLSIM_EXACT, 1, stream)
+    torch.cuda.synchronize()
+    exp = orc.wreduce([models[0][0].numpy(), models[0][0].numpy(), models[2][0].numpy()], w32, "f32")
+    assert orc.same_bits(out.cpu().numpy(), exp)
