@@ -329,7 +329,7 @@ PyObject* py_data_ptrs(PyObject*, PyObject* args) {
 // is a torch.multiprocessing file_system shared-memory file (what a worker of
 // the reference receives, worker.py:6): (the first tensor's shm file name,
 // a 64-bit FNV-style hash over every tensor's file name, storage offset,
-// numel and dtype). A file name names one storage allocation for the run, so a key
+// numel, dtype and strides). A file name names one storage allocation for the run, so a key
 // seen again by this process is the same model's memory (device_cache.py);
 // None for a model with any tensor elsewhere. No Python attribute calls.
 // The storages of freshly received models are cold in the CPU caches, and
@@ -375,6 +375,7 @@ PyObject* shm_keys_of(const std::vector<const at::Tensor*>& ts, Py_ssize_t n, Py
         mix(static_cast<uint64_t>(x->storage_offset()));
         mix(static_cast<uint64_t>(x->numel()));
         mix(static_cast<uint64_t>(x->scalar_type()));
+        for (const int64_t st : x->strides()) mix(static_cast<uint64_t>(st));  // a view's layout too
       }
       key = Py_BuildValue("(yK)", names[static_cast<size_t>(i * t)], static_cast<unsigned long long>(h));
       if (!key) {

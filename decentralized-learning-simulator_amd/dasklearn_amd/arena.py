@@ -519,12 +519,13 @@ def _cached_host_reduce(cache, all_params, idx, layout, dt, dev, out, weights_f3
             for j, i in enumerate(rest):
                 rows[i] = b0 + j * stride * esz
         keep, src = [], ptrs  # resident models' pointers go unread
-        if miss and ptrs is None:  # a non-contiguous tensor: copies
-            keep, mp = _data_ptrs([all_params[i] for i in miss], idx)
+        if ptrs is None:  # a non-contiguous tensor somewhere: the misses' copies
             t = len(idx)
             src = [0] * (n * t)
-            for j, i in enumerate(miss):
-                src[i * t:(i + 1) * t] = mp[j * t:(j + 1) * t]
+            if miss:
+                keep, mp = _data_ptrs([all_params[i] for i in miss], idx)
+                for j, i in enumerate(miss):
+                    src[i * t:(i + 1) * t] = mp[j * t:(j + 1) * t]
         pinned_result = HOST_RESULT_PINNED or total * esz >= PAGEABLE_RESULT_BYTES
         host = torch.empty(total, dtype=dt, pin_memory=pinned_result)
         pinned = None

@@ -20,10 +20,14 @@ shapes, dtypes, alignments, weights and special values, for a time budget.
               output on the device or the host at random (in-place tensors,
               registered arenas, uploaded host models, fp64 groups in one
               wave), random release/in-place settings, vs an oracle replay
+  cached      FedAvg.aggregate on host modules in file_system shared memory
+              with the per-worker device cache on (random capacity: hits,
+              misses, evictions, duplicates within a task, non-contiguous
+              parameters) vs the oracle per dtype group
 
 Prints one JSON line with the case counts and the first failures (if any).
 
-    python scripts/fuzz_parity.py [--seconds 120] [--seed 0]
+    python scripts/fuzz_parity.py [--seconds 120] [--seed 0] [--only cached,modules]
 """
 from __future__ import annotations
 
@@ -231,14 +235,70 @@ def executor_case(rng):
                     in_place=ex.tensors_in_place)
 
 
+def _check_modules(models, weights, out):
+    """FedAvg.aggregate's result against the oracle, per dtype group."""
+    n = len(models)
+    ok = True
+    for dt, code in ((torch.float32, "f32"), (torch.bfloat16, "bf16"), (torch.float16, "f16"),
+                     (torch.float64, "f64")):
+        w = orc.reference_weights_f64(n, weights) if code == "f64" else orc.reference_weights(n, weights)
+        rows = []
+        for m in models:
+            ps = [p.detach().reshape(-1).cpu() for p in m.parameters() if p.dtype == dt]
+            if ps:
+                t = torch.cat(ps)
+                rows.append(t.view(torch.int16).numpy().view(np.uint16) if dt in (torch.bfloat16, torch.float16)
+                            else t.numpy())
+        if rows:
+            got = torch.cat([p.detach().reshape(-1).cpu() for p in out.parameters() if p.dtype == dt])
+            ok = ok and orc.same_bits(bits(got), orc.wreduce(rows, w, code))
+    return ok
+
+
+def cached_case(rng):
+    """The device cache (dasklearn_amd/device_cache.py) on a pool of shm host
+    modules: several tasks draw random subsets (duplicates allowed), so models
+    hit, miss and get evicted; every result exact."""
+    import torch.multiprocessing as tmp
+    from dasklearn_amd import arena, device_cache
+    from dasklearn_amd.gradient_aggregation.fedavg import FedAvg
+    prev_strategy = tmp.get_sharing_strategy()
+    prev_cache = device_cache.active()
+    tmp.set_sharing_strategy("file_system")
+    try:
+        base = int(rng.integers(0, 1 << 30))
+        pool = [rand_module(np.random.default_rng(base), base + i, odd=True) for i in range(int(rng.integers(2, 10)))]
+        for m in pool:
+            m.share_memory()
+        biggest = max(sum(p.numel() for p in m.parameters() if p.dtype == d) * torch.empty((), dtype=d).element_size()
+                      for m in pool for d in (torch.float32, torch.bfloat16, torch.float16))
+        rows = int(rng.integers(1, 9))
+        c = device_cache.enable(rows * (arena.row_stride(max(1, biggest), 1) + 4096))
+        ok, tasks = True, int(rng.integers(2, 7))
+        for _ in range(tasks):
+            k = int(rng.integers(1, 9))
+            models = [pool[int(i)] for i in rng.integers(0, len(pool), size=k)]
+            weights = None if rng.random() < 0.4 else [float(v) for v in rng.standard_normal(k)]
+            out = FedAvg.aggregate(models, weights)
+            ok = ok and not any(p.is_cuda for p in out.parameters()) and _check_modules(models, weights, out)
+        st = dict(c.stats)
+        return ok, dict(kind="cached", pool=len(pool), tasks=tasks, cap_rows=rows, hits=st["hits"],
+                        misses=st["misses"], evictions=st["evictions"])
+    finally:
+        device_cache._CACHE = prev_cache
+        tmp.set_sharing_strategy(prev_strategy)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=120.0)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--only", default=None, help="comma-separated families (default: all, weighted)")
     a = ap.parse_args()
+    only = a.only.split(",") if a.only else None
     rng = np.random.default_rng(a.seed)
     counts = {"reduce": 0, "reduce_fast": 0, "tensors": 0, "batched": 0, "chunk_mean": 0, "modules": 0,
-              "reconstruct": 0, "host_reduce": 0, "host_chunk": 0, "executor": 0}
+              "reconstruct": 0, "host_reduce": 0, "host_chunk": 0, "executor": 0, "cached": 0}
     fails = []
     t_end = time.time() + a.seconds
     t_note = time.time() + 20
@@ -248,8 +308,10 @@ def main():
             t_note = time.time() + 20
         dtype = str(rng.choice(["f32", "bf16", "f16", "f64"]))
         which = rng.choice(["reduce", "tensors", "batched", "chunk_mean", "modules", "reconstruct",
-                            "host_reduce", "host_chunk", "executor"],
-                           p=[0.22, 0.1, 0.1, 0.18, 0.1, 0.1, 0.1, 0.05, 0.05])
+                            "host_reduce", "host_chunk", "executor", "cached"],
+                           p=[0.2, 0.1, 0.1, 0.16, 0.1, 0.1, 0.1, 0.05, 0.05, 0.04])
+        if only:
+            which = str(rng.choice(only))
         if dtype == "f64" and which not in ("reduce", "chunk_mean", "host_chunk"):
             dtype = "f32"  # fp64 reduces are the single-task entry (dlsim_wreduce_f64); chunk means take fp64
         try:
@@ -448,6 +510,9 @@ def main():
             elif which == "executor":
                 ok, case = executor_case(rng)
                 counts["executor"] += 1
+            elif which == "cached":
+                ok, case = cached_case(rng)
+                counts["cached"] += 1
             elif which == "host_chunk":
                 from dasklearn_amd.arena import _side_streams
                 cpu_threads = int(rng.choice([1, 2, 4, 8, 16]))

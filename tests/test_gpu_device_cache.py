@@ -147,3 +147,25 @@ def test_calls_on_two_streams_stay_ordered(shm_models):
         assert c.stats["evictions"] > 0 and c.stats["hits"] > 0
     finally:
         device_cache.disable()
+
+
+def test_non_contiguous_shared_parameters(cache):
+    """A shm model with a transposed parameter: misses are copied to a
+    contiguous row first; a task whose models are all resident needs no
+    pointers at all (fuzz_parity 'cached' found this case); exact."""
+    prev = tmp.get_sharing_strategy()
+    tmp.set_sharing_strategy("file_system")
+    try:
+        ms = []
+        for s in range(3):
+            m = Net(s)
+            m.fc.weight = nn.Parameter(m.fc.weight.detach().t().contiguous().t())  # same shape, transposed layout
+            assert not m.fc.weight.is_contiguous()
+            m.share_memory()
+            ms.append(m)
+        _check(ms, None)
+        _check(ms, [0.5, 0.25, 0.25])  # every model resident
+        _check([ms[2], ms[2], ms[0]], None)  # a duplicate, all resident
+        assert cache.stats["hits"] == 6 and cache.stats["misses"] == 3
+    finally:
+        tmp.set_sharing_strategy(prev)
