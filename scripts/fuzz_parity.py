@@ -20,6 +20,10 @@ shapes, dtypes, alignments, weights and special values, for a time budget.
               output on the device or the host at random (in-place tensors,
               registered arenas, uploaded host models, fp64 groups in one
               wave), random release/in-place settings, vs an oracle replay
+  sharded     dlsim_wreduce_sharded and dlsim_sharded_plan (both gathers) as
+              rank r of W on the stub RCCL (tests/native/stub_rccl.hip: the
+              peers' slices come from buffers the case fills): random W, sizes
+              (empty shards included), dtypes, repeated plan runs, vs one GPU
   cached      FedAvg.aggregate on host modules in file_system shared memory
               with the per-worker device cache on (random capacity: hits,
               misses, evictions, duplicates within a task, non-contiguous
@@ -32,6 +36,7 @@ Prints one JSON line with the case counts and the first failures (if any).
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -255,6 +260,81 @@ def _check_modules(models, weights, out):
     return ok
 
 
+STUB = os.path.join(ROOT, "tests", "native", "_build", "libstub_rccl.so")
+_STUB = None
+
+
+def _stub():
+    global _STUB
+    if _STUB is None:
+        lib = ctypes.CDLL(STUB)
+        vp = ctypes.c_void_p
+        lib.stub_comm_create.argtypes = [ctypes.c_int, ctypes.c_int, vp, ctypes.POINTER(vp)]
+        lib.stub_comm_create.restype = vp
+        lib.stub_comm_destroy.argtypes = [vp]
+        lib.stub_comm_set_gather_sources.argtypes = [vp, ctypes.POINTER(vp)]
+        lib.stub_comm_set_out_bytes.argtypes = [vp, ctypes.c_size_t]
+        _STUB = lib
+    return _STUB
+
+
+def sharded_case(rng, dtype):
+    """Rank r of W on the stub RCCL: its slices reduced locally, the other
+    ranks' slices delivered by the stub's broadcast / all-gather from buffers
+    holding what those ranks would send; the assembled output must equal the
+    one-GPU reduce bit for bit."""
+    stub = _stub()
+    world = int(rng.choice([1, 2, 3, 4, 5, 7, 8, 12]))
+    p = int(rng.choice([1, 63, 64, 100, 64 * world, 64 * world + 1, 4099, 70_001]))
+    n = int(rng.choice([1, 2, 3, 8, 17]))
+    gather = str(rng.choice(["bcast", "allgather"]))
+    how = str(rng.choice(["agreed", "plan"]))
+    r = int(rng.integers(0, world))
+    rows = rand_values(rng, n, p, dtype)
+    xs = to_dev(rows, dtype, 0)
+    w = rand_weights(rng, n, dtype)
+    full = torch.empty_like(xs[0])
+    _native.wreduce(xs, w, full)
+    bounds = [_native.shard_range(p, world, q, 64) for q in range(world)]
+    nan = float("nan")
+    peers = []
+    for b, e in bounds:
+        buf = torch.full_like(full, nan)
+        buf[b:e].copy_(full[b:e])
+        peers.append(buf)
+    width = (max(e - b for b, e in bounds) + 63) // 64 * 64
+    srcs = []
+    for b, e in bounds:
+        seg = torch.full((max(width, 1),), nan, dtype=full.dtype, device=full.device)
+        seg[:e - b].copy_(full[b:e])
+        srcs.append(seg)
+    out = torch.full_like(full, nan)
+    vp = ctypes.c_void_p
+    comm = stub.stub_comm_create(world, r, out.data_ptr(), (vp * world)(*[t.data_ptr() for t in peers]))
+    stub.stub_comm_set_out_bytes(comm, out.numel() * out.element_size())
+    stub.stub_comm_set_gather_sources(comm, (vp * world)(*[t.data_ptr() for t in srcs]))
+    _native.rccl_bind(STUB)
+    try:
+        b, e = bounds[r]
+        shards = [x[b:e] for x in xs]
+        if how == "agreed":
+            _native.wreduce_sharded(shards, w, out, comm, gather)
+            runs = 1
+        else:
+            plan = _native.ShardedPlan(comm, p, n, DT[dtype], gather, device=torch.device("cuda", 0))
+            runs = int(rng.integers(1, 4))
+            for _ in range(runs):
+                out.fill_(nan)
+                plan.run(shards, w, out)
+            plan.close()
+        torch.cuda.synchronize()
+        ok = orc.same_bits(bits(out), bits(full))
+    finally:
+        _native.rccl_bind()
+        stub.stub_comm_destroy(comm)
+    return ok, dict(kind="sharded", dtype=dtype, world=world, rank=r, p=p, n=n, gather=gather, how=how, runs=runs)
+
+
 def cached_case(rng):
     """The device cache (dasklearn_amd/device_cache.py) on a pool of shm host
     modules: several tasks draw random subsets (duplicates allowed), so models
@@ -298,7 +378,7 @@ def main():
     only = a.only.split(",") if a.only else None
     rng = np.random.default_rng(a.seed)
     counts = {"reduce": 0, "reduce_fast": 0, "tensors": 0, "batched": 0, "chunk_mean": 0, "modules": 0,
-              "reconstruct": 0, "host_reduce": 0, "host_chunk": 0, "executor": 0, "cached": 0}
+              "reconstruct": 0, "host_reduce": 0, "host_chunk": 0, "executor": 0, "cached": 0, "sharded": 0}
     fails = []
     t_end = time.time() + a.seconds
     t_note = time.time() + 20
@@ -308,11 +388,11 @@ def main():
             t_note = time.time() + 20
         dtype = str(rng.choice(["f32", "bf16", "f16", "f64"]))
         which = rng.choice(["reduce", "tensors", "batched", "chunk_mean", "modules", "reconstruct",
-                            "host_reduce", "host_chunk", "executor", "cached"],
-                           p=[0.2, 0.1, 0.1, 0.16, 0.1, 0.1, 0.1, 0.05, 0.05, 0.04])
+                            "host_reduce", "host_chunk", "executor", "cached", "sharded"],
+                           p=[0.18, 0.1, 0.1, 0.15, 0.1, 0.1, 0.1, 0.05, 0.05, 0.04, 0.03])
         if only:
             which = str(rng.choice(only))
-        if dtype == "f64" and which not in ("reduce", "chunk_mean", "host_chunk"):
+        if dtype == "f64" and which not in ("reduce", "chunk_mean", "host_chunk", "sharded"):
             dtype = "f32"  # fp64 reduces are the single-task entry (dlsim_wreduce_f64); chunk means take fp64
         try:
             if which == "reduce":
@@ -513,6 +593,9 @@ def main():
             elif which == "cached":
                 ok, case = cached_case(rng)
                 counts["cached"] += 1
+            elif which == "sharded":
+                ok, case = sharded_case(rng, dtype)
+                counts["sharded"] += 1
             elif which == "host_chunk":
                 from dasklearn_amd.arena import _side_streams
                 cpu_threads = int(rng.choice([1, 2, 4, 8, 16]))
