@@ -438,6 +438,112 @@ PyObject* py_shm_rows(PyObject*, PyObject* args) {
   return res;
 }
 
+// chunk_scan(chunks) -> (same_dtype, place, device_index, numels, fans, ptrs)
+// for ChunkManager.mean_chunk_indices (chunk_manager.py:38-40 semantics):
+// chunks[i] is the list of contributors of chunk index i. Raises
+// RuntimeError("stack expects each tensor to be equal size") as torch.stack
+// does when one index's tensors differ in shape or dtype. same_dtype: every
+// index has the dtype of chunks[0][0]; place: 1 all on the host, 2 all on one
+// GPU (device_index), 0 otherwise; numels / fans per index; ptrs the data
+// pointers index by index, or None when a tensor is not contiguous. One pass
+// in C instead of several Python loops over every contributor.
+PyObject* py_chunk_scan(PyObject*, PyObject* chunks) {
+  PyObject* cs_all = PySequence_Fast(chunks, "chunks must be a sequence");
+  if (!cs_all) return nullptr;
+  const Py_ssize_t k = PySequence_Fast_GET_SIZE(cs_all);
+  std::vector<const at::Tensor*> ts;
+  std::vector<Py_ssize_t> fans(static_cast<size_t>(k));
+  std::vector<int64_t> numels(static_cast<size_t>(k));
+  bool ok = true, same_dtype = true, all_cpu = true, all_cuda = true, contiguous = true;
+  int dev_index = -2;
+  c10::ScalarType dt0 = c10::ScalarType::Undefined;
+  for (Py_ssize_t i = 0; ok && i < k; ++i) {
+    PyObject* cs = PySequence_Fast(PySequence_Fast_GET_ITEM(cs_all, i), "each index must be a sequence");
+    if (!cs) {
+      ok = false;
+      break;
+    }
+    const Py_ssize_t m = PySequence_Fast_GET_SIZE(cs);
+    if (m < 1) {
+      PyErr_SetString(PyExc_RuntimeError, "stack expects a non-empty TensorList");
+      ok = false;
+    }
+    const at::Tensor* first = nullptr;
+    for (Py_ssize_t j = 0; ok && j < m; ++j) {
+      const at::Tensor* x = tensor_of(PySequence_Fast_GET_ITEM(cs, j));
+      if (!x) {
+        ok = false;
+        break;
+      }
+      if (!first) {
+        first = x;
+        if (dt0 == c10::ScalarType::Undefined) dt0 = x->scalar_type();
+        same_dtype = same_dtype && x->scalar_type() == dt0;
+      } else if (x->sizes() != first->sizes() || x->scalar_type() != first->scalar_type()) {
+        PyErr_SetString(PyExc_RuntimeError, "stack expects each tensor to be equal size");
+        ok = false;
+        break;
+      }
+      const c10::Device d = x->device();
+      if (d.is_cpu()) {
+        all_cuda = false;
+      } else {
+        all_cpu = false;
+        const int di = d.is_cuda() ? static_cast<int>(d.index()) : -3;
+        if (dev_index == -2) dev_index = di;
+        if (!d.is_cuda() || di != dev_index) all_cuda = false;
+      }
+      contiguous = contiguous && x->is_contiguous();
+      ts.push_back(x);
+    }
+    if (ok) {
+      fans[static_cast<size_t>(i)] = m;
+      numels[static_cast<size_t>(i)] = first ? first->numel() : 0;
+    }
+    Py_DECREF(cs);
+  }
+  Py_DECREF(cs_all);
+  if (!ok) return nullptr;
+  const int place = k > 0 && all_cpu ? 1 : (k > 0 && all_cuda ? 2 : 0);
+  PyObject* n_list = PyList_New(k);
+  PyObject* f_list = PyList_New(k);
+  PyObject* p_list = contiguous ? PyList_New(static_cast<Py_ssize_t>(ts.size())) : nullptr;
+  bool built = n_list && f_list && (!contiguous || p_list);
+  for (Py_ssize_t i = 0; built && i < k; ++i) {
+    PyObject* a = PyLong_FromLongLong(numels[static_cast<size_t>(i)]);
+    PyObject* b = PyLong_FromSsize_t(fans[static_cast<size_t>(i)]);
+    if (!a || !b) {
+      Py_XDECREF(a);
+      Py_XDECREF(b);
+      built = false;
+      break;
+    }
+    PyList_SET_ITEM(n_list, i, a);
+    PyList_SET_ITEM(f_list, i, b);
+  }
+  for (size_t q = 0; built && contiguous && q < ts.size(); ++q) {
+    PyObject* v = PyLong_FromVoidPtr(const_cast<void*>(ts[q]->const_data_ptr()));
+    if (!v) {
+      built = false;
+      break;
+    }
+    PyList_SET_ITEM(p_list, static_cast<Py_ssize_t>(q), v);
+  }
+  if (!built) {
+    Py_XDECREF(n_list);
+    Py_XDECREF(f_list);
+    Py_XDECREF(p_list);
+    return nullptr;
+  }
+  PyObject* ptrs = p_list;
+  if (!ptrs) {
+    ptrs = Py_None;
+    Py_INCREF(ptrs);
+  }
+  return Py_BuildValue("(NiiNNN)", PyBool_FromLong(same_dtype), place, place == 2 ? dev_index : -1, n_list,
+                       f_list, ptrs);
+}
+
 // checked_params(module, signature) -> module_params(module) if it matches the
 // signature, else None
 PyObject* py_checked_params(PyObject*, PyObject* args) {
@@ -1096,6 +1202,8 @@ PyMethodDef kMethods[] = {
     {"data_ptrs", py_data_ptrs, METH_VARARGS, "data pointers of rows[i][k] for k in idx, None if not contiguous"},
     {"shm_keys", py_shm_keys, METH_VARARGS, "per model, the identity of its file_system shm storages, or None"},
     {"shm_rows", py_shm_rows, METH_VARARGS, "(shm_keys(rows, idx), data_ptrs(rows, idx)) in one pass"},
+    {"chunk_scan", py_chunk_scan, METH_O,
+     "chunk_scan(chunks) -> (same_dtype, place, device_index, numels, fans, ptrs or None)"},
     {"clone_init", py_clone_init, METH_VARARGS,
      "clone_init(plain_cache, plain_fn, atomic_types, setstate_keys, deepcopy, OrderedDict)"},
     {"clone_module", py_clone_module, METH_VARARGS, "clone_module(module, memo): arena._clone_module in C"},

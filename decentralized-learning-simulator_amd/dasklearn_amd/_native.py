@@ -454,6 +454,32 @@ def chunk_mean_batched(tasks, threads=None, stream=None):
     return [t[1] for t in tasks]
 
 
+def chunk_mean_batched_raw(fan, ptrs, out_ptrs, numels, dtype: int, threads: int, stream_handle) -> None:
+    """dlsim_chunk_mean_batched on pointers the caller has validated
+    (ChunkManager.mean_chunk_indices after _pyhost.chunk_scan: contiguous
+    device chunks of one dtype on one device, outputs it allocated)."""
+    b = len(fan)
+    _check("dlsim_chunk_mean_batched",
+           load().dlsim_chunk_mean_batched(b, (ctypes.c_int * b)(*fan), (ctypes.c_void_p * len(ptrs))(*ptrs),
+                                           (ctypes.c_void_p * b)(*out_ptrs), (ctypes.c_size_t * b)(*numels), dtype,
+                                           int(threads), stream_handle))
+
+
+def host_chunk_mean_raw(fan, ptrs, numels, staging_ptr: int, d_staging_ptr: int, staging_elems: int, out_ptrs,
+                        host_ptrs, dtype: int, cpu_threads: int, threads: int, stream_handle, h2d=None,
+                        d2h=None) -> None:
+    """dlsim_host_chunk_mean on pointers the caller has validated (as
+    chunk_mean_batched_raw, host chunks; staging it sized with
+    staged_rows_elems)."""
+    b = len(fan)
+    _check("dlsim_host_chunk_mean",
+           load().dlsim_host_chunk_mean(b, (ctypes.c_int * b)(*fan), (ctypes.c_void_p * len(ptrs))(*ptrs),
+                                        (ctypes.c_size_t * b)(*numels), staging_ptr, d_staging_ptr, staging_elems,
+                                        (ctypes.c_void_p * b)(*out_ptrs),
+                                        None if host_ptrs is None else (ctypes.c_void_p * b)(*host_ptrs), dtype,
+                                        int(cpu_threads), int(threads), stream_handle, h2d, d2h))
+
+
 def staged_rows_elems(numels, fan_in, esz: int) -> int:
     """Staging size dlsim_host_chunk_mean needs: every input row at a 256-B
     aligned offset."""

@@ -39,7 +39,7 @@ import torch
 from torch import nn
 
 from . import _native
-from .arena import _side_streams, _target_device
+from .arena import _elem_size, _pyhost, _side_streams, _target_device
 
 
 ORDER_PINNED_TORCH = "2.10"
@@ -115,6 +115,9 @@ class ChunkManager:
         per-row H2D, per-index mean and D2H, overlapped). Each result lives
         where its first chunk lives."""
         _check_order_scope()
+        fast = _fast_means(chunks, device)
+        if fast is not None:
+            return fast[0]
         for cs in chunks:
             first = cs[0]
             for c in cs:
@@ -187,10 +190,13 @@ class ChunkManager:
     def reconstruct_model(chunks: List[List[torch.Tensor]], model: nn.Module) -> nn.Module:
         for idx in range(len(chunks)):
             assert chunks[idx], "No chunks received at index %d!" % idx
-        means = ChunkManager.mean_chunk_indices(chunks)  # one launch for every index
+        _check_order_scope()
+        fast = _fast_means(chunks, None)
+        means, flat_params = fast if fast is not None else (ChunkManager.mean_chunk_indices(chunks), None)
         for chunk_idx in range(len(chunks)):
             chunks[chunk_idx] = means[chunk_idx]
-        flat_params = _span(chunks)
+        if flat_params is None:
+            flat_params = _span(chunks)
         if flat_params is None:
             flat_params = torch.cat(chunks)
         # chunk_manager.py:45-52: copy consecutive slices of the flat means
@@ -215,6 +221,69 @@ class ChunkManager:
                 for d, src in zip(dsts, srcs):
                     d.copy_(src)
         return model
+
+
+def _fast_means(chunks, device):
+    """mean_chunk_indices for the common case, validated in one C pass
+    (_pyhost.chunk_scan) instead of Python loops over every contributor:
+    one dtype, every chunk contiguous and non-empty, all on the host (the
+    reference's case: dlsim_host_chunk_mean) or all on the target GPU
+    (dlsim_chunk_mean_batched). Returns (means, flat) — flat the means back to
+    back as one tensor (torch.cat(means) without the copy), or None when the
+    device outputs are padded — or None for any other case (the general path
+    below then runs)."""
+    same, place, dix, numels, fans, ptrs = _pyhost.chunk_scan(chunks)  # raises as torch.stack would
+    if not chunks or not same or ptrs is None or place == 0 or 0 in numels:
+        return None
+    first0 = chunks[0][0]
+    dt = first0.dtype
+    dev = _target_device([first0], device)
+    if place == 2 and dev.index != dix:
+        return None
+    esz = _elem_size(dt)
+    al = 256 // esz
+    # outputs back to back when every chunk but the last keeps the next one
+    # 16-B aligned (as the general path lays them out)
+    tight = all(k * esz % 16 == 0 for k in numels[:-1])
+    out_off, n_out = [], 0
+    for k in numels:
+        out_off.append(n_out)
+        n_out += k if tight else (k + al - 1) // al * al
+    code = _native.dtype_code(dt, single_task=True)
+    threads = torch.get_num_threads()
+    d_out = torch.empty(n_out, dtype=dt, device=dev)
+    d0 = d_out.data_ptr()
+    d_ptrs = [d0 + o * esz for o in out_off]
+    with torch.no_grad():
+        if place == 2:
+            _native.chunk_mean_batched_raw(fans, ptrs, d_ptrs, numels, code, threads,
+                                           torch._C._cuda_getCurrentRawStream(dev.index))
+            res, offs, flat = d_out, out_off, (d_out if tight else None)
+        else:
+            total = sum(numels)
+            host = torch.empty(total, dtype=dt, pin_memory=True)
+            h0 = host.data_ptr()
+            offs, h = [], 0
+            for k in numels:
+                offs.append(h)
+                h += k
+            need = _native.staged_rows_elems(numels, fans, esz)
+            stage = torch.empty(need, dtype=dt, pin_memory=True)
+            d_in = torch.empty(need, dtype=dt, device=dev)
+            stream = torch.cuda.current_stream(dev)
+            h2d, d2h = _side_streams(dev) if need * esz >= PIPELINE_SIDE_STREAM_BYTES else (None, None)
+            _native.host_chunk_mean_raw(fans, ptrs, numels, stage.data_ptr(), d_in.data_ptr(), need, d_ptrs,
+                                        [h0 + o * esz for o in offs], code, threads, threads, stream.cuda_stream,
+                                        None if h2d is None else h2d.cuda_stream,
+                                        None if d2h is None else d2h.cuda_stream)
+            stream.synchronize()
+            res, flat = host, host
+    means = []
+    for cs, o, k in zip(chunks, offs, numels):
+        m = res[o:o + k]
+        f = cs[0]
+        means.append(m if f.dim() == 1 else m.view(f.shape))
+    return means, flat
 
 
 def _overlapping(ts: List[torch.Tensor]) -> bool:

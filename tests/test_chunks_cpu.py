@@ -203,3 +203,25 @@ def test_f64_chunk_mean_oracle_matches_torch(threads):
                 assert np.array_equal(got.view(np.int64), exp.view(np.int64)), (m, n)
     finally:
         torch.set_num_threads(prev)
+
+
+def test_chunk_scan_classifies_and_validates():
+    """_pyhost.chunk_scan, the one-pass check ahead of the fast chunk-mean path
+    (chunk_manager._fast_means): torch.stack's error for unequal contributors,
+    the place code, per-index sizes and fan-in, the pointers in order, and None
+    pointers when a chunk is not contiguous."""
+    from dasklearn_amd.arena import _pyhost
+    a = [torch.randn(5) for _ in range(3)]
+    b = [torch.randn(7) for _ in range(2)]
+    same, place, dix, numels, fans, ptrs = _pyhost.chunk_scan([a, b])
+    assert (same, place, dix, numels, fans) == (True, 1, -1, [5, 7], [3, 2])
+    assert ptrs == [t.data_ptr() for t in a + b]
+    assert _pyhost.chunk_scan([a, [torch.randn(6, 2).t()]])[5] is None  # non-contiguous
+    assert _pyhost.chunk_scan([a, [torch.randn(7, dtype=torch.float64)]])[0] is False  # two dtypes
+    with pytest.raises(RuntimeError, match="stack expects each tensor to be equal size"):
+        _pyhost.chunk_scan([[torch.randn(5), torch.randn(4)]])
+    with pytest.raises(RuntimeError, match="stack expects each tensor to be equal size"):
+        _pyhost.chunk_scan([[torch.randn(5), torch.randn(5, dtype=torch.float64)]])
+    with pytest.raises(RuntimeError):
+        _pyhost.chunk_scan([[]])
+    assert _pyhost.chunk_scan([])[1] == 0
