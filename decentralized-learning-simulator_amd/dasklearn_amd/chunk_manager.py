@@ -191,29 +191,41 @@ class ChunkManager:
         for idx in range(len(chunks)):
             assert chunks[idx], "No chunks received at index %d!" % idx
         _check_order_scope()
-        fast = _fast_means(chunks, None)
-        means, flat_params = fast if fast is not None else (ChunkManager.mean_chunk_indices(chunks), None)
-        for chunk_idx in range(len(chunks)):
-            chunks[chunk_idx] = means[chunk_idx]
-        if flat_params is None:
-            flat_params = _span(chunks)
-        if flat_params is None:
-            flat_params = torch.cat(chunks)
-        # chunk_manager.py:45-52: copy consecutive slices of the flat means
-        # into every state_dict tensor (parameters and buffers, with the
-        # dtype conversion of copy_). The copies go out as one
-        # torch._foreach_copy_ (a few multi-tensor launches for a device
-        # model instead of one per tensor) unless two destinations share
-        # memory: a tied parameter is in state_dict() under each of its names,
-        # and the reference's copies run in order (the later one wins), which
-        # a multi-tensor launch does not guarantee.
-        dsts, srcs = [], []
-        pointer = 0
-        for param in model.state_dict().values():
-            numel = param.data.numel()
-            dsts.append(param.data)
-            srcs.append(flat_params[pointer:pointer + numel].view(param.data.shape))
-            pointer += numel
+        # host chunks: the means' copies are still in flight when this
+        # returns; the state_dict walk below runs meanwhile, and nothing reads
+        # the means before `pending` is synchronised
+        fast = _fast_means(chunks, None, sync=False)
+        pending = None
+        if fast is not None:
+            means, flat_params, pending = fast
+        else:
+            means, flat_params = ChunkManager.mean_chunk_indices(chunks), None
+        try:
+            for chunk_idx in range(len(chunks)):
+                chunks[chunk_idx] = means[chunk_idx]
+            if flat_params is None:
+                flat_params = _span(chunks)
+            if flat_params is None:
+                flat_params = torch.cat(chunks)
+            # chunk_manager.py:45-52: copy consecutive slices of the flat
+            # means into every state_dict tensor (parameters and buffers, with
+            # the dtype conversion of copy_). The copies go out as one
+            # torch._foreach_copy_ (a few multi-tensor launches for a device
+            # model instead of one per tensor) unless two destinations share
+            # memory: a tied parameter is in state_dict() under each of its
+            # names, and the reference's copies run in order (the later one
+            # wins), which a multi-tensor launch does not guarantee.
+            dsts, srcs = [], []
+            pointer = 0
+            for param in model.state_dict().values():
+                numel = param.data.numel()
+                dsts.append(param.data)
+                srcs.append(flat_params[pointer:pointer + numel].view(param.data.shape))
+                pointer += numel
+        finally:
+            if pending is not None:
+                pending[0].synchronize()  # the means are complete (pending[1:] kept their buffers alive)
+                pending = None
         with torch.no_grad():
             if dsts and all(d.device == flat_params.device for d in dsts) and not _overlapping(dsts):
                 torch._foreach_copy_(dsts, srcs)
@@ -223,7 +235,7 @@ class ChunkManager:
         return model
 
 
-def _fast_means(chunks, device):
+def _fast_means(chunks, device, sync: bool = True):
     """mean_chunk_indices for the common case, validated in one C pass
     (_pyhost.chunk_scan) instead of Python loops over every contributor:
     one dtype, every chunk contiguous and non-empty, all on the host (the
@@ -231,7 +243,10 @@ def _fast_means(chunks, device):
     (dlsim_chunk_mean_batched). Returns (means, flat) — flat the means back to
     back as one tensor (torch.cat(means) without the copy), or None when the
     device outputs are padded — or None for any other case (the general path
-    below then runs)."""
+    below then runs). sync=False: (means, flat, pending) instead, pending None
+    or (stream, buffers...) for host chunks whose copies are still in flight:
+    the caller synchronises pending[0] before reading the means and keeps
+    the tuple (the staging the DMAs read) alive until then."""
     same, place, dix, numels, fans, ptrs = _pyhost.chunk_scan(chunks)  # raises as torch.stack would
     if not chunks or not same or ptrs is None or place == 0 or 0 in numels:
         return None
@@ -251,6 +266,7 @@ def _fast_means(chunks, device):
         n_out += k if tight else (k + al - 1) // al * al
     code = _native.dtype_code(dt, single_task=True)
     threads = torch.get_num_threads()
+    pending = None
     d_out = torch.empty(n_out, dtype=dt, device=dev)
     d0 = d_out.data_ptr()
     d_ptrs = [d0 + o * esz for o in out_off]
@@ -276,14 +292,17 @@ def _fast_means(chunks, device):
                                         [h0 + o * esz for o in offs], code, threads, threads, stream.cuda_stream,
                                         None if h2d is None else h2d.cuda_stream,
                                         None if d2h is None else d2h.cuda_stream)
-            stream.synchronize()
+            if sync:
+                stream.synchronize()
+            else:
+                pending = (stream, stage, d_in, d_out)
             res, flat = host, host
     means = []
     for cs, o, k in zip(chunks, offs, numels):
         m = res[o:o + k]
         f = cs[0]
         means.append(m if f.dim() == 1 else m.view(f.shape))
-    return means, flat
+    return (means, flat) if sync else (means, flat, pending)
 
 
 def _overlapping(ts: List[torch.Tensor]) -> bool:
