@@ -1,7 +1,7 @@
 """The sharded path with the HIP kernel as the local reduce in more than one
 process (GPU).
 
-Two fresh rank processes (tests/_sharded_hip_child.py) share the one
+Two or four fresh rank processes (tests/_sharded_hip_child.py) share the one
 MI355X of the box with a gloo control plane: each runs
 aggregate_param_sharded (gathered and not), a plan's repeated runs and
 aggregate_model_sharded(exact=True) with ShardedAggregator's default local
@@ -31,8 +31,9 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def test_two_processes_hip_local_reduce_bit_exact():
-    world, port = 2, _free_port()
+@pytest.mark.parametrize("world", [2, 4])
+def test_processes_hip_local_reduce_bit_exact(world):
+    port = _free_port()
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
