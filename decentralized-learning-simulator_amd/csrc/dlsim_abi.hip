@@ -89,8 +89,17 @@ size_t pack_helpers_min_bytes() {
   return static_cast<size_t>(kb > 0 ? kb : 0) << 10;
 }
 
+// DLSIM_PACK_THREADS=k (read per call; deployment A/B runs): pack on k
+// threads whatever the caller asked for.
+int pack_threads(int threads) {
+  const char* e = std::getenv("DLSIM_PACK_THREADS");
+  const long k = e ? std::strtol(e, nullptr, 10) : 0;
+  return k > 0 ? static_cast<int>(std::min<long>(k, 64)) : threads;
+}
+
 template <class F>
 void pack_and_dispatch(dlsim::PackJob& job, int threads, size_t in_bytes, F&& on_units) {
+  threads = pack_threads(threads);
   const int helpers = in_bytes < pack_helpers_min_bytes() ? 0 : std::min(std::max(threads, 1), 64) - 1;
   dlsim::PackPool& pool = dlsim::PackPool::get();
   std::lock_guard<std::mutex> lk(pool.call_mutex());
