@@ -80,6 +80,11 @@ def module_params_py(module: nn.Module) -> List[nn.Parameter]:
     return out
 
 
+class ZipMismatch(ValueError):
+    """A model's parameter list differs from models[0]'s (count, shape or
+    dtype): it cannot share models[0]'s arena layout."""
+
+
 def _contiguous_strides(shape) -> Tuple[int, ...]:
     strides, acc = [], 1
     for d in reversed(tuple(shape)):
@@ -150,15 +155,15 @@ class ParamLayout:
         if ps is not None:
             return ps
         ps = module_params(module)
-        # The reference zips parameters() (fedavg.py:24) and silently truncates
-        # on a mismatch; equal shapes are what it assumes, so insist on them
-        # (INTEGRATION.md §3 lists this deviation).
+        # Not the arena's signature: the reference zips parameters()
+        # (fedavg.py:23-24), which aggregate_modules restates per parameter
+        # (_aggregate_zip); the one-launch paths refuse such a model.
         if not self.matches(ps):
             if len(ps) != len(self.params):
-                raise ValueError("models have different numbers of parameters")
+                raise ZipMismatch("models have different numbers of parameters")
             for k, (a, (shape, dt)) in enumerate(zip(ps, self._signature)):
                 if a.dtype is not dt or a.shape != shape:
-                    raise ValueError(f"parameter {k}: shape/dtype differs from models[0]")
+                    raise ZipMismatch(f"parameter {k}: shape/dtype differs from models[0]")
         return ps
 
     def arena_view(self, params: Sequence[torch.Tensor], dt: torch.dtype) -> Optional[torch.Tensor]:
@@ -938,8 +943,11 @@ def aggregate_modules(models: List[nn.Module], weights: Optional[Sequence[float]
         assert len(weights) == len(models)
     model0 = models[0]  # IndexError for an empty list, as the reference
     w32 = _native.fp32_weights(weights)
-    layout, arenas, dev, on_host, host_out, staged, pending = reduce_modules_to_arenas(
-        models, w32, mode, device, timing, to_host, weights_f64=weights, defer_host_sync=timing is None)
+    try:
+        layout, arenas, dev, on_host, host_out, staged, pending = reduce_modules_to_arenas(
+            models, w32, mode, device, timing, to_host, weights_f64=weights, defer_host_sync=timing is None)
+    except ZipMismatch:  # raised by the layout check, before any device work
+        return _aggregate_zip(models, weights, mode, device, to_host)
     if timing is None and not (host_out and not on_host):
         # the output module is built while a host result's copies may still
         # run (pending); it only makes views of the result
@@ -957,6 +965,57 @@ def aggregate_modules(models: List[nn.Module], weights: Optional[Sequence[float]
         _restride(out, layout)
     st.mark("module")
     return out
+
+
+def _aggregate_zip(models: List[nn.Module], weights: Sequence[float], mode: int,
+                   device=None, to_host: Optional[bool] = None) -> nn.Module:
+    """The reference's pairing for models whose parameter lists differ from
+    models[0]'s (fedavg.py:23-24): `zip(center.parameters(), m.parameters())`
+    stops at the shorter list, so output parameter t sums, in model order,
+    w_i * p_i[t] over the models that have a t-th parameter (models[0]
+    always does; a model's extra parameters are ignored), starting from
+    models[0][t] * 0; `c1.add_(w * p1)` broadcasts a p1 whose shape
+    broadcasts to c1's and raises RuntimeError otherwise, as torch does.
+    A p1 of another dtype raises ValueError (the reference would add a
+    product rounded in p1's dtype). One reduce launch per
+    parameter, on the GPU; a host model's tensors are copied in first. A rare
+    path: simulations aggregate one architecture and take the one-launch
+    paths above."""
+    weights = [float(w) for w in weights]
+    n = len(models)
+    plists = [module_params(m) for m in models]
+    p0 = plists[0]
+    layout = ParamLayout(models[0], p0)
+    dev = _target_device(p0, device)
+    host_out = (not any(p.is_cuda for p in p0)) if to_host is None else to_host
+    with torch.no_grad():
+        arenas = {dt: arena_empty(layout.totals[dt], dt, dev) for dt in layout.groups}
+        for t, c in enumerate(p0):
+            rows, ws = [], []
+            for i in range(n):
+                if len(plists[i]) <= t:
+                    continue
+                q = plists[i][t].detach()
+                if q.dtype != c.dtype:
+                    raise ValueError(f"parameter {t} of model {i}: dtype {q.dtype} differs from models[0]'s "
+                                     f"{c.dtype}")
+                if q.shape != c.shape:
+                    if torch.broadcast_shapes(q.shape, c.shape) != c.shape:
+                        raise RuntimeError(f"output with shape {list(c.shape)} doesn't match the broadcast "
+                                           f"shape {list(torch.broadcast_shapes(q.shape, c.shape))}")
+                    q = q.expand(c.shape)
+                rows.append(q.to(dev).contiguous().reshape(-1))
+                ws.append(weights[i])
+            if c.numel() == 0:
+                continue
+            off = layout.offsets[t]
+            out = arenas[c.dtype][off:off + c.numel()]
+            w = _native.weights_for_dtype(ws, c.dtype)
+            _native.wreduce(rows, w, out, mode)
+        if host_out:
+            arenas = arenas_to_host(arenas, torch.cuda.current_stream(dev))
+    out = module_from_arenas(models[0], layout, arenas)
+    return _restride(out, layout)
 
 
 def _restride(out: nn.Module, layout: ParamLayout) -> nn.Module:

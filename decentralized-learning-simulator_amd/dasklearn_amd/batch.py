@@ -17,7 +17,7 @@ import torch
 from torch import nn
 
 from . import _native
-from .arena import aggregate_modules, arena_empty, input_arenas, module_from_arenas
+from .arena import ZipMismatch, aggregate_modules, arena_empty, input_arenas, module_from_arenas
 
 
 def _resolve(models, weights) -> List[float]:
@@ -43,7 +43,10 @@ def aggregate_batch(tasks: Sequence[Tuple[List[nn.Module], Optional[Sequence[flo
     for ti, (models, weights) in enumerate(tasks):
         ws = _resolve(models, weights)
         model0 = models[0]  # IndexError for an empty task, as the reference
-        layout, _, views = input_arenas(models)
+        try:
+            layout, _, views = input_arenas(models)
+        except ZipMismatch:  # parameter lists differ: the per-parameter zip path
+            layout, views = None, None
         if _device_views(views) is None:
             results[ti] = aggregate_modules(models, weights, mode)
             continue

@@ -30,8 +30,8 @@ import torch
 from torch import nn
 
 from . import _native
-from .arena import (ParamLayout, _target_device, aligned_empty, base_align, layout_of, module_params,
-                    registered_arenas, row_stride)
+from .arena import (ParamLayout, ZipMismatch, _target_device, aggregate_modules, aligned_empty, base_align,
+                    layout_of, module_params, registered_arenas, row_stride)
 from .batch import _device_views, _resolve, aggregate_arena_tasks
 
 Task = Tuple[str, str, dict]  # (task_name, func_name, data with placeholders)
@@ -261,20 +261,30 @@ class RoundExecutor:
             resolved.append((models, ws))
         walked: dict = {}
         self._upload_host_models([m for models, _ in resolved for m in models], cache, walked)
-        for models, ws in resolved:
+        single = {}  # task position -> result of the per-parameter zip path
+        for j, (models, ws) in enumerate(resolved):
             ents = [self._arena_of(m, cache, walked) for m in models]
             layout0 = ents[0][0]
             sig = layout0._signature
-            for i in range(1, len(ents)):
-                lay = ents[i][0]
-                if lay._signature is not sig and lay._signature != sig:
-                    layout0.check_compatible(models[i])  # raises the shape/dtype error
+            try:
+                for i in range(1, len(ents)):
+                    lay = ents[i][0]
+                    if lay._signature is not sig and lay._signature != sig:
+                        layout0.check_compatible(models[i])
+            except ZipMismatch:  # parameter lists differ (fedavg.py:23-24 zip)
+                single[j] = aggregate_modules(models, ws, self.mode, to_host=False)
+                continue
             views = {dt: [a[dt] for _, a in ents] for dt in layout0.groups}
             prepared.append((models[0], layout0, views, ws, [lay.params for lay, _ in ents]))
+        n_tasks = len(resolved)
         resolved.clear()
         cache.clear()
         walked.clear()
-        return aggregate_arena_tasks(prepared, self.mode, on_launched)
+        outs = aggregate_arena_tasks(prepared, self.mode, on_launched)
+        if not single:
+            return outs
+        it = iter(outs)
+        return [single[j] if j in single else next(it) for j in range(n_tasks)]
 
     def run(self, tasks: Sequence[Task], seed: Optional[Dict[str, list]] = None) -> Dict[str, list]:
         """Execute `tasks`; `seed` pre-populates results (e.g. initial models).

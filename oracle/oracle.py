@@ -192,6 +192,43 @@ def chunk_mean(xs, dtype: str = "f32", threads: int = 4) -> np.ndarray:
     return out.view(np.float16) if dtype == "f16" else out
 
 
+def wreduce_zip(params_by_model, weights, dtype: str = "f32", mode: str = "exact"):
+    """FedAvg.aggregate over models whose parameter lists may differ
+    (fedavg.py:23-24): `zip(center.parameters(), m.parameters())` stops at the
+    shorter list, so output parameter t folds, in model order, the models that
+    have a t-th parameter (models[0] always; extra parameters are ignored),
+    and `c1.add_(w * p1)` broadcasts p1 to c1's shape (numpy's broadcast_to
+    stands in for torch's: RuntimeError when it does not reach c1's shape).
+
+    params_by_model: per model, the list of its parameter arrays (float32 /
+    float64, or uint16 bits for bf16 / f16). weights: the reference's argument
+    (None / [] / list), resolved with fedavg.py:14-17 over all N models.
+    Returns the list of output arrays in models[0]'s shapes."""
+    n = len(params_by_model)
+    if n < 1:
+        raise IndexError("list index out of range")
+    w = reference_weights_f64(n, weights) if dtype == "f64" else reference_weights(n, weights)
+    outs = []
+    for t, c in enumerate(params_by_model[0]):
+        c = np.asarray(c)
+        rows, ws = [], []
+        for i, ps in enumerate(params_by_model):
+            if len(ps) <= t:
+                continue
+            q = np.asarray(ps[t])
+            if q.shape != c.shape:
+                try:
+                    q = np.broadcast_to(q, c.shape)
+                except ValueError as e:
+                    raise RuntimeError(f"output with shape {list(c.shape)} doesn't match the broadcast "
+                                       f"shape of {list(q.shape)}") from e
+            rows.append(np.ascontiguousarray(q).reshape(-1))
+            ws.append(w[i])
+        outs.append(wreduce(rows, np.asarray(ws), dtype=dtype, mode=mode).reshape(c.shape)
+                    if c.size else c.copy())
+    return outs
+
+
 def chunk_mean_ilp_begin(m: int, n: int, threads: int, dtype: str = "f32") -> int:
     """First column that PyTorch's CPU sum folds in row_sum (ILP) order."""
     if dtype == "f64":

@@ -22,7 +22,33 @@ def pytest_configure(config):
 
 
 def golden_paths():
-    return sorted(glob.glob(os.path.join(GOLDEN, "*.npz")))
+    """The same-signature fixtures (make_golden.py): N models, one (N, P) row block."""
+    return sorted(p for p in glob.glob(os.path.join(GOLDEN, "*.npz"))
+                  if not os.path.basename(p).startswith("mismatch_"))
+
+
+def mismatch_paths():
+    """Fixtures of models whose parameter lists differ (make_golden_mismatch.py)."""
+    return sorted(glob.glob(os.path.join(GOLDEN, "mismatch_*.npz")))
+
+
+def load_mismatch(path):
+    """One mismatch fixture (no pickle): meta, per-model lists of parameter
+    arrays (bf16/f16 as uint16 bits), the weights argument, expected or None."""
+    with np.load(path, allow_pickle=False) as z:
+        d = {k: z[k] for k in z.files}
+    meta = json.loads(str(d["meta"]))
+    flat, off, params = d["inputs"], 0, []
+    for shapes in meta["shapes"]:
+        ps = []
+        for s in shapes:
+            k = int(np.prod(s)) if s else 1
+            ps.append(flat[off:off + k].reshape(s))
+            off += k
+        params.append(ps)
+    assert off == flat.size
+    w = [float(v) for v in d["weights"]] if "weights" in d else None
+    return meta, params, w, d.get("expected")
 
 
 def load_golden(path):
