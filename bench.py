@@ -198,6 +198,16 @@ def time_steps(launch, k_steps: int, sync, barrier, new_event):
     return ev_ms, wall_ms
 
 
+def _rows_alloc() -> str:
+    """How the input rows were allocated (arena.resident_empty)."""
+    from dasklearn_amd.arena import RESIDENT_BLOCKS
+    if RESIDENT_BLOCKS["contiguous"] and not RESIDENT_BLOCKS["fallback"]:
+        return "physically contiguous (dlsim_device_alloc)"
+    if RESIDENT_BLOCKS["fallback"]:
+        return "hipMalloc (the driver had no contiguous block)"
+    return "torch caching allocator"
+
+
 def n_sets(bytes_per_set: int) -> int:
     return max(3, min(256, math.ceil(MIN_SET_FOOTPRINT / max(1, bytes_per_set))))
 
@@ -216,7 +226,7 @@ class ReduceWorkload:
 
     def __init__(self, n, p, dtype, w32, mode, batch, dev, seed, stream):
         from dasklearn_amd import _native
-        from dasklearn_amd.arena import aligned_empty, arena_empty, base_align, row_stride
+        from dasklearn_amd.arena import aligned_empty, arena_empty, base_align, resident_empty, row_stride
         tdt = TORCH_DTYPE[dtype]
         esz = ELEM_BYTES[dtype]
         self.stream = stream
@@ -234,13 +244,14 @@ class ReduceWorkload:
         al = base_align(p * esz, esz)
         self.plans, self.probe_plans, self.outs, self._keep = [], [], [], []
         # every set's rows in ONE allocation, as the staging buffer holds a
-        # call's rows: rows in separate per-set allocations measured 0.5-2.5 %
-        # slower and varied with where the driver placed them
-        # (profiles/r03_bench_gap.jsonl)
+        # call's rows, and allocated as the staging is (arena.resident_empty:
+        # physically contiguous from 64 MiB on): rows in separate per-set
+        # allocations measured 0.5-2.5 % slower and varied with where the
+        # driver placed them (profiles/r03_bench_gap.jsonl)
         if per_set:
-            rows = [aligned_empty(batch * n * p_pad, tdt, dev, al).view(batch, n, p_pad) for _ in range(self.sets)]
+            rows = [resident_empty(batch * n * p_pad, tdt, dev, al).view(batch, n, p_pad) for _ in range(self.sets)]
         else:
-            rows = aligned_empty(self.sets * batch * n * p_pad, tdt, dev, al).view(self.sets, batch, n, p_pad)
+            rows = resident_empty(self.sets * batch * n * p_pad, tdt, dev, al).view(self.sets, batch, n, p_pad)
         self._keep.append(rows)
         # DLSIM_BENCH_OUTS_FIRST: every output allocated before any fill (A/B
         # knob of scripts/probes/probe_bench_setup.py)
@@ -609,7 +620,8 @@ def run_rank(args, rank: int, world: int, local: int):
                        "n_models": n, "params_total": p_cfg if strong or split > 1 else p * world,
                        "params_rank0": p, "tasks_per_step": B, "mode": args.mode,
                        "parallelism": f"param-shard x{world}",
-                       "bytes_per_step_rank0": wl.bytes_per_step},
+                       "bytes_per_step_rank0": wl.bytes_per_step,
+                       "rows_alloc": _rows_alloc()},
             "timing": {"value_from": "HIP events around the K launches on each rank's launch stream; "
                                      "value = all ranks' bytes / max over ranks; barriers outside the window",
                        "kernel_avg_us_per_rank": rank_us,

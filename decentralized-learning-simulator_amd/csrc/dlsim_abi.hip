@@ -741,6 +741,36 @@ int dlsim_probe_pattern(const void* const* d_inputs, int n, void* d_out, size_t 
   return run<dlsim::XorProbe<2>>(d_inputs, n, nullptr, d_out, n_elems, st);
 }
 
+int dlsim_device_alloc(size_t nbytes, int flags, void** d_out, int* contiguous) {
+  g_err.clear();
+  if (!d_out) return fail(DLSIM_E_ARG, "null d_out");
+  *d_out = nullptr;
+  if (contiguous) *contiguous = 0;
+  if (nbytes == 0) return fail(DLSIM_E_ARG, "zero-byte allocation");
+  if (flags & ~DLSIM_ALLOC_CONTIGUOUS) return fail(DLSIM_E_ARG, "unknown flags 0x%x", flags);
+  if (flags & DLSIM_ALLOC_CONTIGUOUS) {
+    void* p = nullptr;
+    if (hipExtMallocWithFlags(&p, nbytes, hipDeviceMallocContiguous) == hipSuccess && p) {
+      *d_out = p;
+      if (contiguous) *contiguous = 1;
+      return DLSIM_OK;
+    }
+    (void)hipGetLastError();  // best effort: the plain allocation below decides
+  }
+  void* p = nullptr;
+  hipError_t e = hipMalloc(&p, nbytes);
+  if (e != hipSuccess) return hip_fail(e, "hipMalloc");
+  *d_out = p;
+  return DLSIM_OK;
+}
+
+int dlsim_device_free(void* d_ptr) {
+  g_err.clear();
+  if (!d_ptr) return DLSIM_OK;
+  hipError_t e = hipFree(d_ptr);
+  return e == hipSuccess ? DLSIM_OK : hip_fail(e, "hipFree");
+}
+
 const char* dlsim_last_error(void) { return g_err.c_str(); }
 
 int dlsim_version(void) { return (1 << 16) | 1; }

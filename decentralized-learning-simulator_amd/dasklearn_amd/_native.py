@@ -47,6 +47,8 @@ EXPORTS = (
     "dlsim_rccl_bind",
     "dlsim_wreduce_sharded",
     "dlsim_wreduce_sharded_f64",
+    "dlsim_device_alloc",
+    "dlsim_device_free",
     "dlsim_sharded_plan_create",
     "dlsim_sharded_plan_run",
     "dlsim_sharded_plan_run_f64",
@@ -153,6 +155,10 @@ def load() -> ctypes.CDLL:
         lib.dlsim_shard_range.restype = i
         lib.dlsim_probe_pattern.argtypes = [ctypes.POINTER(vp), i, vp, sz, i, vp]
         lib.dlsim_probe_pattern.restype = i
+        lib.dlsim_device_alloc.argtypes = [sz, i, ctypes.POINTER(vp), ctypes.POINTER(i)]
+        lib.dlsim_device_alloc.restype = i
+        lib.dlsim_device_free.argtypes = [vp]
+        lib.dlsim_device_free.restype = i
         lib.dlsim_last_error.argtypes = []
         lib.dlsim_last_error.restype = ctypes.c_char_p
         lib.dlsim_version.argtypes = []
@@ -281,6 +287,53 @@ class ReducePlan:
         rc = self._lib.dlsim_wreduce(self._ptrs, self.n, self._wp, self._out, self.numel,
                                      self.dtype, self.mode, _stream_handle(self.device, stream))
         _check("dlsim_wreduce", rc)
+
+
+DLSIM_ALLOC_CONTIGUOUS = 1
+
+
+class DeviceBlock:
+    """One dlsim_device_alloc block on `device`, seen by torch through
+    `__cuda_array_interface__` (torch.as_tensor wraps it without a copy and
+    keeps this object alive while any view of it exists; the last view's
+    release frees the block with dlsim_device_free, which synchronises the
+    device — so only long-lived buffers come from here).
+    contiguous: the driver gave physically contiguous memory."""
+
+    def __init__(self, nbytes: int, device, contiguous: bool = True):
+        import torch
+        dev = torch.device(device)
+        idx = dev.index if dev.index is not None else torch.cuda.current_device()
+        lib = load()
+        p, got = ctypes.c_void_p(), ctypes.c_int(0)
+        with torch.cuda.device(idx):
+            _check("dlsim_device_alloc",
+                   lib.dlsim_device_alloc(int(nbytes), DLSIM_ALLOC_CONTIGUOUS if contiguous else 0,
+                                          ctypes.byref(p), ctypes.byref(got)))
+        self.ptr, self.nbytes, self.device_index = p.value, int(nbytes), idx
+        self.contiguous = bool(got.value)
+        self.pid = os.getpid()  # a forked child never frees its parent's block
+        self.__cuda_array_interface__ = {"shape": (self.nbytes,), "typestr": "|u1", "data": (self.ptr, False),
+                                         "version": 2, "strides": None}
+
+    def tensor(self):
+        """A uint8 torch tensor over the whole block (no copy)."""
+        import torch
+        with torch.cuda.device(self.device_index):
+            t = torch.as_tensor(self, device=torch.device("cuda", self.device_index))
+        if t.data_ptr() != self.ptr:
+            raise RuntimeError("torch copied the device block instead of wrapping it")
+        return t
+
+    def __del__(self):
+        ptr, self.ptr = getattr(self, "ptr", None), None
+        if ptr and _lib is not None and self.pid == os.getpid():
+            try:
+                import torch
+                with torch.cuda.device(self.device_index):
+                    _lib.dlsim_device_free(ptr)
+            except Exception:  # interpreter shutdown: the process exit frees it
+                pass
 
 
 def wreduce(inputs, weights_f32, out, mode: int = DLSIM_EXACT, stream=None):

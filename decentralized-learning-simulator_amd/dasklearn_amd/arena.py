@@ -264,8 +264,122 @@ def aligned_empty(numel: int, dtype: torch.dtype, device, align: int) -> torch.T
 
 def arena_empty(numel: int, dtype: torch.dtype, device) -> torch.Tensor:
     """A fresh aggregate output (one dtype arena of a model), aligned like a
-    row of its size (base_align)."""
-    return aligned_empty(numel, dtype, device, base_align(numel * _elem_size(dtype), _elem_size(dtype)))
+    row of its size (base_align). From 16 MiB on it comes from OUTPUT_POOL
+    (physically contiguous blocks); below, torch's allocator."""
+    esz = _elem_size(dtype)
+    al = base_align(numel * esz, esz)
+    if numel * esz >= OUT_POOL_MIN and torch.device(device).type == "cuda":
+        t = OUTPUT_POOL.take(numel, dtype, device)
+        if t is not None:
+            return t
+    return aligned_empty(numel, dtype, device, al)
+
+
+OUT_POOL_MIN = ROW_ALIGN_MIN  # bytes
+
+
+class _OutputPool:
+    """Physically contiguous device blocks for large aggregate outputs.
+
+    The output arena's placement sets the rate of the whole reduce: with the
+    north star's rows fixed, outputs in torch's allocator ran at 61.2-62.5 us
+    per launch depending on the pages the driver handed out, outputs in a
+    contiguous block at 60.9-61.3 us in every process
+    (profiles/r04s2_contig2/). A contiguous block cannot come
+    from torch's caching allocator, and hipMalloc/hipFree per call would cost
+    more than the kernel (hipFree synchronises the device), so the pool caches
+    blocks like torch's allocator does: grow-only lists keyed by (device,
+    stream, size rounded up to 2 MiB); a block is reused once no tensor views
+    its storage any more (the storage's use count), and only for an
+    allocation on the stream it was made for, so the stream orders the reuse
+    after every kernel queued on the block (the caching allocator's rule;
+    like it, a caller that hands an output to another stream must keep it
+    alive until that stream is done). A forked child starts an empty pool.
+    `release()` frees the blocks no tensor uses. DLSIM_CONTIGUOUS=0 turns
+    the pool off (A/B)."""
+
+    def __init__(self):
+        self.pid = os.getpid()
+        self.blocks: Dict[Tuple[int, int, int], List[torch.Tensor]] = {}
+        self.lock = threading.Lock()
+        self.made = 0
+
+    @staticmethod
+    def _in_use(base: torch.Tensor) -> bool:
+        # the pool's base tensor and the temporary storage object hold 2
+        return torch._C._storage_Use_Count(base.untyped_storage()._cdata) > 2
+
+    def take(self, numel: int, dtype: torch.dtype, device) -> Optional[torch.Tensor]:
+        if os.environ.get("DLSIM_CONTIGUOUS", "1") == "0":
+            return None
+        if self.pid != os.getpid():
+            self.__init__()
+        dev = torch.device(device)
+        idx = dev.index if dev.index is not None else torch.cuda.current_device()
+        nbytes = numel * _elem_size(dtype)
+        size = (nbytes + ROW_ALIGN - 1) // ROW_ALIGN * ROW_ALIGN
+        key = (idx, torch._C._cuda_getCurrentRawStream(idx), size)
+        with self.lock:
+            lst = self.blocks.setdefault(key, [])
+            for base in lst:
+                if not self._in_use(base):
+                    return base[:nbytes].view(dtype)  # the view marks it in use before the lock drops
+            blk = _native.DeviceBlock(size + ROW_ALIGN, torch.device("cuda", idx))
+            RESIDENT_BLOCKS["contiguous" if blk.contiguous else "fallback"] += 1
+            raw = blk.tensor()
+            skip = (-raw.data_ptr()) % ROW_ALIGN
+            base = raw[skip:skip + size]
+            del raw
+            lst.append(base)
+            self.made += 1
+            return base[:nbytes].view(dtype)
+
+    def cached_bytes(self) -> int:
+        with self.lock:
+            return sum(k[2] * len(v) for k, v in self.blocks.items())
+
+    def release(self) -> int:
+        """Free (hipFree, synchronising) every block no tensor uses; returns
+        the number freed."""
+        freed = 0
+        with self.lock:
+            for key in list(self.blocks):
+                keep = [b for b in self.blocks[key] if self._in_use(b)]
+                freed += len(self.blocks[key]) - len(keep)
+                self.blocks[key] = keep
+        return freed
+
+
+OUTPUT_POOL = _OutputPool()
+
+
+RESIDENT_CONTIG_MIN = 64 << 20  # bytes
+RESIDENT_BLOCKS = {"contiguous": 0, "fallback": 0}  # library blocks made, by kind
+
+
+def resident_empty(numel: int, dtype: torch.dtype, device, align: int) -> torch.Tensor:
+    """A LONG-LIVED device buffer (the grow-only staging rows, the device
+    cache's model blocks) starting at an `align`-byte boundary. From
+    RESIDENT_CONTIG_MIN bytes on it is physically contiguous memory from the
+    library (dlsim_device_alloc, DLSIM_ALLOC_CONTIGUOUS; hipMalloc if the
+    driver has none): rows in torch's allocator land on whatever physical
+    pages the driver hands out, and the north star's 8 rows ran 1-2 % apart
+    between two such allocations of one process, where contiguous blocks ran
+    at the fast end every time (profiles/r04s2_contig/).
+    Freeing such a block synchronises the device, so per-call buffers
+    (aggregate outputs, a wave's uploads) stay in torch's caching allocator.
+    DLSIM_CONTIGUOUS=0 turns it off (A/B)."""
+    esz = _elem_size(dtype)
+    nbytes = numel * esz
+    if nbytes < RESIDENT_CONTIG_MIN or os.environ.get("DLSIM_CONTIGUOUS", "1") == "0" \
+            or torch.device(device).type != "cuda":
+        return aligned_empty(numel, dtype, device, align)
+    align = max(align, 256)
+    blk = _native.DeviceBlock(nbytes + align, device)
+    RESIDENT_BLOCKS["contiguous" if blk.contiguous else "fallback"] += 1
+    raw = blk.tensor()
+    skip = (-raw.data_ptr()) % align
+    return raw[skip:skip + nbytes].view(dtype)
 
 
 class _Staging:
@@ -326,7 +440,7 @@ class _Staging:
             need = max(1, n * stride)
             al = base_align(numel * esz, esz)
             # aligned as this call needs (a later call that needs 2 MiB rows regrows the buffer)
-            flat = self._grow(self.dev, key, need, lambda k: aligned_empty(k, dt, device, al), align=al)
+            flat = self._grow(self.dev, key, need, lambda k: resident_empty(k, dt, device, al), align=al)
             hflat = self._grow(self.host, key, need, lambda k: torch.empty(k, dtype=dt, pin_memory=True)) \
                 if pinned else None
             last = self._views.get(key)

@@ -61,10 +61,10 @@ class _Slab:
 
     def grow(self) -> int:
         """One more block; returns the bytes it took."""
-        from .arena import _elem_size, aligned_empty, base_align
+        from .arena import _elem_size, base_align, resident_empty
         esz = _elem_size(self.dt)
         al = base_align(self.stride * esz, esz)
-        blk = aligned_empty(self.per_block * self.stride, self.dt, self.dev, al)
+        blk = resident_empty(self.per_block * self.stride, self.dt, self.dev, al)
         b = len(self.blocks)
         self.blocks.append(blk)
         self.bases.append(blk.data_ptr())

@@ -456,6 +456,22 @@ int dlsim_shard_range(size_t n_elems, int world, int rank, size_t align_elems,
 int dlsim_probe_pattern(const void* const* d_inputs, int n, void* d_out, size_t n_elems, int dtype,
                         void* stream);
 
+/*
+ * dlsim_device_alloc / dlsim_device_free — device memory for long-lived
+ * large buffers (staging rows, resident model blocks) on the calling
+ * thread's current device. flags DLSIM_ALLOC_CONTIGUOUS asks the driver for
+ * physically contiguous memory (hipExtMallocWithFlags with
+ * hipDeviceMallocContiguous): the HBM channel and page placement of a
+ * buffer's rows is then the same in every process (DESIGN.md §5b measured
+ * 1-3 % between allocations of the default kind). If the driver cannot
+ * provide it, the call falls back to hipMalloc and sets *contiguous = 0.
+ * dlsim_device_free synchronises the device (hipFree): for buffers that
+ * live long, not per call. (New: the reference allocates nothing on a GPU.)
+ */
+#define DLSIM_ALLOC_CONTIGUOUS 1
+int dlsim_device_alloc(size_t nbytes, int flags, void** d_out, int* contiguous);
+int dlsim_device_free(void* d_ptr);
+
 /* Message for the last failing call on this thread ("" if none). */
 const char* dlsim_last_error(void);
 

@@ -18,5 +18,5 @@ python3 -c "import json; d=json.load(open('$O/bench_default.json')); print(d['va
 timeout -k 10 120 python3 bench.py --steps 20 --warmup 5 > $O/bench_driver.json 2> $O/bench_driver.err || exit $?
 python3 -c "import json; d=json.load(open('$O/bench_driver.json')); print('driver shape', d['ms_per_step'], d['roofline']['frac'])"
 step rocprof
-cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 $R/bench.py --no-cpu-baseline > $O/prof_bench.json 2> $O/prof_bench.err || exit $?
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/prof -o run -- python3 $R/bench.py --no-cpu-baseline > $O/prof_bench.json 2> $O/prof_bench.err || exit $?
 step done

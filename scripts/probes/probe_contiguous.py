@@ -63,7 +63,25 @@ class Sets:
         row_bytes = P_PAD * ESZ
         out_bytes = row_stride(P, ESZ) * ESZ
         self.keep, self.rc = [], 0
-        if alloc == "torch":
+        if alloc == "contig_rows":  # rows in a contiguous block, outputs from torch (the product's split)
+            total = n_sets * N * row_bytes + AL
+            raw, self.rc = hip_malloc_contig(total)
+            if self.rc != 0:
+                raise RuntimeError(f"hipExtMallocWithFlags(contiguous, {total}) -> {self.rc}")
+            base = (raw + AL - 1) // AL * AL
+            outs = [arena_empty(P, torch.float32, dev) for _ in range(n_sets)]
+            self.keep += outs
+            out_ptrs = [o.data_ptr() for o in outs]
+        elif alloc == "contig_outs":  # rows from torch, outputs in a contiguous block
+            rows = aligned_empty(n_sets * N * P_PAD, torch.float32, dev, AL)
+            self.keep.append(rows)
+            base = rows.data_ptr()
+            raw, self.rc = hip_malloc_contig(n_sets * out_bytes + AL)
+            if self.rc != 0:
+                raise RuntimeError(f"hipExtMallocWithFlags(contiguous) -> {self.rc}")
+            ob = (raw + AL - 1) // AL * AL
+            out_ptrs = [ob + s * out_bytes for s in range(n_sets)]
+        elif alloc == "torch":
             rows = aligned_empty(n_sets * N * P_PAD, torch.float32, dev, AL)
             self.keep.append(rows)
             base = rows.data_ptr()
@@ -117,8 +135,13 @@ def main():
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
     stream = torch.cuda.current_stream(dev)
     variants = {}
-    for name, alloc, n_sets in (("torch_a", "torch", 3), ("contig_a", "contig", 3), ("torch_b", "torch", 3),
-                                ("contig_b", "contig", 3), ("torch12", "torch", 12), ("contig12", "contig", 12)):
+    only12 = os.environ.get("PROBE_NO12") is None
+    specs = [("torch_a", "torch", 3), ("contig_a", "contig", 3), ("rows_a", "contig_rows", 3),
+             ("outs_a", "contig_outs", 3), ("torch_b", "torch", 3), ("contig_b", "contig", 3),
+             ("rows_b", "contig_rows", 3), ("outs_b", "contig_outs", 3)]
+    if only12:
+        specs += [("torch12", "torch", 12), ("contig12", "contig", 12)]
+    for name, alloc, n_sets in specs:
         try:
             variants[name] = Sets(alloc, n_sets, 1234)
         except RuntimeError as e:

@@ -1,0 +1,177 @@
+"""Long-lived device buffers from the library (dlsim_device_alloc /
+dlsim_device_free, DLSIM_ALLOC_CONTIGUOUS): the torch view, alignment,
+freeing, and the staging rows of a large host aggregate (arena.resident_empty)."""
+from __future__ import annotations
+
+import gc
+
+import numpy as np
+import pytest
+import torch
+from torch import nn
+
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+from dasklearn_amd import _native, arena  # noqa: E402
+from dasklearn_amd.gradient_aggregation.fedavg import FedAvg  # noqa: E402
+
+
+def test_device_block_is_wrapped_not_copied():
+    blk = _native.DeviceBlock(3 << 20, "cuda")
+    t = blk.tensor()
+    assert t.is_cuda and t.dtype == torch.uint8 and t.numel() == 3 << 20
+    assert t.data_ptr() == blk.ptr
+    t.fill_(7)
+    assert int(t.sum().item()) == 7 * (3 << 20)
+    del blk  # the tensor keeps the block alive
+    gc.collect()
+    t[5] = 1
+    assert int(t[:8].sum().item()) == 7 * 7 + 1
+    del t
+    gc.collect()
+    torch.cuda.synchronize()
+
+
+def test_device_alloc_rejects_bad_arguments():
+    lib = _native.load()
+    import ctypes
+    p, c = ctypes.c_void_p(), ctypes.c_int(0)
+    assert lib.dlsim_device_alloc(0, 1, ctypes.byref(p), ctypes.byref(c)) == -1
+    assert lib.dlsim_device_alloc(256, 8, ctypes.byref(p), ctypes.byref(c)) == -1
+    assert lib.dlsim_device_alloc(256, 1, None, ctypes.byref(c)) == -1
+    assert lib.dlsim_device_free(None) == 0
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float64])
+def test_resident_empty_large_is_a_library_block(dt):
+    before = dict(arena.RESIDENT_BLOCKS)
+    esz = torch.tensor([], dtype=dt).element_size()
+    numel = (80 << 20) // esz + 3
+    x = arena.resident_empty(numel, dt, "cuda", 2 << 20)
+    assert sum(arena.RESIDENT_BLOCKS.values()) == sum(before.values()) + 1
+    assert x.dtype == dt and x.numel() == numel and x.data_ptr() % (2 << 20) == 0
+    x.fill_(1.5)
+    assert float(x[-1].item()) == 1.5
+    small = arena.resident_empty(1000, dt, "cuda", 256)
+    assert sum(arena.RESIDENT_BLOCKS.values()) == sum(before.values()) + 1  # torch's allocator
+    del x, small
+    gc.collect()
+    torch.cuda.synchronize()
+
+
+def test_reduce_reads_resident_rows_bit_exact():
+    n, p = 8, 3_000_001
+    rows = arena.resident_empty(n * arena.row_stride(p, 4), torch.float32, "cuda", 2 << 20)
+    stride = arena.row_stride(p, 4)
+    x = np.random.default_rng(5).standard_normal((n, p)).astype(np.float32) * np.float32(0.05)
+    views = []
+    for i in range(n):
+        v = rows[i * stride:i * stride + p]
+        v.copy_(torch.from_numpy(x[i]))
+        views.append(v)
+    w = orc.reference_weights(n, [float(a) for a in np.random.default_rng(6).dirichlet(np.ones(n))])
+    out = arena.arena_empty(p, torch.float32, "cuda")
+    _native.wreduce(views, w, out)
+    assert orc.same_bits(out.cpu().numpy(), orc.wreduce_rows_f32(x, w))
+
+
+class Big(nn.Module):
+    def __init__(self, k):
+        super().__init__()
+        self.a = nn.Parameter(torch.randn(k) * 0.05)
+        self.b = nn.Parameter(torch.randn(1000) * 0.05)
+
+
+def test_large_host_aggregate_stages_through_a_resident_block():
+    torch.manual_seed(11)
+    models = [Big(9_000_000) for _ in range(3)]  # 3 rows of 36 MB: staging >= 64 MiB
+    arena.STAGING.clear()
+    before = sum(arena.RESIDENT_BLOCKS.values())
+    out = FedAvg.aggregate(models, [0.2, 0.3, 0.5])
+    assert sum(arena.RESIDENT_BLOCKS.values()) >= before + 1
+    assert not out.a.is_cuda
+    xs = [np.concatenate([m.a.detach().numpy(), m.b.detach().numpy()]) for m in models]
+    ref = orc.wreduce(xs, orc.reference_weights(3, [0.2, 0.3, 0.5]))
+    got = np.concatenate([out.a.detach().numpy(), out.b.detach().numpy()])
+    assert orc.same_bits(got, ref)
+    arena.STAGING.clear()
+    gc.collect()
+    torch.cuda.synchronize()
+
+
+BIG = (20 << 20) // 4  # fp32 elements of a 20 MiB arena: the pool's size class
+
+
+def test_output_pool_reuses_a_block_only_when_unused():
+    pool = arena.OUTPUT_POOL
+    a = arena.arena_empty(BIG, torch.float32, "cuda")
+    pa = a.data_ptr()
+    assert pa % (2 << 20) == 0
+    b = arena.arena_empty(BIG, torch.float32, "cuda")
+    assert b.data_ptr() != pa  # a is alive
+    view = a[100:200]
+    del a
+    c = arena.arena_empty(BIG, torch.float32, "cuda")
+    assert c.data_ptr() != pa  # a view of a is still alive
+    del view
+    d = arena.arena_empty(BIG, torch.float32, "cuda")
+    assert d.data_ptr() == pa  # no tensor uses a's block any more
+    e = arena.arena_empty(BIG - 1000, torch.float32, "cuda")  # same 2 MiB size class
+    assert e.data_ptr() not in (pa, b.data_ptr(), c.data_ptr())
+    del b, c, d, e
+    assert pool.release() >= 3
+    torch.cuda.synchronize()
+
+
+def test_output_pool_is_per_stream():
+    a = arena.arena_empty(BIG, torch.float32, "cuda")
+    pa = a.data_ptr()
+    del a
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        b = arena.arena_empty(BIG, torch.float32, "cuda")
+    assert b.data_ptr() != pa  # a block made for the default stream is not reused on another
+    c = arena.arena_empty(BIG, torch.float32, "cuda")
+    assert c.data_ptr() == pa
+    del b, c
+    torch.cuda.synchronize()
+    arena.OUTPUT_POOL.release()
+
+
+def test_output_pool_off_switch(monkeypatch):
+    monkeypatch.setenv("DLSIM_CONTIGUOUS", "0")
+    made = arena.OUTPUT_POOL.made
+    a = arena.arena_empty(BIG, torch.float32, "cuda")
+    assert arena.OUTPUT_POOL.made == made and a.data_ptr() % (2 << 20) == 0
+
+
+class Wide(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.w = nn.Parameter(torch.randn(2048, 3000) * 0.05)
+        self.b = nn.Parameter(torch.randn(3000) * 0.05)
+
+
+def test_aggregate_outputs_from_the_pool_bit_exact_and_recycled():
+    """Module outputs (parameters are views of a pooled arena): the block is
+    busy while the module lives and returns when it is gone; results stay
+    bit-exact while blocks are recycled under queued kernels."""
+    torch.manual_seed(2)
+    models = [arena.to_device_arena(Wide().cuda()) for _ in range(4)]
+    host = [np.concatenate([m.w.detach().cpu().numpy().ravel(), m.b.detach().cpu().numpy()]) for m in models]
+    for trial in range(6):
+        w = [float(v) for v in np.random.default_rng(trial).dirichlet(np.ones(4))]
+        out = FedAvg.aggregate(models, w)
+        ptr = out.w.data_ptr()
+        again = FedAvg.aggregate(models, w)
+        assert again.w.data_ptr() != ptr  # out still holds its block
+        ref = orc.wreduce(host, orc.reference_weights(4, w))
+        got = np.concatenate([out.w.detach().cpu().numpy().ravel(), out.b.detach().cpu().numpy()])
+        assert orc.same_bits(got, ref)
+        got2 = np.concatenate([again.w.detach().cpu().numpy().ravel(), again.b.detach().cpu().numpy()])
+        assert orc.same_bits(got2, ref)
+        del out, again
+    torch.cuda.synchronize()
+    arena.OUTPUT_POOL.release()
