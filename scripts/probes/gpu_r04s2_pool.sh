@@ -8,7 +8,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/${1:-r04s2_pool}
 mkdir -p $O
 echo "[$(date +%T)] pytest"
-timeout -k 10 900 python3 -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 180 --timeout-method thread > $O/pytest_gpu.log 2>&1
+timeout -k 10 900 python3 -u -m pytest ${PYTEST_TARGET:-tests} -m gpu -q -p no:cacheprovider --timeout 180 --timeout-method thread > $O/pytest_gpu.log 2>&1
 rc=$?; tail -25 $O/pytest_gpu.log | grep -vE "^\s*$" | tail -4
 if [ $rc -ne 0 ]; then exit $rc; fi
 for i in 1 2 3 4; do

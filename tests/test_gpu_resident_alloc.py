@@ -106,6 +106,8 @@ BIG = (20 << 20) // 4  # fp32 elements of a 20 MiB arena: the pool's size class
 
 def test_output_pool_reuses_a_block_only_when_unused():
     pool = arena.OUTPUT_POOL
+    gc.collect()
+    pool.release()  # only this test's blocks from here on
     a = arena.arena_empty(BIG, torch.float32, "cuda")
     pa = a.data_ptr()
     assert pa % (2 << 20) == 0
@@ -126,6 +128,8 @@ def test_output_pool_reuses_a_block_only_when_unused():
 
 
 def test_output_pool_is_per_stream():
+    gc.collect()
+    arena.OUTPUT_POOL.release()
     a = arena.arena_empty(BIG, torch.float32, "cuda")
     pa = a.data_ptr()
     del a
