@@ -300,14 +300,17 @@ class _OutputPool:
 
     def __init__(self):
         self.pid = os.getpid()
-        self.blocks: Dict[Tuple[int, int, int], List[torch.Tensor]] = {}
+        self.blocks: Dict[Tuple[int, int, int], List[Tuple[torch.Tensor, int]]] = {}  # (base, idle use count)
         self.lock = threading.Lock()
         self.made = 0
 
     @staticmethod
-    def _in_use(base: torch.Tensor) -> bool:
-        # the pool's base tensor and the temporary storage object hold 2
-        return torch._C._storage_Use_Count(base.untyped_storage()._cdata) > 2
+    def _uses(base: torch.Tensor) -> int:
+        return torch._C._storage_Use_Count(base.untyped_storage()._cdata)
+
+    def _in_use(self, entry) -> bool:
+        base, idle = entry  # idle: the storage's use count with no view handed out
+        return self._uses(base) > idle
 
     def take(self, numel: int, dtype: torch.dtype, device) -> Optional[torch.Tensor]:
         if os.environ.get("DLSIM_CONTIGUOUS", "1") == "0":
@@ -321,16 +324,18 @@ class _OutputPool:
         key = (idx, torch._C._cuda_getCurrentRawStream(idx), size)
         with self.lock:
             lst = self.blocks.setdefault(key, [])
-            for base in lst:
-                if not self._in_use(base):
-                    return base[:nbytes].view(dtype)  # the view marks it in use before the lock drops
+            for entry in lst:
+                if not self._in_use(entry):
+                    return entry[0][:nbytes].view(dtype)  # the view marks it in use before the lock drops
             blk = _native.DeviceBlock(size + ROW_ALIGN, torch.device("cuda", idx))
             RESIDENT_BLOCKS["contiguous" if blk.contiguous else "fallback"] += 1
             raw = blk.tensor()
             skip = (-raw.data_ptr()) % ROW_ALIGN
-            base = raw[skip:skip + size]
+            # a tensor set on the storage, not a view of `raw` (a view would
+            # keep `raw` alive as its base and hold one more reference)
+            base = torch.empty(0, dtype=torch.uint8, device=raw.device).set_(raw.untyped_storage(), skip, (size,))
             del raw
-            lst.append(base)
+            lst.append((base, self._uses(base)))
             self.made += 1
             return base[:nbytes].view(dtype)
 
