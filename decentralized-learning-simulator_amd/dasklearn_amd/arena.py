@@ -264,8 +264,9 @@ def aligned_empty(numel: int, dtype: torch.dtype, device, align: int) -> torch.T
 
 def arena_empty(numel: int, dtype: torch.dtype, device) -> torch.Tensor:
     """A fresh aggregate output (one dtype arena of a model), aligned like a
-    row of its size (base_align). From 16 MiB on it comes from OUTPUT_POOL
-    (physically contiguous blocks); below, torch's allocator."""
+    row of its size (base_align). From OUT_POOL_MIN (4 MiB) on it comes from
+    OUTPUT_POOL (physically contiguous blocks); below, torch's
+    allocator."""
     esz = _elem_size(dtype)
     al = base_align(numel * esz, esz)
     if numel * esz >= OUT_POOL_MIN and torch.device(device).type == "cuda":
@@ -275,7 +276,10 @@ def arena_empty(numel: int, dtype: torch.dtype, device) -> torch.Tensor:
     return aligned_empty(numel, dtype, device, al)
 
 
-OUT_POOL_MIN = ROW_ALIGN_MIN  # bytes
+# 4 MiB: the 8-rank slice of the north star (5.6 MB outputs) ran 9.55-9.60 us
+# with pooled outputs against 9.71-9.97 us in torch's allocator; cfg2's 4 MB
+# outputs measured neutral (profiles/r04s2_small/)
+OUT_POOL_MIN = int(float(os.environ.get("DLSIM_OUT_POOL_MIN_MB", "4")) * (1 << 20))  # bytes
 
 
 class _OutputPool:
