@@ -534,6 +534,49 @@ static void case_errors(hipStream_t st) {
   printf("%-46s DLSIM_E_ARG / _DTYPE / _MODE with messages\n", "error codes");
 }
 
+/* dlsim_device_alloc: a contiguous block holds the rows and the output of
+ * a reduce (the arena placement of DESIGN.md §5c), then dlsim_device_free. */
+static void case_device_block(hipStream_t st) {
+  const int n = 4;
+  const size_t p = 3000017, stride = (p + 63) / 64 * 64;
+  float* h[4];
+  const void* d[4];
+  float w[4];
+  weights(w, n);
+  void* blk = NULL;
+  int contiguous = -1;
+  DLCK(dlsim_device_alloc((n + 1) * stride * sizeof(float), DLSIM_ALLOC_CONTIGUOUS, &blk, &contiguous));
+  if (!blk || (contiguous != 0 && contiguous != 1)) {
+    fprintf(stderr, "dlsim_device_alloc: block %p contiguous %d\n", blk, contiguous);
+    exit(1);
+  }
+  for (int i = 0; i < n; ++i) {
+    h[i] = (float*)malloc(p * sizeof(float));
+    fill_f32(h[i], p);
+    d[i] = (const float*)blk + i * stride;
+    HIPCK(hipMemcpy((void*)d[i], h[i], p * sizeof(float), hipMemcpyHostToDevice));
+  }
+  float* exp = (float*)malloc(p * sizeof(float));
+  float* got = (float*)malloc(p * sizeof(float));
+  oracle_wreduce_f32((const float* const*)h, n, w, exp, p);
+  void* dout = (float*)blk + n * stride;
+  DLCK(dlsim_wreduce(d, n, w, dout, p, DLSIM_F32, DLSIM_EXACT, st));
+  HIPCK(hipStreamSynchronize(st));
+  HIPCK(hipMemcpy(got, dout, p * sizeof(float), hipMemcpyDeviceToHost));
+  expect_same(contiguous ? "dlsim_device_alloc (contiguous) rows + output" : "dlsim_device_alloc (hipMalloc) rows + output",
+              got, exp, p * sizeof(float));
+  DLCK(dlsim_device_free(blk));
+  DLCK(dlsim_device_free(NULL));
+  void* none = NULL;
+  if (dlsim_device_alloc(0, DLSIM_ALLOC_CONTIGUOUS, &none, NULL) != DLSIM_E_ARG || none) {
+    fprintf(stderr, "dlsim_device_alloc(0): expected DLSIM_E_ARG\n");
+    exit(1);
+  }
+  for (int i = 0; i < n; ++i) free(h[i]);
+  free(exp);
+  free(got);
+}
+
 int main(void) {
   if ((dlsim_version() >> 16) != 1) {
     fprintf(stderr, "unexpected ABI major version %d\n", dlsim_version() >> 16);
@@ -560,6 +603,7 @@ int main(void) {
   case_host_wreduce_resident(st);
   case_table_batch(st);
   case_host_chunk_mean(st);
+  case_device_block(st);
   case_errors(st);
   HIPCK(hipStreamDestroy(st));
   printf("c_host_check OK\n");

@@ -18,4 +18,5 @@ def test_c_host_check():
     r = subprocess.run([BIN], capture_output=True, text=True, timeout=100)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.strip().endswith("c_host_check OK"), r.stdout
-    assert r.stdout.count("bit-identical") == 26, r.stdout
+    assert r.stdout.count("bit-identical") == 27, r.stdout
+    assert "dlsim_device_alloc" in r.stdout, r.stdout
