@@ -331,7 +331,14 @@ class _OutputPool:
             for entry in lst:
                 if not self._in_use(entry):
                     return entry[0][:nbytes].view(dtype)  # the view marks it in use before the lock drops
-            blk = _native.DeviceBlock(size + ROW_ALIGN, torch.device("cuda", idx))
+            try:
+                blk = _native.DeviceBlock(size + ROW_ALIGN, torch.device("cuda", idx))
+            except _native.DlsimError:
+                # out of memory: give back what no tensor uses (ours and
+                # torch's cache), then try once more
+                self._release_locked()
+                torch.cuda.empty_cache()
+                blk = _native.DeviceBlock(size + ROW_ALIGN, torch.device("cuda", idx))
             RESIDENT_BLOCKS["contiguous" if blk.contiguous else "fallback"] += 1
             raw = blk.tensor()
             skip = (-raw.data_ptr()) % ROW_ALIGN
@@ -350,12 +357,15 @@ class _OutputPool:
     def release(self) -> int:
         """Free (hipFree, synchronising) every block no tensor uses; returns
         the number freed."""
-        freed = 0
         with self.lock:
-            for key in list(self.blocks):
-                keep = [b for b in self.blocks[key] if self._in_use(b)]
-                freed += len(self.blocks[key]) - len(keep)
-                self.blocks[key] = keep
+            return self._release_locked()
+
+    def _release_locked(self) -> int:
+        freed = 0
+        for key in list(self.blocks):
+            keep = [b for b in self.blocks[key] if self._in_use(b)]
+            freed += len(self.blocks[key]) - len(keep)
+            self.blocks[key] = keep
         return freed
 
 
