@@ -498,6 +498,15 @@ void add_r03(std::vector<Variant>& vs, int n) {
     vs.push_back({p + "_V4_sc1_wave_b", launch_ts<Op, NF, 8, 4, 1, 16, true>, 0});
     return;
   }
+  if (getenv("DLSIM_TUNE_STORES")) {  // store policies and shapes on contiguous blocks (round 4)
+    vs.push_back({p + "_V4_nt_wave", launch_ts<Op, NF, 8, 4, 1, kStNT, true>, 0});
+    vs.push_back({p + "_V4_plain_wave", launch_ts<Op, NF, 8, 4, 1, kStPlain, true>, 0});
+    vs.push_back({p + "_V4_sc1_blk", launch_ts<Op, NF, 8, 4, 1, 16, false>, 0});
+    vs.push_back({p + "_V2_sc1_wave", launch_ts<Op, NF, 8, 2, 1, 16, true>, 0});
+    vs.push_back({p + "_V8_sc1_wave", launch_ts<Op, NF, 8, 8, 1, 16, true>, 0});
+    vs.push_back({p + "_xorprobe", launch_probe<Op, NF>, 0});
+    return;
+  }
   if (getenv("DLSIM_TUNE_TLB")) {  // tile orders against translation reach
     vs.push_back({p + "_xorprobe", launch_probe<Op, NF>, 0});
     vs.push_back({p + "_xcd_split", launch_x<Op, NF, 4>, 0});
@@ -659,7 +668,10 @@ int run(int n, size_t P, int reps, double peak_gbs) {
   if (stg || alg) {
     const size_t stagger = stg ? strtoull(stg, nullptr, 10) & ~(size_t)255 : 0;
     const size_t stride = ((bytes + align - 1) / align) * align + stagger;
-    CK(hipMalloc(&arena, stride * in.size() + align));
+    if (getenv("DLSIM_TUNE_CONTIG"))  // physically contiguous
+      CK(hipExtMallocWithFlags(&arena, stride * in.size() + align, hipDeviceMallocContiguous));
+    else
+      CK(hipMalloc(&arena, stride * in.size() + align));
     char* base = (char*)((((uintptr_t)arena) + align - 1) / align * align);
     for (size_t k = 0; k < in.size(); ++k) in[k] = base + k * stride;
     printf("layout=arena stride=%zu stagger=%zu align=%zu\n", stride, stagger, align);
@@ -672,7 +684,10 @@ int run(int n, size_t P, int reps, double peak_gbs) {
   const size_t out_off = getenv("DLSIM_TUNE_OUT_OFFSET") ? strtoull(getenv("DLSIM_TUNE_OUT_OFFSET"), nullptr, 10) & ~(size_t)15 : 0;
   std::vector<void*> out_alloc(sets);
   for (int k = 0; k < sets; ++k) {
-    CK(hipMalloc(&out_alloc[k], bytes + 256 + out_off));
+    if (getenv("DLSIM_TUNE_CONTIG"))
+      CK(hipExtMallocWithFlags(&out_alloc[k], bytes + 256 + out_off, hipDeviceMallocContiguous));
+    else
+      CK(hipMalloc(&out_alloc[k], bytes + 256 + out_off));
     out[k] = (char*)out_alloc[k] + out_off;
   }
   printf("addr_mod_2MiB in0=%zu in1=%zu out0=%zu\n", (size_t)((uintptr_t)in[0] % (2u << 20)),
