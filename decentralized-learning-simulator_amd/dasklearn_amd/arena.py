@@ -362,10 +362,10 @@ class _OutputPool:
 
     def _release_locked(self) -> int:
         freed = 0
-        for key in list(self.blocks):
-            keep = [b for b in self.blocks[key] if self._in_use(b)]
-            freed += len(self.blocks[key]) - len(keep)
-            self.blocks[key] = keep
+        for lst in self.blocks.values():
+            keep = [b for b in lst if self._in_use(b)]
+            freed += len(lst) - len(keep)
+            lst[:] = keep  # in place: take() may hold this list
         return freed
 
 
