@@ -112,5 +112,5 @@ def test_off_switch_and_fork(pool, monkeypatch):
 def test_arena_empty_routes_by_size_and_device():
     small = arena.arena_empty(1000, torch.float32, "cpu")
     big = arena.arena_empty(N, torch.float32, "cpu")  # host arenas never use the pool
-    assert small.numel() == 1000 and big.numel() == N and big.data_ptr() % 256 == 0
+    assert small.numel() == 1000 and big.numel() == N and not big.is_cuda
     assert arena.OUT_POOL_MIN == 4 << 20 or os.environ.get("DLSIM_OUT_POOL_MIN_MB")
