@@ -289,7 +289,7 @@ class _OutputPool:
     north star's rows fixed, outputs in torch's allocator ran at 61.2-62.5 us
     per launch depending on the pages the driver handed out, outputs in a
     contiguous block at 60.9-61.3 us in every process
-    (profiles/r04s2_contig2/, DESIGN.md §5b). A contiguous block cannot come
+    (profiles/r04s2_contig2/, DESIGN.md §5c). A contiguous block cannot come
     from torch's caching allocator, and hipMalloc/hipFree per call would cost
     more than the kernel (hipFree synchronises the device), so the pool caches
     blocks like torch's allocator does: grow-only lists keyed by (device,
