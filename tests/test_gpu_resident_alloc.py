@@ -179,3 +179,34 @@ def test_aggregate_outputs_from_the_pool_bit_exact_and_recycled():
         del out, again
     torch.cuda.synchronize()
     arena.OUTPUT_POOL.release()
+
+
+def test_output_pool_soak_recycles_under_queued_kernels():
+    """Random large aggregates whose outputs are kept or dropped at random,
+    so pooled blocks are recycled while earlier kernels are still queued on
+    the stream; every kept result is checked bit for bit at the end."""
+    rng = np.random.default_rng(2024)
+    sizes = [1_100_003, 1_500_000, 2_750_011]  # 4.4-11 MB fp32 outputs: pooled
+    inputs = {p: [torch.from_numpy(rng.standard_normal(p).astype(np.float32) * np.float32(0.05)).cuda()
+                  for _ in range(6)] for p in sizes}
+    kept = []
+    for it in range(40):
+        p = sizes[int(rng.integers(len(sizes)))]
+        n = int(rng.integers(2, 7))
+        idx = rng.choice(6, size=n, replace=False)
+        w = [float(v) for v in rng.dirichlet(np.ones(n))]
+        out = arena.arena_empty(p, torch.float32, "cuda")
+        _native.wreduce([inputs[p][i] for i in idx], orc.reference_weights(n, w), out)
+        if rng.random() < 0.4:
+            kept.append((p, idx, w, out))
+        # else: dropped at once; its block returns to the pool with the kernel still queued
+    torch.cuda.synchronize()
+    host = {p: [x.cpu().numpy() for x in xs] for p, xs in inputs.items()}
+    assert kept
+    ptrs = [o.data_ptr() for *_, o in kept]
+    assert len(set(ptrs)) == len(ptrs)  # no two live outputs share a block
+    for p, idx, w, out in kept:
+        ref = orc.wreduce([host[p][i] for i in idx], orc.reference_weights(len(idx), w))
+        assert orc.same_bits(out.cpu().numpy(), ref)
+    del kept
+    arena.OUTPUT_POOL.release()
