@@ -208,6 +208,14 @@ def _rows_alloc() -> str:
     return "torch caching allocator"
 
 
+def _outputs_alloc() -> str:
+    """Where the aggregate outputs came from (arena.arena_empty)."""
+    from dasklearn_amd.arena import OUTPUT_POOL
+    if OUTPUT_POOL.made:
+        return f"contiguous output pool (arena.OUTPUT_POOL, {OUTPUT_POOL.made} blocks)"
+    return "torch caching allocator"
+
+
 def n_sets(bytes_per_set: int) -> int:
     return max(3, min(256, math.ceil(MIN_SET_FOOTPRINT / max(1, bytes_per_set))))
 
@@ -621,7 +629,7 @@ def run_rank(args, rank: int, world: int, local: int):
                        "params_rank0": p, "tasks_per_step": B, "mode": args.mode,
                        "parallelism": f"param-shard x{world}",
                        "bytes_per_step_rank0": wl.bytes_per_step,
-                       "rows_alloc": _rows_alloc()},
+                       "rows_alloc": _rows_alloc(), "outputs_alloc": _outputs_alloc()},
             "timing": {"value_from": "HIP events around the K launches on each rank's launch stream; "
                                      "value = all ranks' bytes / max over ranks; barriers outside the window",
                        "kernel_avg_us_per_rank": rank_us,
