@@ -39,7 +39,7 @@ import torch
 from torch import nn
 
 from . import _native
-from .arena import _elem_size, _pyhost, _side_streams, _target_device
+from .arena import _elem_size, _pyhost, _side_streams, _target_device, arena_empty
 
 
 ORDER_PINNED_TORCH = "2.10"
@@ -144,7 +144,7 @@ class ChunkManager:
                     n_out += k if tight else rnd(k)
                 on_dev = all(c.is_cuda and c.device == dev for ci in idxs for c in chunks[ci])
                 if on_dev:
-                    d_out = torch.empty(max(n_out, 1), dtype=dt, device=dev)
+                    d_out = arena_empty(max(n_out, 1), dt, dev)  # contiguous from 4 MiB
                     tasks = []
                     for ci, k, o in zip(idxs, sizes, out_off):
                         out = d_out[o:o + k]
@@ -267,7 +267,7 @@ def _fast_means(chunks, device, sync: bool = True):
     code = _native.dtype_code(dt, single_task=True)
     threads = torch.get_num_threads()
     pending = None
-    d_out = torch.empty(n_out, dtype=dt, device=dev)
+    d_out = arena_empty(n_out, dt, dev)  # contiguous from 4 MiB
     d0 = d_out.data_ptr()
     d_ptrs = [d0 + o * esz for o in out_off]
     with torch.no_grad():
