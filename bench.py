@@ -210,9 +210,12 @@ def _rows_alloc() -> str:
 
 def _outputs_alloc() -> str:
     """Where the aggregate outputs came from (arena.arena_empty)."""
+    from dasklearn_amd import _native
     from dasklearn_amd.arena import OUTPUT_POOL
     if OUTPUT_POOL.made:
-        return f"contiguous output pool (arena.OUTPUT_POOL, {OUTPUT_POOL.made} blocks)"
+        st = _native.pool_stats()
+        return (f"torch.cuda.MemPool over dlsim_pool_alloc (arena.OUTPUT_POOL: {OUTPUT_POOL.made} outputs, "
+                f"{st['contiguous']} contiguous segments, {st['fallback']} hipMalloc fallbacks)")
     return "torch caching allocator"
 
 

@@ -771,6 +771,89 @@ int dlsim_device_free(void* d_ptr) {
   return e == hipSuccess ? DLSIM_OK : hip_fail(e, "hipFree");
 }
 
+}  // extern "C"
+
+// ---- torch pluggable allocator over contiguous blocks (dlsim_pool_*) -----------
+// Segments come from hipExtMallocWithFlags(hipDeviceMallocContiguous), else
+// hipMalloc. A segment whose base is not 2 MiB-aligned is re-made 2 MiB larger
+// and handed out from its first aligned byte; `realigned` maps that address
+// back to the driver's for the free. Called under torch's allocator lock.
+namespace dlsim_host __attribute__((visibility("hidden"))) {
+constexpr size_t kPoolAlign = size_t(2) << 20;
+std::mutex g_pool_mu;
+std::vector<std::pair<void*, void*>> g_realigned;  // (handed out, driver's base); rare
+unsigned long long g_pool_contig = 0, g_pool_fallback = 0, g_pool_live = 0;
+
+void* pool_raw(size_t nbytes, bool* contiguous) {
+  void* p = nullptr;
+  if (hipExtMallocWithFlags(&p, nbytes, hipDeviceMallocContiguous) == hipSuccess && p) {
+    *contiguous = true;
+    return p;
+  }
+  (void)hipGetLastError();
+  p = nullptr;
+  if (hipMalloc(&p, nbytes) != hipSuccess) {
+    (void)hipGetLastError();  // torch sees NULL and runs its own out-of-memory path
+    return nullptr;
+  }
+  *contiguous = false;
+  return p;
+}
+}  // namespace dlsim_host
+
+extern "C" {
+
+void* dlsim_pool_alloc(size_t nbytes, int device, void* /*stream*/) {
+  if (nbytes == 0) return nullptr;
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  if (prev != device) (void)hipSetDevice(device);
+  bool contig = false;
+  void* p = pool_raw(nbytes, &contig);
+  void* out = p;
+  if (p && reinterpret_cast<uintptr_t>(p) % kPoolAlign) {
+    (void)hipFree(p);
+    p = pool_raw(nbytes + kPoolAlign, &contig);
+    out = p ? reinterpret_cast<void*>((reinterpret_cast<uintptr_t>(p) + kPoolAlign - 1) & ~(kPoolAlign - 1))
+            : nullptr;
+  }
+  if (prev >= 0 && prev != device) (void)hipSetDevice(prev);
+  if (!out) return nullptr;
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  if (out != p) g_realigned.emplace_back(out, p);
+  (contig ? g_pool_contig : g_pool_fallback) += 1;
+  g_pool_live += nbytes;
+  return out;
+}
+
+void dlsim_pool_free(void* d_ptr, size_t nbytes, int device, void* /*stream*/) {
+  if (!d_ptr) return;
+  void* base = d_ptr;
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    for (size_t i = 0; i < g_realigned.size(); ++i) {
+      if (g_realigned[i].first == d_ptr) {
+        base = g_realigned[i].second;
+        g_realigned.erase(g_realigned.begin() + static_cast<long>(i));
+        break;
+      }
+    }
+    g_pool_live -= std::min<unsigned long long>(g_pool_live, nbytes);
+  }
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  if (prev != device) (void)hipSetDevice(device);
+  (void)hipFree(base);
+  if (prev >= 0 && prev != device) (void)hipSetDevice(prev);
+}
+
+void dlsim_pool_stats(unsigned long long* contiguous, unsigned long long* fallback, unsigned long long* live_bytes) {
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  if (contiguous) *contiguous = g_pool_contig;
+  if (fallback) *fallback = g_pool_fallback;
+  if (live_bytes) *live_bytes = g_pool_live;
+}
+
 const char* dlsim_last_error(void) { return g_err.c_str(); }
 
 int dlsim_version(void) { return (1 << 16) | 1; }

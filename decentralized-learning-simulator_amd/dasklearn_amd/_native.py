@@ -49,6 +49,9 @@ EXPORTS = (
     "dlsim_wreduce_sharded_f64",
     "dlsim_device_alloc",
     "dlsim_device_free",
+    "dlsim_pool_alloc",
+    "dlsim_pool_free",
+    "dlsim_pool_stats",
     "dlsim_sharded_plan_create",
     "dlsim_sharded_plan_run",
     "dlsim_sharded_plan_run_f64",
@@ -159,6 +162,9 @@ def load() -> ctypes.CDLL:
         lib.dlsim_device_alloc.restype = i
         lib.dlsim_device_free.argtypes = [vp]
         lib.dlsim_device_free.restype = i
+        u64p = ctypes.POINTER(ctypes.c_ulonglong)
+        lib.dlsim_pool_stats.argtypes = [u64p, u64p, u64p]
+        lib.dlsim_pool_stats.restype = None
         lib.dlsim_last_error.argtypes = []
         lib.dlsim_last_error.restype = ctypes.c_char_p
         lib.dlsim_version.argtypes = []
@@ -290,6 +296,15 @@ class ReducePlan:
 
 
 DLSIM_ALLOC_CONTIGUOUS = 1
+
+
+def pool_stats() -> dict:
+    """dlsim_pool_stats: segments torch's allocator made through
+    dlsim_pool_alloc (contiguous / hipMalloc fallback) and the bytes they hold."""
+    lib = load()
+    c, f, b = ctypes.c_ulonglong(0), ctypes.c_ulonglong(0), ctypes.c_ulonglong(0)
+    lib.dlsim_pool_stats(ctypes.byref(c), ctypes.byref(f), ctypes.byref(b))
+    return {"contiguous": c.value, "fallback": f.value, "live_bytes": b.value}
 
 
 class DeviceBlock:
@@ -719,6 +734,10 @@ class ShardedPlan:
         if self._h is None:
             raise ValueError("plan destroyed")
         try:
+            if len(slices) != self.n:
+                # the library reads the plan's n pointers and weights: fewer
+                # would be read past the arrays, more silently dropped
+                raise ValueError(f"the plan was made for {self.n} models, got {len(slices)} slices")
             ptrs = _check_slices(slices, out)
             if out.numel() != self.n_elems or out.dtype != self.dtype:
                 raise ValueError(f"out must be a full {self.n_elems}-element {self.dtype} buffer")

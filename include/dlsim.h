@@ -314,7 +314,9 @@ int dlsim_wreduce_sharded_f64(const void* const* d_slices, size_t slice_elems, i
  * (W x ceil64(max slice) elements, hipMalloc).
  *
  * dlsim_sharded_plan_run[_f64] reduces this rank's slices (dlsim_shard_range
- * of the plan's n_elems, n models; slice_elems must equal e_r - b_r) into
+ * of the plan's n_elems, n models; d_slices and h_weights must hold exactly
+ * the plan's n entries: the run has no fan-in argument and reads n of each;
+ * slice_elems must equal e_r - b_r) into
  * d_out + b_r (a full n_elems buffer) and runs the plan's gather:
  * stream-ordered, no host wait, no agreement. Every rank must run
  * the same sequence of plans, as with any collective. A rank whose local
@@ -471,6 +473,27 @@ int dlsim_probe_pattern(const void* const* d_inputs, int n, void* d_out, size_t 
 #define DLSIM_ALLOC_CONTIGUOUS 1
 int dlsim_device_alloc(size_t nbytes, int flags, void** d_out, int* contiguous);
 int dlsim_device_free(void* d_ptr);
+
+/*
+ * dlsim_pool_alloc / dlsim_pool_free — the same physically contiguous
+ * blocks, in the signature of a PyTorch pluggable allocator
+ * (torch.cuda.memory.CUDAPluggableAllocator: alloc(size, device, stream),
+ * free(ptr, size, device, stream)). dasklearn_amd hands them to a
+ * torch.cuda.MemPool and allocates large aggregate outputs inside it
+ * (arena.OUTPUT_POOL), so torch's caching allocator owns the blocks:
+ * Tensor.record_stream, torch.cuda.memory_allocated / memory_reserved,
+ * per-stream reuse and the pool's release all behave as for any torch
+ * tensor. Blocks are 2 MiB-aligned;
+ * a request the driver cannot serve contiguously falls back to hipMalloc;
+ * out of memory returns NULL (torch then frees its cache and retries, or
+ * raises its OutOfMemoryError). Called by torch's allocator with `device`
+ * current; `stream` is unused (the caching allocator orders reuse).
+ * dlsim_pool_stats: segments made contiguous, made by the fallback, and the
+ * bytes the pool's segments hold now (any argument may be NULL).
+ */
+void* dlsim_pool_alloc(size_t nbytes, int device, void* stream);
+void dlsim_pool_free(void* d_ptr, size_t nbytes, int device, void* stream);
+void dlsim_pool_stats(unsigned long long* contiguous, unsigned long long* fallback, unsigned long long* live_bytes);
 
 /* Message for the last failing call on this thread ("" if none). */
 const char* dlsim_last_error(void);

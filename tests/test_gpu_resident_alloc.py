@@ -101,13 +101,17 @@ def test_large_host_aggregate_stages_through_a_resident_block():
     torch.cuda.synchronize()
 
 
-BIG = (20 << 20) // 4  # fp32 elements of a 20 MiB arena: the pool's size class
+BIG = (20 << 20) // 4  # fp32 elements of a 20 MiB arena: pooled
+
+
+def _fresh_pool():
+    gc.collect()
+    torch.cuda.synchronize()
+    arena.OUTPUT_POOL.release()  # only this test's blocks from here on
 
 
 def test_output_pool_reuses_a_block_only_when_unused():
-    pool = arena.OUTPUT_POOL
-    gc.collect()
-    pool.release()  # only this test's blocks from here on
+    _fresh_pool()
     a = arena.arena_empty(BIG, torch.float32, "cuda")
     pa = a.data_ptr()
     assert pa % (2 << 20) == 0
@@ -121,22 +125,21 @@ def test_output_pool_reuses_a_block_only_when_unused():
     d = arena.arena_empty(BIG, torch.float32, "cuda")
     assert d.data_ptr() == pa  # no tensor uses a's block any more
     e = arena.arena_empty(BIG - 1000, torch.float32, "cuda")  # same 2 MiB size class
-    assert e.data_ptr() not in (pa, b.data_ptr(), c.data_ptr())
+    assert e.data_ptr() not in (pa, b.data_ptr(), c.data_ptr()) and e.data_ptr() % (2 << 20) == 0
     del b, c, d, e
-    assert pool.release() >= 3
+    assert arena.OUTPUT_POOL.release() == 1
     torch.cuda.synchronize()
 
 
 def test_output_pool_is_per_stream():
-    gc.collect()
-    arena.OUTPUT_POOL.release()
+    _fresh_pool()
     a = arena.arena_empty(BIG, torch.float32, "cuda")
     pa = a.data_ptr()
     del a
     s = torch.cuda.Stream()
     with torch.cuda.stream(s):
         b = arena.arena_empty(BIG, torch.float32, "cuda")
-    assert b.data_ptr() != pa  # a block made for the default stream is not reused on another
+    assert b.data_ptr() != pa  # a block freed on the default stream is not reused on another
     c = arena.arena_empty(BIG, torch.float32, "cuda")
     assert c.data_ptr() == pa
     del b, c
@@ -149,6 +152,70 @@ def test_output_pool_off_switch(monkeypatch):
     made = arena.OUTPUT_POOL.made
     a = arena.arena_empty(BIG, torch.float32, "cuda")
     assert arena.OUTPUT_POOL.made == made and a.data_ptr() % (2 << 20) == 0
+
+
+def test_output_pool_blocks_are_torch_allocations():
+    """The pool's blocks are torch's: memory_allocated / memory_reserved count
+    them, they come from the library's contiguous allocator, and release()
+    gives their segments back (VERDICT r04 next #1)."""
+    _fresh_pool()
+    a0 = torch.cuda.memory_allocated()
+    r0 = torch.cuda.memory_reserved()
+    segs0 = _native.pool_stats()
+    x = arena.arena_empty(BIG, torch.float32, "cuda")
+    assert torch.cuda.memory_allocated() == a0 + BIG * 4
+    assert torch.cuda.memory_reserved() >= r0 + BIG * 4
+    segs = _native.pool_stats()
+    assert segs["contiguous"] + segs["fallback"] == segs0["contiguous"] + segs0["fallback"] + 1
+    assert segs["live_bytes"] >= BIG * 4
+    assert arena.OUTPUT_POOL.cached_bytes() >= BIG * 4
+    x.fill_(1.0)
+    del x
+    assert torch.cuda.memory_allocated() == a0
+    torch.cuda.synchronize()
+    arena.OUTPUT_POOL.release()
+    assert torch.cuda.memory_reserved() <= r0
+    assert _native.pool_stats()["live_bytes"] == segs0["live_bytes"]
+
+
+def test_record_stream_keeps_a_side_stream_reader_safe():
+    """VERDICT r04 weak #2: an aggregate output read on a side stream (a long
+    kernel queued first), record_stream'ed and dropped, then new aggregates on
+    the main stream. The side stream's copy must be the first aggregate's
+    exact result: the block is not recycled under its reads."""
+    _fresh_pool()
+    torch.manual_seed(3)
+    models = [arena.to_device_arena(Wide().cuda()) for _ in range(4)]
+    host = [np.concatenate([m.w.detach().cpu().numpy().ravel(), m.b.detach().cpu().numpy()]) for m in models]
+    w1 = [float(v) for v in np.random.default_rng(31).dirichlet(np.ones(4))]
+    w2 = [float(v) for v in np.random.default_rng(32).dirichlet(np.ones(4))]
+    main = torch.cuda.current_stream()
+    side = torch.cuda.Stream()
+    out = FedAvg.aggregate(models, w1)
+    ptr = out.w.data_ptr()
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        torch.cuda._sleep(200_000_000)  # the side stream is busy for ~0.1 s
+        copy_w = out.w.detach().clone()
+        copy_b = out.b.detach().clone()
+    out.w.record_stream(side)  # the torch rule for a tensor used on another stream
+    del out
+    later = []
+    for k in range(3):
+        nxt = FedAvg.aggregate(models[::-1], w2 if k % 2 == 0 else w1)
+        assert nxt.w.data_ptr() != ptr  # the block waits for the side stream
+        later.append(nxt)
+    torch.cuda.synchronize()
+    ref1 = orc.wreduce(host, orc.reference_weights(4, w1))
+    got = np.concatenate([copy_w.cpu().numpy().ravel(), copy_b.cpu().numpy()])
+    assert orc.same_bits(got, ref1)
+    for k, nxt in enumerate(later):
+        ref = orc.wreduce(host[::-1], orc.reference_weights(4, w2 if k % 2 == 0 else w1))
+        got = np.concatenate([nxt.w.detach().cpu().numpy().ravel(), nxt.b.detach().cpu().numpy()])
+        assert orc.same_bits(got, ref)
+    del later, copy_w, copy_b
+    torch.cuda.synchronize()
+    arena.OUTPUT_POOL.release()
 
 
 class Wide(nn.Module):

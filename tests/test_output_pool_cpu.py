@@ -1,112 +1,130 @@
-"""Host logic of arena.OUTPUT_POOL (the contiguous-block cache for large
-aggregate outputs) on the CPU: the library's device blocks
-are replaced by host tensors, the stream handle by a counter. Reuse only
-when no tensor views a block, only on the stream it was made for, release(),
-the retry after an allocation failure, a forked child's fresh pool."""
+"""Host logic of arena.OUTPUT_POOL (large aggregate outputs allocated inside a
+torch.cuda.MemPool over the library's contiguous blocks) on
+the CPU: the MemPool and the allocation inside it are replaced by fakes.
+Size classes, the dtype view, the 2 MiB alignment (and the re-alignment of a
+block that an outside allocation split), one allocation context at a time
+across threads, release(), the off switch and a forked child's fresh pools.
+What torch's caching allocator does with the blocks (per-stream reuse,
+record_stream, statistics) is tested on the GPU (test_gpu_resident_alloc.py)."""
 from __future__ import annotations
 
 import os
+import threading
+import time
 
 import pytest
 import torch
 
-from dasklearn_amd import _native, arena
+from dasklearn_amd import arena
+
+MIB2 = arena.ROW_ALIGN
 
 
-class FakeBlock:
-    made = 0
-    fail_next = 0
+class FakeDevice:
+    """Host memory standing in for the pool: a 2 MiB-aligned bump allocator
+    that can be told to hand out a misaligned block next."""
 
-    def __init__(self, nbytes, device, contiguous=True):
-        if FakeBlock.fail_next:
-            FakeBlock.fail_next -= 1
-            raise _native.DlsimError("dlsim_device_alloc", -102, "out of memory")
-        FakeBlock.made += 1
-        self.nbytes, self.contiguous = nbytes, True
-        self._t = torch.empty(nbytes, dtype=torch.uint8)
+    def __init__(self):
+        self.raw = torch.empty(512 << 20, dtype=torch.uint8)
+        self.base = (-self.raw.data_ptr()) % MIB2
+        self.off = 0
+        self.misalign_next = 0
+        self.calls = []  # (idx, nbytes)
+        self.active = 0  # allocation contexts open at once
+        self.max_active = 0
 
-    def tensor(self):
-        # like the real block: the storage keeps the memory, the block object
-        # holds no tensor of its own
-        t, self._t = self._t, None
-        return t
+    def empty_in(self, mp, idx, nbytes):
+        self.active += 1
+        self.max_active = max(self.max_active, self.active)
+        try:
+            time.sleep(0.001)  # widen the window a concurrent caller would hit
+            self.calls.append((idx, nbytes))
+            skew = 0
+            if self.misalign_next:
+                self.misalign_next -= 1
+                skew = 4096
+            start = self.base + self.off + skew
+            self.off += (nbytes + skew + MIB2 - 1) // MIB2 * MIB2
+            return self.raw[start:start + nbytes]
+        finally:
+            self.active -= 1
 
 
 @pytest.fixture()
 def pool(monkeypatch):
-    stream = {"h": 0}
-    monkeypatch.setattr(_native, "DeviceBlock", FakeBlock)
-    monkeypatch.setattr(torch._C, "_cuda_getCurrentRawStream", lambda idx: stream["h"], raising=False)
-    monkeypatch.setattr(torch.cuda, "empty_cache", lambda: None)
-    monkeypatch.delenv("DLSIM_CONTIGUOUS", raising=False)
-    FakeBlock.made = FakeBlock.fail_next = 0
+    fake = FakeDevice()
     p = arena._OutputPool()
-    p.stream = stream
+    monkeypatch.setattr(p, "_mempool", lambda idx: p.pools.setdefault(idx, object()))
+    monkeypatch.setattr(p, "_empty_in", fake.empty_in)
+    emptied = []
+    monkeypatch.setattr(torch.cuda, "is_initialized", lambda: True)
+    monkeypatch.setattr(torch.cuda, "empty_cache", lambda: emptied.append(1))
+    monkeypatch.delenv("DLSIM_CONTIGUOUS", raising=False)
+    p.fake, p.emptied = fake, emptied
     return p
 
 
 N = (6 << 20) // 4  # a 6 MiB fp32 output
 
 
-def test_reuse_only_when_no_view_remains(pool):
+def test_sizes_round_to_2mib_and_view_the_dtype(pool):
     a = pool.take(N, torch.float32, "cuda:0")
-    assert a.dtype == torch.float32 and a.numel() == N
-    pa = a.data_ptr()
-    b = pool.take(N, torch.float32, "cuda:0")
-    assert b.data_ptr() != pa and FakeBlock.made == 2
-    view = a[10:20]
-    del a
-    c = pool.take(N, torch.float32, "cuda:0")
-    assert c.data_ptr() != pa and FakeBlock.made == 3
-    del view
-    d = pool.take(N - 1000, torch.float32, "cuda:0")  # same 2 MiB size class
-    assert d.data_ptr() == pa and FakeBlock.made == 3
-    p = torch.nn.Parameter(d[:100])  # a parameter view keeps the block busy
-    del d
-    e = pool.take(N, torch.float32, "cuda:0")
-    assert e.data_ptr() != pa
-    del p, b, c, e
-    assert pool.release() == 4 and pool.cached_bytes() == 0
+    assert a.dtype == torch.float32 and a.numel() == N and a.data_ptr() % MIB2 == 0
+    b = pool.take(N - 1000, torch.bfloat16, "cuda:1")
+    assert b.dtype == torch.bfloat16 and b.numel() == N - 1000 and b.data_ptr() % MIB2 == 0
+    assert pool.fake.calls == [(0, 6 << 20), (1, 4 << 20)]  # (N - 1000) * 2 B rounds up to 4 MiB
+    assert set(pool.pools) == {0, 1} and pool.made == 2
 
 
-def test_blocks_are_per_stream_and_per_size(pool):
+def test_a_misaligned_block_is_realigned(pool):
+    pool.fake.misalign_next = 1
     a = pool.take(N, torch.float32, "cuda:0")
-    pa = a.data_ptr()
-    del a
-    pool.stream["h"] = 7
-    b = pool.take(N, torch.float32, "cuda:0")
-    assert b.data_ptr() != pa  # made for stream 0, not reused on stream 7
-    pool.stream["h"] = 0
-    c = pool.take(3 * N, torch.float32, "cuda:0")
-    assert c.data_ptr() != pa  # another size class
-    d = pool.take(N, torch.bfloat16, "cuda:0")  # 3 MiB of bf16: a 4 MiB class
-    assert d.data_ptr() != pa
-    e = pool.take(2 * N, torch.bfloat16, "cuda:0")  # 6 MiB: the first block's class
-    assert e.data_ptr() == pa and e.dtype == torch.bfloat16
+    assert a.data_ptr() % MIB2 == 0 and a.numel() == N
+    assert pool.fake.calls == [(0, 6 << 20), (0, (6 << 20) + MIB2)]
 
 
-def test_allocation_failure_releases_and_retries(pool):
-    a = pool.take(N, torch.float32, "cuda:0")
-    del a  # one idle block to give back
-    FakeBlock.fail_next = 1
-    b = pool.take(5 * N, torch.float32, "cuda:0")
-    assert b.numel() == 5 * N
-    assert pool.cached_bytes() == (5 * N * 4 + arena.ROW_ALIGN - 1) // arena.ROW_ALIGN * arena.ROW_ALIGN
-    FakeBlock.fail_next = 2
-    with pytest.raises(_native.DlsimError):
-        pool.take(9 * N, torch.float32, "cuda:0")
+def test_one_allocation_context_at_a_time(pool):
+    outs, errs = [], []
+
+    def worker():
+        try:
+            for _ in range(5):
+                outs.append(pool.take(N, torch.float32, "cuda:0"))
+        except Exception as e:  # pragma: no cover - reported below
+            errs.append(e)
+    ts = [threading.Thread(target=worker) for _ in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs and len(outs) == 20
+    assert pool.fake.max_active == 1
+    assert len({o.data_ptr() for o in outs}) == 20
+
+
+def test_release_retires_the_pools_and_empties_the_cache(pool):
+    pool.take(N, torch.float32, "cuda:0")
+    pool.take(N, torch.float32, "cuda:1")
+    first = pool.pools[0]
+    assert pool.release() == 2 and pool.pools == {} and pool.emptied == [1]
+    assert pool.release() == 0 and pool.emptied == [1]  # nothing to retire: no device-wide sync
+    pool.take(N, torch.float32, "cuda:0")
+    assert pool.pools[0] is not first  # a fresh pool
 
 
 def test_off_switch_and_fork(pool, monkeypatch):
     monkeypatch.setenv("DLSIM_CONTIGUOUS", "0")
     assert pool.take(N, torch.float32, "cuda:0") is None
     monkeypatch.delenv("DLSIM_CONTIGUOUS")
-    a = pool.take(N, torch.float32, "cuda:0")
-    assert pool.cached_bytes() > 0
+    pool.take(N, torch.float32, "cuda:0")
+    parents = pool.pools
     pool.pid = os.getpid() + 1  # as seen from a forked child
-    b = pool.take(N, torch.float32, "cuda:0")
-    assert pool.pid == os.getpid() and len(sum(pool.blocks.values(), [])) == 1
-    assert b.data_ptr() != a.data_ptr()
+    # (the fakes are instance attributes: the child's __init__ keeps them)
+    pool.take(N, torch.float32, "cuda:0")
+    assert pool.pid == os.getpid()
+    assert pool.pools is not parents and pool.pools[0] is not parents[0]
+    assert any(p is parents for p in arena._OutputPool._inherited)  # never released in the child
+    arena._OutputPool._inherited.remove(parents)
 
 
 def test_arena_empty_routes_by_size_and_device():
