@@ -127,6 +127,9 @@ def parse(argv=None):
                     help="diagnostic: also time the K steps alternating over two streams (field two_streams); "
                          "off by default because those overlapping dispatches would enter a rocprof average "
                          "of the same command")
+    ap.add_argument("--xor-probe", action="store_true",
+                    help="diagnostic: also time dlsim_probe_pattern (the step's dispatch with an XOR fold; "
+                         "field xor_probe; not a bound)")
     ap.add_argument("--no-single-gpu-reference", action="store_true",
                     help="N > 1: skip rank 0's timing of the whole config alone (the speed-up base)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
@@ -296,11 +299,13 @@ class ReduceWorkload:
         self.probe_plans[k % self.sets].launch(self.stream)
 
 
-def pattern_ceiling(wl, k_steps: int, sync, new_event, achieved_gbps: float):
+def xor_probe(wl, k_steps: int, sync, new_event, achieved_gbps: float):
     """dlsim_probe_pattern over the same rotating sets: the reduce's own
     dispatch (kernel, launch shape, nt loads, store policy) with the weighted
-    fold replaced by a bitwise XOR — what the memory system allows for exactly
-    this read/write mix, measured in the same run."""
+    fold replaced by a bitwise XOR. Opt-in (--xor-probe), and NOT a bound:
+    rounds 1-3 read it as the memory system's ceiling for this read/write
+    mix, but at round 4's HEAD it ran 3-4 % slower than the reduce it was
+    meant to bound (VERDICT r04 weak #5), so the line no longer carries it."""
     for k in range(10):
         wl.launch_probe(k)
     ev_ms, _ = time_steps(wl.launch_probe, k_steps, sync, lambda: None, new_event)
@@ -308,7 +313,8 @@ def pattern_ceiling(wl, k_steps: int, sync, new_event, achieved_gbps: float):
     gbps = wl.bytes_per_step / (us * 1e-6) / 1e9
     return {"GBps": round(gbps, 1), "frac": round(gbps / HBM_PEAK_GBPS, 4), "us_per_launch": round(us, 3),
             "reduce_over_probe": round(achieved_gbps / gbps, 4),
-            "kernel": "dlsim_probe_pattern: same dispatch and shapes, XOR fold (memory only)"}
+            "kernel": "dlsim_probe_pattern: same dispatch and shapes, XOR fold",
+            "note": "diagnostic only, not a bound (the reduce has run faster than it)"}
 
 
 def launch_floor(wl, n, dtype, w32, mode, dev, k_steps: int, sync, new_event, step_us: float):
@@ -596,7 +602,7 @@ def run_rank(args, rank: int, world: int, local: int):
         achieved = wl.bytes_per_step / (ev_ms / K * 1e-3) / 1e9
         traffic, traffic_src = (pmc_traffic(args.config, args.mode, split) if B == 1
                                 else (None, "no committed PMC summary for batched launches"))
-        probe = pattern_ceiling(wl, K, sync, new_event, achieved) if B == 1 else None
+        probe = xor_probe(wl, K, sync, new_event, achieved) if B == 1 and args.xor_probe else None
         floor = launch_floor(wl, n, dtype, w32, mode, dev, K, sync, new_event, ev_ms / K * 1e3) \
             if B == 1 else None
         # opt-in: its concurrent launches share the reduce's kernel name, so
@@ -642,10 +648,11 @@ def run_rank(args, rank: int, world: int, local: int):
                          "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": wl.kernel, "kernel_avg_us": round(ev_ms / K * 1e3, 3),
                          "timing": "rank 0: HIP events around the K timed launches on the launch stream"},
-            "pattern_ceiling": probe,
             "launch_floor": floor,
             "two_streams": overlap,
         }
+        if probe:
+            result["xor_probe"] = probe
         if single:
             result["single_gpu_reference"] = single
         if gather:

@@ -9,7 +9,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <type_traits>
 #include <vector>
@@ -87,10 +89,35 @@ template <class Op, int C> constexpr Shape fixed_shape() {
     else return Shape{4, dlsim::kStNT, false};
   }
 }
-template <class Op> int size_class(size_t nelem) {
+//
+// Round 5 (profiles/r05c/, fp32 rows of 0.5-2 M elements, n = 2, 4, 8): below
+// 8 MB a one-tile-per-block grid has every block resident at once, and the
+// launch runs at the pace of the CUs that hold the most whole tiles — about
+// 37 GB/s per CU, so a CU with ceil(x) tiles where the average is x sets the
+// time once ceil(x)/x exceeds ~1.25. For fan-in >= 6 the VPT 4 grid is the
+// faster one whenever its tiles spread evenly (x4 = tiles per CU,
+// ceil(x4)/x4 <= 1.25): n = 8 at 1.05 M (cfg2) 7.56 against 7.87 us, 1.70 M
+// 11.09 against 11.78, 1.84 M 11.58 against 12.03; where they do not (the
+// 8-rank slice of the north star, 1.4 M: x4 = 1.33) VPT 2 stays (9.60 against
+// 10.45 us). Fan-in 2-4 showed no such rule and keep VPT 2.
+inline bool v4_tiles_even(size_t nvec) {
+  const double x = static_cast<double>(nvec / (static_cast<size_t>(dlsim::kBlock) * 4)) / 256.0;
+  return x >= 0.75 && std::ceil(x) / x <= 1.25;
+}
+// DLSIM_SMALL_SHAPE_R04 (read once; A/B runs): round 4's rule, VPT 2 below 8 MB.
+inline bool small_shape_r04() {
+  static const bool on = std::getenv("DLSIM_SMALL_SHAPE_R04") != nullptr;
+  return on;
+}
+template <class Op> int size_class(size_t nelem, int fixed_fan_in = 0) {
   const size_t bytes = nelem * Op::kBytes;  // per stream
-  if constexpr (Op::kBytes >= 4) return bytes < 8000000 ? 0 : bytes < 20000000 ? 1 : 2;
-  else return bytes < 96000000 ? 0 : 2;
+  if constexpr (Op::kBytes >= 4) {
+    if (bytes < 8000000)
+      return Op::kBytes == 4 && fixed_fan_in >= 6 && !small_shape_r04() && v4_tiles_even(nelem / Op::E) ? 1 : 0;
+    return bytes < 20000000 ? 1 : 2;
+  } else {
+    return bytes < 96000000 ? 0 : 2;
+  }
 }
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
@@ -132,7 +159,7 @@ hipError_t launch_class(const S& s, int n, void* out, size_t nelem, hipStream_t 
 template <class Op, class S, int NF>
 hipError_t launch_tiles(const S& s, int n, void* out, size_t nelem, hipStream_t st) {
   if constexpr (NF > 0) {
-    switch (size_class<Op>(nelem)) {
+    switch (size_class<Op>(nelem, NF)) {
       case 0: return launch_class<Op, S, NF, 0>(s, n, out, nelem, st);
       case 1: return launch_class<Op, S, NF, 1>(s, n, out, nelem, st);
       default: return launch_class<Op, S, NF, 2>(s, n, out, nelem, st);

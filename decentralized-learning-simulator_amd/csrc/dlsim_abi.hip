@@ -741,6 +741,47 @@ int dlsim_probe_pattern(const void* const* d_inputs, int n, void* d_out, size_t 
   return run<dlsim::XorProbe<2>>(d_inputs, n, nullptr, d_out, n_elems, st);
 }
 
+int dlsim_wreduce_mixed(const void* const* d_inputs, const int* dtypes, int n, const double* h_weights,
+                        void* d_out, int out_dtype, size_t n_elems, void* stream) {
+  g_err.clear();
+  if (n < 1) return fail(DLSIM_E_ARG, "n must be >= 1 (got %d)", n);
+  if (!d_inputs || !dtypes || !h_weights) return fail(DLSIM_E_ARG, "null inputs, dtypes or weights array");
+  if (out_dtype < DLSIM_F32 || out_dtype > DLSIM_F64) return fail(DLSIM_E_DTYPE, "unsupported dtype %d", out_dtype);
+  for (int i = 0; i < n; ++i)
+    if (dtypes[i] < DLSIM_F32 || dtypes[i] > DLSIM_F64)
+      return fail(DLSIM_E_DTYPE, "unsupported dtype %d at index %d", dtypes[i], i);
+  if (dtypes[0] != out_dtype)
+    return fail(DLSIM_E_ARG, "input 0 (models[0]'s parameter) must have the output's dtype");
+  if (n_elems == 0) return DLSIM_OK;
+  if (!d_out) return fail(DLSIM_E_ARG, "null output pointer");
+  const uintptr_t o0 = reinterpret_cast<uintptr_t>(d_out), o1 = o0 + n_elems * elem_bytes(out_dtype);
+  for (int i = 0; i < n; ++i) {
+    if (!d_inputs[i]) return fail(DLSIM_E_ARG, "null input pointer at index %d", i);
+    const uintptr_t a0 = reinterpret_cast<uintptr_t>(d_inputs[i]), a1 = a0 + n_elems * elem_bytes(dtypes[i]);
+    // later passes (n > 32) read the output back: no input may share its bytes
+    if (a0 < o1 && o0 < a1) return fail(DLSIM_E_ARG, "output overlaps input %d", i);
+  }
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const size_t blocks = std::min<size_t>((n_elems + dlsim::kBlock - 1) / dlsim::kBlock, 2048);
+  for (int i0 = 0; i0 < n; i0 += dlsim::kMixedMaxInputs) {
+    dlsim::MixedSlots s;
+    std::memset(&s, 0, sizeof(s));
+    s.n = std::min(n - i0, dlsim::kMixedMaxInputs);
+    s.out_dt = out_dtype;
+    s.seed = i0 == 0;
+    for (int k = 0; k < s.n; ++k) {
+      s.p[k] = d_inputs[i0 + k];
+      s.w[k] = h_weights[i0 + k];
+      s.dt[k] = dtypes[i0 + k];
+    }
+    hipLaunchKernelGGL(dlsim::k_wreduce_mixed<dlsim::MixedSlots>, dim3(static_cast<unsigned>(blocks)),
+                       dim3(dlsim::kBlock), 0, st, s, d_out, n_elems);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "k_wreduce_mixed launch");
+  }
+  return DLSIM_OK;
+}
+
 int dlsim_device_alloc(size_t nbytes, int flags, void** d_out, int* contiguous) {
   g_err.clear();
   if (!d_out) return fail(DLSIM_E_ARG, "null d_out");

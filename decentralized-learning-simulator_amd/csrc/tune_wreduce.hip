@@ -481,6 +481,144 @@ void launch_ring(const Slots<128>& s, int, void* out, size_t nvec, size_t, hipSt
                      out, nvec);
 }
 
+// Round 5: small slices. A one-tile-per-block grid at
+// 1.4 M elements has every block resident at once: all loads issue at the
+// start and all stores at the end, read and write phases apart. The
+// pipelined grid keeps gm*256 blocks; block b takes tiles b-1, b-1+W, ...
+// (W = blocks - 1; block 0 the ragged end) and issues the loads of its next
+// tile before it folds and stores the current one (two register buffers),
+// so stores overlap loads inside every block. Same fold order: bit-exact.
+template <class Op, int NF, int VPT, int VS>
+__device__ __forceinline__ void pipe_load(const Slots<128>& s, size_t v0, size_t nvec, u32x4 (&r)[NF][VPT]) {
+#pragma unroll
+  for (int i = 0; i < NF; ++i) load_tile<Op, VPT, 1, false, VS>(s.ptr(i), v0, nvec, r[i]);
+}
+template <class Op, int NF, int VPT, int VS>
+__device__ __forceinline__ void pipe_fold_store(const Slots<128>& s, const OutRef& o, size_t v0,
+                                                const u32x4 (&r)[NF][VPT]) {
+  acc_t<Op> a[VPT][Op::E];
+  init_tile<Op, VPT>(a, r[0], false);
+#pragma unroll
+  for (int i = 0; i < NF; ++i) fold_tile<Op, VPT>(a, s.wt(i), r[i]);
+#pragma unroll
+  for (int v = 0; v < VPT; ++v) store_vec<16>(o, v0 + static_cast<size_t>(v) * VS, pack<Op>(a[v], s.divisor()));
+}
+template <class Op, int NF, int VPT, bool WM>
+__global__ __launch_bounds__(kBlock) void k_tiles_pipe(const Slots<128> s, int n, void* __restrict__ out,
+                                                       size_t nvec, size_t nelem) {
+  constexpr size_t kTile = (size_t)kBlock * VPT;
+  constexpr int VS = WM ? 64 : kBlock;
+  const size_t full = nvec / kTile;
+  const OutRef o = make_out<16>(out, nvec);
+  if (blockIdx.x == 0) {
+    if (full * kTile < nvec)
+      reduce_tile<Op, Slots<128>, NF, 8, VPT, 1, true, 16>(s, n, o, full * kTile + threadIdx.x, nvec);
+    const size_t j = nvec * Op::E + threadIdx.x;
+    if (j < nelem) fold_scalar<Op, Slots<128>>(s, n, out, j);
+    return;
+  }
+  const size_t W = gridDim.x - 1;
+  const size_t lo = WM ? (threadIdx.x >> 6) * 64 * VPT + (threadIdx.x & 63) : threadIdx.x;
+  size_t t = blockIdx.x - 1;
+  if (t >= full) return;
+  u32x4 ra[NF][VPT], rb[NF][VPT];
+  pipe_load<Op, NF, VPT, VS>(s, t * kTile + lo, nvec, ra);
+  while (true) {
+    size_t t2 = t + W;
+    if (t2 < full) pipe_load<Op, NF, VPT, VS>(s, t2 * kTile + lo, nvec, rb);
+    pipe_fold_store<Op, NF, VPT, VS>(s, o, t * kTile + lo, ra);
+    if (t2 >= full) break;
+    t = t2;
+    t2 = t + W;
+    if (t2 < full) pipe_load<Op, NF, VPT, VS>(s, t2 * kTile + lo, nvec, ra);
+    pipe_fold_store<Op, NF, VPT, VS>(s, o, t * kTile + lo, rb);
+    if (t2 >= full) break;
+    t = t2;
+  }
+}
+// gm > 0: 1 + gm*256 blocks; gm < 0: 1 + ceil(full / -gm) blocks (-gm tiles per block)
+template <class Op, int NF, int VPT, bool WM>
+void launch_pipe(const Slots<128>& s, int n, void* out, size_t nvec, size_t nelem, hipStream_t st, int gm) {
+  const size_t full = nvec / ((size_t)kBlock * VPT);
+  size_t workers = gm > 0 ? (size_t)gm * 256 : (full + (size_t)(-gm) - 1) / (size_t)(-gm);
+  workers = std::max<size_t>(1, std::min(workers, full));
+  hipLaunchKernelGGL((k_tiles_pipe<Op, NF, VPT, WM>), dim3((unsigned)(workers + 1)), dim3(kBlock), 0, st, s, n, out,
+                     nvec, nelem);
+}
+// Balanced one-shot grid (round 5): B = 256*k blocks, block b owns the
+// vectors [b*nvec/B, (b+1)*nvec/B) (boundaries rounded down to 8 vectors,
+// 128 B), every lane loads its up to VPT vectors of every input at once
+// (masked), folds and stores: each CU gets the same bytes, where a grid of
+// whole tiles leaves some CUs one tile more than others (at 1.4 M fp32 the
+// VPT 2 grid has 2.67 tiles per CU, the VPT 4 grid 1.33). Block 0 also folds
+// the scalar tail. LDS > 0: dynamic LDS that caps the blocks per CU.
+template <class Op, int NF, int VPT>
+__global__ __launch_bounds__(kBlock) void k_bal(const Slots<128> s, int n, void* __restrict__ out, size_t nvec,
+                                                size_t nelem) {
+  const size_t B = gridDim.x, b = blockIdx.x;
+  const size_t r0 = (b * nvec / B) & ~(size_t)7;
+  const size_t r1 = b + 1 == B ? nvec : ((b + 1) * nvec / B) & ~(size_t)7;
+  const OutRef o = make_out<16>(out, nvec);
+  reduce_tile<Op, Slots<128>, NF, 8, VPT, 1, true, 16>(s, n, o, r0 + threadIdx.x, r1);
+  if (b == 0) {
+    const size_t j = nvec * Op::E + threadIdx.x;
+    if (j < nelem) fold_scalar<Op, Slots<128>>(s, n, out, j);
+  }
+}
+template <class Op, int NF, int V>
+void bal_go(const Slots<128>& s, int n, void* out, size_t nvec, size_t nelem, hipStream_t st, size_t B, size_t lds) {
+  hipLaunchKernelGGL((k_bal<Op, NF, V>), dim3((unsigned)B), dim3(kBlock), lds, st, s, n, out, nvec, nelem);
+}
+template <class Op, int NF, int LDSK>
+void launch_bal(const Slots<128>& s, int n, void* out, size_t nvec, size_t nelem, hipStream_t st, int gm) {
+  const size_t B = (size_t)gm * 256;
+  const size_t per = (nvec + B - 1) / B + 8;  // + the 128-B rounding of the boundaries
+  const size_t vpt = (per + kBlock - 1) / kBlock;
+  const size_t lds = LDSK ? (160 * 1024) / LDSK - 512 : 0;
+  switch (vpt) {
+    case 1: bal_go<Op, NF, 1>(s, n, out, nvec, nelem, st, B, lds); break;
+    case 2: bal_go<Op, NF, 2>(s, n, out, nvec, nelem, st, B, lds); break;
+    case 3: bal_go<Op, NF, 3>(s, n, out, nvec, nelem, st, B, lds); break;
+    case 4: bal_go<Op, NF, 4>(s, n, out, nvec, nelem, st, B, lds); break;
+    case 5: bal_go<Op, NF, 5>(s, n, out, nvec, nelem, st, B, lds); break;
+    case 6: bal_go<Op, NF, 6>(s, n, out, nvec, nelem, st, B, lds); break;
+    case 7: bal_go<Op, NF, 7>(s, n, out, nvec, nelem, st, B, lds); break;
+    case 8: bal_go<Op, NF, 8>(s, n, out, nvec, nelem, st, B, lds); break;
+    default: fprintf(stderr, "k_bal: %zu vectors per lane\n", vpt); exit(1);
+  }
+}
+
+template <class Op, int NF>
+void add_small(std::vector<Variant>& vs, int n) {
+  if constexpr (!std::is_same<Op, F32Exact>::value) return;
+  else {
+  if (n != NF) return;
+  const std::string p = "NF" + std::to_string(NF);
+  vs.push_back({p + "_V2_sc1_blk", launch_ts<Op, NF, 8, 2, 1, 16, false>, 0});  // shipped below 2 M fp32
+  vs.push_back({p + "_V1_sc1_blk", launch_ts<Op, NF, 8, 1, 1, 16, false>, 0});
+  vs.push_back({p + "_V4_sc1_blk", launch_ts<Op, NF, 8, 4, 1, 16, false>, 0});
+  vs.push_back({p + "_xorprobe_V4w", launch_probe<Op, NF>, 0});
+  vs.push_back({p + "_bal_k1", launch_bal<Op, NF, 0>, 1});
+  vs.push_back({p + "_bal_k2", launch_bal<Op, NF, 0>, 2});
+  vs.push_back({p + "_bal_k3", launch_bal<Op, NF, 0>, 3});
+  vs.push_back({p + "_bal_k4", launch_bal<Op, NF, 0>, 4});
+  vs.push_back({p + "_bal_k1_lds1", launch_bal<Op, NF, 1>, 1});
+  vs.push_back({p + "_bal_k2_lds2", launch_bal<Op, NF, 2>, 2});
+  vs.push_back({p + "_bal_k3_lds3", launch_bal<Op, NF, 3>, 3});
+  if (getenv("DLSIM_TUNE_SMALL_BAL")) return;
+  vs.push_back({p + "_pipe_V1_blk_g1", launch_pipe<Op, NF, 1, false>, 1});
+  vs.push_back({p + "_pipe_V1_blk_g2", launch_pipe<Op, NF, 1, false>, 2});
+  vs.push_back({p + "_pipe_V1_blk_g3", launch_pipe<Op, NF, 1, false>, 3});
+  vs.push_back({p + "_pipe_V1_blk_t2", launch_pipe<Op, NF, 1, false>, -2});
+  vs.push_back({p + "_pipe_V1_blk_t3", launch_pipe<Op, NF, 1, false>, -3});
+  vs.push_back({p + "_pipe_V1_wave_g2", launch_pipe<Op, NF, 1, true>, 2});
+  vs.push_back({p + "_pipe_V2_blk_g1", launch_pipe<Op, NF, 2, false>, 1});
+  vs.push_back({p + "_pipe_V2_blk_t2", launch_pipe<Op, NF, 2, false>, -2});
+  vs.push_back({p + "_pipe_V2_wave_g1", launch_pipe<Op, NF, 2, true>, 1});
+  vs.push_back({p + "_pipe_V2_wave_t2", launch_pipe<Op, NF, 2, true>, -2});
+  }
+}
+
 // Round 3: the shipped large shape, the memory-only
 // probe, read-only and write-only probes of the same tiles, and pipelined
 // LDS-DMA rings (nt and default policy) at 1-2 blocks per CU.
@@ -710,9 +848,18 @@ int run(int n, size_t P, int reps, double peak_gbs) {
   for (auto& e : ev) CK(hipEventCreate(&e));
   const double alg_bytes = (double)(n + 1) * bytes;
 
-  const bool r03 = getenv("DLSIM_TUNE_R03") != nullptr || getenv("DLSIM_TUNE_LAYOUT") != nullptr;
+  const bool r03 = getenv("DLSIM_TUNE_R03") != nullptr || getenv("DLSIM_TUNE_LAYOUT") != nullptr ||
+                   getenv("DLSIM_TUNE_SMALL") != nullptr;
   std::vector<Variant> vs;
-  if (getenv("DLSIM_TUNE_LAYOUT")) {
+  if (getenv("DLSIM_TUNE_SMALL")) {
+    add_small<Op, 2>(vs, n);
+    add_small<Op, 4>(vs, n);
+    add_small<Op, 8>(vs, n);
+    if (vs.empty()) {
+      fprintf(stderr, "DLSIM_TUNE_SMALL needs f32 exact, n = 2, 4 or 8\n");
+      return 1;
+    }
+  } else if (getenv("DLSIM_TUNE_LAYOUT")) {
     add_layout<Op>(vs, n);
   } else if (r03) {
     add_r03<Op, 8>(vs, n);

@@ -795,4 +795,92 @@ struct XorProbe {
   __device__ static float finish(float a, float) { return a; }
 };
 
+// ---- parameters of different dtypes at one position (round 5) -----------------
+// fedavg.py:20-25 when a model's parameter t has another dtype than
+// models[0]'s: c1 (models[0]'s dtype cd) starts as
+// models[0][t] * 0, then per input i `c1.add_(w_i * p1)` with torch's type
+// promotion: the product in p1's dtype pd (float(w) * x rounded to fp32 and then
+// to pd for fp32 / bf16 / fp16; the exact double w times x for fp64), the add
+// in result_type(cd, pd) (fp32 for any pair of fp32 / bf16 / fp16, fp64 with a
+// double on either side), cast back into cd the way c10 casts (a double to
+// bf16 / fp16 goes through float). Pinned by tests/golden/mixed_*.npz, made by
+// running the reference. One element per lane, values carried as exact
+// doubles; a rare path (simulations aggregate one architecture), so no
+// vector loads. dtype codes are include/dlsim.h's DLSIM_F32/BF16/F16/F64.
+constexpr int kMixedMaxInputs = 32;
+struct MixedSlots {
+  const void* p[kMixedMaxInputs];
+  double w[kMixedMaxInputs];
+  int dt[kMixedMaxInputs];
+  int n;       // inputs of this pass
+  int out_dt;  // cd
+  int seed;    // 1: start from input 0 * 0; 0: continue from the output (a later pass)
+};
+
+__device__ __forceinline__ double pin_f64(double v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+__device__ __forceinline__ double mixed_load(const void* p, int dt, size_t j) {
+  switch (dt) {
+    case 0: return static_cast<double>(static_cast<const float*>(p)[j]);
+    case 1: return static_cast<double>(__uint_as_float(static_cast<uint32_t>(static_cast<const uint16_t*>(p)[j]) << 16));
+    case 2: return static_cast<double>(static_cast<float>(static_cast<const _Float16*>(p)[j]));
+    default: return static_cast<const double*>(p)[j];
+  }
+}
+
+// a float result cast to dt (f32 / bf16 / f16), as an exact double
+__device__ __forceinline__ double mixed_round_f32(float x, int dt) {
+  x = pin_f32(x);
+  if (dt == 1) return static_cast<double>(bf16_round(x));
+  if (dt == 2) return static_cast<double>(pin_f32(f16_round(x)));
+  return static_cast<double>(x);
+}
+
+// a double result cast to dt: c10 converts a double to float first, and a
+// bf16 / fp16 from that float
+__device__ __forceinline__ double mixed_round_f64(double x, int dt) {
+  if (dt == 3) return x;
+  return mixed_round_f32(static_cast<float>(x), dt);
+}
+
+__device__ __forceinline__ void mixed_store(void* p, int dt, size_t j, double v) {
+  switch (dt) {  // v is exactly representable in dt (bf16: a canonical NaN if NaN)
+    case 0: static_cast<float*>(p)[j] = static_cast<float>(v); break;
+    case 1: static_cast<uint16_t*>(p)[j] = static_cast<uint16_t>(__float_as_uint(static_cast<float>(v)) >> 16); break;
+    case 2: static_cast<_Float16*>(p)[j] = static_cast<_Float16>(static_cast<float>(v)); break;
+    default: static_cast<double*>(p)[j] = v;
+  }
+}
+
+// (a template so that the header, included by every unit, defines it once:
+// instantiated with MixedSlots by dlsim_abi.hip)
+template <class S>
+__global__ __launch_bounds__(kBlock) void k_wreduce_mixed(const S s, void* __restrict__ out, size_t nelem) {
+  const int cd = s.out_dt;
+  for (size_t j = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; j < nelem;
+       j += static_cast<size_t>(gridDim.x) * kBlock) {
+    double acc;
+    if (s.seed) {
+      const double x0 = mixed_load(s.p[0], cd, j);
+      acc = cd == 3 ? pin_f64(x0 * 0.0) : mixed_round_f32(static_cast<float>(x0) * 0.0f, cd);
+    } else {
+      acc = mixed_load(out, cd, j);
+    }
+    for (int i = 0; i < s.n; ++i) {
+      const int pd = s.dt[i];
+      const double x = mixed_load(s.p[i], pd, j);
+      const double prod = pd == 3 ? pin_f64(s.w[i] * x)
+                                  : mixed_round_f32(static_cast<float>(s.w[i]) * static_cast<float>(x), pd);
+      if (cd == 3 || pd == 3)
+        acc = mixed_round_f64(pin_f64(acc + prod), cd);
+      else
+        acc = mixed_round_f32(static_cast<float>(acc) + static_cast<float>(prod), cd);
+    }
+    mixed_store(out, cd, j, acc);
+  }
+}
+
 }  // namespace dlsim

@@ -47,6 +47,7 @@ EXPORTS = (
     "dlsim_rccl_bind",
     "dlsim_wreduce_sharded",
     "dlsim_wreduce_sharded_f64",
+    "dlsim_wreduce_mixed",
     "dlsim_device_alloc",
     "dlsim_device_free",
     "dlsim_pool_alloc",
@@ -158,6 +159,9 @@ def load() -> ctypes.CDLL:
         lib.dlsim_shard_range.restype = i
         lib.dlsim_probe_pattern.argtypes = [ctypes.POINTER(vp), i, vp, sz, i, vp]
         lib.dlsim_probe_pattern.restype = i
+        lib.dlsim_wreduce_mixed.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(i), i, ctypes.POINTER(ctypes.c_double),
+                                            vp, i, sz, vp]
+        lib.dlsim_wreduce_mixed.restype = i
         lib.dlsim_device_alloc.argtypes = [sz, i, ctypes.POINTER(vp), ctypes.POINTER(i)]
         lib.dlsim_device_alloc.restype = i
         lib.dlsim_device_free.argtypes = [vp]
@@ -293,6 +297,30 @@ class ReducePlan:
         rc = self._lib.dlsim_wreduce(self._ptrs, self.n, self._wp, self._out, self.numel,
                                      self.dtype, self.mode, _stream_handle(self.device, stream))
         _check("dlsim_wreduce", rc)
+
+
+def wreduce_mixed(inputs, weights, out, stream=None):
+    """dlsim_wreduce_mixed: out = the reference's fold of inputs of different
+    dtypes (flat device tensors; inputs[0] has out's dtype), with the
+    Python-float weights as doubles. Exact only."""
+    n = len(inputs)
+    if n < 1:
+        raise IndexError("list index out of range")
+    if len(weights) != n:
+        raise AssertionError("weights/models length mismatch")
+    numel = out.numel()
+    for t in list(inputs) + [out]:
+        if not t.is_cuda or t.device != out.device:
+            raise ValueError("wreduce_mixed needs device tensors on one device (no CPU path)")
+        if t.numel() != numel or not t.is_contiguous():
+            raise ValueError("inputs and output must be contiguous and of one size")
+    codes = (ctypes.c_int * n)(*[dtype_code(t.dtype, single_task=True) for t in inputs])
+    ptrs = (ctypes.c_void_p * n)(*[t.data_ptr() for t in inputs])
+    w = (ctypes.c_double * n)(*[float(x) for x in weights])
+    _check("dlsim_wreduce_mixed",
+           load().dlsim_wreduce_mixed(ptrs, codes, n, w, out.data_ptr(), dtype_code(out.dtype, single_task=True),
+                                      numel, _stream_handle(out.device, stream)))
+    return out
 
 
 DLSIM_ALLOC_CONTIGUOUS = 1

@@ -1132,11 +1132,12 @@ def _aggregate_zip(models: List[nn.Module], weights: Sequence[float], mode: int,
     always does; a model's extra parameters are ignored), starting from
     models[0][t] * 0; `c1.add_(w * p1)` broadcasts a p1 whose shape
     broadcasts to c1's and raises RuntimeError otherwise, as torch does.
-    A p1 of another dtype raises ValueError (the reference would add a
-    product rounded in p1's dtype). One reduce launch per
-    parameter, on the GPU; a host model's tensors are copied in first. A rare
-    path: simulations aggregate one architecture and take the one-launch
-    paths above."""
+    A p1 of another dtype follows torch's type promotion: the product in
+    p1's dtype, the add in the promoted dtype, rounded into c1's
+    (dlsim_wreduce_mixed; pinned by tests/golden/mixed_*.npz, made by running
+    the reference). One reduce launch per parameter, on the GPU; a host
+    model's tensors are copied in first. A rare path: simulations aggregate
+    one architecture and take the one-launch paths above."""
     weights = [float(w) for w in weights]
     n = len(models)
     plists = [module_params(m) for m in models]
@@ -1152,9 +1153,6 @@ def _aggregate_zip(models: List[nn.Module], weights: Sequence[float], mode: int,
                 if len(plists[i]) <= t:
                     continue
                 q = plists[i][t].detach()
-                if q.dtype != c.dtype:
-                    raise ValueError(f"parameter {t} of model {i}: dtype {q.dtype} differs from models[0]'s "
-                                     f"{c.dtype}")
                 if q.shape != c.shape:
                     if torch.broadcast_shapes(q.shape, c.shape) != c.shape:
                         raise RuntimeError(f"output with shape {list(c.shape)} doesn't match the broadcast "
@@ -1166,6 +1164,9 @@ def _aggregate_zip(models: List[nn.Module], weights: Sequence[float], mode: int,
                 continue
             off = layout.offsets[t]
             out = arenas[c.dtype][off:off + c.numel()]
+            if any(r.dtype != c.dtype for r in rows):
+                _native.wreduce_mixed(rows, ws, out)  # exact: torch's promotion, step by step
+                continue
             w = _native.weights_for_dtype(ws, c.dtype)
             _native.wreduce(rows, w, out, mode)
         if host_out:

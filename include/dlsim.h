@@ -459,6 +459,24 @@ int dlsim_probe_pattern(const void* const* d_inputs, int n, void* d_out, size_t 
                         void* stream);
 
 /*
+ * dlsim_wreduce_mixed — one output parameter whose inputs differ in dtype
+ * (fedavg.py:20-25 when a model's parameter at this position has another
+ * dtype than models[0]'s). d_out has out_dtype, which is
+ * input 0's (models[0] defines c1). d_out = input 0 * 0, then per input i in
+ * order the reference's `c1.add_(w_i * p1)` with torch's type promotion: the
+ * product in dtypes[i] (float(w_i) * x rounded to fp32 and then to dtypes[i]
+ * for DLSIM_F32 / BF16 / F16, the exact double w_i times x for DLSIM_F64), the
+ * add in the promoted dtype (fp32 for any pair of fp32 / bf16 / fp16, fp64
+ * with a double on either side), cast back into out_dtype as c10 casts (a
+ * double to bf16 / fp16 goes through float). h_weights are the Python-float
+ * weights as doubles. Exact only; one element per lane (a rare path), in
+ * passes of 32 inputs for larger n, so the output must not overlap any input.
+ * Bit-exact to the reference (tests/golden/mixed_*.npz). Stream-ordered.
+ */
+int dlsim_wreduce_mixed(const void* const* d_inputs, const int* dtypes, int n, const double* h_weights,
+                        void* d_out, int out_dtype, size_t n_elems, void* stream);
+
+/*
  * dlsim_device_alloc / dlsim_device_free — device memory for long-lived
  * large buffers (staging rows, resident model blocks) on the calling
  * thread's current device. flags DLSIM_ALLOC_CONTIGUOUS asks the driver for

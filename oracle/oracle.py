@@ -229,6 +229,121 @@ def wreduce_zip(params_by_model, weights, dtype: str = "f32", mode: str = "exact
     return outs
 
 
+# ---- parameters of different dtypes at one position (fedavg.py:25 with torch's
+# type promotion; pinned by tests/golden/mixed_*.npz) ---------------------------
+
+def _mixed_promote(a: str, b: str) -> str:
+    """torch.result_type of two floating tensors: equal -> itself; with a
+    double -> double; any other pair of f32 / bf16 / f16 -> float32."""
+    if a == b:
+        return a
+    return "f64" if "f64" in (a, b) else "f32"
+
+
+def _mixed_to_f64(x, dt: str) -> np.ndarray:
+    """Stored values (float32 / float64, or uint16 bits for bf16 / f16) as
+    exact doubles."""
+    x = np.asarray(x)
+    if dt == "bf16":
+        return bf16_bits_to_f32(x).astype(np.float64)
+    if dt == "f16":
+        return f16_bits_to_f32(x).astype(np.float64)
+    return x.astype(np.float64)
+
+
+def _mixed_round_f32(x32: np.ndarray, dt: str) -> np.ndarray:
+    """A float32 result cast to dt (RNE), returned as exact doubles."""
+    x32 = np.asarray(x32, dtype=np.float32)
+    if dt == "bf16":
+        return bf16_bits_to_f32(f32_to_bf16_bits(x32)).astype(np.float64)
+    if dt == "f16":
+        return f32_to_f16_bits(x32).astype(np.float64)
+    return x32.astype(np.float64)  # f32 (and f64: exact)
+
+
+def _mixed_round_f64(x64: np.ndarray, dt: str) -> np.ndarray:
+    """A double result cast to dt as c10 does: to float (RNE), and for bf16 /
+    f16 from that float (their constructors take a float)."""
+    if dt == "f64":
+        return x64
+    with np.errstate(over="ignore"):
+        return _mixed_round_f32(x64.astype(np.float32), dt)
+
+
+def _mixed_encode(acc: np.ndarray, dt: str) -> np.ndarray:
+    if dt == "f64":
+        return acc
+    x32 = acc.astype(np.float32)
+    if dt == "bf16":
+        return f32_to_bf16_bits(x32)
+    if dt == "f16":
+        return f32_to_f16_bits(x32).view(np.uint16)
+    return x32
+
+
+def wreduce_mixed(xs, dtypes, weights_f64, out_dtype: str) -> np.ndarray:
+    """One output parameter whose inputs differ in dtype (fedavg.py:20-25):
+    acc = models[0]'s parameter * 0 in out_dtype (models[0] defines c1, so
+    dtypes[0] == out_dtype), then per input, in order,
+      prod = w * x in x's dtype: float(w) * x rounded to float and then to x's
+             format for f32 / bf16 / f16, the exact double w times x for f64;
+      acc  = add_ in the promoted dtype of (out_dtype, x's dtype): a float sum
+             (or a double sum with f64 on either side), cast back to out_dtype.
+    xs: flat arrays as stored (uint16 bits for bf16 / f16); weights_f64: the
+    Python-float weights. Returns out_dtype's storage (uint16 bits for bf16 /
+    f16)."""
+    if dtypes[0] != out_dtype:
+        raise ValueError("models[0]'s parameter defines the output dtype")
+    x0 = _mixed_to_f64(xs[0], out_dtype)
+    with np.errstate(all="ignore"):
+        if out_dtype == "f64":
+            acc = x0 * 0.0
+        else:
+            acc = (x0.astype(np.float32) * np.float32(0.0)).astype(np.float64)
+        for x, dt, w in zip(xs, dtypes, weights_f64):
+            xv = _mixed_to_f64(x, dt)
+            if dt == "f64":
+                prod = np.float64(w) * xv
+            else:
+                prod = _mixed_round_f32(np.float32(w) * xv.astype(np.float32), dt)
+            if _mixed_promote(out_dtype, dt) == "f64":
+                acc = _mixed_round_f64(acc + prod, out_dtype)
+            else:
+                acc = _mixed_round_f32(acc.astype(np.float32) + prod.astype(np.float32), out_dtype)
+    return _mixed_encode(acc, out_dtype)
+
+
+def wreduce_zip_mixed(params_by_model, dtypes_by_model, weights):
+    """wreduce_zip for models whose parameters may also differ in dtype:
+    the zip pairing and broadcasting of wreduce_zip, each output parameter
+    folded by wreduce_mixed in models[0]'s dtype. weights: the reference's
+    argument (None / [] / list), resolved with fedavg.py:14-17 as doubles."""
+    n = len(params_by_model)
+    if n < 1:
+        raise IndexError("list index out of range")
+    w = reference_weights_f64(n, weights)
+    outs = []
+    for t, c in enumerate(params_by_model[0]):
+        c = np.asarray(c)
+        rows, dts, ws = [], [], []
+        for i, ps in enumerate(params_by_model):
+            if len(ps) <= t:
+                continue
+            q = np.asarray(ps[t])
+            if q.shape != c.shape:
+                try:
+                    q = np.broadcast_to(q, c.shape)
+                except ValueError as e:
+                    raise RuntimeError(f"output with shape {list(c.shape)} doesn't match the broadcast "
+                                       f"shape of {list(q.shape)}") from e
+            rows.append(np.ascontiguousarray(q).reshape(-1))
+            dts.append(dtypes_by_model[i][t])
+            ws.append(w[i])
+        outs.append(wreduce_mixed(rows, dts, ws, dtypes_by_model[0][t]).reshape(c.shape)
+                    if c.size else c.copy())
+    return outs
+
+
 def chunk_mean_ilp_begin(m: int, n: int, threads: int, dtype: str = "f32") -> int:
     """First column that PyTorch's CPU sum folds in row_sum (ILP) order."""
     if dtype == "f64":

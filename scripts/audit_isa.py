@@ -25,7 +25,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "decentralized-learning-simulator_amd", "dasklearn_amd", "lib", "libdlsim_hip.so")
 LLVM = "/opt/rocm/lib/llvm/bin"
 POLICIES = ("BF16Exact", "BF16Fast", "BF16Mean", "F16Exact", "F16Fast", "F16Mean", "F32Exact", "F32Fast",
-            "F32Mean", "F64Exact", "F64Fast")
+            "F32Mean", "F64Exact", "F64Fast", "MixedSlots")
+# exact like the *Exact policies: the mixed-dtype fold (k_wreduce_mixed, round 5)
+EXACT_KEYS = tuple(k for k in POLICIES if k.endswith("Exact")) + ("MixedSlots",)
 # encodings are suffixed in the disassembly (v_fmac_f32_e32, v_fma_f32_e64)
 FMA_RE = re.compile(r"\bv_(pk_)?(fmac?|mac|mad|fma_legacy|fmac_legacy)_f(32|64)(_e(32|64|64_dpp|32_dpp))?\b")
 MIX_RE = re.compile(r"\bv_\w*_mix\w*\b")
@@ -104,7 +106,7 @@ def audit(path=LIB):
             mix = len(MIX_RE.findall(body))
             e["fma"] += fma
             e["mix"] += mix
-            if key.endswith("Exact") and (fma or mix):
+            if key in EXACT_KEYS and (fma or mix):
                 bad.append({"kernel": name, "fma": fma, "mix": mix})
     return {"target": "gfx950", "library": os.path.relpath(path, ROOT), "code_objects": ncos, "per_policy": stats,
             "exact_policies_clean": not bad, "offending_kernels": bad}

@@ -66,6 +66,21 @@ def main():
         local = [x.to(dev) for x in xs[first:first + counts[rank]]]
         full2 = agg.aggregate_model_sharded(local, counts, ws, exact=True)
         checks[f"model_sharded_exact_{name}"] = bool(full2.is_cuda and orc.same_bits(bits(full2), exp))
+        # FAST: local partial sums with the HIP fma
+        # reduce, reduce-scatter, all-gather; within SURVEY §8e's tolerance of
+        # the exact sum: (n + W) * 2^-23 of sum|w_i x_i| for fp32; the per-rank
+        # bf16 rounding of the partial and the final cast, (W + 2) * 2^-8, for bf16
+        full3 = agg.aggregate_model_sharded(local, counts, ws, exact=False)
+        xf = np.stack([x.float().numpy().astype(np.float64) for x in xs])
+        wf = np.asarray(w32, dtype=np.float64)[:, None]
+        truth = (wf * xf).sum(0)
+        mag = (np.abs(wf * xf)).sum(0)
+        tol = (n + world) * 2.0 ** -23 if name == "f32" else (world + 2) * 2.0 ** -8
+        got = full3.detach().float().cpu().numpy().astype(np.float64)
+        err = np.abs(got - truth)
+        checks[f"model_sharded_fast_{name}"] = bool(full3.is_cuda and full3.dtype == xs[0].dtype
+                                                    and np.all(err <= tol * mag + 1e-30))
+        checks[f"model_sharded_fast_{name}_not_trivial"] = bool(np.any(got != 0.0))
     torch.cuda.synchronize()
     print(json.dumps({"rank": rank, "world": world, "checks": checks}), flush=True)
     dist.destroy_process_group()

@@ -24,7 +24,7 @@ def pytest_configure(config):
 def golden_paths():
     """The same-signature fixtures (make_golden.py): N models, one (N, P) row block."""
     return sorted(p for p in glob.glob(os.path.join(GOLDEN, "*.npz"))
-                  if not os.path.basename(p).startswith("mismatch_"))
+                  if not os.path.basename(p).startswith(("mismatch_", "mixed_")))
 
 
 def mismatch_paths():
@@ -49,6 +49,34 @@ def load_mismatch(path):
     assert off == flat.size
     w = [float(v) for v in d["weights"]] if "weights" in d else None
     return meta, params, w, d.get("expected")
+
+
+def mixed_paths():
+    """Fixtures of models whose parameters differ in dtype (make_golden_mixed.py)."""
+    return sorted(glob.glob(os.path.join(GOLDEN, "mixed_*.npz")))
+
+
+def load_mixed(path):
+    """One mixed-dtype fixture (no pickle): meta, per-model lists of parameter
+    arrays in their shapes (bf16/f16 as uint16 bits), per-model dtype names,
+    the weights argument, and the expected outputs (flat, models[0]'s dtypes)
+    or None."""
+    with np.load(path, allow_pickle=False) as z:
+        d = {k: z[k] for k in z.files}
+    meta = json.loads(str(d["meta"]))
+    params = [[d[f"x{i}_{t}"].reshape(s) for t, s in enumerate(shapes)] for i, shapes in enumerate(meta["shapes"])]
+    w = [float(v) for v in d["weights"]] if "weights" in d else None
+    expected = None if meta["error"] else [d[f"y{t}"] for t in range(len(meta["shapes"][0]))]
+    return meta, params, meta["dtypes"], w, expected
+
+
+def same_bits_as(a, b, dt):
+    """same_bits for storage of dtype name dt (f16 bits compared as binary16)."""
+    from oracle import oracle as orc
+    a, b = np.asarray(a), np.asarray(b)
+    if dt == "f16":
+        return orc.same_bits(a.astype(np.uint16).view(np.float16), b.astype(np.uint16).view(np.float16))
+    return orc.same_bits(a, b)
 
 
 def load_golden(path):

@@ -2,7 +2,10 @@
 pairing (fedavg.py:23-24 — truncation at the shorter list, extra parameters
 ignored, `add_` broadcasting, RuntimeError where torch's add_ raises) through
 FedAvg.aggregate and aggregate_batch, against the reference's own outputs
-(tests/golden/mismatch_*.npz, make_golden_mismatch.py) and the oracle."""
+(tests/golden/mismatch_*.npz, make_golden_mismatch.py) and the oracle; and
+models whose parameters at one position differ in dtype (torch's type
+promotion in `c1.add_(w * p1)`, fedavg.py:25; tests/golden/mixed_*.npz,
+make_golden_mixed.py) through dlsim_wreduce_mixed."""
 from __future__ import annotations
 
 import os
@@ -12,7 +15,7 @@ import pytest
 import torch
 from torch import nn
 
-from conftest import load_mismatch, mismatch_paths
+from conftest import load_mismatch, load_mixed, mismatch_paths, mixed_paths, same_bits_as
 from oracle import oracle as orc
 
 pytestmark = pytest.mark.gpu
@@ -105,14 +108,110 @@ def test_batch_zip_beside_same_signature_tasks(path):
         assert np.array_equal(flat_bits(o, meta["dtype"]), flat_bits(ref, meta["dtype"]))
 
 
-def test_zip_dtype_mismatch_is_refused():
-    """A parameter of another dtype at the same position: the reference would
-    add a product rounded in that dtype; this path raises ValueError
-    (INTEGRATION.md §3)."""
-    a = nn.Linear(4, 3).cuda()
-    b = nn.Linear(4, 3).cuda().to(torch.bfloat16)
-    with pytest.raises(ValueError, match="dtype"):
-        FedAvg.aggregate([a, b], None)
+class MixedShaped(nn.Module):
+    """A model whose parameters each have their own dtype (fixture arrays:
+    uint16 bits for bf16 / f16)."""
+
+    def __init__(self, arrays, dtypes):
+        super().__init__()
+        ps = []
+        for a, d in zip(arrays, dtypes):
+            dt = TDT[d]
+            if dt in (torch.bfloat16, torch.float16):
+                t = torch.from_numpy(np.ascontiguousarray(a).view(np.int16).copy()).view(dt)
+            else:
+                t = torch.from_numpy(np.ascontiguousarray(a).copy())
+            ps.append(nn.Parameter(t))
+        self.ps = nn.ParameterList(ps)
+
+
+def build_mixed(params, dtypes, where):
+    models = [MixedShaped(ps, ds) for ps, ds in zip(params, dtypes)]
+    if where == "device":
+        models = [m.cuda() for m in models]
+    elif where == "arena":
+        models = [arena.to_device_arena(m.cuda()) for m in models]
+    return models
+
+
+def param_bits(p):
+    t = p.detach().reshape(-1).cpu()
+    if t.dtype in (torch.bfloat16, torch.float16):
+        return t.view(torch.int16).numpy().view(np.uint16)
+    return t.numpy()
+
+
+def check_mixed(out, meta, dtypes, expected):
+    ps = list(out.parameters())
+    assert len(ps) == len(expected)
+    for t, (p, exp) in enumerate(zip(ps, expected)):
+        assert p.dtype == TDT[dtypes[0][t]], (meta["case"], t)
+        assert same_bits_as(param_bits(p), exp, dtypes[0][t]), (meta["case"], t)
+
+
+@pytest.mark.parametrize("where", ["host", "device", "arena"])
+@pytest.mark.parametrize("path", mixed_paths(), ids=lambda p: os.path.basename(p)[:-4])
+def test_fedavg_mixed_dtypes_match_reference(path, where):
+    """A parameter of another dtype at one position:
+    the product in that dtype, the add in the promoted dtype, rounded into
+    models[0]'s — bit for bit the reference's output (make_golden_mixed.py),
+    from host, device and arena models."""
+    meta, params, dtypes, w, expected = load_mixed(path)
+    models = build_mixed(params, dtypes, where)
+    out = FedAvg.aggregate(models, w)
+    torch.cuda.synchronize()
+    on_host = where == "host"
+    assert all(p.is_cuda != on_host for p in out.parameters())
+    check_mixed(out, meta, dtypes, expected)
+
+
+@pytest.mark.parametrize("path", [p for p in mixed_paths() if "fewer" not in p and "broadcast" not in p],
+                         ids=lambda p: os.path.basename(p)[:-4])
+def test_batch_and_wave_mixed_task(path):
+    """aggregate_batch and a RoundExecutor wave: a mixed-dtype task beside
+    ordinary ones keeps its place and the reference's result."""
+    from test_gpu_dag_replay import Settings
+    from dasklearn_amd.rounds import RoundExecutor
+
+    meta, params, dtypes, w, expected = load_mixed(path)
+    mixed = build_mixed(params, dtypes, "device")
+    same = [MixedShaped(params[0], dtypes[0]).cuda() for _ in range(2)]
+    outs = aggregate_batch([(same, None), (mixed, w), (same, [0.25, 0.75])])
+    torch.cuda.synchronize()
+    check_mixed(outs[1], meta, dtypes, expected)
+    n = len(mixed)
+    tasks = [("agg_same", "aggregate", {"models": [("same", 0), ("same", 1)], "round": 1, "peer": 0}),
+             ("agg_mix", "aggregate", {"models": [("mixed", i) for i in range(n)], "weights": w,
+                                       "round": 1, "peer": 1})]
+    got = RoundExecutor({}, Settings()).run(tasks, seed={"mixed": mixed, "same": same})
+    torch.cuda.synchronize()
+    check_mixed(got["agg_mix"][0], meta, dtypes, expected)
+
+
+def test_wreduce_mixed_many_inputs_and_checks():
+    """dlsim_wreduce_mixed directly: n = 70 inputs of rotating dtypes (three
+    passes of at most 32) against the oracle, an in-order fold; the argument
+    checks (models[0]'s dtype, overlap, unknown dtype)."""
+    from dasklearn_amd import _native
+    rng = np.random.default_rng(70)
+    names = ["f32", "bf16", "f16", "f64"]
+    for out_dt in names:
+        n, p = 70, 5003
+        dts = [out_dt] + [names[(i * 3) % 4] for i in range(1, n)]
+        xs = [(torch.from_numpy(rng.standard_normal(p) * 0.05)).to(TDT[d]).cuda() for d in dts]
+        ws = [float(v) for v in rng.dirichlet(np.ones(n))]
+        out = torch.empty(p, dtype=TDT[out_dt], device="cuda")
+        _native.wreduce_mixed(xs, ws, out)
+        exp = orc.wreduce_mixed([param_bits(x) for x in xs], dts, ws, out_dt)
+        assert same_bits_as(param_bits(out), exp, out_dt), out_dt
+    x0 = torch.randn(64, device="cuda")
+    x1 = torch.randn(64, device="cuda", dtype=torch.bfloat16)
+    with pytest.raises(_native.DlsimError, match="dtype"):
+        _native.wreduce_mixed([x1, x0], [0.5, 0.5], torch.empty(64, device="cuda"))  # input 0 is not the out dtype
+    with pytest.raises(_native.DlsimError, match="overlaps"):
+        _native.wreduce_mixed([x0, x1], [0.5, 0.5], x0)
+    with pytest.raises(TypeError):
+        _native.wreduce_mixed([x0, x0.to(torch.int32)], [0.5, 0.5], torch.empty(64, device="cuda"))
 
 
 def test_zip_noncontiguous_model0_keeps_its_strides():

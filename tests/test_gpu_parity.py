@@ -271,13 +271,17 @@ def test_cfg4_2way_125M_bf16_properties():
 
 
 @pytest.mark.parametrize("dtype,p", [("f32", 1_999_999), ("f32", 2_000_003), ("f32", 4_999_997), ("f32", 5_000_003),
-                                     ("bf16", 47_999_993), ("bf16", 48_000_007)])
-@pytest.mark.parametrize("n", [2, 8])
+                                     ("bf16", 47_999_993), ("bf16", 48_000_007),
+                                     # round 5: below 2 M, VPT 4 where its tiles spread evenly (n >= 6)
+                                     ("f32", 786_431), ("f32", 917_507), ("f32", 1_048_577), ("f32", 1_179_651),
+                                     ("f32", 1_397_760), ("f32", 1_703_939)])
+@pytest.mark.parametrize("n", [2, 6, 8, 14])
 def test_launch_shapes_either_side_of_the_size_switch(dtype, p, n):
-    """The fixed fan-in kernels change launch shape by size (dlsim_abi.hip
-    fixed_shape: fp32 VPT 2 / VPT 4 block map at 2 M elements, block/wave map at
-    5 M, bf16 VPT 1 sc1 / VPT 4 nt at 48 M): every shape bit-exact against the
-    oracle over every element."""
+    """The fixed fan-in kernels change launch shape by size (dispatch.hpp
+    fixed_shape / size_class: fp32 VPT 2 / VPT 4 block map at 2 M elements and,
+    for n >= 6, below it where the VPT 4 tiles spread evenly over the CUs;
+    block/wave map at 5 M, bf16 VPT 1 sc1 / VPT 4 nt at 48 M): every shape
+    bit-exact against the oracle over every element."""
     g = torch.Generator(device=dev()).manual_seed(p + n)
     tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
     xs = [(torch.randn(p, generator=g, device=dev()) * 0.05).to(tdt) for _ in range(n)]

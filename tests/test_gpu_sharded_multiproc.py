@@ -3,9 +3,10 @@ process (GPU).
 
 Two or four fresh rank processes (tests/_sharded_hip_child.py) share the one
 MI355X of the box with a gloo control plane: each runs
-aggregate_param_sharded (gathered and not), a plan's repeated runs and
-aggregate_model_sharded(exact=True) with ShardedAggregator's default local
-reduce, the HIP kernel, on fp32 and bf16 models; the gathers go through host
+aggregate_param_sharded (gathered and not), a plan's repeated runs,
+aggregate_model_sharded(exact=True) and (round 5) its FAST form (partial
+sums, reduce-scatter, all-gather; SURVEY §8e's tolerance) with
+ShardedAggregator's default local reduce, the HIP kernel, on fp32 and bf16 models; the gathers go through host
 tensors (gloo). Every rank's assembled output must be bit-identical to the
 oracle's single fold ("results are bit-identical to 1 GPU").
 The ranks are started as fresh interpreters, as bench.py starts its ranks:

@@ -27,16 +27,17 @@ def report():
 
 def test_every_translation_unit_with_device_code_is_audited(report):
     # one code object per inst_*.hip unit, plus sharded_abi.hip's unpad copy
-    # kernel (dlsim_abi.hip carries no kernels)
+    # kernel and dlsim_abi.hip's mixed-dtype fold (round 5)
     units = [f for f in os.listdir(os.path.join(ROOT, "decentralized-learning-simulator_amd", "csrc"))
              if f.startswith("inst_") and f.endswith(".hip")]
-    assert report["code_objects"] == len(units) + 1
+    assert report["code_objects"] == len(units) + 2
 
 
 def test_exact_kernels_have_no_fused_or_mixed_ops(report):
     assert report["exact_policies_clean"], json.dumps(report["offending_kernels"][:10], indent=1)
     for pol in ("F32Exact", "BF16Exact", "F16Exact", "F64Exact"):
         assert report["per_policy"][pol]["kernels"] > 40, pol
+    assert report["per_policy"]["MixedSlots"]["kernels"] == 1  # k_wreduce_mixed, audited as exact
 
 
 def test_audit_sees_the_round2_shapes():
