@@ -55,6 +55,7 @@ METRIC = "device-resident GB/s, N-way weighted model-tensor reduce; 1/2/4/8 MI35
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 RESNET18_P = 11_181_642
 MIN_SET_FOOTPRINT = 1 << 30  # rotate >= 1 GiB of inputs: 4x the 256 MiB Infinity Cache
+MIN_OUT_FOOTPRINT = 1 << 30  # and >= 1 GiB of outputs (round 5)
 
 GNLENET_SHAPES = [(32, 3, 5, 5), (32,), (32,), (32,), (32, 32, 5, 5), (32,), (32,), (32,),
                   (64, 32, 5, 5), (64,), (64,), (64,), (10, 576), (10,)]
@@ -235,8 +236,9 @@ def weights_for(kind: str, n: int) -> list:
 
 
 class ReduceWorkload:
-    """Rotating input sets and prepared launches of one config's aggregate on
-    one device: `launch(k)` runs step k (set k mod S)."""
+    """Rotating input sets and outputs, and prepared launches of one
+    config's aggregate on one device: `launch(k)` runs step k (input set
+    k mod S into output k mod O; S and O each >= 1 GiB, O a multiple of S)."""
 
     def __init__(self, n, p, dtype, w32, mode, batch, dev, seed, stream):
         from dasklearn_amd import _native
@@ -267,36 +269,48 @@ class ReduceWorkload:
         else:
             rows = resident_empty(self.sets * batch * n * p_pad, tdt, dev, al).view(self.sets, batch, n, p_pad)
         self._keep.append(rows)
-        # DLSIM_BENCH_OUTS_FIRST: every output allocated before any fill (A/B
-        # knob of scripts/probes/probe_bench_setup.py)
-        outs_first = [arena_empty(p, tdt, dev) for _ in range(self.sets)] \
-            if batch == 1 and os.environ.get("DLSIM_BENCH_OUTS_FIRST") else None
+        # the outputs rotate too, over >= 1 GiB (round 5): outputs that rotate
+        # over a few buffers (rounds 1-4: one per input set, 134 MB for the
+        # north star) stay in the 256 MiB Infinity Cache and their rewrites
+        # never reach HBM -- 5-8 % of a north-star step. A
+        # multiple of the input sets, so step k reads set k mod S.
+        # DLSIM_BENCH_OUT_SETS=k overrides (A/B runs of that study only).
+        out_bytes = batch * p * esz
+        need = max(self.sets, math.ceil(MIN_OUT_FOOTPRINT / max(1, out_bytes)))
+        self.out_sets = int(os.environ.get("DLSIM_BENCH_OUT_SETS", "0")) or \
+            -(-need // self.sets) * self.sets
         for s in range(self.sets):
             if batch == 1:
                 x = rows[s][0]
                 x[:, :p].copy_((torch.randn((n, p), generator=g, device=dev) * 0.05).to(tdt))
-                out = outs_first[s] if outs_first else arena_empty(p, tdt, dev)
-                plan = _native.ReducePlan([x[i, :p] for i in range(n)], w32, out, mode)
-                assert all(t.data_ptr() % 16 == 0 for t in plan._keep[0]), "arena rows must be 16-B aligned"
-                self.outs.append(out)
             else:
                 x = rows[s]
                 x[:, :, :p].copy_((torch.randn((batch, n, p), generator=g, device=dev) * 0.05).to(tdt))
+            self._keep.append(x)
+        for j in range(self.out_sets):
+            x = rows[j % self.sets][0] if batch == 1 else rows[j % self.sets]
+            if batch == 1:
+                out = arena_empty(p, tdt, dev)
+                plan = _native.ReducePlan([x[i, :p] for i in range(n)], w32, out, mode)
+                assert all(t.data_ptr() % 16 == 0 for t in plan._keep[0]), "arena rows must be 16-B aligned"
+                self.outs.append(out)
+                if j < self.sets:
+                    self.probe_plans.append(_native.ReducePlan([x[i, :p] for i in range(n)], w32, out, mode,
+                                                               probe=True))
+            else:
                 ob = aligned_empty(batch * p_pad, tdt, dev, al).view(batch, p_pad)
                 plan = _native.BatchPlan([([x[b, i, :p] for i in range(n)], w32, ob[b, :p]) for b in range(batch)],
                                          mode)
                 self.outs.append(ob[0, :p])
+                self._keep.append(ob)
             self.plans.append(plan)
-            if batch == 1:
-                self.probe_plans.append(_native.ReducePlan([x[i, :p] for i in range(n)], w32, out, mode, probe=True))
-            self._keep.append(x)
         self.kernel = "dlsim::k_wreduce_tiles" if batch == 1 else "dlsim::k_wreduce_batch_table"
 
     def launch(self, k):
-        self.plans[k % self.sets].launch(self.stream)
+        self.plans[k % self.out_sets].launch(self.stream)
 
     def launch_probe(self, k):
-        self.probe_plans[k % self.sets].launch(self.stream)
+        self.probe_plans[k % len(self.probe_plans)].launch(self.stream)
 
 
 def xor_probe(wl, k_steps: int, sync, new_event, achieved_gbps: float):
@@ -381,13 +395,13 @@ def two_streams(wl, k_steps: int, sync, dev):
     a = wl.stream
     b = torch.cuda.Stream(dev)
     for k in range(10):
-        wl.plans[k % wl.sets].launch(a if k % 2 == 0 else b)
+        wl.plans[k % wl.out_sets].launch(a if k % 2 == 0 else b)
     sync()
     e0, e1, eb = (torch.cuda.Event(enable_timing=True) for _ in range(3))
     e0.record(a)
     b.wait_event(e0)
     for k in range(k_steps):
-        wl.plans[k % wl.sets].launch(a if k % 2 == 0 else b)
+        wl.plans[k % wl.out_sets].launch(a if k % 2 == 0 else b)
     eb.record(b)
     a.wait_event(eb)
     e1.record(a)
@@ -631,7 +645,9 @@ def run_rank(args, rank: int, world: int, local: int):
             "vs_baseline": None,
             "dtype": dtype,
             "data": f"synthetic: torch.randn*0.05 on device, {wl.sets} rotating input sets "
-                    f"(>= 1 GiB); {wkind} weights",
+                    f"(>= 1 GiB) into {wl.out_sets} rotating outputs "
+                    f"({wl.out_sets * wl.bytes_per_step // (n + 1) / 1e9:.2f} GB: none stays in the "
+                    f"256 MiB Infinity Cache); {wkind} weights",
             "config": {"workload": workload,
                        "backend": (backend_note or args.backend) if world > 1 else None,
                        "n_models": n, "params_total": p_cfg if strong or split > 1 else p * world,

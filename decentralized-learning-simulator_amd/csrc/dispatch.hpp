@@ -46,16 +46,21 @@ int batch_vpt(const size_t* nelem, int t0, int t1) {
   return mx * Op::kBytes < kBatchSmallBytes ? 1 : 4;
 }
 constexpr bool kNT = true;
-// Output stores are buffer_store_dwordx4 with sc1 (write-through): no dirty
-// output lines are left in L2 for the kernel-boundary writeback, which was
-// worth 3-4% per launch on the north star (profiles/r01_tune_store_*.log).
+// Output stores: buffer_store_dwordx4 with the nt bit (round 5). Rounds 1-4
+// shipped sc1 (write-through), measured with outputs that rotated over 3
+// buffers: those stay in the 256 MiB Infinity Cache, so their rewrites never
+// reached HBM. With outputs that do not stay there (the bench now rotates
+// >= 1 GiB of them, as a simulation's distinct aggregate outputs do) the nt
+// store is faster in every shipped shape: north star 64.2 against 67.1 us,
+// 2.8 M x 8 17.3 against 18.1, n = 17 at 11.2 M 126.0 against 130.9, bf16
+// n = 2 at 31 M 30.2 against 30.5 (profiles/r05j/).
 // The buffer's 32-bit byte offsets cap one launch's output at 2 GiB; longer
 // outputs are split into independent launches over element ranges.
-constexpr int kStore = 16;  // sc1
-// Per element type (profiles/r01_tune_*): fp32 takes sc1 write-through stores
-// and the wave-contiguous lane map (each wave sweeps 4 KiB per stream, +1.3%
-// on the north star); bf16, whose output is a third of the traffic in the
-// 2-way merge, keeps non-temporal stores (+2% there) and the block map.
+constexpr int kStore = 2;  // buffer store, nt
+// Per element type (profiles/r01_tune_*): fp32 takes the buffer stores and
+// the wave-contiguous lane map (each wave sweeps 4 KiB per stream, +1.3% on
+// the north star); bf16, whose output is a third of the traffic in the
+// 2-way merge, global non-temporal stores (+2% there) and the block map.
 // These are the policies of the grouped (runtime fan-in) kernel and of the
 // batched kernels.
 // fp64 elements take the fp32 shapes (a 16-byte vector is 4 VGPRs in both).
@@ -67,13 +72,15 @@ template <class Op> constexpr int group_size() { return Op::kBytes >= 4 ? 8 : 4;
 
 // Launch shape of the fixed fan-in kernels, chosen by the per-stream size
 // class (size sweeps with arena rows as in bench.py and >= 1 GiB of rotating
-// inputs: profiles/r01_tune_shape_sweep.log, profiles/r02_tune_slices/):
-//   fp32  < 2 M elements   : VPT 2, block map, sc1 (+7% at the 8-rank slice
+// inputs: profiles/r01_tune_shape_sweep.log, profiles/r02_tune_slices/; the
+// store policy re-chosen in round 5 with >= 1 GiB of rotating outputs,
+// profiles/r05j/; "kStore" = buffer store, nt):
+//   fp32  < 2 M elements   : VPT 2, block map, kStore (+7% at the 8-rank slice
 //                            of the north star, 1.4 M: 9.85 vs 10.57 us)
-//   fp32  2 M .. 5 M       : VPT 4, block map, sc1 (1-4% over the wave map)
-//   fp32 >= 5 M            : VPT 4, wave map,  sc1 (~1% at 6-11 M)
-//   bf16  < 48 M elements  : VPT 1, wave map, sc1  (+7-12% at 4-33 M for n = 2)
-//   bf16 >= 48 M           : VPT 4, block map, nt  (+1.5-2.5% at 64-125 M)
+//   fp32  2 M .. 5 M       : VPT 4, block map, kStore (1-4% over the wave map)
+//   fp32 >= 5 M            : VPT 4, wave map,  kStore (~1% at 6-11 M)
+//   bf16  < 48 M elements  : VPT 1, wave map, kStore (+7-12% at 4-33 M for n = 2)
+//   bf16 >= 48 M           : VPT 4, block map, global nt (+1.5-2.5% at 64-125 M)
 struct Shape {
   int vpt;
   int store;
@@ -136,11 +143,11 @@ hipError_t launch_shape(const S& s, int n, void* out, size_t nelem, hipStream_t 
 // Launch shape of the grouped (runtime fan-in, n > max_fixed_fan_in) kernel
 // by the same size classes (sweeps: profiles/r02_tune_grouped/, fp32 n = 17
 // and 100 at 11.2 M and at the 8-rank slice, 1.4 M; bf16 n = 17 and 12):
-//   4/8-byte  < 8 MB per stream : VPT 1, wave map,  sc1 (0.837 against 0.791
+//   4/8-byte  < 8 MB per stream : VPT 1, wave map,  kStore (0.837 against 0.791
 //                                 at n = 100, 0.646 against 0.595 at n = 17)
-//   4/8-byte  larger            : VPT 4, block map, sc1 (0.801 against 0.791
+//   4/8-byte  larger            : VPT 4, block map, kStore (0.801 against 0.791
 //                                 at n = 100 -- the memory-only probe's 0.802)
-//   2-byte    < 96 MB per stream: VPT 1, wave map,  sc1 (bf16 n = 17: 0.724
+//   2-byte    < 96 MB per stream: VPT 1, wave map,  kStore (bf16 n = 17: 0.724
 //                                 against 0.691 at 11.2 M, 0.400 against 0.309
 //                                 at 1.4 M)
 //   2-byte    larger            : VPT 4, block map, nt (0.771 at n = 12, 62.5 M)

@@ -467,6 +467,67 @@ int dlsim_host_wreduce(int n, int t, const void* const* h_srcs, const size_t* nu
   return ln.rc;
 }
 
+int dlsim_host_wreduce_zc(int n, int t, const void* const* h_srcs, const size_t* numels, const float* h_weights,
+                          void* h_staging, size_t row_stride, void* h_out, int dtype, int mode, int threads,
+                          void* stream) {
+  g_err.clear();
+  if (!known_dtype(dtype)) return dtype_fail(dtype);
+  if (mode != DLSIM_EXACT && mode != DLSIM_FAST) return fail(DLSIM_E_MODE, "unsupported mode %d", mode);
+  if (n < 1 || t < 0) return fail(DLSIM_E_ARG, "need n >= 1 and t >= 0 (got %d, %d)", n, t);
+  if (!h_weights || (t > 0 && (!h_srcs || !numels))) return fail(DLSIM_E_ARG, "null array argument");
+  const size_t esz = elem_bytes(dtype);
+  size_t total = 0;
+  for (int k = 0; k < t; ++k) total += numels[k];
+  if (total == 0) return DLSIM_OK;
+  if (!h_staging || !h_out) return fail(DLSIM_E_ARG, "null staging or output");
+  if (!aligned16(h_staging) || row_stride % 8 != 0)
+    return fail(DLSIM_E_ARG, "staging rows must be 16-B aligned with a stride that is a multiple of 8");
+  if (row_stride < total) return fail(DLSIM_E_ARG, "row_stride %zu < %zu elements", row_stride, total);
+  const size_t row_bytes = row_stride * esz;
+  {
+    const uintptr_t r0 = reinterpret_cast<uintptr_t>(h_staging), r1 = r0 + static_cast<size_t>(n) * row_bytes;
+    const uintptr_t o0 = reinterpret_cast<uintptr_t>(h_out), o1 = o0 + total * esz;
+    if (o0 < r1 && r0 < o1) return fail(DLSIM_E_ARG, "h_out overlaps the staging rows");
+  }
+  for (size_t j = 0; j < static_cast<size_t>(n) * t; ++j)
+    if (!h_srcs[j] && numels[j % t] > 0) return fail(DLSIM_E_ARG, "null source pointer at index %zu", j);
+  // The kernel reads the rows and writes the result over PCIe: both must be
+  // page-locked memory the device maps. Anything else would fault the GPU,
+  // so it is refused here, before any launch.
+  void* d_stage = nullptr;
+  void* d_res = nullptr;
+  if (hipHostGetDevicePointer(&d_stage, h_staging, 0) != hipSuccess || !d_stage) {
+    (void)hipGetLastError();
+    return fail(DLSIM_E_ARG, "h_staging is not page-locked host memory the device maps (hipHostMalloc)");
+  }
+  if (hipHostGetDevicePointer(&d_res, h_out, 0) != hipSuccess || !d_res) {
+    (void)hipGetLastError();
+    return fail(DLSIM_E_ARG, "h_out is not page-locked host memory the device maps (hipHostMalloc)");
+  }
+  char* stage = static_cast<char*>(h_staging);
+  // one unit per model: its tensors packed into its row
+  dlsim::PackJob job;
+  for (int i = 0; i < n; ++i) {
+    size_t off = 0;
+    for (int k = 0; k < t; ++k) {
+      if (numels[k] > 0)
+        job.add(static_cast<uint32_t>(i), static_cast<const char*>(h_srcs[static_cast<size_t>(i) * t + k]),
+                stage + i * row_bytes + off * esz, numels[k] * esz);
+      off += numels[k];
+    }
+  }
+  job.seal(static_cast<size_t>(n));
+  int rc = DLSIM_OK;
+  std::vector<const void*> ins(static_cast<size_t>(n));
+  for (int r = 0; r < n; ++r) ins[r] = static_cast<const char*>(d_stage) + r * row_bytes;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  pack_and_dispatch(job, threads, total * esz * n, [&](size_t, size_t u1) {
+    if (u1 == static_cast<size_t>(n) && rc == DLSIM_OK)
+      rc = dispatch(ins.data(), n, h_weights, d_res, total, dtype, mode, st);
+  });
+  return rc;
+}
+
 int dlsim_host_wreduce_resident(int n, int t, const void* const* h_srcs, const size_t* numels,
                                 const float* h_weights, const int* resident, void* const* d_rows, void* h_staging,
                                 size_t staging_stride, void* d_out, void* h_out, int dtype, int mode, int threads,

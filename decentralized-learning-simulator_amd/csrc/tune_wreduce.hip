@@ -127,17 +127,17 @@ __global__ __launch_bounds__(kBlock) void k_probe_rdonly(const Slots<128> s, voi
 
 // Write-only probe: the same tiles and sc1 buffer stores of the output, no
 // loads (the value is the vector index, so the stores cannot be merged away).
-template <int VPT>
+template <int VPT, int STP = 16>
 __global__ __launch_bounds__(kBlock) void k_probe_wronly(void* __restrict__ out, size_t nvec) {
   constexpr size_t kTile = static_cast<size_t>(kBlock) * VPT;
   const size_t t = blockIdx.x;
   if (t >= nvec / kTile) return;
-  const OutRef o = make_out<16>(out, nvec);
+  const OutRef o = make_out<STP>(out, nvec);
   const size_t v0 = t * kTile + (threadIdx.x >> 6) * 64 * VPT + (threadIdx.x & 63);
 #pragma unroll
   for (int v = 0; v < VPT; ++v) {
     const uint32_t k = static_cast<uint32_t>(v0 + v * 64);
-    store_vec<16>(o, v0 + v * 64, u32x4{k, k + 1, k + 2, k + 3});
+    store_vec<STP>(o, v0 + v * 64, u32x4{k, k + 1, k + 2, k + 3});
   }
 }
 
@@ -151,7 +151,7 @@ __global__ __launch_bounds__(kBlock) void k_probe_wronly(void* __restrict__ out,
 // is at least (ST-1)*NF loads (plus stores), so it is safe whether stores
 // retire in order with the loads or not. Full wave tiles only; the harness
 // sizes keep the ragged rest out of the comparison (the `same` column).
-template <class Op, int NF, int ST, int AUX, int WPB>
+template <class Op, int NF, int ST, int AUX, int WPB, int STP = 16>
 __global__ __launch_bounds__(64 * WPB) void k_wreduce_ldsring(const Slots<128> s, void* __restrict__ out,
                                                               size_t nvec) {
   __shared__ u32x4 ring[WPB][ST][NF][64];
@@ -160,7 +160,7 @@ __global__ __launch_bounds__(64 * WPB) void k_wreduce_ldsring(const Slots<128> s
   const size_t nwt = nvec / 64;  // full wave tiles
   const size_t gw = static_cast<size_t>(blockIdx.x) * WPB + wave;
   const size_t stride = static_cast<size_t>(gridDim.x) * WPB;
-  const OutRef o = make_out<16>(out, nvec);
+  const OutRef o = make_out<STP>(out, nvec);
   auto issue = [&](size_t wt, int slot) {
 #pragma unroll
     for (int i = 0; i < NF; ++i) {
@@ -194,7 +194,7 @@ __global__ __launch_bounds__(64 * WPB) void k_wreduce_ldsring(const Slots<128> s
     }
     // the slot is refilled by the next iteration's DMA: its reads must be done
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    store_vec<16>(o, wt * 64 + lane, pack<Op>(a[0], s.div));
+    store_vec<STP>(o, wt * 64 + lane, pack<Op>(a[0], s.div));
     slot = (slot + 1) % ST;
   }
 }
@@ -469,16 +469,16 @@ void launch_rdonly(const Slots<128>& s, int, void* out, size_t nvec, size_t, hip
   hipLaunchKernelGGL((k_probe_rdonly<NF, VPT>), dim3((unsigned)(nvec / ((size_t)kBlock * VPT))), dim3(kBlock), 0, st,
                      s, out, nvec);
 }
-template <int VPT>
+template <int VPT, int STP = 16>
 void launch_wronly(const Slots<128>&, int, void* out, size_t nvec, size_t, hipStream_t st, int) {
-  hipLaunchKernelGGL((k_probe_wronly<VPT>), dim3((unsigned)(nvec / ((size_t)kBlock * VPT))), dim3(kBlock), 0, st, out,
-                     nvec);
+  hipLaunchKernelGGL((k_probe_wronly<VPT, STP>), dim3((unsigned)(nvec / ((size_t)kBlock * VPT))), dim3(kBlock), 0, st,
+                     out, nvec);
 }
 // gm = blocks per CU of the persistent ring grid (256 CUs)
-template <class Op, int NF, int ST, int AUX, int WPB>
+template <class Op, int NF, int ST, int AUX, int WPB, int STP = 16>
 void launch_ring(const Slots<128>& s, int, void* out, size_t nvec, size_t, hipStream_t st, int gm) {
-  hipLaunchKernelGGL((k_wreduce_ldsring<Op, NF, ST, AUX, WPB>), dim3((unsigned)(gm * 256)), dim3(64 * WPB), 0, st, s,
-                     out, nvec);
+  hipLaunchKernelGGL((k_wreduce_ldsring<Op, NF, ST, AUX, WPB, STP>), dim3((unsigned)(gm * 256)), dim3(64 * WPB), 0, st,
+                     s, out, nvec);
 }
 
 // Round 5: small slices. A one-tile-per-block grid at
@@ -493,7 +493,7 @@ __device__ __forceinline__ void pipe_load(const Slots<128>& s, size_t v0, size_t
 #pragma unroll
   for (int i = 0; i < NF; ++i) load_tile<Op, VPT, 1, false, VS>(s.ptr(i), v0, nvec, r[i]);
 }
-template <class Op, int NF, int VPT, int VS>
+template <class Op, int NF, int VPT, int VS, int STP = 16>
 __device__ __forceinline__ void pipe_fold_store(const Slots<128>& s, const OutRef& o, size_t v0,
                                                 const u32x4 (&r)[NF][VPT]) {
   acc_t<Op> a[VPT][Op::E];
@@ -501,18 +501,18 @@ __device__ __forceinline__ void pipe_fold_store(const Slots<128>& s, const OutRe
 #pragma unroll
   for (int i = 0; i < NF; ++i) fold_tile<Op, VPT>(a, s.wt(i), r[i]);
 #pragma unroll
-  for (int v = 0; v < VPT; ++v) store_vec<16>(o, v0 + static_cast<size_t>(v) * VS, pack<Op>(a[v], s.divisor()));
+  for (int v = 0; v < VPT; ++v) store_vec<STP>(o, v0 + static_cast<size_t>(v) * VS, pack<Op>(a[v], s.divisor()));
 }
-template <class Op, int NF, int VPT, bool WM>
+template <class Op, int NF, int VPT, bool WM, int STP = 16>
 __global__ __launch_bounds__(kBlock) void k_tiles_pipe(const Slots<128> s, int n, void* __restrict__ out,
                                                        size_t nvec, size_t nelem) {
   constexpr size_t kTile = (size_t)kBlock * VPT;
   constexpr int VS = WM ? 64 : kBlock;
   const size_t full = nvec / kTile;
-  const OutRef o = make_out<16>(out, nvec);
+  const OutRef o = make_out<STP>(out, nvec);
   if (blockIdx.x == 0) {
     if (full * kTile < nvec)
-      reduce_tile<Op, Slots<128>, NF, 8, VPT, 1, true, 16>(s, n, o, full * kTile + threadIdx.x, nvec);
+      reduce_tile<Op, Slots<128>, NF, 8, VPT, 1, true, STP>(s, n, o, full * kTile + threadIdx.x, nvec);
     const size_t j = nvec * Op::E + threadIdx.x;
     if (j < nelem) fold_scalar<Op, Slots<128>>(s, n, out, j);
     return;
@@ -526,23 +526,23 @@ __global__ __launch_bounds__(kBlock) void k_tiles_pipe(const Slots<128> s, int n
   while (true) {
     size_t t2 = t + W;
     if (t2 < full) pipe_load<Op, NF, VPT, VS>(s, t2 * kTile + lo, nvec, rb);
-    pipe_fold_store<Op, NF, VPT, VS>(s, o, t * kTile + lo, ra);
+    pipe_fold_store<Op, NF, VPT, VS, STP>(s, o, t * kTile + lo, ra);
     if (t2 >= full) break;
     t = t2;
     t2 = t + W;
     if (t2 < full) pipe_load<Op, NF, VPT, VS>(s, t2 * kTile + lo, nvec, ra);
-    pipe_fold_store<Op, NF, VPT, VS>(s, o, t * kTile + lo, rb);
+    pipe_fold_store<Op, NF, VPT, VS, STP>(s, o, t * kTile + lo, rb);
     if (t2 >= full) break;
     t = t2;
   }
 }
 // gm > 0: 1 + gm*256 blocks; gm < 0: 1 + ceil(full / -gm) blocks (-gm tiles per block)
-template <class Op, int NF, int VPT, bool WM>
+template <class Op, int NF, int VPT, bool WM, int STP = 16>
 void launch_pipe(const Slots<128>& s, int n, void* out, size_t nvec, size_t nelem, hipStream_t st, int gm) {
   const size_t full = nvec / ((size_t)kBlock * VPT);
   size_t workers = gm > 0 ? (size_t)gm * 256 : (full + (size_t)(-gm) - 1) / (size_t)(-gm);
   workers = std::max<size_t>(1, std::min(workers, full));
-  hipLaunchKernelGGL((k_tiles_pipe<Op, NF, VPT, WM>), dim3((unsigned)(workers + 1)), dim3(kBlock), 0, st, s, n, out,
+  hipLaunchKernelGGL((k_tiles_pipe<Op, NF, VPT, WM, STP>), dim3((unsigned)(workers + 1)), dim3(kBlock), 0, st, s, n, out,
                      nvec, nelem);
 }
 // Balanced one-shot grid (round 5): B = 256*k blocks, block b owns the
@@ -585,6 +585,47 @@ void launch_bal(const Slots<128>& s, int n, void* out, size_t nvec, size_t nelem
     case 7: bal_go<Op, NF, 7>(s, n, out, nvec, nelem, st, B, lds); break;
     case 8: bal_go<Op, NF, 8>(s, n, out, nvec, nelem, st, B, lds); break;
     default: fprintf(stderr, "k_bal: %zu vectors per lane\n", vpt); exit(1);
+  }
+}
+
+// Round 5: the shipped shapes with sc1 (write-through) stores against
+// non-temporal buffer stores (nt = 2), for fixed fan-in 2 / 8 and the grouped
+// kernel, fp32 and bf16 (DLSIM_TUNE_NTSWEEP; run with DLSIM_TUNE_OUT_SETS so
+// the outputs do not stay in the Infinity Cache).
+template <class Op>
+void add_ntsweep(std::vector<Variant>& vs, int n) {
+  if constexpr (Op::kBytes >= 4) {
+    if (n == 8) {
+      vs.push_back({"NF8_V2_sc1_blk", launch_ts<Op, 8, 8, 2, 1, 16, false>, 0});
+      vs.push_back({"NF8_V2_bnt_blk", launch_ts<Op, 8, 8, 2, 1, 2, false>, 0});
+      vs.push_back({"NF8_V4_sc1_blk", launch_ts<Op, 8, 8, 4, 1, 16, false>, 0});
+      vs.push_back({"NF8_V4_bnt_blk", launch_ts<Op, 8, 8, 4, 1, 2, false>, 0});
+      vs.push_back({"NF8_V4_sc1_wave", launch_ts<Op, 8, 8, 4, 1, 16, true>, 0});
+      vs.push_back({"NF8_V4_bnt_wave", launch_ts<Op, 8, 8, 4, 1, 2, true>, 0});
+      vs.push_back({"NF8_V4_nt_wave", launch_ts<Op, 8, 8, 4, 1, kStNT, true>, 0});
+    } else if (n == 2) {
+      vs.push_back({"NF2_V2_sc1_blk", launch_ts<Op, 2, 8, 2, 1, 16, false>, 0});
+      vs.push_back({"NF2_V2_bnt_blk", launch_ts<Op, 2, 8, 2, 1, 2, false>, 0});
+      vs.push_back({"NF2_V4_sc1_wave", launch_ts<Op, 2, 8, 4, 1, 16, true>, 0});
+      vs.push_back({"NF2_V4_bnt_wave", launch_ts<Op, 2, 8, 4, 1, 2, true>, 0});
+    } else {
+      vs.push_back({"T_G8_V1_sc1_wave", launch_ts<Op, 0, 8, 1, 1, 16, true>, 0});
+      vs.push_back({"T_G8_V1_bnt_wave", launch_ts<Op, 0, 8, 1, 1, 2, true>, 0});
+      vs.push_back({"T_G8_V4_sc1_blk", launch_ts<Op, 0, 8, 4, 1, 16, false>, 0});
+      vs.push_back({"T_G8_V4_bnt_blk", launch_ts<Op, 0, 8, 4, 1, 2, false>, 0});
+    }
+  } else {
+    if (n == 2) {
+      vs.push_back({"NF2_V1_sc1_wave", launch_ts<Op, 2, 4, 1, 1, 16, true>, 0});
+      vs.push_back({"NF2_V1_bnt_wave", launch_ts<Op, 2, 4, 1, 1, 2, true>, 0});
+      vs.push_back({"NF2_V4_nt_blk", launch_ts<Op, 2, 4, 4, 1, kStNT, false>, 0});
+      vs.push_back({"NF2_V4_bnt_blk", launch_ts<Op, 2, 4, 4, 1, 2, false>, 0});
+      vs.push_back({"NF2_V4_sc1_blk", launch_ts<Op, 2, 4, 4, 1, 16, false>, 0});
+    } else {
+      vs.push_back({"T_G4_V1_sc1_wave", launch_ts<Op, 0, 4, 1, 1, 16, true>, 0});
+      vs.push_back({"T_G4_V1_bnt_wave", launch_ts<Op, 0, 4, 1, 1, 2, true>, 0});
+      vs.push_back({"T_G4_V4_nt_blk", launch_ts<Op, 0, 4, 4, 1, kStNT, false>, 0});
+    }
   }
 }
 
@@ -634,6 +675,37 @@ void add_r03(std::vector<Variant>& vs, int n) {
     vs.push_back({p + "_V4_sc1_wave_S16", launch_ts16<Op, NF, 8, 4, 1, 16, true>, 0});
     vs.push_back({p + "_V4_sc1_wave_dev", launch_tsdev<Op, NF, 8, 4, 1, 16, true>, 0});
     vs.push_back({p + "_V4_sc1_wave_b", launch_ts<Op, NF, 8, 4, 1, 16, true>, 0});
+    return;
+  }
+  if (getenv("DLSIM_TUNE_HONEST")) {  // round 5: shapes with nt buffer stores, outputs beyond the MALL
+    vs.push_back({p + "_V4_bnt_wave", launch_ts<Op, NF, 8, 4, 1, 2, true>, 0});
+    vs.push_back({p + "_V8_bnt_wave", launch_ts<Op, NF, 8, 8, 1, 2, true>, 0});
+    vs.push_back({p + "_V2_bnt_wave", launch_ts<Op, NF, 8, 2, 1, 2, true>, 0});
+    vs.push_back({p + "_V1_bnt_wave", launch_ts<Op, NF, 8, 1, 1, 2, true>, 0});
+    vs.push_back({p + "_V4_bnt_g2", launch_ts<Op, NF, 8, 4, 1, 2, true>, 2});
+    vs.push_back({p + "_V4_bnt_g4", launch_ts<Op, NF, 8, 4, 1, 2, true>, 4});
+    vs.push_back({p + "_pipe_V2w_bnt_g1", launch_pipe<Op, NF, 2, true, 2>, 1});
+    vs.push_back({p + "_pipe_V4w_bnt_g1", launch_pipe<Op, NF, 4, true, 2>, 1});
+    vs.push_back({p + "_pipe_V2w_bnt_g2", launch_pipe<Op, NF, 2, true, 2>, 2});
+    vs.push_back({p + "_ring_S3_nt_W4_g1_bnt", launch_ring<Op, NF, 3, 2, 4, 2>, 1});
+    vs.push_back({p + "_ring_S4_nt_W4_g1_bnt", launch_ring<Op, NF, 4, 2, 4, 2>, 1});
+    vs.push_back({p + "_rdonly_V4w", launch_rdonly<NF, 4>, 0, (double)NF / (NF + 1)});
+    vs.push_back({p + "_wronly_V4w_bnt", launch_wronly<4, 2>, 0, 1.0 / (NF + 1)});
+    vs.push_back({p + "_wronly_V4w_sc1", launch_wronly<4, 16>, 0, 1.0 / (NF + 1)});
+    return;
+  }
+  if (getenv("DLSIM_TUNE_STPOL")) {  // every buffer-store cache policy (round 5: outputs beyond the MALL)
+    vs.push_back({p + "_V4_sc1_wave", launch_ts<Op, NF, 8, 4, 1, 16, true>, 0});
+    vs.push_back({p + "_V4_nt_wave", launch_ts<Op, NF, 8, 4, 1, kStNT, true>, 0});
+    vs.push_back({p + "_V4_b0_wave", launch_ts<Op, NF, 8, 4, 1, 0, true>, 0});
+    vs.push_back({p + "_V4_bsc0_wave", launch_ts<Op, NF, 8, 4, 1, 1, true>, 0});
+    vs.push_back({p + "_V4_bnt_wave", launch_ts<Op, NF, 8, 4, 1, 2, true>, 0});
+    vs.push_back({p + "_V4_bsc0nt_wave", launch_ts<Op, NF, 8, 4, 1, 3, true>, 0});
+    vs.push_back({p + "_V4_bsc01_wave", launch_ts<Op, NF, 8, 4, 1, 17, true>, 0});
+    vs.push_back({p + "_V4_bsc1nt_wave", launch_ts<Op, NF, 8, 4, 1, 18, true>, 0});
+    vs.push_back({p + "_V4_bsc01nt_wave", launch_ts<Op, NF, 8, 4, 1, 19, true>, 0});
+    vs.push_back({p + "_V4_sc1_ldb_nt", launch_ts<Op, NF, 8, 4, kLdBuffer + 2, 16, true>, 0});
+    vs.push_back({p + "_V4_nt_ldb_nt", launch_ts<Op, NF, 8, 4, kLdBuffer + 2, kStNT, true>, 0});
     return;
   }
   if (getenv("DLSIM_TUNE_STORES")) {  // store policies and shapes on contiguous blocks (round 4)
@@ -792,7 +864,12 @@ int run(int n, size_t P, int reps, double peak_gbs) {
   printf("sets=%d footprint=%.0fMB\n", sets, sets * set_bytes / 1e6);
   const size_t nvec = P / Op::E;
   std::vector<void*> in((size_t)sets * n);
-  std::vector<void*> out(sets);
+  // DLSIM_TUNE_OUT_SETS=k: the outputs rotate over k buffers instead of one
+  // per input set (round 5: does the 256 MiB Infinity Cache hold a short
+  // rotation of outputs, so their writes never reach HBM?)
+  const int osets = getenv("DLSIM_TUNE_OUT_SETS") ? std::max(1, atoi(getenv("DLSIM_TUNE_OUT_SETS"))) : sets;
+  printf("out_sets=%d\n", osets);
+  std::vector<void*> out(osets);
   // Input layout experiment: DLSIM_TUNE_STAGGER unset = one hipMalloc per
   // input; set to S (bytes, multiple of 256) = all inputs rows of one arena,
   // row stride = bytes rounded up to 256 B, plus S more per row (S = 0 is the
@@ -820,8 +897,8 @@ int run(int n, size_t P, int reps, double peak_gbs) {
   // DLSIM_TUNE_OUT_OFFSET=B: each output starts B bytes past its (2 MiB
   // aligned) allocation
   const size_t out_off = getenv("DLSIM_TUNE_OUT_OFFSET") ? strtoull(getenv("DLSIM_TUNE_OUT_OFFSET"), nullptr, 10) & ~(size_t)15 : 0;
-  std::vector<void*> out_alloc(sets);
-  for (int k = 0; k < sets; ++k) {
+  std::vector<void*> out_alloc(osets);
+  for (int k = 0; k < osets; ++k) {
     if (getenv("DLSIM_TUNE_CONTIG"))
       CK(hipExtMallocWithFlags(&out_alloc[k], bytes + 256 + out_off, hipDeviceMallocContiguous));
     else
@@ -849,9 +926,11 @@ int run(int n, size_t P, int reps, double peak_gbs) {
   const double alg_bytes = (double)(n + 1) * bytes;
 
   const bool r03 = getenv("DLSIM_TUNE_R03") != nullptr || getenv("DLSIM_TUNE_LAYOUT") != nullptr ||
-                   getenv("DLSIM_TUNE_SMALL") != nullptr;
+                   getenv("DLSIM_TUNE_SMALL") != nullptr || getenv("DLSIM_TUNE_NTSWEEP") != nullptr;
   std::vector<Variant> vs;
-  if (getenv("DLSIM_TUNE_SMALL")) {
+  if (getenv("DLSIM_TUNE_NTSWEEP")) {
+    add_ntsweep<Op>(vs, n);
+  } else if (getenv("DLSIM_TUNE_SMALL")) {
     add_small<Op, 2>(vs, n);
     add_small<Op, 4>(vs, n);
     add_small<Op, 8>(vs, n);
@@ -903,10 +982,10 @@ int run(int n, size_t P, int reps, double peak_gbs) {
   std::vector<std::vector<double>> med(vs.size()), bat(vs.size());
   for (int r = 0; r < rounds; ++r) {
     for (size_t v = 0; v < vs.size(); ++v) {
-      for (int w = 0; w < 10; ++w) vs[v].launch(slots[w % sets], n, out[w % sets], nvec, P, st, vs[v].gm);
+      for (int w = 0; w < 10; ++w) vs[v].launch(slots[w % sets], n, out[w % osets], nvec, P, st, vs[v].gm);
       for (int k = 0; k < reps; ++k) {
         CK(hipEventRecord(ev[2 * k], st));
-        vs[v].launch(slots[k % sets], n, out[k % sets], nvec, P, st, vs[v].gm);
+        vs[v].launch(slots[k % sets], n, out[k % osets], nvec, P, st, vs[v].gm);
         CK(hipEventRecord(ev[2 * k + 1], st));
       }
       CK(hipStreamSynchronize(st));
@@ -920,7 +999,7 @@ int run(int n, size_t P, int reps, double peak_gbs) {
       med[v].push_back(t[reps / 2]);
       // batch: one event pair around `reps` back-to-back launches
       CK(hipEventRecord(ev[0], st));
-      for (int k = 0; k < reps; ++k) vs[v].launch(slots[k % sets], n, out[k % sets], nvec, P, st, vs[v].gm);
+      for (int k = 0; k < reps; ++k) vs[v].launch(slots[k % sets], n, out[k % osets], nvec, P, st, vs[v].gm);
       CK(hipEventRecord(ev[1], st));
       CK(hipEventSynchronize(ev[1]));
       float bms;

@@ -58,6 +58,7 @@ EXPORTS = (
     "dlsim_sharded_plan_run_f64",
     "dlsim_sharded_plan_destroy",
     "dlsim_host_wreduce",
+    "dlsim_host_wreduce_zc",
     "dlsim_host_wreduce_resident",
     "dlsim_host_chunk_mean",
     "dlsim_host_pack",
@@ -146,6 +147,9 @@ def load() -> ctypes.CDLL:
                                            ctypes.POINTER(ctypes.c_float), vp, vp, sz, vp, vp, i, i, sz, i,
                                            vp, vp, vp]
         lib.dlsim_host_wreduce.restype = i
+        lib.dlsim_host_wreduce_zc.argtypes = [i, i, ctypes.POINTER(vp), ctypes.POINTER(sz),
+                                              ctypes.POINTER(ctypes.c_float), vp, sz, vp, i, i, i, vp]
+        lib.dlsim_host_wreduce_zc.restype = i
         lib.dlsim_host_wreduce_resident.argtypes = [i, i, ctypes.POINTER(vp), ctypes.POINTER(sz),
                                                     ctypes.POINTER(ctypes.c_float), ctypes.POINTER(i),
                                                     ctypes.POINTER(vp), vp, sz, vp, vp, i, i, i, vp]
@@ -921,6 +925,22 @@ def host_wreduce_raw(src_ptrs: Sequence[int], n: int, numels: Sequence[int], wei
         stream_handle, None if h2d_stream is None else h2d_stream.cuda_stream,
         None if d2h_stream is None else d2h_stream.cuda_stream)
     _check("dlsim_host_wreduce", rc)
+
+
+def host_wreduce_zc_raw(src_ptrs: Sequence[int], n: int, numels: Sequence[int], weights_f32, staging, host_out,
+                        dtype: int, mode: int, threads: int, stream_handle) -> None:
+    """dlsim_host_wreduce_zc on host pointers the caller has validated (the
+    arena path): `staging` a page-locked [n, stride] row buffer, `host_out` a
+    page-locked result; the reduce reads and writes them over PCIe."""
+    if staging.is_cuda or host_out.is_cuda or staging.dim() != 2:
+        raise ValueError("staging: a page-locked [n, >= total] host buffer; host_out: a page-locked host tensor")
+    t = len(numels)
+    w = np.ascontiguousarray(weights_f32, dtype=np.float32)
+    rc = load().dlsim_host_wreduce_zc(
+        n, t, (ctypes.c_void_p * len(src_ptrs))(*src_ptrs), (ctypes.c_size_t * t)(*numels),
+        w.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), staging.data_ptr(), staging.stride(0),
+        host_out.data_ptr(), dtype, mode, threads, stream_handle)
+    _check("dlsim_host_wreduce_zc", rc)
 
 
 def host_wreduce_resident_raw(src_ptrs: Sequence[int], n: int, numels: Sequence[int], weights_f32,

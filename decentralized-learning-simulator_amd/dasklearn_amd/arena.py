@@ -592,6 +592,61 @@ def pipeline_chunk_elems(total: int, esz: int) -> int:
 # memory (the runtime stages that copy, and the library call waits for it).
 PAGEABLE_RESULT_BYTES = 4 << 20
 HOST_RESULT_PINNED = os.environ.get("DLSIM_HOST_RESULT", "pinned") != "pageable"
+# torch's caching host allocator never gives page-locked memory back to the
+# OS and rounds blocks up to powers of two, so a caller that keeps many small
+# results alive (an in-process simulation holding one model per peer) would
+# pin up to twice their bytes. Once the allocator holds more than
+# this many page-locked bytes, small results come back in pageable memory
+# (round 3's rule: a synchronous D2H); large ones stay page-locked.
+# DLSIM_PINNED_RESULT_BUDGET_MB overrides the 2 GiB.
+PINNED_RESULT_BUDGET = int(float(os.environ.get("DLSIM_PINNED_RESULT_BUDGET_MB", "2048")) * (1 << 20))
+
+
+class _PinnedBudget:
+    """Whether small host results may still be page-locked: the caching host
+    allocator's reserved bytes against PINNED_RESULT_BUDGET, read every
+    CHECK_EVERY small results (reading the statistics costs microseconds)."""
+    CHECK_EVERY = 32
+
+    def __init__(self):
+        self.calls = 0
+        self.over = False
+
+    @staticmethod
+    def reserved() -> int:
+        st = torch.cuda.memory.host_memory_stats()  # flat: "reserved_bytes.current", ...
+        return int(st.get("reserved_bytes.current", st.get("allocated_bytes.current", 0)))
+
+    def allow(self) -> bool:
+        if self.calls % self.CHECK_EVERY == 0:
+            try:
+                self.over = self.reserved() > PINNED_RESULT_BUDGET
+            except (AttributeError, RuntimeError, TypeError, ValueError):
+                self.over = False
+        self.calls += 1
+        return not self.over
+
+
+PINNED_BUDGET = _PinnedBudget()
+
+
+def pinned_result(nbytes: int) -> bool:
+    """Whether a host result of nbytes comes back page-locked (see above)."""
+    if nbytes >= PAGEABLE_RESULT_BYTES:
+        return True
+    return HOST_RESULT_PINNED and PINNED_BUDGET.allow()
+
+
+# Zero-copy host tasks (round 5; VERDICT r04 next #5, DESIGN.md §6e): host
+# models of at most ZC_MAX_BYTES of staged rows whose result goes back to the
+# host are packed into page-locked rows that the reduce kernel reads in place
+# over PCIe, and the kernel writes the page-locked result: no H2D and no D2H
+# DMA (dlsim_host_wreduce_zc). 2 x GNLeNet: the library call with its wait
+# 81 -> 63 us (profiles/r05d/zero_copy.json). DLSIM_ZERO_COPY=0 turns it off,
+# DLSIM_ZC_MAX_KB moves the 4 MiB.
+ZERO_COPY = os.environ.get("DLSIM_ZERO_COPY", "1") != "0"
+ZC_MAX_BYTES = int(float(os.environ.get("DLSIM_ZC_MAX_KB", "4096")) * 1024)
+ZC_CALLS = [0]  # zero-copy dtype groups reduced (tests and probes)
 
 
 def _host_pipeline(all_params, idx, layout, dt, dev, out, weights_f32, mode, stream, want_host, defer=False):
@@ -611,23 +666,39 @@ def _host_pipeline(all_params, idx, layout, dt, dev, out, weights_f32, mode, str
     result; otherwise this call has waited)."""
     n = len(all_params)
     total = layout.totals[dt]
-    esz = out.element_size()
-    chunk = pipeline_chunk_elems(total, esz)
-    h2d, d2h = _side_streams(dev) if chunk else (None, None)
+    esz = _elem_size(dt)
     host = None
-    pinned_result = want_host and (HOST_RESULT_PINNED or total * esz >= PAGEABLE_RESULT_BYTES)
+    pinned_out = want_host and pinned_result(total * esz)
     if want_host:
-        host = torch.empty(total, dtype=dt, pin_memory=pinned_result)
+        host = torch.empty(total, dtype=dt, pin_memory=pinned_out)
     # the layout checked every tensor's shape and dtype against models[0];
     # the library reads data pointers, so only non-contiguous ones are copied
     keep, ptrs = _data_ptrs(all_params, idx)
+    if out is None:  # the zero-copy form (reduce_modules_to_arenas chose it)
+        if pinned_out:
+            ZC_CALLS[0] += 1
+            _, rows = STAGING.acquire(dev, dt, n, total, stream, device_rows=False)
+            synced = False
+            try:
+                _native.host_wreduce_zc_raw(ptrs, n, layout.split_sizes[dt], weights_f32, rows, host,
+                                            _native.dtype_code(dt), mode, torch.get_num_threads(),
+                                            stream.cuda_stream)
+                if not defer:
+                    stream.synchronize()
+                    synced = True
+            finally:
+                STAGING.release(dev, dt, stream, synced, device_rows=False)
+            return host, bool(keep), not synced
+        out = arena_empty(total, dt, dev)  # past the page-locked budget: the DMA pipeline
+    chunk = pipeline_chunk_elems(total, esz)
+    h2d, d2h = _side_streams(dev) if chunk else (None, None)
     dev_rows, pinned = STAGING.acquire(dev, dt, n, total, stream)
     synced = False
     try:
         _native.host_wreduce_raw(ptrs, n, layout.split_sizes[dt], weights_f32, pinned, dev_rows, out, host,
                                  _native.dtype_code(dt), mode, chunk, torch.get_num_threads(), stream.cuda_stream,
                                  h2d, d2h)
-        if want_host and not (defer and pinned_result):
+        if want_host and not (defer and pinned_out):
             # the host result is complete once `stream` is: wait here, and
             # hand the rows back free
             stream.synchronize()
@@ -686,8 +757,8 @@ def _cached_host_reduce(cache, all_params, idx, layout, dt, dev, out, weights_f3
                     keep, mp = _data_ptrs([all_params[i] for i in miss], idx)
                     for j, i in enumerate(miss):
                         src[i * t:(i + 1) * t] = mp[j * t:(j + 1) * t]
-            pinned_result = HOST_RESULT_PINNED or total * esz >= PAGEABLE_RESULT_BYTES
-            host = torch.empty(total, dtype=dt, pin_memory=pinned_result)
+            pinned_out = pinned_result(total * esz)
+            host = torch.empty(total, dtype=dt, pin_memory=pinned_out)
             pinned = None
             if miss:
                 # pinned rows for all n models, of which the misses use the
@@ -701,7 +772,7 @@ def _cached_host_reduce(cache, all_params, idx, layout, dt, dev, out, weights_f3
                                               rows, pinned, out, host,
                                               _native.dtype_code(dt), mode, torch.get_num_threads(),
                                               stream.cuda_stream)
-            if not (defer and pinned_result):
+            if not (defer and pinned_out):
                 stream.synchronize()
                 synced = True
         except BaseException:
@@ -800,7 +871,11 @@ def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, m
             f64 = dt == torch.float64
             w = (_native.f64_weights(weights_f64) if weights_f64 is not None else weights_f32.astype(np.float64)) \
                 if f64 else weights_f32
-            out = arena_empty(total, dt, dev)
+            # small host models whose result goes back to the host: no device
+            # output (dlsim_host_wreduce_zc writes the page-locked result)
+            zc = piped and not f64 and ZERO_COPY and n * total * _elem_size(dt) <= ZC_MAX_BYTES \
+                and device_cache.active() is None
+            out = None if zc and total else arena_empty(total, dt, dev)
             outs[dt] = out
             if total == 0:
                 if piped:
@@ -867,12 +942,13 @@ def reduce_modules_to_arenas(models: List[nn.Module], weights_f32: np.ndarray, m
 
 def arenas_to_host(arenas: Dict[torch.dtype, torch.Tensor], stream) -> Dict[torch.dtype, torch.Tensor]:
     """D2H into page-locked memory from torch's caching host allocator (the
-    block returns to the cache when the returned module is freed), then wait
-    for the copies: the output module may be used as soon as this returns."""
+    block returns to the cache when the returned module is freed; small
+    results in pageable memory past PINNED_RESULT_BUDGET), then wait for the
+    copies: the output module may be used as soon as this returns."""
     host = {}
     with torch.cuda.stream(stream):
         for dt, a in arenas.items():
-            h = torch.empty(a.numel(), dtype=dt, pin_memory=True)
+            h = torch.empty(a.numel(), dtype=dt, pin_memory=pinned_result(a.numel() * a.element_size()))
             h.copy_(a, non_blocking=True)
             host[dt] = h
     stream.synchronize()

@@ -261,6 +261,12 @@ int dlsim_rccl_bind(const char* librccl_path);
  * an RCCL communicator (one process per GPU, xGMI). SURVEY.md §8b's
  * `dlsim_wreduce_sharded(..., rcclComm)`; no reference counterpart (the
  * reference is single-process CPU, fedavg.py:12-26).
+ * COST: every call agrees with its peers first (an all-reduce read back by
+ * the host), so every call is a host round trip (81 us at W = 2 on the stub
+ * communicator against 12 us for a plan run). For repeated
+ * aggregates of one shape -- the steady state of a simulation -- create a
+ * plan once (dlsim_sharded_plan_create, below) and run it
+ * (dlsim_sharded_plan_run): stream-ordered, no agreement, no host wait.
  *   rank r of W (from the communicator) owns elements [b_r, e_r) =
  *   dlsim_shard_range(n_elems, W, r, 64); d_slices[i] points at that slice of
  *   model i (slice_elems elements, which must equal e_r - b_r, else
@@ -376,6 +382,25 @@ int dlsim_host_wreduce(int n, int t, const void* const* h_srcs, const size_t* nu
                        const float* h_weights, void* h_staging, void* d_rows, size_t row_stride,
                        void* d_out, void* h_out, int dtype, int mode, size_t chunk_elems, int threads,
                        void* stream, void* h2d_stream, void* d2h_stream);
+
+/*
+ * dlsim_host_wreduce_zc — dlsim_host_wreduce for SMALL host models with no
+ * DMA in either direction (round 5): the models are
+ * packed into page-locked staging rows on `threads` host threads as above,
+ * then the reduce kernel reads those rows in place over PCIe and writes the
+ * result straight into h_out. h_staging (n rows of row_stride elements,
+ * 16-B aligned, row_stride a multiple of 8 and >= sum(numels)) and h_out
+ * (sum(numels) elements) must be page-locked memory the device maps
+ * (hipHostMalloc, torch's pin_memory); anything else is refused with
+ * DLSIM_E_ARG before any launch. One launch after the pack; returns after
+ * queueing it: synchronise `stream` before reading h_out or reusing the rows.
+ * Results are bit-identical to dlsim_wreduce over the packed rows. For a
+ * 2 x GNLeNet task (683 KB of rows) the kernel's PCIe reads cost less than
+ * the two DMAs' setup; larger models take dlsim_host_wreduce.
+ */
+int dlsim_host_wreduce_zc(int n, int t, const void* const* h_srcs, const size_t* numels, const float* h_weights,
+                          void* h_staging, size_t row_stride, void* h_out, int dtype, int mode, int threads,
+                          void* stream);
 
 /*
  * dlsim_host_wreduce_resident — dlsim_host_wreduce when some models are

@@ -215,6 +215,24 @@ def test_host_result_placement_and_stage_timing_works():
         assert orc.same_bits(flat_of(out), g["expected"])
     finally:
         arena.HOST_RESULT_PINNED = saved
+    # past the page-locked budget small results come back pageable,
+    # device-model results copied to the host too; exact either way
+    saved_budget = arena.PINNED_RESULT_BUDGET
+    arena.PINNED_RESULT_BUDGET = 0
+    arena.PINNED_BUDGET.calls = 0  # re-read the allocator's statistics now
+    try:
+        out = aggregate_modules(models, None, _native.DLSIM_EXACT)
+        assert not next(out.parameters()).is_pinned()
+        assert orc.same_bits(flat_of(out), g["expected"])
+        dev_models = [m.cuda() for m in modules_from_golden(g)]
+        out = aggregate_modules(dev_models, None, _native.DLSIM_EXACT, to_host=True)
+        assert not next(out.parameters()).is_cuda and not next(out.parameters()).is_pinned()
+        assert orc.same_bits(flat_of(out), g["expected"])
+    finally:
+        arena.PINNED_RESULT_BUDGET = saved_budget
+        arena.PINNED_BUDGET.calls = 0
+    out = aggregate_modules(models, None, _native.DLSIM_EXACT)
+    assert next(out.parameters()).is_pinned()
     torch.manual_seed(9)
     big = [Ragged([(arena.PAGEABLE_RESULT_BYTES // 4 + 1000,), (77,)]) for _ in range(3)]
     with torch.no_grad():
@@ -393,3 +411,72 @@ def test_non_contiguous_parameters_keep_models0_strides(where):
         assert pa.shape == pb.shape and pa.stride() == pb.stride(), (na, pa.stride(), pb.stride())
         assert pa.is_cuda == (where == "device")
         assert torch.equal(pa.detach().cpu().contiguous().view(torch.int32), pb.detach().contiguous().view(torch.int32)), na
+
+
+def test_zero_copy_small_host_tasks():
+    """Round 5: small host models with a host result
+    take dlsim_host_wreduce_zc (the kernel reads the page-locked rows and
+    writes the page-locked result over PCIe, no DMA): bit-exact against the
+    reference's fixtures, fp32 / bf16 / fp16, one to many models, a
+    non-contiguous parameter; larger models, DLSIM_ZERO_COPY=0 and device
+    results keep the DMA pipeline; the C entry refuses pageable memory
+    before any launch."""
+    from dasklearn_amd import _native, arena
+    from dasklearn_amd.arena import aggregate_modules
+    before = arena.ZC_CALLS[0]
+    for name in ("cfg1_gnlenet_f32_n2_none", "cfg2_gnlenet_f32_n8_none",  # 17 x GNLeNet: 5.8 MB, the DMAs
+                 "ragged_bf16_n3_list", "ragged_bf16_n17_list", "ragged_f32_n100_list"):
+        g = load_golden(os.path.join(GOLDEN, name + ".npz"))
+        models = modules_from_golden(g)
+        calls = arena.ZC_CALLS[0]
+        out = aggregate_modules(models, g["weights_arg"], _native.DLSIM_EXACT)
+        assert arena.ZC_CALLS[0] == calls + 1, name
+        p0 = next(out.parameters())
+        assert not p0.is_cuda and p0.is_pinned()
+        assert orc.same_bits(flat_of(out), g["expected"]), name
+    # a transposed (non-contiguous) parameter: copied, then packed
+    torch.manual_seed(21)
+    ms = [torch.nn.Linear(40, 30) for _ in range(3)]
+    for m in ms:
+        m.weight.data = m.weight.data.t().contiguous().t()
+    out = aggregate_modules(ms, [0.5, 0.25, 0.25], _native.DLSIM_EXACT)
+    exp = orc.wreduce([np.concatenate([m.weight.detach().numpy().ravel(), m.bias.detach().numpy()]) for m in ms],
+                      orc.reference_weights(3, [0.5, 0.25, 0.25]), "f32")
+    got = np.concatenate([out.weight.detach().contiguous().numpy().ravel(), out.bias.detach().numpy()])
+    assert orc.same_bits(got, exp)
+    assert arena.ZC_CALLS[0] > before
+    # off switch and size limit: the DMA pipeline, same bits
+    g = load_golden(os.path.join(GOLDEN, "cfg1_gnlenet_f32_n2_none.npz"))
+    models = modules_from_golden(g)
+    for attr, val in (("ZERO_COPY", False), ("ZC_MAX_BYTES", 1000)):
+        saved = getattr(arena, attr)
+        setattr(arena, attr, val)
+        try:
+            calls = arena.ZC_CALLS[0]
+            out = aggregate_modules(models, None, _native.DLSIM_EXACT)
+            assert arena.ZC_CALLS[0] == calls
+            assert orc.same_bits(flat_of(out), g["expected"])
+        finally:
+            setattr(arena, attr, saved)
+    # the C entry refuses memory the device does not map (no launch, no fault)
+    lib = _native.load()
+    import ctypes
+    src = torch.randn(64)
+    pinned = torch.empty(2, 64, pin_memory=True)
+    pageable = torch.empty(2, 64)
+    res_pinned = torch.empty(64, pin_memory=True)
+    srcs = (ctypes.c_void_p * 2)(src.data_ptr(), src.data_ptr())
+    numels = (ctypes.c_size_t * 1)(64)
+    w = (ctypes.c_float * 2)(0.5, 0.5)
+    for stage, res in ((pageable, res_pinned), (pinned, torch.empty(64))):
+        rc = lib.dlsim_host_wreduce_zc(2, 1, srcs, numels, w, stage.data_ptr(), 64, res.data_ptr(),
+                                       _native.DLSIM_F32, _native.DLSIM_EXACT, 1,
+                                       torch.cuda.current_stream().cuda_stream)
+        assert rc == _native.DLSIM_E_ARG, rc
+        assert b"page-locked" in lib.dlsim_last_error()
+    rc = lib.dlsim_host_wreduce_zc(2, 1, srcs, numels, w, pinned.data_ptr(), 64, res_pinned.data_ptr(),
+                                   _native.DLSIM_F32, _native.DLSIM_EXACT, 1, torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert orc.same_bits(res_pinned.numpy(), orc.wreduce([src.numpy(), src.numpy()],
+                                                         orc.reference_weights(2, [0.5, 0.5]), "f32"))

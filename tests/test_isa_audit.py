@@ -47,10 +47,11 @@ def test_audit_sees_the_round2_shapes():
     for co in audit_isa.code_objects(audit_isa.LIB):
         names |= set(audit_isa.kernels(audit_isa.disassemble(co)))
     exact = [n for n in names if "8F32Exact" in n and "k_wreduce_tiles" in n]
-    # template args <Op, S, NF, G, VPT, NT, STP, WAVE>: ...ELi<VPT>ELi1ELi16ELb<wave>E
-    assert any("ELi2ELi1ELi16ELb0E" in n for n in exact), "fixed VPT 2 block map missing"
-    assert any("ELi0ELi8ELi1ELi1ELi16ELb1E" in n for n in exact), "grouped VPT 1 wave map missing"
-    assert any("ELi4ELi1ELi16ELb1E" in n for n in exact), "VPT 4 wave map missing"
+    # template args <Op, S, NF, G, VPT, NT, STP, WAVE>: ...ELi<VPT>ELi1ELi<STP>ELb<wave>E,
+    # STP = 2 (buffer store, nt; round 5)
+    assert any("ELi2ELi1ELi2ELb0E" in n for n in exact), "fixed VPT 2 block map missing"
+    assert any("ELi0ELi8ELi1ELi1ELi2ELb1E" in n for n in exact), "grouped VPT 1 wave map missing"
+    assert any("ELi4ELi1ELi2ELb1E" in n for n in exact), "VPT 4 wave map missing"
 
 
 def test_detector_catches_contraction(report):

@@ -132,3 +132,25 @@ def test_arena_empty_routes_by_size_and_device():
     big = arena.arena_empty(N, torch.float32, "cpu")  # host arenas never use the pool
     assert small.numel() == 1000 and big.numel() == N and not big.is_cuda
     assert arena.OUT_POOL_MIN == 4 << 20 or os.environ.get("DLSIM_OUT_POOL_MIN_MB")
+
+
+def test_pinned_result_budget(monkeypatch):
+    """small host results are page-locked until torch's caching
+    host allocator holds more than PINNED_RESULT_BUDGET; the statistics are
+    read every CHECK_EVERY small results; large results stay page-locked."""
+    b = arena._PinnedBudget()
+    reserved = {"v": 0}
+    monkeypatch.setattr(arena._PinnedBudget, "reserved", staticmethod(lambda: reserved["v"]))
+    monkeypatch.setattr(arena, "PINNED_BUDGET", b)
+    monkeypatch.setattr(arena, "PINNED_RESULT_BUDGET", 100)
+    monkeypatch.setattr(arena, "HOST_RESULT_PINNED", True)
+    assert arena.pinned_result(1000)
+    reserved["v"] = 101
+    for _ in range(b.CHECK_EVERY - 1):  # not re-read yet
+        assert arena.pinned_result(1000)
+    assert not arena.pinned_result(1000)  # re-read: over the budget
+    assert arena.pinned_result(arena.PAGEABLE_RESULT_BYTES)  # large: always
+    monkeypatch.setattr(arena, "HOST_RESULT_PINNED", False)
+    reserved["v"] = 0
+    b.calls = 0
+    assert not arena.pinned_result(1000)  # DLSIM_HOST_RESULT=pageable
