@@ -598,7 +598,7 @@ HOST_RESULT_PINNED = os.environ.get("DLSIM_HOST_RESULT", "pinned") != "pageable"
 # pin up to twice their bytes. Once the allocator holds more than
 # this many page-locked bytes, small results come back in pageable memory
 # (round 3's rule: a synchronous D2H); large ones stay page-locked.
-# DLSIM_PINNED_RESULT_BUDGET_MB overrides the 2 GiB (INTEGRATION.md §4).
+# DLSIM_PINNED_RESULT_BUDGET_MB overrides the 2 GiB (INTEGRATION.md §3).
 PINNED_RESULT_BUDGET = int(float(os.environ.get("DLSIM_PINNED_RESULT_BUDGET_MB", "2048")) * (1 << 20))
 
 
