@@ -588,6 +588,78 @@ void launch_bal(const Slots<128>& s, int n, void* out, size_t nvec, size_t nelem
   }
 }
 
+// Round 5: deferred stores. With the outputs beyond the Infinity Cache the
+// reduce runs at a copy's rate (6.3 TB/s) while its eight read streams alone
+// reach 0.84 of peak: the read/write turnaround costs ~8 %. Here every block
+// folds R tiles (256 vectors each) and keeps the R packed results in
+// registers, then stores them all at the end: with one residency wave of
+// blocks (R chosen so the grid fits the chip) the whole chip reads first and
+// writes last, so HBM turns around far less often. U tiles' loads are issued
+// together. Same fold order as reduce_tile: bit-exact.
+template <class Op, int NF, int R, int U, int STP, bool CHECK>
+__device__ __forceinline__ void defer_body(const Slots<128>& s, const OutRef& o, size_t base, size_t nvec) {
+  u32x4 res[R];
+#pragma unroll
+  for (int r0 = 0; r0 < R; r0 += U) {
+    u32x4 x[NF][U];
+#pragma unroll
+    for (int i = 0; i < NF; ++i)
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const size_t v = base + static_cast<size_t>(r0 + u) * kBlock;
+        if constexpr (CHECK) {
+          x[i][u] = u32x4{0u, 0u, 0u, 0u};
+          if (v < nvec) x[i][u] = ld16<1>(s.p[i], v);
+        } else {
+          x[i][u] = ld16<1>(s.p[i], v);
+        }
+      }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      acc_t<Op> a[1][Op::E];
+      u32x4 r0v[1] = {x[0][u]};
+      init_tile<Op, 1>(a, r0v, false);
+#pragma unroll
+      for (int i = 0; i < NF; ++i) {
+        u32x4 ri[1] = {x[i][u]};
+        fold_tile<Op, 1>(a, s.w[i], ri);
+      }
+      res[r0 + u] = pack<Op>(a[0], s.div);
+    }
+    // keep the next group's loads behind this fold: hoisting every group's
+    // loads to the top would need NF * R vector registers and spill
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const size_t v = base + static_cast<size_t>(r) * kBlock;
+    if (!CHECK || v < nvec) store_vec<STP>(o, v, res[r]);
+  }
+}
+template <class Op, int NF, int R, int U, int STP>
+__global__ __launch_bounds__(kBlock, 2) void k_defer(const Slots<128> s, int n, void* __restrict__ out, size_t nvec,
+                                                     size_t nelem) {
+  const size_t base = static_cast<size_t>(blockIdx.x) * kBlock * R + threadIdx.x;
+  const OutRef o = make_out<STP>(out, nvec);
+  if (static_cast<size_t>(blockIdx.x + 1) * kBlock * R <= nvec) {
+    defer_body<Op, NF, R, U, STP, false>(s, o, base, nvec);
+  } else {  // the last, partial block: tile by tile with bounds checks
+    for (int r = 0; r < R; ++r)
+      reduce_tile<Op, Slots<128>, NF, 8, 1, 1, true, STP>(s, n, o, base + static_cast<size_t>(r) * kBlock, nvec);
+  }
+  if (blockIdx.x == 0) {
+    const size_t j = nvec * Op::E + threadIdx.x;
+    if (j < nelem) fold_scalar<Op, Slots<128>>(s, n, out, j);
+  }
+}
+template <class Op, int NF, int R, int U, int STP>
+void launch_defer(const Slots<128>& s, int n, void* out, size_t nvec, size_t nelem, hipStream_t st, int) {
+  const size_t per = static_cast<size_t>(kBlock) * R;
+  hipLaunchKernelGGL((k_defer<Op, NF, R, U, STP>), dim3((unsigned)((nvec + per - 1) / per)), dim3(kBlock), 0, st, s,
+                     n, out, nvec, nelem);
+}
+
 // Round 5: the shipped shapes with sc1 (write-through) stores against
 // non-temporal buffer stores (nt = 2), for fixed fan-in 2 / 8 and the grouped
 // kernel, fp32 and bf16 (DLSIM_TUNE_NTSWEEP; run with DLSIM_TUNE_OUT_SETS so
@@ -675,6 +747,19 @@ void add_r03(std::vector<Variant>& vs, int n) {
     vs.push_back({p + "_V4_sc1_wave_S16", launch_ts16<Op, NF, 8, 4, 1, 16, true>, 0});
     vs.push_back({p + "_V4_sc1_wave_dev", launch_tsdev<Op, NF, 8, 4, 1, 16, true>, 0});
     vs.push_back({p + "_V4_sc1_wave_b", launch_ts<Op, NF, 8, 4, 1, 16, true>, 0});
+    return;
+  }
+  if (getenv("DLSIM_TUNE_DEFER")) {  // round 5: deferred stores (k_defer), outputs beyond the MALL
+    vs.push_back({p + "_V4_bnt_wave", launch_ts<Op, NF, 8, 4, 1, 2, true>, 0});
+    vs.push_back({p + "_defer_R22_U1", launch_defer<Op, NF, 22, 1, 2>, 0});
+    vs.push_back({p + "_defer_R22_U2", launch_defer<Op, NF, 22, 2, 2>, 0});
+    vs.push_back({p + "_defer_R24_U4", launch_defer<Op, NF, 24, 4, 2>, 0});
+    vs.push_back({p + "_defer_R16_U2", launch_defer<Op, NF, 16, 2, 2>, 0});
+    vs.push_back({p + "_defer_R11_U1", launch_defer<Op, NF, 11, 1, 2>, 0});
+    vs.push_back({p + "_defer_R11_U1_sc1", launch_defer<Op, NF, 11, 1, 16>, 0});
+    vs.push_back({p + "_defer_R8_U2", launch_defer<Op, NF, 8, 2, 2>, 0});
+    vs.push_back({p + "_defer_R44_U1", launch_defer<Op, NF, 44, 1, 2>, 0});
+    vs.push_back({p + "_rdonly_V4w", launch_rdonly<NF, 4>, 0, (double)NF / (NF + 1)});
     return;
   }
   if (getenv("DLSIM_TUNE_HONEST")) {  // round 5: shapes with nt buffer stores, outputs beyond the MALL
