@@ -109,6 +109,9 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="north_star", choices=sorted(CONFIGS))
+    ap.add_argument("--shape", default=None,
+                    help="n:params[:dtype] instead of --config (launch-shape studies; the line's "
+                         "config.workload is then 'custom', not a BASELINE.json config)")
     ap.add_argument("--mode", default="exact", choices=["exact", "fast"])
     ap.add_argument("--weak", action="store_true",
                     help="weak scaling: every rank reduces the config's full parameter count "
@@ -304,7 +307,7 @@ class ReduceWorkload:
                 self.outs.append(ob[0, :p])
                 self._keep.append(ob)
             self.plans.append(plan)
-        self.kernel = "dlsim::k_wreduce_tiles" if batch == 1 else "dlsim::k_wreduce_batch_table"
+        self.kernel = _native.kernel_name(n, p, tdt, mode) if batch == 1 else "dlsim::k_wreduce_batch_table"
 
     def launch(self, k):
         self.plans[k % self.out_sets].launch(self.stream)
@@ -555,6 +558,12 @@ def run_rank(args, rank: int, world: int, local: int):
     barrier = (lambda: dist.barrier()) if world > 1 else (lambda: None)
 
     n, p_cfg, dtype, wkind, desc = CONFIGS[args.config]
+    if args.shape:
+        f = args.shape.split(":")
+        n, p_cfg = int(f[0]), int(f[1])
+        dtype = f[2] if len(f) > 2 else "f32"
+        wkind, desc = "dirichlet", f"custom {n}-way Dirichlet-weighted {dtype} reduce, {p_cfg:,} params"
+        args.config = "custom"
     strong = world > 1 and not args.weak
     split = world if strong else (args.slice_of if world == 1 else 1)
     b0, e0 = _native.shard_range(p_cfg, split, rank if strong else 0, 64) if split > 1 else (0, p_cfg)

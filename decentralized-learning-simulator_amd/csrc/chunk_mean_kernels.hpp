@@ -43,6 +43,12 @@
 
 namespace dlsim {
 
+// Output stores of the chunk means: buffer stores with the nt bit for 4/8-byte
+// elements (round 5; sc1 before, measured with outputs that stayed in the
+// Infinity Cache, as the reduce's), global nt for 2-byte.
+template <class Op> inline constexpr int kCmStore = Op::kBytes >= 4 ? 2 : kStNT;
+
+
 constexpr int kCmMaxTasks = 32;
 constexpr int kCmMaxPtrs = 192;
 constexpr int kCmTailRows = 64;  // rows staged per LDS round in block 0
@@ -284,7 +290,7 @@ __device__ __forceinline__ void cm_tile(const A& a, int m, const OutRef& o, size
     const size_t idx = v0 + static_cast<size_t>(v) * SH::VS;
     if (CHECK && idx >= nvec) continue;
     if constexpr (VEC) {
-      store_vec<Op::kBytes >= 4 ? 16 : kStNT>(o, idx, pack<Op>(acc[0][v], div));
+      store_vec<kCmStore<Op>>(o, idx, pack<Op>(acc[0][v], div));
     } else {
 #pragma unroll
       for (int e = 0; e < Op::E; ++e) {
@@ -373,7 +379,7 @@ __device__ __forceinline__ void cm_task(const A& a, int m, void* out, size_t n, 
   constexpr size_t kTile = static_cast<size_t>(kBlock) * SH::VPT;
   const size_t full = nvec / kTile;
   const bool vec = (flags & kCmVec) != 0;
-  const OutRef o = make_out<Op::kBytes >= 4 ? 16 : kStNT>(static_cast<char*>(out) + hb, vec ? nvec : 0);
+  const OutRef o = make_out<kCmStore<Op>>(static_cast<char*>(out) + hb, vec ? nvec : 0);
   const size_t ncol = ilp_begin - head;
   if (local == 0) {
     if (full * kTile < nvec) {  // the partial tile, block map (bounds-checked)

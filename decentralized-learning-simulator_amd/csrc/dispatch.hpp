@@ -163,10 +163,113 @@ hipError_t launch_class(const S& s, int n, void* out, size_t nelem, hipStream_t 
   return launch_shape<Op, S, NF, k.vpt, k.store, k.wave>(s, n, out, nelem, st);
 }
 
+// Deferred stores (dlsim::k_wreduce_defer): fp32 policies,
+// fixed fan-in >= 4, >= 20 MB per stream (size class 2; use_defer). One block (512
+// lanes, ~190-250 VGPRs: one block per CU) folds R rows of 512 vectors.
+// defer_rows picks R (profiles/r05v/ .. r05z/, bench A/B in fresh
+// processes, outputs rotating beyond the Infinity Cache):
+// * when ceil(rows / CUs) <= RMAX, that: one round of blocks with every CU
+//   busy. North star (8 x 11.2 M, 2,795,410 vectors, 256 CUs): R = 22, 249
+//   blocks, 63.07-63.10 us against 63.40-63.72 for the tiled kernel (R = 12,
+//   455 blocks, 62.71-62.74, is a little faster at n = 8 but 3.4% slower at
+//   n = 4: 36.88 against 35.63 us);
+// * otherwise R in [RMAX/2, RMAX] from a cost model of rounds of blocks: full
+//   rounds cost R each, a last round with a fraction x of the CUs busy costs
+//   R * max(x, 0.38 + 0.45 x) (fewer CUs each stream more, up to ~2.2x their
+//   fair share), every round adds 0.1. 8 x 44.7 M: R = 30, 251.6 against
+//   261.7 us; 6 x 20 M: R = 22, 87.1 against 90.7. A thin last round is
+//   what to avoid (north star R = 10: 546 blocks, 70.9 us; R = 20: 273
+//   blocks, 82.8).
+// DLSIM_DEFER=0 (read once): the tiled kernel (A/B runs); DLSIM_DEFER_R=r
+// (read once): that R.
+constexpr int kDeferU = 2, kDeferRMin = 4;
+// results per lane a block can hold: 32 (128 VGPRs) while the fan-in's loads
+// fit beside them, 24 from fan-in 12 (no spills: tests/test_isa_audit.py)
+template <int NF> constexpr int defer_rmax() { return NF >= 12 ? 24 : 32; }
+// Instantiated for fan-in 4..14. Fan-in 11-14 defers only from 16 rows per
+// CU (8.4 M fp32 elements on 256 CUs): 12 and 14 x 11.2 M 89.9 / 103.4 us
+// against 92.1 / 106.2 tiled, but 14 x 5 M 48.4 against 46.9
+// (profiles/r05y/, r05z/). DLSIM_DEFER_MAX_FAN_IN=k (read once; A/B runs):
+// no deferred launch above fan-in k.
+template <class Op, int NF> constexpr bool defer_eligible() { return Op::kBytes == 4 && NF >= 4; }
+constexpr int kDeferWideFanIn = 10;
+constexpr size_t kDeferWideRowsPerCu = 16;
+inline bool defer_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("DLSIM_DEFER");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+inline int defer_max_fan_in() {
+  static const int k = [] {
+    const char* e = std::getenv("DLSIM_DEFER_MAX_FAN_IN");
+    return e ? std::atoi(e) : 14;
+  }();
+  return k;
+}
+int device_cus();  // multiProcessorCount of the current device (cached per device; dlsim_abi.hip)
+inline int defer_r_override() {
+  static const int r = [] {
+    const char* e = std::getenv("DLSIM_DEFER_R");
+    return e ? std::atoi(e) : 0;
+  }();
+  return r;
+}
+inline int defer_rows(size_t nvec, size_t cus, int rmax) {
+  if (defer_r_override() > 0) return std::min(defer_r_override(), rmax);
+  const size_t T = (nvec + dlsim::kDeferBlock - 1) / dlsim::kDeferBlock;
+  const size_t one = (T + cus - 1) / cus;  // one round, every CU busy
+  if (one <= static_cast<size_t>(rmax)) return std::max(static_cast<int>(one), kDeferRMin);
+  int best = rmax;
+  double best_cost = 1e300;
+  for (int R = rmax / 2; R <= rmax; ++R) {
+    const double w = static_cast<double>((T + R - 1) / R) / static_cast<double>(cus);  // rounds (> 1)
+    const double full = std::floor(w), x = w - full;
+    const double cost = R * (full + (x > 0 ? std::max(x, 0.38 + 0.45 * x) : 0.0)) + 0.1 * std::ceil(w);
+    if (cost < best_cost - 1e-9) {
+      best_cost = cost;
+      best = R;
+    }
+  }
+  return best;
+}
+
+// Does a fixed fan-in launch of nelem elements (size class 2) defer?
+template <class Op> bool use_defer(int n, size_t nelem) {
+  if (Op::kBytes != 4 || n < 4 || n > max_fixed_fan_in<Op>() || n > defer_max_fan_in() || !defer_on()) return false;
+  if (size_class<Op>(nelem, n) != 2) return false;
+  if (n <= kDeferWideFanIn) return true;
+  const size_t rows = nelem / Op::E / dlsim::kDeferBlock;
+  return rows >= kDeferWideRowsPerCu * static_cast<size_t>(device_cus());
+}
+
+// The kernel run<Op> launches for n aligned inputs (dlsim_kernel_name).
+template <class Op> const char* kernel_name(int n, size_t nelem) {
+  if (nelem == 0 || n < 1) return "";
+  const size_t first = std::min(nelem, kMaxLaunchOutBytes / Op::kBytes);
+  return use_defer<Op>(n, first) ? "dlsim::k_wreduce_defer" : "dlsim::k_wreduce_tiles";
+}
+
+template <class Op, class S, int NF>
+hipError_t launch_defer(const S& s, void* out, size_t nelem, hipStream_t st) {
+  const size_t nvec = nelem / Op::E;
+  const int R = defer_rows(nvec, static_cast<size_t>(device_cus()), defer_rmax<NF>());
+  const size_t span = static_cast<size_t>(dlsim::kDeferBlock) * static_cast<size_t>(R);
+  const size_t blocks = (nvec + span - 1) / span;
+  if (blocks == 0 || blocks > 0x7fffffffu) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((dlsim::k_wreduce_defer<Op, S, NF, defer_rmax<NF>(), kDeferU, kStore>),
+                     dim3(static_cast<unsigned>(blocks)), dim3(dlsim::kDeferBlock), 0, st, s, R, out, nvec, nelem);
+  return hipGetLastError();
+}
+
 template <class Op, class S, int NF>
 hipError_t launch_tiles(const S& s, int n, void* out, size_t nelem, hipStream_t st) {
   if constexpr (NF > 0) {
-    switch (size_class<Op>(nelem, NF)) {
+    const int c = size_class<Op>(nelem, NF);
+    if constexpr (defer_eligible<Op, NF>())
+      if (c == 2 && use_defer<Op>(NF, nelem)) return launch_defer<Op, S, NF>(s, out, nelem, st);
+    switch (c) {
       case 0: return launch_class<Op, S, NF, 0>(s, n, out, nelem, st);
       case 1: return launch_class<Op, S, NF, 1>(s, n, out, nelem, st);
       default: return launch_class<Op, S, NF, 2>(s, n, out, nelem, st);

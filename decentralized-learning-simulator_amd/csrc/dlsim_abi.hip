@@ -168,6 +168,29 @@ int d2h_one_span(int b, void* const* d_outs, void* const* h_outs, const size_t* 
   return e == hipSuccess ? DLSIM_OK : hip_fail(e, "result D2H");
 }
 
+const char* with_mean_policy_name(int dtype, int n, size_t n_elems) {
+  const char* name = "";
+  with_mean_policy(dtype, [&](auto op) {
+    name = kernel_name<decltype(op)>(n, n_elems);
+    return 0;
+  });
+  return name;
+}
+
+// CUs of the current device, for the deferred-store grid (dispatch.hpp).
+// Read once per device; 256 (MI355X) if the query fails.
+int device_cus() {
+  constexpr int kMaxDev = 64;
+  static int cus[kMaxDev] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return 256;
+  int c = __atomic_load_n(&cus[dev], __ATOMIC_RELAXED);
+  if (c > 0) return c;
+  if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
+  __atomic_store_n(&cus[dev], c, __ATOMIC_RELAXED);
+  return c;
+}
+
 }  // namespace dlsim_host
 
 // the per-policy entries live in the inst_*.hip units
@@ -957,6 +980,18 @@ void dlsim_pool_stats(unsigned long long* contiguous, unsigned long long* fallba
 }
 
 const char* dlsim_last_error(void) { return g_err.c_str(); }
+
+const char* dlsim_kernel_name(int n, size_t n_elems, int dtype, int mode) {
+  if (dtype != DLSIM_F32 && dtype != DLSIM_BF16 && dtype != DLSIM_F16) return "";
+  if (mode == -1) return with_mean_policy_name(dtype, n, n_elems);
+  if (mode != DLSIM_EXACT && mode != DLSIM_FAST) return "";
+  const char* name = "";
+  with_policy(dtype, mode, [&](auto op) {
+    name = kernel_name<decltype(op)>(n, n_elems);
+    return 0;
+  });
+  return name;
+}
 
 int dlsim_version(void) { return (1 << 16) | 1; }
 

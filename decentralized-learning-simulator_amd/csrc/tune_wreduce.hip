@@ -596,8 +596,8 @@ void launch_bal(const Slots<128>& s, int n, void* out, size_t nvec, size_t nelem
 // blocks (R chosen so the grid fits the chip) the whole chip reads first and
 // writes last, so HBM turns around far less often. U tiles' loads are issued
 // together. Same fold order as reduce_tile: bit-exact.
-template <class Op, int NF, int R, int U, int STP, bool CHECK>
-__device__ __forceinline__ void defer_body(const Slots<128>& s, const OutRef& o, size_t base, size_t nvec) {
+template <class Op, int NF, int R, int U, int STP, int BS>
+__device__ __forceinline__ void defer_body(const Slots<128>& s, const OutRef& o, size_t base) {
   u32x4 res[R];
 #pragma unroll
   for (int r0 = 0; r0 < R; r0 += U) {
@@ -605,15 +605,7 @@ __device__ __forceinline__ void defer_body(const Slots<128>& s, const OutRef& o,
 #pragma unroll
     for (int i = 0; i < NF; ++i)
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const size_t v = base + static_cast<size_t>(r0 + u) * kBlock;
-        if constexpr (CHECK) {
-          x[i][u] = u32x4{0u, 0u, 0u, 0u};
-          if (v < nvec) x[i][u] = ld16<1>(s.p[i], v);
-        } else {
-          x[i][u] = ld16<1>(s.p[i], v);
-        }
-      }
+      for (int u = 0; u < U; ++u) x[i][u] = ld16<1>(s.p[i], base + static_cast<size_t>(r0 + u) * BS);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       acc_t<Op> a[1][Op::E];
@@ -632,32 +624,45 @@ __device__ __forceinline__ void defer_body(const Slots<128>& s, const OutRef& o,
     __builtin_amdgcn_sched_barrier(0);
   }
 #pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const size_t v = base + static_cast<size_t>(r) * kBlock;
-    if (!CHECK || v < nvec) store_vec<STP>(o, v, res[r]);
-  }
+  for (int r = 0; r < R; ++r) store_vec<STP>(o, base + static_cast<size_t>(r) * BS, res[r]);
 }
-template <class Op, int NF, int R, int U, int STP>
-__global__ __launch_bounds__(kBlock, 2) void k_defer(const Slots<128> s, int n, void* __restrict__ out, size_t nvec,
-                                                     size_t nelem) {
-  const size_t base = static_cast<size_t>(blockIdx.x) * kBlock * R + threadIdx.x;
+// BS threads per block; LDS > 0: that much dynamic LDS per block pins one
+// block per CU (the grid is sized to about one block per CU).
+template <class Op, int NF, int R, int U, int STP, int MINB = 2, int BS = kBlock>
+__global__ __launch_bounds__(BS, MINB) void k_defer(const Slots<128> s, int n, void* __restrict__ out, size_t nvec,
+                                                    size_t nelem) {
+  const size_t base = static_cast<size_t>(blockIdx.x) * BS * R + threadIdx.x;
   const OutRef o = make_out<STP>(out, nvec);
-  if (static_cast<size_t>(blockIdx.x + 1) * kBlock * R <= nvec) {
-    defer_body<Op, NF, R, U, STP, false>(s, o, base, nvec);
+  if (static_cast<size_t>(blockIdx.x + 1) * BS * R <= nvec) {
+    defer_body<Op, NF, R, U, STP, BS>(s, o, base);
   } else {  // the last, partial block: tile by tile with bounds checks
     for (int r = 0; r < R; ++r)
-      reduce_tile<Op, Slots<128>, NF, 8, 1, 1, true, STP>(s, n, o, base + static_cast<size_t>(r) * kBlock, nvec);
+      reduce_tile<Op, Slots<128>, NF, 8, 1, 1, true, STP, BS>(s, n, o, base + static_cast<size_t>(r) * BS, nvec);
   }
-  if (blockIdx.x == 0) {
+  if (blockIdx.x == 0 && threadIdx.x < kBlock) {
     const size_t j = nvec * Op::E + threadIdx.x;
     if (j < nelem) fold_scalar<Op, Slots<128>>(s, n, out, j);
   }
 }
-template <class Op, int NF, int R, int U, int STP>
+template <class Op, int NF, int R, int U, int STP, int MINB = 2, int BS = kBlock, int LDSKB = 0>
 void launch_defer(const Slots<128>& s, int n, void* out, size_t nvec, size_t nelem, hipStream_t st, int) {
-  const size_t per = static_cast<size_t>(kBlock) * R;
-  hipLaunchKernelGGL((k_defer<Op, NF, R, U, STP>), dim3((unsigned)((nvec + per - 1) / per)), dim3(kBlock), 0, st, s,
-                     n, out, nvec, nelem);
+  const size_t per = static_cast<size_t>(BS) * R;
+  hipLaunchKernelGGL((k_defer<Op, NF, R, U, STP, MINB, BS>), dim3((unsigned)((nvec + per - 1) / per)), dim3(BS),
+                     (size_t)LDSKB * 1024, st, s, n, out, nvec, nelem);
+}
+
+// k_defer with R chosen from the size: the smallest R of the list with
+// ceil(nvec / (BS * R)) <= 256 blocks (one per CU), or the largest R (then
+// more than one block per CU).
+template <class Op, int NF, int U, int BS, int LDSKB>
+void launch_defer_auto(const Slots<128>& s, int n, void* out, size_t nvec, size_t nelem, hipStream_t st, int gm) {
+  const size_t cus = gm > 0 ? (size_t)gm : 256;
+  const size_t need = (nvec + cus * BS - 1) / (cus * BS);
+#define DEFER_R(RR) \
+  if (need <= RR) return launch_defer<Op, NF, RR, (RR % U == 0 ? U : 1), 2, 1, BS, LDSKB>(s, n, out, nvec, nelem, st, 0);
+  DEFER_R(1) DEFER_R(2) DEFER_R(4) DEFER_R(6) DEFER_R(8) DEFER_R(12) DEFER_R(16) DEFER_R(22) DEFER_R(28)
+#undef DEFER_R
+  launch_defer<Op, NF, 32, U, 2, 1, BS, LDSKB>(s, n, out, nvec, nelem, st, 0);
 }
 
 // Round 5: the shipped shapes with sc1 (write-through) stores against
@@ -732,6 +737,28 @@ void add_small(std::vector<Variant>& vs, int n) {
   }
 }
 
+// Round 5: deferred stores (k_defer), outputs beyond the MALL.
+template <class Op, int NF>
+void add_defer(std::vector<Variant>& vs, int n) {
+  if constexpr (!std::is_same<Op, F32Exact>::value) return;
+  else {
+  if (n != NF) return;
+  const std::string p = "NF" + std::to_string(NF);
+  vs.push_back({p + "_V4_sc1_wave", launch_ts<Op, NF, 8, 4, 1, 16, true>, 0});
+    {
+      vs.push_back({p + "_V4_bnt_wave", launch_ts<Op, NF, 8, 4, 1, 2, true>, 0});
+      vs.push_back({p + "_V4_bnt_blk", launch_ts<Op, NF, 8, 4, 1, 2, false>, 0});
+      vs.push_back({p + "_V2_bnt_blk", launch_ts<Op, NF, 8, 2, 1, 2, false>, 0});
+    }
+    vs.push_back({p + "_dauto_B512_U2_lds", launch_defer_auto<Op, NF, 2, 512, 96>, 0});
+    vs.push_back({p + "_dauto_B512_U2", launch_defer_auto<Op, NF, 2, 512, 0>, 0});
+    vs.push_back({p + "_dauto_B512_U1_lds", launch_defer_auto<Op, NF, 1, 512, 96>, 0});
+    vs.push_back({p + "_dauto_B256_U2_lds", launch_defer_auto<Op, NF, 2, 256, 96>, 0});
+    vs.push_back({p + "_dauto_B1024_U2_lds", launch_defer_auto<Op, NF, 2, 1024, 96>, 0});
+    vs.push_back({p + "_dauto_B512_U2_lds_c2", launch_defer_auto<Op, NF, 2, 512, 60>, 512});
+  }
+}
+
 // Round 3: the shipped large shape, the memory-only
 // probe, read-only and write-only probes of the same tiles, and pipelined
 // LDS-DMA rings (nt and default policy) at 1-2 blocks per CU.
@@ -749,19 +776,7 @@ void add_r03(std::vector<Variant>& vs, int n) {
     vs.push_back({p + "_V4_sc1_wave_b", launch_ts<Op, NF, 8, 4, 1, 16, true>, 0});
     return;
   }
-  if (getenv("DLSIM_TUNE_DEFER")) {  // round 5: deferred stores (k_defer), outputs beyond the MALL
-    vs.push_back({p + "_V4_bnt_wave", launch_ts<Op, NF, 8, 4, 1, 2, true>, 0});
-    vs.push_back({p + "_defer_R22_U1", launch_defer<Op, NF, 22, 1, 2>, 0});
-    vs.push_back({p + "_defer_R22_U2", launch_defer<Op, NF, 22, 2, 2>, 0});
-    vs.push_back({p + "_defer_R24_U4", launch_defer<Op, NF, 24, 4, 2>, 0});
-    vs.push_back({p + "_defer_R16_U2", launch_defer<Op, NF, 16, 2, 2>, 0});
-    vs.push_back({p + "_defer_R11_U1", launch_defer<Op, NF, 11, 1, 2>, 0});
-    vs.push_back({p + "_defer_R11_U1_sc1", launch_defer<Op, NF, 11, 1, 16>, 0});
-    vs.push_back({p + "_defer_R8_U2", launch_defer<Op, NF, 8, 2, 2>, 0});
-    vs.push_back({p + "_defer_R44_U1", launch_defer<Op, NF, 44, 1, 2>, 0});
-    vs.push_back({p + "_rdonly_V4w", launch_rdonly<NF, 4>, 0, (double)NF / (NF + 1)});
-    return;
-  }
+  if (getenv("DLSIM_TUNE_DEFER")) return add_defer<Op, NF>(vs, n);
   if (getenv("DLSIM_TUNE_HONEST")) {  // round 5: shapes with nt buffer stores, outputs beyond the MALL
     vs.push_back({p + "_V4_bnt_wave", launch_ts<Op, NF, 8, 4, 1, 2, true>, 0});
     vs.push_back({p + "_V8_bnt_wave", launch_ts<Op, NF, 8, 8, 1, 2, true>, 0});
@@ -1027,6 +1042,10 @@ int run(int n, size_t P, int reps, double peak_gbs) {
     add_layout<Op>(vs, n);
   } else if (r03) {
     add_r03<Op, 8>(vs, n);
+    if (getenv("DLSIM_TUNE_DEFER")) {
+      add_defer<Op, 2>(vs, n);
+      add_defer<Op, 4>(vs, n);
+    }
     if (vs.empty()) {
       fprintf(stderr, "DLSIM_TUNE_R03 needs f32 exact, n = 8\n");
       return 1;

@@ -634,6 +634,79 @@ __global__ __launch_bounds__(kBlock) void k_wreduce_tiles(const S s, int n, void
   }
 }
 
+// ---- deferred-store kernel (round 5) -----------------------------------------
+// HBM pays a bus turnaround each time the traffic switches between reads and
+// writes; the tiled kernel's blocks interleave their 16 KiB stores with the
+// other blocks' loads all along the launch. Here the output is cut into rows
+// of kDeferBlock vectors (lane t of a block owns vector t of a row) and block
+// b folds rows [b*R, (b+1)*R): the R results per lane stay in registers until
+// all R rows are folded, then go out together, so each CU writes R * 8 KiB
+// at a time instead of 16 KiB. The host picks R so the grid's last round of
+// blocks keeps most CUs busy (dispatch.hpp defer_rows; DESIGN.md §5e,
+// profiles/r05s/ .. r05y/).
+//
+// R is a runtime argument (uniform, 1 <= R <= RMAX): the loads of U rows
+// issue back to back, then fold (a row past R re-reads row r0, which the
+// same wave's first load already brings in: no extra HBM traffic); the
+// compiler must not hoist later groups' loads above the fold (NF * RMAX live
+// vectors would spill), hence the barrier per group. Uniform `if`s instead
+// of `break`s keep the loops unrolled and res[] in VGPRs.
+constexpr int kDeferBlock = 512;
+template <class Op, class S, int NF, int RMAX, int U, int STP>
+__device__ __forceinline__ void defer_rows(const S& s, const OutRef& o, size_t base, int R) {
+  u32x4 res[RMAX];
+#pragma unroll
+  for (int r0 = 0; r0 < RMAX; r0 += U) {
+    if (r0 < R) {
+      u32x4 x[NF][U];
+#pragma unroll
+      for (int i = 0; i < NF; ++i)
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int row = r0 + u < R ? r0 + u : r0;
+          x[i][u] = ld16<1>(s.ptr(i), base + static_cast<size_t>(row) * kDeferBlock);
+        }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        acc_t<Op> a[1][Op::E];
+        const u32x4 x0[1] = {x[0][u]};
+        init_tile<Op, 1>(a, x0, false);
+#pragma unroll
+        for (int i = 0; i < NF; ++i) {
+          const u32x4 xi[1] = {x[i][u]};
+          fold_tile<Op, 1>(a, s.wt(i), xi);
+        }
+        res[r0 + u] = pack<Op>(a[0], s.divisor());
+      }
+    }
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int r = 0; r < RMAX; ++r)
+    if (r < R) store_vec<STP>(o, base + static_cast<size_t>(r) * kDeferBlock, res[r]);
+}
+// Full blocks defer; the grid's last block, when partial, folds its rows one
+// at a time with bounds checks; block 0 also folds the < E scalar tail.
+template <class Op, class S, int NF, int RMAX, int U, int STP>
+__global__ __launch_bounds__(kDeferBlock) void k_wreduce_defer(const S s, int R, void* __restrict__ out, size_t nvec,
+                                                               size_t nelem) {
+  const size_t span = static_cast<size_t>(kDeferBlock) * static_cast<size_t>(R);
+  const size_t base = static_cast<size_t>(blockIdx.x) * span + threadIdx.x;
+  const OutRef o = make_out<STP>(out, nvec);
+  if (static_cast<size_t>(blockIdx.x + 1) * span <= nvec) {
+    defer_rows<Op, S, NF, RMAX, U, STP>(s, o, base, R);
+  } else {
+    for (int r = 0; r < R; ++r)
+      reduce_tile<Op, S, NF, 1, 1, 1, true, STP, kDeferBlock>(s, NF, o, base + static_cast<size_t>(r) * kDeferBlock,
+                                                              nvec);
+  }
+  if (blockIdx.x == 0) {
+    const size_t j = nvec * Op::E + threadIdx.x;
+    if (j < nelem) fold_scalar<Op, S>(s, NF, out, j);
+  }
+}
+
 // ---- batched launch: many independent aggregates in one grid -----------------
 // The aggregate tasks of one simulated round (every peer's neighbour mix) are
 // independent; small models (GNLeNet: 3 MB per task) are launch-bound when

@@ -64,6 +64,7 @@ EXPORTS = (
     "dlsim_host_pack",
     "dlsim_shard_range",
     "dlsim_probe_pattern",
+    "dlsim_kernel_name",
     "dlsim_last_error",
     "dlsim_version",
 )
@@ -173,12 +174,21 @@ def load() -> ctypes.CDLL:
         u64p = ctypes.POINTER(ctypes.c_ulonglong)
         lib.dlsim_pool_stats.argtypes = [u64p, u64p, u64p]
         lib.dlsim_pool_stats.restype = None
+        lib.dlsim_kernel_name.argtypes = [i, sz, i, i]
+        lib.dlsim_kernel_name.restype = ctypes.c_char_p
         lib.dlsim_last_error.argtypes = []
         lib.dlsim_last_error.restype = ctypes.c_char_p
         lib.dlsim_version.argtypes = []
         lib.dlsim_version.restype = i
         _lib = lib
         return lib
+
+
+def kernel_name(n: int, numel: int, torch_dtype, mode: Optional[int] = DLSIM_EXACT) -> str:
+    """Name of the kernel dlsim_wreduce (mode DLSIM_EXACT / DLSIM_FAST) or
+    dlsim_mean (mode None) launches for n aligned inputs of numel elements
+    (dlsim_kernel_name), e.g. "dlsim::k_wreduce_defer"."""
+    return load().dlsim_kernel_name(n, numel, dtype_code(torch_dtype), -1 if mode is None else mode).decode()
 
 
 def _check(fn: str, rc: int) -> None:

@@ -538,6 +538,18 @@ void* dlsim_pool_alloc(size_t nbytes, int device, void* stream);
 void dlsim_pool_free(void* d_ptr, size_t nbytes, int device, void* stream);
 void dlsim_pool_stats(unsigned long long* contiguous, unsigned long long* fallback, unsigned long long* live_bytes);
 
+/*
+ * dlsim_kernel_name — the kernel dlsim_wreduce (mode DLSIM_EXACT or
+ * DLSIM_FAST) or dlsim_mean (mode -1) launches for n 16-byte-aligned inputs
+ * of n_elems elements of dtype on the current device: "dlsim::k_wreduce_defer"
+ * (fp32, 4 <= n <= 14, >= 20 MB per stream),
+ * "dlsim::k_wreduce_tiles" otherwise (misaligned buffers take
+ * "dlsim::k_wreduce_scalar"), "" for no launch (n_elems == 0) or bad
+ * arguments. A static string, for profilers and benches that look a kernel up
+ * by name. (New: no reference counterpart.)
+ */
+const char* dlsim_kernel_name(int n, size_t n_elems, int dtype, int mode);
+
 /* Message for the last failing call on this thread ("" if none). */
 const char* dlsim_last_error(void);
 

@@ -31,6 +31,8 @@ EXACT_KEYS = tuple(k for k in POLICIES if k.endswith("Exact")) + ("MixedSlots",)
 # encodings are suffixed in the disassembly (v_fmac_f32_e32, v_fma_f32_e64)
 FMA_RE = re.compile(r"\bv_(pk_)?(fmac?|mac|mad|fma_legacy|fmac_legacy)_f(32|64)(_e(32|64|64_dpp|32_dpp))?\b")
 MIX_RE = re.compile(r"\bv_\w*_mix\w*\b")
+# register spills (gfx950 spills through scratch_* instructions)
+SPILL_RE = re.compile(r"\bscratch_(load|store)_\w+")
 BUNDLE_MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
 
 
@@ -92,10 +94,14 @@ def kernels(asm):
 def audit(path=LIB):
     stats = {}
     bad = []
+    spills = []
     ncos = 0
     for co in code_objects(path):
         ncos += 1
         for name, body in kernels(disassemble(co)).items():
+            nsp = len(SPILL_RE.findall(body))
+            if nsp:
+                spills.append({"kernel": name, "scratch_ops": nsp})
             # Itanium mangling prefixes every name with its length: 9BF16Exact, 8F16Exact
             key = next((k for k in POLICIES if f"{len(k)}{k}" in name), None)
             if key is None:
@@ -109,7 +115,7 @@ def audit(path=LIB):
             if key in EXACT_KEYS and (fma or mix):
                 bad.append({"kernel": name, "fma": fma, "mix": mix})
     return {"target": "gfx950", "library": os.path.relpath(path, ROOT), "code_objects": ncos, "per_policy": stats,
-            "exact_policies_clean": not bad, "offending_kernels": bad}
+            "exact_policies_clean": not bad, "offending_kernels": bad, "spilling_kernels": spills}
 
 
 def main():

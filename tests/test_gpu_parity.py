@@ -293,6 +293,41 @@ def test_launch_shapes_either_side_of_the_size_switch(dtype, p, n):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("n,p", [
+    (4, 5_000_003),            # ragged last block (bounds-checked rows) and an E tail of 3
+    (5, 4 * 512 * 10 * 245),   # whole rows only, no tail
+    (7, 11_181_642 + 1),       # the north star's grid (R = 12), E tail of 1
+    (10, 8_392_711),           # the largest deferred fan-in, odd R (duplicate-row loads)
+    (9, 5_000_011),
+    (12, 11_181_642 + 3),      # fan-in 11-14 from 16 rows per CU (RMAX 24)
+    (6, 20_000_003),           # more rows than one round holds: R from the cost model
+    (4, 67_108_864 + 5),       # many rounds of blocks
+])
+def test_deferred_store_kernel_bit_exact(n, p):
+    """dlsim::k_wreduce_defer (fp32, fixed fan-in >= 4, >= 20 MB per stream;
+    dispatch.hpp launch_defer): full blocks keep R results per lane in
+    registers and store them at the end, the last block folds its partial
+    rows with bounds checks, block 0 the scalar tail. Every element against
+    the oracle, for the weighted reduce (exact and fast) and the mean."""
+    assert _native.kernel_name(n, p, torch.float32) == "dlsim::k_wreduce_defer"
+    g = torch.Generator(device=dev()).manual_seed(p + n)
+    xs = [(torch.randn(p, generator=g, device=dev()) * 0.05) for _ in range(n)]
+    host = np.stack([x.cpu().numpy() for x in xs])
+    w = orc.reference_weights(n, list(np.random.default_rng(n).dirichlet(np.ones(n))))
+    out = torch.empty_like(xs[0])
+    _native.wreduce(xs, w, out)
+    assert orc.same_bits(out.cpu().numpy(), orc.wreduce_rows_f32(host, w))
+    if p < 20_000_000:
+        _native.mean(xs, out)
+        assert orc.same_bits(out.cpu().numpy(), orc.mean(list(host), "f32"))
+        _native.wreduce(xs, w, out, _native.DLSIM_FAST)
+        # the fma chain the fast oracle computes (within n * 2^-23 of the
+        # exact fold, relative to sum |w_i x_i|: test_fast_mode_f32_within_tolerance)
+        assert orc.same_bits(out.cpu().numpy(), orc.wreduce(list(host), w, "f32", mode="fast"))
+    del xs, out, host
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("dtype,p", [("f32", 1_999_999), ("f32", 2_000_003), ("f32", 4_999_997),
                                      ("f64", 999_999), ("f64", 1_000_003),
                                      ("bf16", 47_999_993), ("bf16", 48_000_007)])

@@ -63,3 +63,20 @@ def test_detector_catches_contraction(report):
                 "v_fma_f64 v[0:1], v[2:3], v[4:5], v[6:7]"):
         assert audit_isa.FMA_RE.search(ins), ins
     assert audit_isa.MIX_RE.search("v_fma_mixlo_f16 v1, v2, v3, v4")
+
+
+def test_no_kernel_spills_and_deferred_kernels_present(report):
+    """No kernel of the library spills registers to scratch (the deferred-store
+    kernel keeps up to 32 results per lane in VGPRs: a rolled loop would put
+    them in scratch), and the deferred kernels exist for fp32 fixed fan-in
+    4..14 (dispatch.hpp defer_eligible)."""
+    assert report["spilling_kernels"] == [], json.dumps(report["spilling_kernels"][:10], indent=1)
+    names = set()
+    for co in audit_isa.code_objects(audit_isa.LIB):
+        names |= set(audit_isa.kernels(audit_isa.disassemble(co)))
+    for pol in ("8F32Exact", "7F32Fast", "7F32Mean"):
+        got = sorted(n for n in names if "k_wreduce_defer" in n and pol in n)
+        # template args <Op, S, NF, RMAX, U, STP>: ...ELi<NF>ELi<RMAX>ELi2ELi2EE (RMAX 24 from NF 12)
+        for nf in range(4, 15):
+            assert any(f"ELi{nf}ELi{32 if nf < 12 else 24}ELi2ELi2EE" in n for n in got), (pol, nf)
+        assert not any(f"ELi{nf}ELi{32 if nf < 12 else 24}ELi2ELi2EE" in n for n in got for nf in (1, 2, 3)), pol
