@@ -166,23 +166,25 @@ hipError_t launch_class(const S& s, int n, void* out, size_t nelem, hipStream_t 
 // Deferred stores (dlsim::k_wreduce_defer): fp32 policies,
 // fixed fan-in >= 4, >= 20 MB per stream (size class 2; use_defer). One block (512
 // lanes, ~190-250 VGPRs: one block per CU) folds R rows of 512 vectors.
-// defer_rows picks R (profiles/r05v/ .. r05z/, bench A/B in fresh
-// processes, outputs rotating beyond the Infinity Cache):
-// * when ceil(rows / CUs) <= RMAX, that: one round of blocks with every CU
-//   busy. North star (8 x 11.2 M, 2,795,410 vectors, 256 CUs): R = 22, 249
-//   blocks, 63.07-63.10 us against 63.40-63.72 for the tiled kernel (R = 12,
-//   455 blocks, 62.71-62.74, is a little faster at n = 8 but 3.4% slower at
-//   n = 4: 36.88 against 35.63 us);
-// * otherwise R in [RMAX/2, RMAX] from a cost model of rounds of blocks: full
+// defer_rows picks an even R (profiles/r05_defer/, bench A/B in fresh
+// processes, outputs rotating beyond the Infinity Cache; odd R re-reads a
+// row per group and measured slower):
+// * one round of blocks with every CU busy, R = ceil(rows / CUs), up to 24
+//   rows: north star (8 x 11.2 M, 2,795,410 vectors, 256 CUs) R = 22, 249
+//   blocks, 63.0 us against 63.4 tiled; n = 4 / 6 / 10 at 11.2 M 35.5 / 48.9 /
+//   76.4 against 37.0 / 51.0 / 78.0;
+// * else two rounds, R = ceil(rows / 2 CUs): a single round of 32 rows loses
+//   to two of 16 at 16 M (n = 8: 90.1 against 88.3 us; n = 10: 111.3 against
+//   107.6; tiled 92.2 / 113.1);
+// * else R in [RMAX/2, RMAX] from a cost model of rounds of blocks: full
 //   rounds cost R each, a last round with a fraction x of the CUs busy costs
 //   R * max(x, 0.38 + 0.45 x) (fewer CUs each stream more, up to ~2.2x their
 //   fair share), every round adds 0.1. 8 x 44.7 M: R = 30, 251.6 against
-//   261.7 us; 6 x 20 M: R = 22, 87.1 against 90.7. A thin last round is
-//   what to avoid (north star R = 10: 546 blocks, 70.9 us; R = 20: 273
-//   blocks, 82.8).
+//   261.7 us. A thin last round is what to avoid (north star R = 10: 546
+//   blocks, 70.9 us; R = 20: 273 blocks, 82.8).
 // DLSIM_DEFER=0 (read once): the tiled kernel (A/B runs); DLSIM_DEFER_R=r
 // (read once): that R.
-constexpr int kDeferU = 2, kDeferRMin = 4;
+constexpr int kDeferU = 2, kDeferRMin = 4, kDeferOneRoundMax = 24;
 // results per lane a block can hold: 32 (128 VGPRs) while the fan-in's loads
 // fit beside them, 24 from fan-in 12 (no spills: tests/test_isa_audit.py)
 template <int NF> constexpr int defer_rmax() { return NF >= 12 ? 24 : 32; }
@@ -219,11 +221,13 @@ inline int defer_r_override() {
 inline int defer_rows(size_t nvec, size_t cus, int rmax) {
   if (defer_r_override() > 0) return std::min(defer_r_override(), rmax);
   const size_t T = (nvec + dlsim::kDeferBlock - 1) / dlsim::kDeferBlock;
-  const size_t one = (T + cus - 1) / cus;  // one round, every CU busy
-  if (one <= static_cast<size_t>(rmax)) return std::max(static_cast<int>(one), kDeferRMin);
+  const size_t one = ((T + cus - 1) / cus + 1) & ~size_t{1};  // one round, every CU busy; even
+  if (one <= static_cast<size_t>(std::min(rmax, kDeferOneRoundMax))) return std::max(static_cast<int>(one), kDeferRMin);
+  const size_t two = ((T + 2 * cus - 1) / (2 * cus) + 1) & ~size_t{1};  // two rounds
+  if (two <= static_cast<size_t>(rmax)) return static_cast<int>(two);
   int best = rmax;
   double best_cost = 1e300;
-  for (int R = rmax / 2; R <= rmax; ++R) {
+  for (int R = rmax / 2; R <= rmax; R += 2) {
     const double w = static_cast<double>((T + R - 1) / R) / static_cast<double>(cus);  // rounds (> 1)
     const double full = std::floor(w), x = w - full;
     const double cost = R * (full + (x > 0 ? std::max(x, 0.38 + 0.45 * x) : 0.0)) + 0.1 * std::ceil(w);
