@@ -164,7 +164,8 @@ hipError_t launch_class(const S& s, int n, void* out, size_t nelem, hipStream_t 
 }
 
 // Deferred stores (dlsim::k_wreduce_defer): fp32 policies,
-// fixed fan-in >= 4, >= 20 MB per stream (size class 2; use_defer). One block (512
+// fan-in >= 4 (fixed, and the grouped form above 14), >= 20 MB per stream
+// (size class 2; use_defer). One block (512
 // lanes, ~190-250 VGPRs: one block per CU) folds R rows of 512 vectors.
 // defer_rows picks an even R (profiles/r05_defer/, bench A/B in fresh
 // processes, outputs rotating beyond the Infinity Cache; odd R re-reads a
@@ -187,7 +188,7 @@ hipError_t launch_class(const S& s, int n, void* out, size_t nelem, hipStream_t 
 constexpr int kDeferU = 2, kDeferRMin = 4, kDeferOneRoundMax = 24;
 // results per lane a block can hold: 32 (128 VGPRs) while the fan-in's loads
 // fit beside them, 24 from fan-in 12 (no spills: tests/test_isa_audit.py)
-template <int NF> constexpr int defer_rmax() { return NF >= 12 ? 24 : 32; }
+template <int NF> constexpr int defer_rmax() { return NF >= 12 ? 24 : 32; }  // NF = 0 (grouped): 32
 // Instantiated for fan-in 4..14. Fan-in 11-14 defers only from 16 rows per
 // CU (8.4 M fp32 elements on 256 CUs): 12 and 14 x 11.2 M 89.9 / 103.4 us
 // against 92.1 / 106.2 tiled, but 14 x 5 M 48.4 against 46.9
@@ -206,7 +207,7 @@ inline bool defer_on() {
 inline int defer_max_fan_in() {
   static const int k = [] {
     const char* e = std::getenv("DLSIM_DEFER_MAX_FAN_IN");
-    return e ? std::atoi(e) : 14;
+    return e ? std::atoi(e) : 1 << 30;
   }();
   return k;
 }
@@ -239,10 +240,23 @@ inline int defer_rows(size_t nvec, size_t cus, int rmax) {
   return best;
 }
 
-// Does a fixed fan-in launch of nelem elements (size class 2) defer?
+// Does a launch of n inputs of nelem elements defer? Fixed fan-in: size class
+// 2 (>= 20 MB per stream), fan-in 11-14 from 16 rows per CU. Grouped (runtime)
+// fan-in, n > 14: from 20 MB (cfg3, 17 x 11.2 M: 123.8 -> 120.8 us; cfg5,
+// 100 x 11.2 M: 676.6 -> 659.0; 17 x 16 M 182.5 -> 171.9; 30 x 11.2 M 212.6
+// -> 204.3; profiles/r05_defer/r05ad_*). DLSIM_DEFER_GROUPED=0 (read once;
+// A/B runs): the tiled grouped kernel.
+inline bool defer_grouped_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("DLSIM_DEFER_GROUPED");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 template <class Op> bool use_defer(int n, size_t nelem) {
-  if (Op::kBytes != 4 || n < 4 || n > max_fixed_fan_in<Op>() || n > defer_max_fan_in() || !defer_on()) return false;
-  if (size_class<Op>(nelem, n) != 2) return false;
+  if (Op::kBytes != 4 || n < 4 || n > defer_max_fan_in() || !defer_on()) return false;
+  if (size_class<Op>(nelem, n <= max_fixed_fan_in<Op>() ? n : 0) != 2) return false;
+  if (n > max_fixed_fan_in<Op>()) return defer_grouped_on();
   if (n <= kDeferWideFanIn) return true;
   const size_t rows = nelem / Op::E / dlsim::kDeferBlock;
   return rows >= kDeferWideRowsPerCu * static_cast<size_t>(device_cus());
@@ -256,14 +270,14 @@ template <class Op> const char* kernel_name(int n, size_t nelem) {
 }
 
 template <class Op, class S, int NF>
-hipError_t launch_defer(const S& s, void* out, size_t nelem, hipStream_t st) {
+hipError_t launch_defer(const S& s, int n, void* out, size_t nelem, hipStream_t st) {
   const size_t nvec = nelem / Op::E;
   const int R = defer_rows(nvec, static_cast<size_t>(device_cus()), defer_rmax<NF>());
   const size_t span = static_cast<size_t>(dlsim::kDeferBlock) * static_cast<size_t>(R);
   const size_t blocks = (nvec + span - 1) / span;
   if (blocks == 0 || blocks > 0x7fffffffu) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((dlsim::k_wreduce_defer<Op, S, NF, defer_rmax<NF>(), kDeferU, kStore>),
-                     dim3(static_cast<unsigned>(blocks)), dim3(dlsim::kDeferBlock), 0, st, s, R, out, nvec, nelem);
+  hipLaunchKernelGGL((dlsim::k_wreduce_defer<Op, S, NF, group_size<Op>(), defer_rmax<NF>(), kDeferU, kStore>),
+                     dim3(static_cast<unsigned>(blocks)), dim3(dlsim::kDeferBlock), 0, st, s, n, R, out, nvec, nelem);
   return hipGetLastError();
 }
 
@@ -272,13 +286,15 @@ hipError_t launch_tiles(const S& s, int n, void* out, size_t nelem, hipStream_t 
   if constexpr (NF > 0) {
     const int c = size_class<Op>(nelem, NF);
     if constexpr (defer_eligible<Op, NF>())
-      if (c == 2 && use_defer<Op>(NF, nelem)) return launch_defer<Op, S, NF>(s, out, nelem, st);
+      if (c == 2 && use_defer<Op>(NF, nelem)) return launch_defer<Op, S, NF>(s, n, out, nelem, st);
     switch (c) {
       case 0: return launch_class<Op, S, NF, 0>(s, n, out, nelem, st);
       case 1: return launch_class<Op, S, NF, 1>(s, n, out, nelem, st);
       default: return launch_class<Op, S, NF, 2>(s, n, out, nelem, st);
     }
   } else {
+    if constexpr (Op::kBytes == 4)
+      if (use_defer<Op>(n, nelem)) return launch_defer<Op, S, 0>(s, n, out, nelem, st);
     return size_class<Op>(nelem) == 0 ? launch_class<Op, S, 0, 0>(s, n, out, nelem, st)
                                       : launch_class<Op, S, 0, 2>(s, n, out, nelem, st);
   }

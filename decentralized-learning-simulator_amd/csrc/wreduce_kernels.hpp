@@ -652,31 +652,71 @@ __global__ __launch_bounds__(kBlock) void k_wreduce_tiles(const S s, int n, void
 // vectors would spill), hence the barrier per group. Uniform `if`s instead
 // of `break`s keep the loops unrolled and res[] in VGPRs.
 constexpr int kDeferBlock = 512;
-template <class Op, class S, int NF, int RMAX, int U, int STP>
-__device__ __forceinline__ void defer_rows(const S& s, const OutRef& o, size_t base, int R) {
+// U rows' vectors of one group of inputs [i0, i0 + cnt) (cnt <= G; NF > 0: all
+// NF inputs, cnt unused).
+template <class Op, class S, int NF, int G, int U>
+__device__ __forceinline__ void defer_fold_group(const S& s, int i0, int cnt, size_t base, int r0, int R, bool first,
+                                                 acc_t<Op> (&a)[U][1][Op::E]) {
+  constexpr int K = NF > 0 ? NF : G;
+  u32x4 x[K][U];
+#pragma unroll
+  for (int g = 0; g < K; ++g)
+    if (NF > 0 || g < cnt)
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int row = r0 + u < R ? r0 + u : r0;
+        x[g][u] = ld16<1>(s.ptr(i0 + g), base + static_cast<size_t>(row) * kDeferBlock);
+      }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (first) {
+      const u32x4 x0[1] = {x[0][u]};
+      init_tile<Op, 1>(a[u], x0, false);
+    }
+#pragma unroll
+    for (int g = 0; g < K; ++g)
+      if (NF > 0 || g < cnt) {
+        const u32x4 xg[1] = {x[g][u]};
+        fold_tile<Op, 1>(a[u], s.wt(i0 + g), xg);
+      }
+  }
+}
+template <class Op, class S, int NF, int G, int RMAX, int U, int STP>
+__device__ __forceinline__ void defer_rows(const S& s, int n, const OutRef& o, size_t base, int R) {
   u32x4 res[RMAX];
 #pragma unroll
   for (int r0 = 0; r0 < RMAX; r0 += U) {
     if (r0 < R) {
-      u32x4 x[NF][U];
+      if constexpr (NF > 0) {
+        // (this exact form: folding through defer_fold_group, as the grouped
+        // form does, schedules differently and lost the north star's 0.5 us)
+        u32x4 x[NF][U];
 #pragma unroll
-      for (int i = 0; i < NF; ++i)
+        for (int i = 0; i < NF; ++i)
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const int row = r0 + u < R ? r0 + u : r0;
+            x[i][u] = ld16<1>(s.ptr(i), base + static_cast<size_t>(row) * kDeferBlock);
+          }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          const int row = r0 + u < R ? r0 + u : r0;
-          x[i][u] = ld16<1>(s.ptr(i), base + static_cast<size_t>(row) * kDeferBlock);
-        }
+          acc_t<Op> a[1][Op::E];
+          const u32x4 x0[1] = {x[0][u]};
+          init_tile<Op, 1>(a, x0, false);
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        acc_t<Op> a[1][Op::E];
-        const u32x4 x0[1] = {x[0][u]};
-        init_tile<Op, 1>(a, x0, false);
-#pragma unroll
-        for (int i = 0; i < NF; ++i) {
-          const u32x4 xi[1] = {x[i][u]};
-          fold_tile<Op, 1>(a, s.wt(i), xi);
+          for (int i = 0; i < NF; ++i) {
+            const u32x4 xi[1] = {x[i][u]};
+            fold_tile<Op, 1>(a, s.wt(i), xi);
+          }
+          res[r0 + u] = pack<Op>(a[0], s.divisor());
         }
-        res[r0 + u] = pack<Op>(a[0], s.divisor());
+      } else {  // runtime fan-in in groups of G, input order; the first seeds x0 * 0
+        acc_t<Op> a[U][1][Op::E];
+        defer_fold_group<Op, S, 0, G, U>(s, 0, n < G ? n : G, base, r0, R, true, a);
+        for (int i0 = G; i0 < n; i0 += G)
+          defer_fold_group<Op, S, 0, G, U>(s, i0, (n - i0) < G ? (n - i0) : G, base, r0, R, false, a);
+#pragma unroll
+        for (int u = 0; u < U; ++u) res[r0 + u] = pack<Op>(a[u][0], s.divisor());
       }
     }
     asm volatile("" ::: "memory");
@@ -688,22 +728,32 @@ __device__ __forceinline__ void defer_rows(const S& s, const OutRef& o, size_t b
 }
 // Full blocks defer; the grid's last block, when partial, folds its rows one
 // at a time with bounds checks; block 0 also folds the < E scalar tail.
-template <class Op, class S, int NF, int RMAX, int U, int STP>
-__global__ __launch_bounds__(kDeferBlock) void k_wreduce_defer(const S s, int R, void* __restrict__ out, size_t nvec,
-                                                               size_t nelem) {
+// NF > 0: fixed fan-in n == NF; NF == 0: runtime n in groups of G.
+template <class Op, class S, int NF, int G, int RMAX, int U, int STP>
+__global__ __launch_bounds__(kDeferBlock) void k_wreduce_defer(const S s, int n, int R, void* __restrict__ out,
+                                                               size_t nvec, size_t nelem) {
   const size_t span = static_cast<size_t>(kDeferBlock) * static_cast<size_t>(R);
   const size_t base = static_cast<size_t>(blockIdx.x) * span + threadIdx.x;
   const OutRef o = make_out<STP>(out, nvec);
   if (static_cast<size_t>(blockIdx.x + 1) * span <= nvec) {
-    defer_rows<Op, S, NF, RMAX, U, STP>(s, o, base, R);
+    if constexpr (NF > 0) {
+      defer_rows<Op, S, NF, G, RMAX, U, STP>(s, n, o, base, R);
+    } else {
+      // The grouped form indexes the slots at run time from 16 unrolled row
+      // groups; read through `s` the compiler keeps a private copy of the
+      // whole argument (1.5 KiB of scratch per lane for Slots<128>). `s` is
+      // the first kernel argument: read it in place in the kernarg segment.
+      const S* ks = (const S*)__builtin_amdgcn_kernarg_segment_ptr();
+      defer_rows<Op, S, NF, G, RMAX, U, STP>(*ks, n, o, base, R);
+    }
   } else {
     for (int r = 0; r < R; ++r)
-      reduce_tile<Op, S, NF, 1, 1, 1, true, STP, kDeferBlock>(s, NF, o, base + static_cast<size_t>(r) * kDeferBlock,
-                                                              nvec);
+      reduce_tile<Op, S, NF, G, 1, 1, true, STP, kDeferBlock>(s, NF > 0 ? NF : n, o,
+                                                              base + static_cast<size_t>(r) * kDeferBlock, nvec);
   }
   if (blockIdx.x == 0) {
     const size_t j = nvec * Op::E + threadIdx.x;
-    if (j < nelem) fold_scalar<Op, S>(s, NF, out, j);
+    if (j < nelem) fold_scalar<Op, S>(s, NF > 0 ? NF : n, out, j);
   }
 }
 

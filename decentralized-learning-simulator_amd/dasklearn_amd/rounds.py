@@ -30,7 +30,7 @@ import torch
 from torch import nn
 
 from . import _native
-from .arena import (ParamLayout, ZipMismatch, _target_device, aggregate_modules, aligned_empty, base_align,
+from .arena import (ParamLayout, ZipMismatch, _target_device, aggregate_modules, aligned_empty, arena_empty, base_align,
                     layout_of, module_params, registered_arenas, row_stride)
 from .batch import _device_views, _resolve, aggregate_arena_tasks
 
@@ -237,7 +237,12 @@ class RoundExecutor:
             size = max(off, 1)
             stage = self._stage(g % 2, size)
             _native.host_pack(srcs, offs, stage[:size])
-            buf = aligned_empty(size, torch.uint8, dev, align)
+            # from 4 MiB the output pool's physically contiguous blocks (a
+            # torch MemPool: freed after the wave, reused by the next), as for
+            # single calls' staging rows; 2 MiB-aligned
+            buf = arena_empty(size, torch.uint8, dev)
+            if buf.data_ptr() % align:
+                buf = aligned_empty(size, torch.uint8, dev, align)
             buf.copy_(stage[:size], non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(stream)

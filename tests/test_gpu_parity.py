@@ -302,6 +302,8 @@ def test_launch_shapes_either_side_of_the_size_switch(dtype, p, n):
     (12, 11_181_642 + 3),      # fan-in 11-14 from 16 rows per CU (RMAX 24)
     (6, 20_000_003),           # more rows than one round holds: R from the cost model
     (4, 67_108_864 + 5),       # many rounds of blocks
+    (17, 5_000_003),           # the grouped form: kernel-argument slots
+    (130, 5_000_001),          # the grouped form: the device table
 ])
 def test_deferred_store_kernel_bit_exact(n, p):
     """dlsim::k_wreduce_defer (fp32, fixed fan-in >= 4, >= 20 MB per stream;

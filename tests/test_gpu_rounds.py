@@ -279,3 +279,37 @@ def test_round_executor_device_cuda_without_index():
     for p in range(4):
         a, b = got[f"agg_{p}_2"][0], exp[f"agg_{p}_2"][0]
         assert orc.same_bits(torch.cat([q.detach().reshape(-1).cpu() for q in a.parameters()]).numpy(), flat(b))
+
+
+def test_round_executor_uploads_from_the_output_pool(monkeypatch):
+    """VERDICT r04 missing #5: a wave's host-model upload buffer of 4 MiB or
+    more comes from arena_empty (the output pool's torch MemPool of physically
+    contiguous blocks), 2 MiB-aligned, and the round stays bit-identical to
+    the sequential oracle replay."""
+    from dasklearn_amd import arena, rounds
+    shapes = [(1024, 1024), (1024,), (512, 1024)]  # 1.5 M fp32 per model (6 MiB)
+    torch.manual_seed(29)
+    init = Shaped(shapes)
+    with torch.no_grad():
+        for p in init.parameters():
+            p.copy_(torch.randn(p.shape) * 0.05)
+    taken = []
+    real = arena.arena_empty
+
+    def spy(numel, dtype, device):
+        t = real(numel, dtype, device)
+        if dtype == torch.uint8:
+            taken.append((numel, t.data_ptr()))
+        return t
+    monkeypatch.setattr(rounds, "arena_empty", spy)
+    made0 = arena.OUTPUT_POOL.made
+    tasks, nb = build_dag(4, 2)
+    ex = RoundExecutor({"train": host_train}, Settings())
+    got = ex.run(tasks, seed={"init": [init]})
+    exp = replay(tasks, {"aggregate": oracle_aggregate, "train": host_train}, init)
+    assert taken and all(n >= 4 << 20 and ptr % (2 << 20) == 0 for n, ptr in taken)
+    assert arena.OUTPUT_POOL.made - made0 >= len(taken)
+    for p in range(4):
+        a = got[f"agg_{p}_2"][0]
+        assert orc.same_bits(torch.cat([q.detach().reshape(-1).cpu() for q in a.parameters()]).numpy(),
+                             flat(exp[f"agg_{p}_2"][0]))

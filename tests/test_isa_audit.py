@@ -68,15 +68,17 @@ def test_detector_catches_contraction(report):
 def test_no_kernel_spills_and_deferred_kernels_present(report):
     """No kernel of the library spills registers to scratch (the deferred-store
     kernel keeps up to 32 results per lane in VGPRs: a rolled loop would put
-    them in scratch), and the deferred kernels exist for fp32 fixed fan-in
-    4..14 (dispatch.hpp defer_eligible)."""
+    them in scratch, and its grouped form reads its kernel-argument slots in
+    place), and the deferred kernels exist for fp32 fixed fan-in 4..14 and the
+    grouped form (dispatch.hpp defer_eligible)."""
     assert report["spilling_kernels"] == [], json.dumps(report["spilling_kernels"][:10], indent=1)
     names = set()
     for co in audit_isa.code_objects(audit_isa.LIB):
         names |= set(audit_isa.kernels(audit_isa.disassemble(co)))
     for pol in ("8F32Exact", "7F32Fast", "7F32Mean"):
         got = sorted(n for n in names if "k_wreduce_defer" in n and pol in n)
-        # template args <Op, S, NF, RMAX, U, STP>: ...ELi<NF>ELi<RMAX>ELi2ELi2EE (RMAX 24 from NF 12)
-        for nf in range(4, 15):
-            assert any(f"ELi{nf}ELi{32 if nf < 12 else 24}ELi2ELi2EE" in n for n in got), (pol, nf)
-        assert not any(f"ELi{nf}ELi{32 if nf < 12 else 24}ELi2ELi2EE" in n for n in got for nf in (1, 2, 3)), pol
+        # template args <Op, S, NF, G, RMAX, U, STP>: ...ELi<NF>ELi8ELi<RMAX>ELi2ELi2EE
+        # (RMAX 24 from NF 12; NF 0 = the grouped form)
+        for nf in list(range(4, 15)) + [0]:
+            assert any(f"ELi{nf}ELi8ELi{32 if nf < 12 else 24}ELi2ELi2EE" in n for n in got), (pol, nf)
+        assert not any(f"ELi{nf}ELi8ELi32ELi2ELi2EE" in n for n in got for nf in (1, 2, 3)), pol
