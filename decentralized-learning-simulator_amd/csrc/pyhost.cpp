@@ -400,9 +400,42 @@ PyObject* py_shm_keys(PyObject*, PyObject* args) {
   return shm_keys_of(ts, n, t);
 }
 
-// shm_rows(rows, idx) -> (shm_keys(rows, idx), data_ptrs(rows, idx)): one
-// pass over the tensors of freshly received models, whose first touch is most
-// of the cost (device cache path, arena._cached_host_reduce)
+// Content fingerprint of model i's tensors [i*t, (i+1)*t) for the device
+// cache's stale-hit check: 8 bytes from the middle of up
+// to kFpTensors tensors spread over the group (the first and the last among
+// them), mixed with their positions. A model written in place after it was
+// cached (the reference trains its input model in place, functions.py:57)
+// changes essentially every element, so a changed word shows it; one word per
+// sampled tensor keeps the cost to a page touch each on freshly mapped shm.
+constexpr Py_ssize_t kFpTensors = 8;
+uint64_t content_fingerprint(const std::vector<const at::Tensor*>& ts, Py_ssize_t i, Py_ssize_t t) {
+  uint64_t h = 0x9e3779b97f4a7c15ull;
+  const Py_ssize_t k = std::min(t, kFpTensors);
+  for (Py_ssize_t s = 0; s < k; ++s) {
+    const Py_ssize_t j = k > 1 ? s * (t - 1) / (k - 1) : 0;
+    const at::Tensor* x = ts[static_cast<size_t>(i * t + j)];
+    const int64_t ne = x->numel();
+    uint64_t w = 0;
+    if (ne > 0) {
+      const size_t esz = x->element_size();
+      const char* base = static_cast<const char*>(x->const_data_ptr());
+      // the middle element of a contiguous tensor, else the first (a strided
+      // view's middle offset need not be inside its storage)
+      const size_t off = x->is_contiguous() ? static_cast<size_t>(ne / 2) * esz : 0;
+      const size_t avail = x->is_contiguous() ? static_cast<size_t>(ne) * esz - off : esz;
+      std::memcpy(&w, base + off, std::min<size_t>(8, avail));
+    }
+    h = (h ^ (w + static_cast<uint64_t>(j))) * 0x100000001b3ull;
+    h ^= h >> 31;
+  }
+  return h;
+}
+
+// shm_rows(rows, idx) -> (shm_keys(rows, idx), data_ptrs(rows, idx),
+// fingerprints): one pass over the tensors of freshly received models, whose
+// first touch is most of the cost (device cache path,
+// arena._cached_host_reduce); fingerprints[i] is content_fingerprint of
+// model i, or None where keys[i] is None.
 PyObject* py_shm_rows(PyObject*, PyObject* args) {
   PyObject *rows, *idx;
   if (!PyArg_ParseTuple(args, "OO", &rows, &idx)) return nullptr;
@@ -411,6 +444,26 @@ PyObject* py_shm_rows(PyObject*, PyObject* args) {
   if (!row_tensors(rows, idx, ts, &n, &t)) return nullptr;
   PyObject* keys = shm_keys_of(ts, n, t);
   if (!keys) return nullptr;
+  PyObject* fps = PyList_New(n);
+  if (!fps) {
+    Py_DECREF(keys);
+    return nullptr;
+  }
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    PyObject* f;
+    if (PyList_GET_ITEM(keys, i) == Py_None) {
+      f = Py_None;
+      Py_INCREF(f);
+    } else {
+      f = PyLong_FromUnsignedLongLong(content_fingerprint(ts, i, t));
+      if (!f) {
+        Py_DECREF(keys);
+        Py_DECREF(fps);
+        return nullptr;
+      }
+    }
+    PyList_SET_ITEM(fps, i, f);
+  }
   bool contiguous = true;
   for (const at::Tensor* x : ts) contiguous = contiguous && x->is_contiguous();
   PyObject* ptrs;
@@ -430,11 +483,13 @@ PyObject* py_shm_rows(PyObject*, PyObject* args) {
   }
   if (!ptrs) {
     Py_DECREF(keys);
+    Py_DECREF(fps);
     return nullptr;
   }
-  PyObject* res = PyTuple_Pack(2, keys, ptrs);
+  PyObject* res = PyTuple_Pack(3, keys, ptrs, fps);
   Py_DECREF(keys);
   Py_DECREF(ptrs);
+  Py_DECREF(fps);
   return res;
 }
 
@@ -1201,7 +1256,8 @@ PyMethodDef kMethods[] = {
     {"matches", py_matches, METH_VARARGS, "params match a [(shape, dtype)] signature"},
     {"data_ptrs", py_data_ptrs, METH_VARARGS, "data pointers of rows[i][k] for k in idx, None if not contiguous"},
     {"shm_keys", py_shm_keys, METH_VARARGS, "per model, the identity of its file_system shm storages, or None"},
-    {"shm_rows", py_shm_rows, METH_VARARGS, "(shm_keys(rows, idx), data_ptrs(rows, idx)) in one pass"},
+    {"shm_rows", py_shm_rows, METH_VARARGS,
+     "(shm_keys(rows, idx), data_ptrs(rows, idx), content fingerprints) in one pass"},
     {"chunk_scan", py_chunk_scan, METH_O,
      "chunk_scan(chunks) -> (same_dtype, place, device_index, numels, fans, ptrs or None)"},
     {"clone_init", py_clone_init, METH_VARARGS,

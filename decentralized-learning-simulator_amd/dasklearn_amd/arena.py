@@ -716,7 +716,7 @@ def _cached_host_reduce(cache, all_params, idx, layout, dt, dev, out, weights_f3
     memory) and cached; then the reduce and the D2H, one
     dlsim_host_wreduce_resident call. None when no model is in shared memory
     (the normal pipeline then runs). Returns as _host_pipeline."""
-    keys, ptrs = _pyhost.shm_rows(all_params, idx)
+    keys, ptrs, fps = _pyhost.shm_rows(all_params, idx)
     if all(k is None for k in keys):
         return None
     n = len(all_params)
@@ -726,7 +726,8 @@ def _cached_host_reduce(cache, all_params, idx, layout, dt, dev, out, weights_f3
     full = [None if k is None else (k, dev.index, dt, total) for k in keys]
     with cache.lock:
         cache.order(stream)
-        rows = [None if k is None else cache.get(k) for k in full]  # device addresses of resident rows
+        # device addresses of resident rows (a stale entry drops out here)
+        rows = [None if k is None else cache.get(k, fps[i]) for i, k in enumerate(full)]
         resident = [r is not None for r in rows]
         miss = [i for i in range(n) if rows[i] is None]
         # cache slots for the keyed misses (one per distinct key), never
@@ -783,7 +784,7 @@ def _cached_host_reduce(cache, all_params, idx, layout, dt, dev, out, weights_f3
             if staged:
                 STAGING.release(dev, dt, stream, synced, device_rows=False)
         for i, t in slot_of.items():
-            cache.put(full[i], t)
+            cache.put(full[i], t, fps[i])
         st = cache.stats
         st["hits"] += n - len(miss)
         st["misses"] += sum(1 for i in miss if full[i] is not None)

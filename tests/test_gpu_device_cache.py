@@ -169,3 +169,20 @@ def test_non_contiguous_shared_parameters(cache):
         assert cache.stats["hits"] == 6 and cache.stats["misses"] == 3
     finally:
         tmp.set_sharing_strategy(prev)
+
+
+def test_a_model_written_in_place_is_not_served_stale(shm_models, cache):
+    """a cached model trained in place afterwards (the
+    reference trains its input model in place, functions.py:57) no longer
+    matches its entry's content fingerprint: the entry is dropped, the model
+    sent again, and the result is the new model's, exact."""
+    ms = shm_models
+    _check(ms[:4], None)
+    assert cache.stats["misses"] == 4
+    with torch.no_grad():
+        for q in ms[1].parameters():
+            q.add_(0.01)  # an SGD-like update of every element, same shm storage
+    _check(ms[:4], None)
+    assert cache.stats["stale"] == 1 and cache.stats["hits"] == 3 and cache.stats["misses"] == 5
+    _check(ms[:4], [0.4, 0.3, 0.2, 0.1])  # the re-sent row is cached again
+    assert cache.stats["hits"] == 7 and cache.stats["stale"] == 1
