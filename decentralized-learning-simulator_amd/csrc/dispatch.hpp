@@ -522,6 +522,10 @@ int run_batched(int b, const int* fan_in, const void* const* in, const float* w,
   auto batchable = [&](int t) {
     if (nelem[t] == 0 || fan_in[t] > 16) return false;
     if (nelem[t] * Op::kBytes > kMaxLaunchOutBytes) return false;
+    // a task the deferred-store kernel takes (>= 20 MB per stream) runs alone
+    // through it: a launch that size amortises its own overhead, and the
+    // batch kernel interleaves its stores
+    if (use_defer<Op>(fan_in[t], nelem[t])) return false;
     if (!aligned16(outs[t])) return false;
     for (int i = 0; i < fan_in[t]; ++i)
       if (!aligned16(in[off[t] + i])) return false;

@@ -447,3 +447,23 @@ def test_randomised_parity_soak():
     r = subprocess.run([sys.executable, os.path.join(root, "scripts", "fuzz_parity.py"), "--seconds", "20",
                         "--seed", "7"], capture_output=True, text=True, timeout=100)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+def test_batched_call_runs_large_tasks_through_the_deferred_kernel():
+    """dlsim_wreduce_batched with tasks of >= 20 MB per stream (RoundExecutor's
+    waves of ResNet-18-sized device models): those run alone through the
+    deferred-store kernel, the small ones ride the batch kernel; every output
+    bit-exact against the oracle."""
+    g = torch.Generator(device=dev()).manual_seed(77)
+    specs = [(4, 5_000_003), (3, 70_001), (7, 5_242_880), (17, 5_000_001), (2, 1_000)]
+    tasks, host = [], []
+    for n, p in specs:
+        xs = [(torch.randn(p, generator=g, device=dev()) * 0.05) for _ in range(n)]
+        w = orc.reference_weights(n, list(np.random.default_rng(n).dirichlet(np.ones(n))))
+        tasks.append((xs, w, torch.empty(p, device=dev())))
+        host.append((np.stack([x.cpu().numpy() for x in xs]), w))
+    _native.wreduce_batched(tasks)
+    for (xs, w, out), (hx, hw) in zip(tasks, host):
+        assert orc.same_bits(out.cpu().numpy(), orc.wreduce_rows_f32(hx, hw))
+    del tasks, host
+    torch.cuda.empty_cache()
