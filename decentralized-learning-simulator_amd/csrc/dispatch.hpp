@@ -164,7 +164,7 @@ hipError_t launch_class(const S& s, int n, void* out, size_t nelem, hipStream_t 
 }
 
 // Deferred stores (dlsim::k_wreduce_defer): fp32 policies,
-// fan-in >= 4 (fixed, and the grouped form above 14), >= 20 MB per stream
+// fan-in >= 3 (fixed, and the grouped form above 14), >= 20 MB per stream
 // (size class 2; use_defer). One block (512
 // lanes, ~190-250 VGPRs: one block per CU) folds R rows of 512 vectors.
 // defer_rows picks an even R (profiles/r05_defer/, bench A/B in fresh
@@ -188,13 +188,27 @@ hipError_t launch_class(const S& s, int n, void* out, size_t nelem, hipStream_t 
 constexpr int kDeferU = 2, kDeferRMin = 4, kDeferOneRoundMax = 24;
 // results per lane a block can hold: 32 (128 VGPRs) while the fan-in's loads
 // fit beside them, 24 from fan-in 12 (no spills: tests/test_isa_audit.py)
-template <int NF> constexpr int defer_rmax() { return NF >= 12 ? 24 : 32; }  // NF = 0 (grouped): 32
-// Instantiated for fan-in 4..14. Fan-in 11-14 defers only from 16 rows per
-// CU (8.4 M fp32 elements on 256 CUs): 12 and 14 x 11.2 M 89.9 / 103.4 us
-// against 92.1 / 106.2 tiled, but 14 x 5 M 48.4 against 46.9
-// (profiles/r05y/, r05z/). DLSIM_DEFER_MAX_FAN_IN=k (read once; A/B runs):
-// no deferred launch above fan-in k.
-template <class Op, int NF> constexpr bool defer_eligible() { return Op::kBytes == 4 && NF >= 4; }
+template <class Op, int NF> constexpr int defer_rmax() { return NF >= 12 ? 24 : 32; }  // NF = 0 (grouped): 32
+// Fan-in 11-14 defers only from 16 rows per CU (8.4 M fp32 elements on 256
+// CUs): 12 and 14 x 11.2 M 89.9 / 103.4 us against 92.1 / 106.2 tiled, but
+// 14 x 5 M 48.4 against 46.9 (profiles/r05_defer/r05y*, r05z*).
+// DLSIM_DEFER_MAX_FAN_IN=k (read once; A/B runs): no deferred launch above
+// fan-in k.
+// Instantiated for fp32 fan-in >= 2 and the grouped form; used from fan-in
+// defer_min_fan_in(), 3: n = 3 at 11.2 M 28.74 against 29.80 us tiled, n = 2
+// loses (23.79 against 22.55 at 11.2 M, 67.06 against 58.56 at 31 M). 2-byte
+// elements were tried (fixed fan-in 2-6) and did not pay: bf16 n = 2 at 125 M
+// (cfg4) 126.8 against 114.9 us, at 31 M 32.66 against 30.04, n = 4 at 11.2 M
+// even (profiles/r05_defer/r05ai_*). DLSIM_DEFER_MIN_FAN_IN=k (read once; A/B
+// runs).
+template <class Op, int NF> constexpr bool defer_eligible() { return Op::kBytes == 4 && (NF >= 2 || NF == 0); }
+inline int defer_min_fan_in() {
+  static const int k = [] {
+    const char* e = std::getenv("DLSIM_DEFER_MIN_FAN_IN");
+    return e ? std::atoi(e) : 3;
+  }();
+  return k;
+}
 constexpr int kDeferWideFanIn = 10;
 constexpr size_t kDeferWideRowsPerCu = 16;
 inline bool defer_on() {
@@ -254,7 +268,7 @@ inline bool defer_grouped_on() {
   return on;
 }
 template <class Op> bool use_defer(int n, size_t nelem) {
-  if (Op::kBytes != 4 || n < 4 || n > defer_max_fan_in() || !defer_on()) return false;
+  if (Op::kBytes != 4 || n < std::max(2, defer_min_fan_in()) || n > defer_max_fan_in() || !defer_on()) return false;
   if (size_class<Op>(nelem, n <= max_fixed_fan_in<Op>() ? n : 0) != 2) return false;
   if (n > max_fixed_fan_in<Op>()) return defer_grouped_on();
   if (n <= kDeferWideFanIn) return true;
@@ -272,11 +286,11 @@ template <class Op> const char* kernel_name(int n, size_t nelem) {
 template <class Op, class S, int NF>
 hipError_t launch_defer(const S& s, int n, void* out, size_t nelem, hipStream_t st) {
   const size_t nvec = nelem / Op::E;
-  const int R = defer_rows(nvec, static_cast<size_t>(device_cus()), defer_rmax<NF>());
+  const int R = defer_rows(nvec, static_cast<size_t>(device_cus()), defer_rmax<Op, NF>());
   const size_t span = static_cast<size_t>(dlsim::kDeferBlock) * static_cast<size_t>(R);
   const size_t blocks = (nvec + span - 1) / span;
   if (blocks == 0 || blocks > 0x7fffffffu) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((dlsim::k_wreduce_defer<Op, S, NF, group_size<Op>(), defer_rmax<NF>(), kDeferU, kStore>),
+  hipLaunchKernelGGL((dlsim::k_wreduce_defer<Op, S, NF, group_size<Op>(), defer_rmax<Op, NF>(), kDeferU, kStore>),
                      dim3(static_cast<unsigned>(blocks)), dim3(dlsim::kDeferBlock), 0, st, s, n, R, out, nvec, nelem);
   return hipGetLastError();
 }
@@ -286,14 +300,14 @@ hipError_t launch_tiles(const S& s, int n, void* out, size_t nelem, hipStream_t 
   if constexpr (NF > 0) {
     const int c = size_class<Op>(nelem, NF);
     if constexpr (defer_eligible<Op, NF>())
-      if (c == 2 && use_defer<Op>(NF, nelem)) return launch_defer<Op, S, NF>(s, n, out, nelem, st);
+      if (use_defer<Op>(NF, nelem)) return launch_defer<Op, S, NF>(s, n, out, nelem, st);
     switch (c) {
       case 0: return launch_class<Op, S, NF, 0>(s, n, out, nelem, st);
       case 1: return launch_class<Op, S, NF, 1>(s, n, out, nelem, st);
       default: return launch_class<Op, S, NF, 2>(s, n, out, nelem, st);
     }
   } else {
-    if constexpr (Op::kBytes == 4)
+    if constexpr (defer_eligible<Op, 0>())
       if (use_defer<Op>(n, nelem)) return launch_defer<Op, S, 0>(s, n, out, nelem, st);
     return size_class<Op>(nelem) == 0 ? launch_class<Op, S, 0, 0>(s, n, out, nelem, st)
                                       : launch_class<Op, S, 0, 2>(s, n, out, nelem, st);

@@ -169,7 +169,7 @@ def test_library_errors_stay_on_the_calling_thread():
 
 def test_kernel_name_follows_the_dispatch():
     """dlsim_kernel_name (host logic only, no GPU: 256 CUs assumed when the
-    device query fails): the deferred-store kernel for fp32 fan-in 4-10 and
+    device query fails): the deferred-store kernel for fp32 fan-in 3-10 and
     above 14 (grouped) from 20 MB per stream, 11-14 from 16 rows of 512
     vectors per CU; the tiled kernel otherwise (dispatch.hpp use_defer)."""
     import torch
@@ -180,7 +180,8 @@ def test_kernel_name_follows_the_dispatch():
     assert _native.kernel_name(8, 11_181_642, f32, None) == d  # dlsim_mean
     assert _native.kernel_name(8, 4_999_999, f32) == t  # below 20 MB
     assert _native.kernel_name(8, 5_000_000, f32) == d
-    assert _native.kernel_name(3, 11_181_642, f32) == t
+    assert _native.kernel_name(3, 11_181_642, f32) == d
+    assert _native.kernel_name(2, 11_181_642, f32) == t
     assert _native.kernel_name(2, 125_000_000, f32) == t
     assert _native.kernel_name(12, 5_000_000, f32) == t  # < 16 rows per CU
     assert _native.kernel_name(12, 11_181_642, f32) == d

@@ -295,6 +295,7 @@ def test_launch_shapes_either_side_of_the_size_switch(dtype, p, n):
 
 @pytest.mark.parametrize("n,p", [
     (4, 5_000_003),            # ragged last block (bounds-checked rows) and an E tail of 3
+    (3, 5_000_002),            # the smallest deferred fan-in
     (5, 4 * 512 * 10 * 245),   # whole rows only, no tail
     (7, 11_181_642 + 1),       # the north star's grid (R = 12), E tail of 1
     (10, 8_392_711),           # the largest deferred fan-in, odd R (duplicate-row loads)

@@ -70,7 +70,8 @@ def test_no_kernel_spills_and_deferred_kernels_present(report):
     kernel keeps up to 32 results per lane in VGPRs: a rolled loop would put
     them in scratch, and its grouped form reads its kernel-argument slots in
     place), and the deferred kernels exist for fp32 fixed fan-in 4..14 and the
-    grouped form (dispatch.hpp defer_eligible)."""
+    grouped form, instantiated from fan-in 2 (dispatch.hpp defer_eligible,
+    DESIGN.md §5e)."""
     assert report["spilling_kernels"] == [], json.dumps(report["spilling_kernels"][:10], indent=1)
     names = set()
     for co in audit_isa.code_objects(audit_isa.LIB):
@@ -79,6 +80,6 @@ def test_no_kernel_spills_and_deferred_kernels_present(report):
         got = sorted(n for n in names if "k_wreduce_defer" in n and pol in n)
         # template args <Op, S, NF, G, RMAX, U, STP>: ...ELi<NF>ELi8ELi<RMAX>ELi2ELi2EE
         # (RMAX 24 from NF 12; NF 0 = the grouped form)
-        for nf in list(range(4, 15)) + [0]:
+        for nf in list(range(2, 15)) + [0]:
             assert any(f"ELi{nf}ELi8ELi{32 if nf < 12 else 24}ELi2ELi2EE" in n for n in got), (pol, nf)
-        assert not any(f"ELi{nf}ELi8ELi32ELi2ELi2EE" in n for n in got for nf in (1, 2, 3)), pol
+        assert not any(f"ELi1ELi8ELi32ELi2ELi2EE" in n for n in got), pol
