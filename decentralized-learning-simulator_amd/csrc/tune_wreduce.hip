@@ -596,8 +596,25 @@ void launch_bal(const Slots<128>& s, int n, void* out, size_t nvec, size_t nelem
 // blocks (R chosen so the grid fits the chip) the whole chip reads first and
 // writes last, so HBM turns around far less often. U tiles' loads are issued
 // together. Same fold order as reduce_tile: bit-exact.
-template <class Op, int NF, int R, int U, int STP, int BS>
-__device__ __forceinline__ void defer_body(const Slots<128>& s, const OutRef& o, size_t base) {
+// Grid-wide rendezvous between the read phase and the stores (round 5
+// experiment): every block adds 1 to a counter that only grows (the launch's
+// target is epoch * grid) and waits, bounded by a ~1 ms timeout after which it
+// stores anyway -- no result depends on it; it only lines the phases up.
+__device__ __forceinline__ void grid_rendezvous(unsigned* counter, unsigned target) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t t0 = wall_clock64();
+    while (__hip_atomic_load(counter, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      if (wall_clock64() - t0 > 100000) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+}
+template <class Op, int NF, int R, int U, int STP, int BS, bool BAR = false>
+__device__ __forceinline__ void defer_body(const Slots<128>& s, const OutRef& o, size_t base,
+                                           unsigned* counter = nullptr, unsigned target = 0) {
   u32x4 res[R];
 #pragma unroll
   for (int r0 = 0; r0 < R; r0 += U) {
@@ -623,6 +640,7 @@ __device__ __forceinline__ void defer_body(const Slots<128>& s, const OutRef& o,
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
   }
+  if constexpr (BAR) grid_rendezvous(counter, target);
 #pragma unroll
   for (int r = 0; r < R; ++r) store_vec<STP>(o, base + static_cast<size_t>(r) * BS, res[r]);
 }
@@ -644,6 +662,41 @@ __global__ __launch_bounds__(BS, MINB) void k_defer(const Slots<128> s, int n, v
     if (j < nelem) fold_scalar<Op, Slots<128>>(s, n, out, j);
   }
 }
+// k_defer with the rendezvous: every block of the grid must be resident at
+// once (grid <= CUs, one block per CU by the LDS pin); the partial last block
+// joins the rendezvous too.
+template <class Op, int NF, int R, int U, int STP, int BS>
+__global__ __launch_bounds__(BS, 1) void k_defer_bar(const Slots<128> s, int n, void* __restrict__ out, size_t nvec,
+                                                     size_t nelem, unsigned* counter, unsigned target) {
+  const size_t base = static_cast<size_t>(blockIdx.x) * BS * R + threadIdx.x;
+  const OutRef o = make_out<STP>(out, nvec);
+  if (static_cast<size_t>(blockIdx.x + 1) * BS * R <= nvec) {
+    defer_body<Op, NF, R, U, STP, BS, true>(s, o, base, counter, target);
+  } else {
+    grid_rendezvous(counter, target);
+    for (int r = 0; r < R; ++r)
+      reduce_tile<Op, Slots<128>, NF, 8, 1, 1, true, STP, BS>(s, n, o, base + static_cast<size_t>(r) * BS, nvec);
+  }
+  if (blockIdx.x == 0 && threadIdx.x < kBlock) {
+    const size_t j = nvec * Op::E + threadIdx.x;
+    if (j < nelem) fold_scalar<Op, Slots<128>>(s, n, out, j);
+  }
+}
+template <class Op, int NF, int R, int U, int STP, int BS, int LDSKB>
+void launch_defer_bar(const Slots<128>& s, int n, void* out, size_t nvec, size_t nelem, hipStream_t st, int) {
+  static unsigned* counter = nullptr;
+  static unsigned epoch = 0;
+  if (!counter) {
+    CK(hipMalloc(&counter, 256));
+    CK(hipMemset(counter, 0, 256));
+  }
+  const size_t per = static_cast<size_t>(BS) * R;
+  const unsigned grid = static_cast<unsigned>((nvec + per - 1) / per);
+  ++epoch;
+  hipLaunchKernelGGL((k_defer_bar<Op, NF, R, U, STP, BS>), dim3(grid), dim3(BS), (size_t)LDSKB * 1024, st, s, n, out,
+                     nvec, nelem, counter, epoch * grid);
+}
+
 template <class Op, int NF, int R, int U, int STP, int MINB = 2, int BS = kBlock, int LDSKB = 0>
 void launch_defer(const Slots<128>& s, int n, void* out, size_t nvec, size_t nelem, hipStream_t st, int) {
   const size_t per = static_cast<size_t>(BS) * R;
@@ -751,6 +804,12 @@ void add_defer(std::vector<Variant>& vs, int n) {
       vs.push_back({p + "_V2_bnt_blk", launch_ts<Op, NF, 8, 2, 1, 2, false>, 0});
     }
     vs.push_back({p + "_dauto_B512_U2_lds", launch_defer_auto<Op, NF, 2, 512, 96>, 0});
+    if constexpr (NF == 8) {
+      // the grid rendezvous before the stores: 167-172 us (profiles/r05_defer/r05ak/)
+      if (getenv("DLSIM_TUNE_RENDEZVOUS"))
+        vs.push_back({p + "_dbar_R22_B512_U2_lds", launch_defer_bar<Op, NF, 22, 2, 2, 512, 96>, 0});
+      vs.push_back({p + "_d_R22_B512_U2_lds", launch_defer<Op, NF, 22, 2, 2, 1, 512, 96>, 0});
+    }
     vs.push_back({p + "_dauto_B512_U2", launch_defer_auto<Op, NF, 2, 512, 0>, 0});
     vs.push_back({p + "_dauto_B512_U1_lds", launch_defer_auto<Op, NF, 1, 512, 96>, 0});
     vs.push_back({p + "_dauto_B256_U2_lds", launch_defer_auto<Op, NF, 2, 256, 96>, 0});
