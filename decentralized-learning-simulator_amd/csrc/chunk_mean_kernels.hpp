@@ -428,4 +428,133 @@ __global__ __launch_bounds__(kBlock) void k_chunk_mean_table(const void* const* 
   cm_task<Op, PtrArgs, SH, 4>(a, m, out, n, ilp_begin, flags, blockIdx.x, 0);
 }
 
+// ---- deferred stores (round 5; the reduce's k_wreduce_defer) ----
+// The cascade columns of every task cut into rows of kDeferBlock vectors; a
+// 512-lane block folds up to R rows of one task (lane t: vector t of each
+// row), keeps the packed means in registers and stores them together. The
+// order per element is cm_tile's: rows of contributors folded in order into
+// level 0 from +0, level 0 into level 1 after every 16, the levels summed at
+// the end, one division.
+//
+// U rows' vectors v0 + u * kDeferBlock (a row past R re-reads row v0's,
+// already in flight) over the m contributors, RF at a time.
+template <class Op, class A, int RF, int U>
+__device__ __forceinline__ void cm_rows_fold(const A& a, int m, size_t v0, int r0, int R, float div,
+                                             u32x4 (&res)[U]) {
+  using T = acc_t<Op>;
+  T acc[2][U][Op::E];
+#pragma unroll
+  for (int l = 0; l < 2; ++l)
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int e = 0; e < Op::E; ++e) acc[l][u][e] = T(0);
+  for (int i0 = 0; i0 < m; i0 += 16) {
+    const int cnt = m - i0 < 16 ? m - i0 : 16;
+#pragma unroll
+    for (int h = 0; h < 16; h += RF) {
+      if (h < cnt) {
+        u32x4 r[RF][U];
+#pragma unroll
+        for (int g = 0; g < RF; ++g) {
+          if (h + g < cnt) {
+            const void* src = a.ptr(i0 + h + g);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+              const int row = r0 + u < R ? r0 + u : r0;
+              r[g][u] = ld16<1>(src, v0 + static_cast<size_t>(row) * kDeferBlock);
+            }
+          }
+        }
+#pragma unroll
+        for (int g = 0; g < RF; ++g) {
+          if (h + g < cnt) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+              T x[Op::E];
+              unpack<Op>(r[g][u], x);
+#pragma unroll
+              for (int e = 0; e < Op::E; ++e) acc[0][u][e] = cm_add<Op>(acc[0][u][e], x[e]);
+            }
+          }
+        }
+      }
+    }
+    if (cnt == 16) {  // m < 256 (kernel-argument batches): two levels
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int e = 0; e < Op::E; ++e) {
+          acc[1][u][e] = cm_add<Op>(acc[1][u][e], acc[0][u][e]);
+          acc[0][u][e] = T(0);
+        }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+#pragma unroll
+    for (int e = 0; e < Op::E; ++e) acc[0][u][e] = cm_add<Op>(acc[0][u][e], acc[1][u][e]);
+    res[u] = pack<Op>(acc[0][u], div);
+  }
+}
+
+// Kernel-argument batch of 16-B aligned tasks (kCmVec), m < 256: blocks
+// 0 .. ntasks-1 are the tasks' ragged blocks (the partial row, the head and
+// the scalar columns, on the first 256 lanes as cm_task's block 0 does them);
+// block ntasks + f is row block f of the concatenated tasks (block_start),
+// rows [j * R, min((j + 1) * R, rows of the task)) of its task.
+template <class Op, int RF, int RMAX, int U>
+__global__ __launch_bounds__(kDeferBlock) void k_chunk_mean_defer(const ChunkMeanSlots s, int R) {
+  const uint32_t bid = blockIdx.x;
+  int t = 0;
+  uint32_t local = 0;
+  if (bid < static_cast<uint32_t>(s.ntasks)) {
+    t = static_cast<int>(bid);
+  } else {
+    const uint32_t f = bid - static_cast<uint32_t>(s.ntasks);
+    while (t + 1 < s.ntasks && f >= s.block_start[t + 1]) ++t;  // wave-uniform scan
+    local = f - s.block_start[t] + 1;
+  }
+  const PtrArgs a{s.p + s.ptr_off[t]};
+  const int m = s.m[t];
+  const size_t n = s.nelem[t], ilp_begin = s.ilp_begin[t];
+  const uint32_t head = s.head[t];
+  const float div = static_cast<float>(m);
+  const size_t hb = static_cast<size_t>(head) * Op::kBytes;
+  const ShiftArgs<PtrArgs> sa{a, hb};
+  const size_t nvec = (ilp_begin - head) / Op::E;
+  const size_t rows = nvec / kDeferBlock;
+  const OutRef o = make_out<kCmStore<Op>>(static_cast<char*>(s.out[t]) + hb, nvec);
+  if (local == 0) {
+    if (threadIdx.x >= kBlock) return;  // whole waves 4-7: the barriers below count the rest
+    if (rows * kDeferBlock < nvec) {  // the partial row: 256 lanes x 2 vectors, bounds-checked
+      using PT = CmShape<kDeferBlock / kBlock, false, RF>;
+      cm_tile<Op, ShiftArgs<PtrArgs>, PT, 2, true, true>(sa, m, o, rows * kDeferBlock + threadIdx.x, nvec,
+                                                         ilp_begin - head, div);
+    }
+    if (head > 0) cm_scalar_cols<Op, PtrArgs>(a, m, s.out[t], 0, head, ilp_begin, false, div);
+    const size_t c0 = head + nvec * Op::E;
+    if (c0 < n) cm_scalar_cols<Op, PtrArgs>(a, m, s.out[t], c0, n, ilp_begin, (s.flags[t] & kCmInner) != 0, div);
+    return;
+  }
+  const size_t first = static_cast<size_t>(local - 1) * static_cast<size_t>(R);
+  const int Rb = static_cast<int>(rows - first < static_cast<size_t>(R) ? rows - first : static_cast<size_t>(R));
+  const size_t v0 = first * kDeferBlock + threadIdx.x;
+  u32x4 res[RMAX];
+#pragma unroll
+  for (int r0 = 0; r0 < RMAX; r0 += U) {
+    if (r0 < Rb) {
+      u32x4 ru[U];
+      cm_rows_fold<Op, ShiftArgs<PtrArgs>, RF, U>(sa, m, v0, r0, Rb, div, ru);
+#pragma unroll
+      for (int u = 0; u < U; ++u) res[r0 + u] = ru[u];
+    }
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int r = 0; r < RMAX; ++r)
+    if (r < Rb) store_vec<kCmStore<Op>>(o, v0 + static_cast<size_t>(r) * kDeferBlock, res[r]);
+}
+
 }  // namespace dlsim

@@ -760,6 +760,39 @@ using CmDefault = dlsim::CmShape<4, true, 8>;
 using CmFewRows = dlsim::CmShape<4, true, 4>;
 constexpr int kCmFewRowsMax = 6;
 
+// Deferred stores for the chunk means (dlsim::k_chunk_mean_defer, DESIGN.md
+// §6b): fp32 launches of 16-B aligned tasks of m >= 16 contributors each, at
+// least 20 MB per stream in all. ResNet-18 chunks, k = 10 (profiles/r05al_ab/,
+// r05am/): m = 16 120.2 against 124.1 us; fewer contributors lose (m = 4
+// 39.0 against 37.1, m = 10 80.8 against 78.5: the tiled kernel keeps more
+// loads in flight per lane there, and U = 4 rows per group did not recover
+// it). R: the fewest even rows per block with every row block of the launch
+// resident at once beside the ragged blocks (up to 24 rows), else two rounds,
+// else RMAX. DLSIM_CHUNK_DEFER=0 (read once): the tiled kernel;
+// DLSIM_DEFER_R=r: that R.
+constexpr int kCmDeferRMax = 32, kCmDeferU = kDeferU, kCmDeferMinRows = 16;
+inline bool chunk_defer_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("DLSIM_CHUNK_DEFER");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+inline int chunk_defer_rows(const std::vector<size_t>& rows, size_t cus) {
+  if (defer_r_override() > 0) return std::min(defer_r_override(), kCmDeferRMax);
+  const size_t nt = rows.size();
+  auto blocks = [&](size_t R) {
+    size_t b = 0;
+    for (size_t r : rows) b += (r + R - 1) / R;
+    return b;
+  };
+  for (size_t R = 4; R <= static_cast<size_t>(kDeferOneRoundMax); R += 2)
+    if (blocks(R) + nt <= cus) return static_cast<int>(R);
+  for (size_t R = 4; R <= static_cast<size_t>(kCmDeferRMax); R += 2)
+    if (blocks(R) + nt <= 2 * cus) return static_cast<int>(R);
+  return kCmDeferRMax;
+}
+
 template <class Op>
 int run_chunk_mean(int b, const int* fan_in, const void* const* in, void* const* outs, const size_t* nelem,
                    int threads, hipStream_t st) {
@@ -802,25 +835,74 @@ int run_chunk_mean(int b, const int* fan_in, const void* const* in, void* const*
   for (int t = 0; t < b; ++t) mmax = fan_in[t] > mmax ? fan_in[t] : mmax;
   const bool few_rows = mmax <= kCmFewRowsMax;
   static_assert(CmFewRows::VPT == CmDefault::VPT, "one block layout for both tile shapes");
-  dlsim::ChunkMeanSlots s;
-  std::memset(&s, 0, sizeof(s));
-  int nt = 0, np = 0;
-  size_t blocks = 0;  // the launch's grid: one ragged-end block per task + the full tiles
+  // one launch's tasks (kernel-argument batch): index, ilp_begin, flags, head
+  struct CmTask {
+    int t;
+    size_t ib;
+    uint8_t flags;
+    uint32_t head;
+  };
+  std::vector<CmTask> batch;
+  int np = 0;
+  size_t tiles = 0;  // the tiled kernel's grid for the batch so far
   auto flush = [&]() -> int {
-    if (nt == 0) return DLSIM_OK;
+    if (batch.empty()) return DLSIM_OK;
+    dlsim::ChunkMeanSlots s;
+    std::memset(&s, 0, sizeof(s));
+    // deferred stores: fp32, every task vector-aligned with m >= 16, >= 20 MB per stream
+    bool defer = Op::kBytes == 4 && chunk_defer_on();
+    size_t cols = 0;
+    std::vector<size_t> rows;
+    for (const CmTask& k : batch) {
+      defer = defer && (k.flags & dlsim::kCmVec) && fan_in[k.t] >= kCmDeferMinRows;
+      cols += nelem[k.t];
+      rows.push_back((k.ib - k.head) / Op::E / dlsim::kDeferBlock);
+    }
+    defer = defer && cols * Op::kBytes >= 20000000;
+    int R = 0;
+    if (defer) R = chunk_defer_rows(rows, static_cast<size_t>(device_cus()));
+    size_t blocks = 0;
+    int nt = 0, p = 0;
+    for (const CmTask& k : batch) {
+      const int m = fan_in[k.t];
+      const size_t tb = defer ? (rows[static_cast<size_t>(nt)] + R - 1) / R + 1 : task_blocks(k.ib, k.head);
+      s.block_start[nt] = static_cast<uint32_t>(blocks - static_cast<size_t>(nt));  // full blocks before task nt
+      s.ptr_off[nt] = static_cast<uint16_t>(p);
+      s.m[nt] = static_cast<uint16_t>(m);
+      s.out[nt] = outs[k.t];
+      s.nelem[nt] = nelem[k.t];
+      s.ilp_begin[nt] = k.ib;
+      s.flags[nt] = k.flags;
+      s.head[nt] = static_cast<uint8_t>(k.head);
+      for (int i = 0; i < m; ++i) s.p[p + i] = in[off[k.t] + i];
+      p += m;
+      blocks += tb;
+      ++nt;
+    }
     s.ntasks = nt;
     s.block_start[nt] = static_cast<uint32_t>(blocks - static_cast<size_t>(nt));
-    if (few_rows)
+    if (blocks > 0x7fffffffu) return fail(DLSIM_E_ARG, "chunk mean batch too large");
+    if (defer) {
+      if constexpr (Op::kBytes == 4) {
+        if (few_rows)
+          hipLaunchKernelGGL((dlsim::k_chunk_mean_defer<Op, CmFewRows::RF, kCmDeferRMax, kCmDeferU>),
+                             dim3(static_cast<unsigned>(blocks)), dim3(dlsim::kDeferBlock), 0, st, s, R);
+        else
+          hipLaunchKernelGGL((dlsim::k_chunk_mean_defer<Op, CmDefault::RF, kCmDeferRMax, kCmDeferU>),
+                             dim3(static_cast<unsigned>(blocks)), dim3(dlsim::kDeferBlock), 0, st, s, R);
+      }
+    } else if (few_rows) {
       hipLaunchKernelGGL((dlsim::k_chunk_mean_batch<Op, CmFewRows>), dim3(static_cast<unsigned>(blocks)),
                          dim3(dlsim::kBlock), 0, st, s);
-    else
+    } else {
       hipLaunchKernelGGL((dlsim::k_chunk_mean_batch<Op, CmDefault>), dim3(static_cast<unsigned>(blocks)),
                          dim3(dlsim::kBlock), 0, st, s);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "chunk mean batch launch");
-    std::memset(&s, 0, sizeof(s));
-    nt = np = 0;
-    blocks = 0;
+    batch.clear();
+    np = 0;
+    tiles = 0;
     return DLSIM_OK;
   };
   for (int t = 0; t < b; ++t) {
@@ -850,22 +932,14 @@ int run_chunk_mean(int b, const int* fan_in, const void* const* in, void* const*
       if (e2 != hipSuccess) return hip_fail(e2, "chunk mean pointer table free");
       continue;
     }
-    if (nt == dlsim::kCmMaxTasks || np + m > dlsim::kCmMaxPtrs || blocks + tb > 0x7fffffffu) {
+    if (static_cast<int>(batch.size()) == dlsim::kCmMaxTasks || np + m > dlsim::kCmMaxPtrs ||
+        tiles + tb > 0x7fffffffu) {
       int rc = flush();
       if (rc != DLSIM_OK) return rc;
     }
-    s.block_start[nt] = static_cast<uint32_t>(blocks - static_cast<size_t>(nt));  // full tiles before task nt
-    s.ptr_off[nt] = static_cast<uint16_t>(np);
-    s.m[nt] = static_cast<uint16_t>(m);
-    s.out[nt] = outs[t];
-    s.nelem[nt] = n;
-    s.ilp_begin[nt] = ib;
-    s.flags[nt] = flags;
-    s.head[nt] = static_cast<uint8_t>(head);
-    for (int i = 0; i < m; ++i) s.p[np + i] = in[off[t] + i];
+    batch.push_back({t, ib, flags, head});
     np += m;
-    blocks += tb;
-    ++nt;
+    tiles += tb;
   }
   return flush();
 }

@@ -450,3 +450,28 @@ def test_reconstruct_tied_parameters_follows_copy_order(where, k):
     assert out.b.weight is out.a.weight and out.again is out.seq
     for (na, ta), (nb, tb) in zip(out.state_dict().items(), ref.state_dict().items()):
         assert na == nb and orc.same_bits(ta.cpu().numpy(), tb.numpy()), na
+
+
+@pytest.mark.parametrize("m,k", [(16, 4), (16, 10), (17, 3), (31, 5), (40, 6), (5, 7)])
+def test_chunk_mean_deferred_launch(m, k):
+    """fp32 chunk launches of >= 20 MB per stream with every task 16-B
+    aligned and m >= 16 take the deferred-store kernel (k_chunk_mean_defer:
+    512-lane blocks of R rows, the ragged block per task):
+    chunks of a 6.3 M-element flat model cut at arbitrary points
+    (line-misaligned heads, partial rows, scalar tails), the level-1 flush at
+    16 rows (m = 16, 17, 31), launches split at the 192-input limit (m = 40:
+    some below 20 MB, tiled), m = 5 tiled: every element bit-identical to the
+    order-exact oracle at 4 worker threads."""
+    P = 6_300_001
+    g = torch.Generator(device=dev()).manual_seed(m * 100 + k)
+    flats = [torch.randn(P, generator=g, device=dev()) * 0.05 for _ in range(m)]
+    rng = np.random.default_rng(m + k)
+    cuts = sorted(set(int(c) // 4 * 4 for c in rng.integers(1, P - 1, size=k - 1)))
+    bounds = list(zip([0] + cuts, cuts + [P]))
+    tasks = [([f[b:e] for f in flats], torch.empty(e - b, device=dev())) for b, e in bounds]
+    _native.chunk_mean_batched(tasks, threads=4)
+    host = [f.cpu().numpy() for f in flats]
+    for (b, e), (_, out) in zip(bounds, tasks):
+        assert orc.same_bits(out.cpu().numpy(), orc.chunk_mean([h[b:e] for h in host], "f32", 4)), (b, e)
+    del flats, tasks
+    torch.cuda.empty_cache()
