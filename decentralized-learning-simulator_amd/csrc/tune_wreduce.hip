@@ -809,6 +809,10 @@ void add_defer(std::vector<Variant>& vs, int n) {
       if (getenv("DLSIM_TUNE_RENDEZVOUS"))
         vs.push_back({p + "_dbar_R22_B512_U2_lds", launch_defer_bar<Op, NF, 22, 2, 2, 512, 96>, 0});
       vs.push_back({p + "_d_R22_B512_U2_lds", launch_defer<Op, NF, 22, 2, 2, 1, 512, 96>, 0});
+      vs.push_back({p + "_d_R24_B512_U2_lds", launch_defer<Op, NF, 24, 2, 2, 1, 512, 96>, 0});
+      vs.push_back({p + "_d_R24_B512_U4_lds", launch_defer<Op, NF, 24, 4, 2, 1, 512, 96>, 0});
+      vs.push_back({p + "_d_R24_B512_U3_lds", launch_defer<Op, NF, 24, 3, 2, 1, 512, 96>, 0});
+      vs.push_back({p + "_d_R12_B1024_U2_lds", launch_defer<Op, NF, 12, 2, 2, 1, 1024, 96>, 0});
     }
     vs.push_back({p + "_dauto_B512_U2", launch_defer_auto<Op, NF, 2, 512, 0>, 0});
     vs.push_back({p + "_dauto_B512_U1_lds", launch_defer_auto<Op, NF, 1, 512, 96>, 0});
