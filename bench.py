@@ -238,6 +238,20 @@ def weights_for(kind: str, n: int) -> list:
     return [float(1.0 / n)] * n  # fedavg.py:14-15
 
 
+def _out_alloc(p, tdt, dev):
+    """An aggregate output as the product allocates it (arena_empty: the
+    output pool), or for placement A/B runs (DLSIM_BENCH_OUT_ALLOC) a
+    separate contiguous library block ("resident") or torch's allocator
+    ("torch"), 2 MiB-aligned."""
+    from dasklearn_amd.arena import aligned_empty, arena_empty, resident_empty
+    kind = os.environ.get("DLSIM_BENCH_OUT_ALLOC", "pool")
+    if kind == "resident":
+        return resident_empty(p, tdt, dev, 2 << 20)
+    if kind == "torch":
+        return aligned_empty(p, tdt, dev, 2 << 20)
+    return arena_empty(p, tdt, dev)
+
+
 class ReduceWorkload:
     """Rotating input sets and outputs, and prepared launches of one
     config's aggregate on one device: `launch(k)` runs step k (input set
@@ -293,7 +307,7 @@ class ReduceWorkload:
         for j in range(self.out_sets):
             x = rows[j % self.sets][0] if batch == 1 else rows[j % self.sets]
             if batch == 1:
-                out = arena_empty(p, tdt, dev)
+                out = _out_alloc(p, tdt, dev)
                 plan = _native.ReducePlan([x[i, :p] for i in range(n)], w32, out, mode)
                 assert all(t.data_ptr() % 16 == 0 for t in plan._keep[0]), "arena rows must be 16-B aligned"
                 self.outs.append(out)

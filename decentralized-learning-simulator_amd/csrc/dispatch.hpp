@@ -283,6 +283,30 @@ template <class Op> const char* kernel_name(int n, size_t nelem) {
   return use_defer<Op>(n, first) ? "dlsim::k_wreduce_defer" : "dlsim::k_wreduce_tiles";
 }
 
+// The exact fp32 policy with a fixed fan-in launches the kernel compiled for
+// its R (every even R up to RMAX): the row groups and stores run unguarded
+// and straight-line. A runtime R guards each with a branch: the north star
+// ran 63.35-63.38 us that way against 61.60-61.63 compiled for R = 22, in one
+// process of the tuning harness (profiles/r05_defer/r05aw/). The other
+// policies (FAST, mean, the probe) and the grouped form take the runtime R.
+template <class Op, class S, int NF, int RC>
+hipError_t launch_defer_rc(const S& s, int n, void* out, size_t nvec, size_t nelem, int R, unsigned blocks,
+                           hipStream_t st) {
+  if constexpr (RC > defer_rmax<Op, NF>()) {
+    hipLaunchKernelGGL((dlsim::k_wreduce_defer<Op, S, NF, group_size<Op>(), defer_rmax<Op, NF>(), kDeferU, kStore>),
+                       dim3(blocks), dim3(dlsim::kDeferBlock), 0, st, s, n, R, out, nvec, nelem);
+    return hipGetLastError();
+  } else {
+    if (R == RC) {
+      hipLaunchKernelGGL(
+          (dlsim::k_wreduce_defer<Op, S, NF, group_size<Op>(), defer_rmax<Op, NF>(), kDeferU, kStore, RC>),
+          dim3(blocks), dim3(dlsim::kDeferBlock), 0, st, s, n, R, out, nvec, nelem);
+      return hipGetLastError();
+    }
+    return launch_defer_rc<Op, S, NF, RC + kDeferU>(s, n, out, nvec, nelem, R, blocks, st);
+  }
+}
+
 template <class Op, class S, int NF>
 hipError_t launch_defer(const S& s, int n, void* out, size_t nelem, hipStream_t st) {
   const size_t nvec = nelem / Op::E;
@@ -290,6 +314,8 @@ hipError_t launch_defer(const S& s, int n, void* out, size_t nelem, hipStream_t 
   const size_t span = static_cast<size_t>(dlsim::kDeferBlock) * static_cast<size_t>(R);
   const size_t blocks = (nvec + span - 1) / span;
   if (blocks == 0 || blocks > 0x7fffffffu) return hipErrorInvalidValue;
+  if constexpr (NF > 0 && std::is_same<Op, dlsim::F32Exact>::value)
+    return launch_defer_rc<Op, S, NF, kDeferU>(s, n, out, nvec, nelem, R, static_cast<unsigned>(blocks), st);
   hipLaunchKernelGGL((dlsim::k_wreduce_defer<Op, S, NF, group_size<Op>(), defer_rmax<Op, NF>(), kDeferU, kStore>),
                      dim3(static_cast<unsigned>(blocks)), dim3(dlsim::kDeferBlock), 0, st, s, n, R, out, nvec, nelem);
   return hipGetLastError();

@@ -704,6 +704,22 @@ void launch_defer(const Slots<128>& s, int n, void* out, size_t nvec, size_t nel
                      (size_t)LDSKB * 1024, st, s, n, out, nvec, nelem);
 }
 
+// The library's deferred kernel (wreduce_kernels.hpp k_wreduce_defer, runtime
+// R) on the harness's buffers: R rows per block, LDSKB of dynamic LDS.
+template <class Op, int NF, int R, int LDSKB>
+void launch_libdefer(const Slots<128>& s, int n, void* out, size_t nvec, size_t nelem, hipStream_t st, int) {
+  const size_t per = static_cast<size_t>(kDeferBlock) * R;
+  hipLaunchKernelGGL((dlsim::k_wreduce_defer<Op, Slots<128>, NF, 8, 32, 2, 2>), dim3((unsigned)((nvec + per - 1) / per)),
+                     dim3(kDeferBlock), (size_t)LDSKB * 1024, st, s, n, R, out, nvec, nelem);
+}
+
+template <class Op, int NF, int R>
+void launch_libdefer_c(const Slots<128>& s, int n, void* out, size_t nvec, size_t nelem, hipStream_t st, int) {
+  const size_t per = static_cast<size_t>(kDeferBlock) * R;
+  hipLaunchKernelGGL((dlsim::k_wreduce_defer<Op, Slots<128>, NF, 8, 32, 2, 2, R>),
+                     dim3((unsigned)((nvec + per - 1) / per)), dim3(kDeferBlock), 0, st, s, n, R, out, nvec, nelem);
+}
+
 // k_defer with R chosen from the size: the smallest R of the list with
 // ceil(nvec / (BS * R)) <= 256 blocks (one per CU), or the largest R (then
 // more than one block per CU).
@@ -809,6 +825,9 @@ void add_defer(std::vector<Variant>& vs, int n) {
       if (getenv("DLSIM_TUNE_RENDEZVOUS"))
         vs.push_back({p + "_dbar_R22_B512_U2_lds", launch_defer_bar<Op, NF, 22, 2, 2, 512, 96>, 0});
       vs.push_back({p + "_d_R22_B512_U2_lds", launch_defer<Op, NF, 22, 2, 2, 1, 512, 96>, 0});
+      vs.push_back({p + "_lib_R22", launch_libdefer<Op, NF, 22, 0>, 0});
+      vs.push_back({p + "_lib_R22_lds", launch_libdefer<Op, NF, 22, 96>, 0});
+      vs.push_back({p + "_libc_R22", launch_libdefer_c<Op, NF, 22>, 0});
       vs.push_back({p + "_d_R24_B512_U2_lds", launch_defer<Op, NF, 24, 2, 2, 1, 512, 96>, 0});
       vs.push_back({p + "_d_R24_B512_U4_lds", launch_defer<Op, NF, 24, 4, 2, 1, 512, 96>, 0});
       vs.push_back({p + "_d_R24_B512_U3_lds", launch_defer<Op, NF, 24, 3, 2, 1, 512, 96>, 0});

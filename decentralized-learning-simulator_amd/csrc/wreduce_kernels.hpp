@@ -681,8 +681,38 @@ __device__ __forceinline__ void defer_fold_group(const S& s, int i0, int cnt, si
       }
   }
 }
+// Compile-time R (RC), fixed fan-in: every row group and store unguarded.
+template <class Op, class S, int NF, int RC, int U, int STP>
+__device__ __forceinline__ void defer_rows_c(const S& s, const OutRef& o, size_t base) {
+  static_assert(NF > 0 && RC % U == 0, "fixed fan-in, whole row groups");
+  u32x4 res[RC];
+#pragma unroll
+  for (int r0 = 0; r0 < RC; r0 += U) {
+    u32x4 x[NF][U];
+#pragma unroll
+    for (int i = 0; i < NF; ++i)
+#pragma unroll
+      for (int u = 0; u < U; ++u) x[i][u] = ld16<1>(s.ptr(i), base + static_cast<size_t>(r0 + u) * kDeferBlock);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      acc_t<Op> a[1][Op::E];
+      const u32x4 x0[1] = {x[0][u]};
+      init_tile<Op, 1>(a, x0, false);
+#pragma unroll
+      for (int i = 0; i < NF; ++i) {
+        const u32x4 xi[1] = {x[i][u]};
+        fold_tile<Op, 1>(a, s.wt(i), xi);
+      }
+      res[r0 + u] = pack<Op>(a[0], s.divisor());
+    }
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int r = 0; r < RC; ++r) store_vec<STP>(o, base + static_cast<size_t>(r) * kDeferBlock, res[r]);
+}
 template <class Op, class S, int NF, int G, int RMAX, int U, int STP>
-__device__ __forceinline__ void defer_rows(const S& s, int n, const OutRef& o, size_t base, int R) {
+__device__ __forceinline__ void defer_rows(const S& s, int n, const OutRef& o, size_t base, int R, size_t nvec) {
   u32x4 res[RMAX];
 #pragma unroll
   for (int r0 = 0; r0 < RMAX; r0 += U) {
@@ -722,29 +752,36 @@ __device__ __forceinline__ void defer_rows(const S& s, int n, const OutRef& o, s
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
   }
+  // The stores run straight-line: a row past R goes to vector nvec, the first
+  // past the output's buffer range, which the hardware drops (a guarded
+  // store per row left a chain of branches around out-of-line stores).
+  static_assert(STP >= 0, "buffer stores: out-of-range rows are dropped");
 #pragma unroll
   for (int r = 0; r < RMAX; ++r)
-    if (r < R) store_vec<STP>(o, base + static_cast<size_t>(r) * kDeferBlock, res[r]);
+    store_vec<STP>(o, r < R ? base + static_cast<size_t>(r) * kDeferBlock : nvec, res[r]);
 }
 // Full blocks defer; the grid's last block, when partial, folds its rows one
 // at a time with bounds checks; block 0 also folds the < E scalar tail.
 // NF > 0: fixed fan-in n == NF; NF == 0: runtime n in groups of G.
-template <class Op, class S, int NF, int G, int RMAX, int U, int STP>
-__global__ __launch_bounds__(kDeferBlock) void k_wreduce_defer(const S s, int n, int R, void* __restrict__ out,
+template <class Op, class S, int NF, int G, int RMAX, int U, int STP, int RC = 0>
+__global__ __launch_bounds__(kDeferBlock) void k_wreduce_defer(const S s, int n, int Rrt, void* __restrict__ out,
                                                                size_t nvec, size_t nelem) {
+  const int R = RC > 0 ? RC : Rrt;
   const size_t span = static_cast<size_t>(kDeferBlock) * static_cast<size_t>(R);
   const size_t base = static_cast<size_t>(blockIdx.x) * span + threadIdx.x;
   const OutRef o = make_out<STP>(out, nvec);
   if (static_cast<size_t>(blockIdx.x + 1) * span <= nvec) {
-    if constexpr (NF > 0) {
-      defer_rows<Op, S, NF, G, RMAX, U, STP>(s, n, o, base, R);
+    if constexpr (RC > 0) {
+      defer_rows_c<Op, S, NF, RC, U, STP>(s, o, base);
+    } else if constexpr (NF > 0) {
+      defer_rows<Op, S, NF, G, RMAX, U, STP>(s, n, o, base, R, nvec);
     } else {
       // The grouped form indexes the slots at run time from 16 unrolled row
       // groups; read through `s` the compiler keeps a private copy of the
       // whole argument (1.5 KiB of scratch per lane for Slots<128>). `s` is
       // the first kernel argument: read it in place in the kernarg segment.
       const S* ks = (const S*)__builtin_amdgcn_kernarg_segment_ptr();
-      defer_rows<Op, S, NF, G, RMAX, U, STP>(*ks, n, o, base, R);
+      defer_rows<Op, S, NF, G, RMAX, U, STP>(*ks, n, o, base, R, nvec);
     }
   } else {
     for (int r = 0; r < R; ++r)

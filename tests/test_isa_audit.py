@@ -78,8 +78,13 @@ def test_no_kernel_spills_and_deferred_kernels_present(report):
         names |= set(audit_isa.kernels(audit_isa.disassemble(co)))
     for pol in ("8F32Exact", "7F32Fast", "7F32Mean"):
         got = sorted(n for n in names if "k_wreduce_defer" in n and pol in n)
-        # template args <Op, S, NF, G, RMAX, U, STP>: ...ELi<NF>ELi8ELi<RMAX>ELi2ELi2EE
-        # (RMAX 24 from NF 12; NF 0 = the grouped form)
+        # template args <Op, S, NF, G, RMAX, U, STP, RC>: ...ELi<NF>ELi8ELi<RMAX>ELi2ELi2ELi<RC>EE
+        # (RMAX 24 from NF 12; NF 0 = the grouped form; RC 0 = runtime R)
         for nf in list(range(2, 15)) + [0]:
-            assert any(f"ELi{nf}ELi8ELi{32 if nf < 12 else 24}ELi2ELi2EE" in n for n in got), (pol, nf)
-        assert not any(f"ELi1ELi8ELi32ELi2ELi2EE" in n for n in got), pol
+            assert any(f"ELi{nf}ELi8ELi{32 if nf < 12 else 24}ELi2ELi2ELi0EE" in n for n in got), (pol, nf)
+        assert not any(f"ELi1ELi8ELi32ELi2ELi2ELi0EE" in n for n in got), pol
+    # the exact policy's fixed fan-in kernels compiled per even R (dispatch.hpp launch_defer_rc)
+    exact = [n for n in names if "k_wreduce_defer" in n and "8F32Exact" in n]
+    for nf, rmax in ((3, 32), (8, 32), (11, 32), (12, 24), (14, 24)):
+        for rc in range(2, rmax + 1, 2):
+            assert any(f"ELi{nf}ELi8ELi{rmax}ELi2ELi2ELi{rc}EE" in n for n in exact), (nf, rc)
