@@ -288,7 +288,9 @@ template <class Op> const char* kernel_name(int n, size_t nelem) {
 // and straight-line. A runtime R guards each with a branch: the north star
 // ran 63.35-63.38 us that way against 61.60-61.63 compiled for R = 22, in one
 // process of the tuning harness (profiles/r05_defer/r05aw/). The other
-// policies (FAST, mean, the probe) and the grouped form take the runtime R.
+// policies (FAST, mean, the probe) and the grouped form take the runtime R
+// (the grouped form compiled per R measured the same: cfg3 120.76-120.90 us,
+// cfg5 661.9-662.3, profiles/r05_defer/r05az_*).
 template <class Op, class S, int NF, int RC>
 hipError_t launch_defer_rc(const S& s, int n, void* out, size_t nvec, size_t nelem, int R, unsigned blocks,
                            hipStream_t st) {

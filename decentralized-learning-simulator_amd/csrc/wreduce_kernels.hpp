@@ -681,16 +681,29 @@ __device__ __forceinline__ void defer_fold_group(const S& s, int i0, int cnt, si
       }
   }
 }
-// Compile-time R (RC), fixed fan-in: every row group and store unguarded.
-template <class Op, class S, int NF, int RC, int U, int STP>
-__device__ __forceinline__ void defer_rows_c(const S& s, const OutRef& o, size_t base) {
-  static_assert(NF > 0 && RC % U == 0, "fixed fan-in, whole row groups");
+// Compile-time R (RC): every row group and store unguarded. NF == 0: the
+// grouped form (runtime fan-in in groups of G, input order).
+template <class Op, class S, int NF, int G, int RC, int U, int STP>
+__device__ __forceinline__ void defer_rows_c(const S& s, int n, const OutRef& o, size_t base) {
+  static_assert(RC % U == 0, "whole row groups");
   u32x4 res[RC];
 #pragma unroll
   for (int r0 = 0; r0 < RC; r0 += U) {
-    u32x4 x[NF][U];
+    if constexpr (NF == 0) {
+      acc_t<Op> a[U][1][Op::E];
+      defer_fold_group<Op, S, 0, G, U>(s, 0, n < G ? n : G, base, r0, RC, true, a);
+      for (int i0 = G; i0 < n; i0 += G)
+        defer_fold_group<Op, S, 0, G, U>(s, i0, (n - i0) < G ? (n - i0) : G, base, r0, RC, false, a);
 #pragma unroll
-    for (int i = 0; i < NF; ++i)
+      for (int u = 0; u < U; ++u) res[r0 + u] = pack<Op>(a[u][0], s.divisor());
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      continue;
+    }
+    constexpr int K = NF > 0 ? NF : 1;
+    u32x4 x[K][U];
+#pragma unroll
+    for (int i = 0; i < K; ++i)
 #pragma unroll
       for (int u = 0; u < U; ++u) x[i][u] = ld16<1>(s.ptr(i), base + static_cast<size_t>(r0 + u) * kDeferBlock);
 #pragma unroll
@@ -699,7 +712,7 @@ __device__ __forceinline__ void defer_rows_c(const S& s, const OutRef& o, size_t
       const u32x4 x0[1] = {x[0][u]};
       init_tile<Op, 1>(a, x0, false);
 #pragma unroll
-      for (int i = 0; i < NF; ++i) {
+      for (int i = 0; i < K; ++i) {
         const u32x4 xi[1] = {x[i][u]};
         fold_tile<Op, 1>(a, s.wt(i), xi);
       }
@@ -771,8 +784,11 @@ __global__ __launch_bounds__(kDeferBlock) void k_wreduce_defer(const S s, int n,
   const size_t base = static_cast<size_t>(blockIdx.x) * span + threadIdx.x;
   const OutRef o = make_out<STP>(out, nvec);
   if (static_cast<size_t>(blockIdx.x + 1) * span <= nvec) {
-    if constexpr (RC > 0) {
-      defer_rows_c<Op, S, NF, RC, U, STP>(s, o, base);
+    if constexpr (RC > 0 && NF > 0) {
+      defer_rows_c<Op, S, NF, G, RC, U, STP>(s, n, o, base);
+    } else if constexpr (RC > 0) {
+      const S* ks = (const S*)__builtin_amdgcn_kernarg_segment_ptr();  // (below)
+      defer_rows_c<Op, S, 0, G, RC, U, STP>(*ks, n, o, base);
     } else if constexpr (NF > 0) {
       defer_rows<Op, S, NF, G, RMAX, U, STP>(s, n, o, base, R, nvec);
     } else {
