@@ -806,6 +806,14 @@ inline bool chunk_defer_on() {
   }();
   return on;
 }
+// DLSIM_CHUNK_DEFER_MIN_M=k (read once; A/B runs): defer from k contributors
+inline int chunk_defer_min_m() {
+  static const int k = [] {
+    const char* e = std::getenv("DLSIM_CHUNK_DEFER_MIN_M");
+    return e ? std::atoi(e) : kCmDeferMinRows;
+  }();
+  return k;
+}
 inline int chunk_defer_rows(const std::vector<size_t>& rows, size_t cus) {
   if (defer_r_override() > 0) return std::min(defer_r_override(), kCmDeferRMax);
   const size_t nt = rows.size();
@@ -819,6 +827,23 @@ inline int chunk_defer_rows(const std::vector<size_t>& rows, size_t cus) {
   for (size_t R = 4; R <= static_cast<size_t>(kCmDeferRMax); R += 2)
     if (blocks(R) + nt <= 2 * cus) return static_cast<int>(R);
   return kCmDeferRMax;
+}
+
+// The chunk kernel compiled for the launch's R (its whole row blocks run
+// unguarded, as the reduce's, launch_defer_rc); R past RMAX: the runtime form.
+template <class Op, int RF, int RC>
+void launch_cm_defer_rc(const dlsim::ChunkMeanSlots& s, int R, unsigned grid, hipStream_t st) {
+  if constexpr (RC > kCmDeferRMax) {
+    hipLaunchKernelGGL((dlsim::k_chunk_mean_defer<Op, RF, kCmDeferRMax, kCmDeferU>), dim3(grid),
+                       dim3(dlsim::kDeferBlock), 0, st, s, R);
+  } else {
+    if (R == RC) {
+      hipLaunchKernelGGL((dlsim::k_chunk_mean_defer<Op, RF, kCmDeferRMax, kCmDeferU, RC>), dim3(grid),
+                         dim3(dlsim::kDeferBlock), 0, st, s, R);
+      return;
+    }
+    launch_cm_defer_rc<Op, RF, RC + kCmDeferU>(s, R, grid, st);
+  }
 }
 
 template <class Op>
@@ -882,7 +907,7 @@ int run_chunk_mean(int b, const int* fan_in, const void* const* in, void* const*
     size_t cols = 0;
     std::vector<size_t> rows;
     for (const CmTask& k : batch) {
-      defer = defer && (k.flags & dlsim::kCmVec) && fan_in[k.t] >= kCmDeferMinRows;
+      defer = defer && (k.flags & dlsim::kCmVec) && fan_in[k.t] >= chunk_defer_min_m();
       cols += nelem[k.t];
       rows.push_back((k.ib - k.head) / Op::E / dlsim::kDeferBlock);
     }
@@ -912,12 +937,11 @@ int run_chunk_mean(int b, const int* fan_in, const void* const* in, void* const*
     if (blocks > 0x7fffffffu) return fail(DLSIM_E_ARG, "chunk mean batch too large");
     if (defer) {
       if constexpr (Op::kBytes == 4) {
+        const unsigned grid = static_cast<unsigned>(blocks);
         if (few_rows)
-          hipLaunchKernelGGL((dlsim::k_chunk_mean_defer<Op, CmFewRows::RF, kCmDeferRMax, kCmDeferU>),
-                             dim3(static_cast<unsigned>(blocks)), dim3(dlsim::kDeferBlock), 0, st, s, R);
+          launch_cm_defer_rc<Op, CmFewRows::RF, kDeferU>(s, R, grid, st);
         else
-          hipLaunchKernelGGL((dlsim::k_chunk_mean_defer<Op, CmDefault::RF, kCmDeferRMax, kCmDeferU>),
-                             dim3(static_cast<unsigned>(blocks)), dim3(dlsim::kDeferBlock), 0, st, s, R);
+          launch_cm_defer_rc<Op, CmDefault::RF, kDeferU>(s, R, grid, st);
       }
     } else if (few_rows) {
       hipLaunchKernelGGL((dlsim::k_chunk_mean_batch<Op, CmFewRows>), dim3(static_cast<unsigned>(blocks)),
