@@ -503,7 +503,7 @@ __device__ __forceinline__ void cm_rows_fold(const A& a, int m, size_t v0, int r
 // the scalar columns, on the first 256 lanes as cm_task's block 0 does them);
 // block ntasks + f is row block f of the concatenated tasks (block_start),
 // rows [j * R, min((j + 1) * R, rows of the task)) of its task.
-template <class Op, int RF, int RMAX, int U, int RC = 0>
+template <class Op, int RF, int RMAX, int U>
 __global__ __launch_bounds__(kDeferBlock) void k_chunk_mean_defer(const ChunkMeanSlots s, int R) {
   const uint32_t bid = blockIdx.x;
   int t = 0;
@@ -540,25 +540,6 @@ __global__ __launch_bounds__(kDeferBlock) void k_chunk_mean_defer(const ChunkMea
   const size_t first = static_cast<size_t>(local - 1) * static_cast<size_t>(R);
   const int Rb = static_cast<int>(rows - first < static_cast<size_t>(R) ? rows - first : static_cast<size_t>(R));
   const size_t v0 = first * kDeferBlock + threadIdx.x;
-  if constexpr (RC > 0) {
-    // a whole block of the launch's R == RC rows: unguarded and straight-line
-    // (a task's last block may hold fewer and takes the guarded loop below)
-    if (Rb == RC) {
-      u32x4 rc[RC];
-#pragma unroll
-      for (int r0 = 0; r0 < RC; r0 += U) {
-        u32x4 ru[U];
-        cm_rows_fold<Op, ShiftArgs<PtrArgs>, RF, U>(sa, m, v0, r0, RC, div, ru);
-#pragma unroll
-        for (int u = 0; u < U; ++u) rc[r0 + u] = ru[u];
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-      }
-#pragma unroll
-      for (int r = 0; r < RC; ++r) store_vec<kCmStore<Op>>(o, v0 + static_cast<size_t>(r) * kDeferBlock, rc[r]);
-      return;
-    }
-  }
   u32x4 res[RMAX];
 #pragma unroll
   for (int r0 = 0; r0 < RMAX; r0 += U) {

@@ -829,23 +829,6 @@ inline int chunk_defer_rows(const std::vector<size_t>& rows, size_t cus) {
   return kCmDeferRMax;
 }
 
-// The chunk kernel compiled for the launch's R (its whole row blocks run
-// unguarded, as the reduce's, launch_defer_rc); R past RMAX: the runtime form.
-template <class Op, int RF, int RC>
-void launch_cm_defer_rc(const dlsim::ChunkMeanSlots& s, int R, unsigned grid, hipStream_t st) {
-  if constexpr (RC > kCmDeferRMax) {
-    hipLaunchKernelGGL((dlsim::k_chunk_mean_defer<Op, RF, kCmDeferRMax, kCmDeferU>), dim3(grid),
-                       dim3(dlsim::kDeferBlock), 0, st, s, R);
-  } else {
-    if (R == RC) {
-      hipLaunchKernelGGL((dlsim::k_chunk_mean_defer<Op, RF, kCmDeferRMax, kCmDeferU, RC>), dim3(grid),
-                         dim3(dlsim::kDeferBlock), 0, st, s, R);
-      return;
-    }
-    launch_cm_defer_rc<Op, RF, RC + kCmDeferU>(s, R, grid, st);
-  }
-}
-
 template <class Op>
 int run_chunk_mean(int b, const int* fan_in, const void* const* in, void* const* outs, const size_t* nelem,
                    int threads, hipStream_t st) {
@@ -939,9 +922,11 @@ int run_chunk_mean(int b, const int* fan_in, const void* const* in, void* const*
       if constexpr (Op::kBytes == 4) {
         const unsigned grid = static_cast<unsigned>(blocks);
         if (few_rows)
-          launch_cm_defer_rc<Op, CmFewRows::RF, kDeferU>(s, R, grid, st);
+          hipLaunchKernelGGL((dlsim::k_chunk_mean_defer<Op, CmFewRows::RF, kCmDeferRMax, kCmDeferU>), dim3(grid),
+                             dim3(dlsim::kDeferBlock), 0, st, s, R);
         else
-          launch_cm_defer_rc<Op, CmDefault::RF, kDeferU>(s, R, grid, st);
+          hipLaunchKernelGGL((dlsim::k_chunk_mean_defer<Op, CmDefault::RF, kCmDeferRMax, kCmDeferU>), dim3(grid),
+                             dim3(dlsim::kDeferBlock), 0, st, s, R);
       }
     } else if (few_rows) {
       hipLaunchKernelGGL((dlsim::k_chunk_mean_batch<Op, CmFewRows>), dim3(static_cast<unsigned>(blocks)),
