@@ -164,8 +164,8 @@ hipError_t launch_class(const S& s, int n, void* out, size_t nelem, hipStream_t 
 }
 
 // Deferred stores (dlsim::k_wreduce_defer): fp32 policies,
-// fan-in >= 3 (fixed, and the grouped form above 14), >= 20 MB per stream
-// (size class 2; use_defer). One block (512
+// fan-in >= 3 (fixed, and the grouped form above 14), >= 10 MB per stream
+// (use_defer). One block (512
 // lanes, ~190-250 VGPRs: one block per CU) folds R rows of 512 vectors.
 // defer_rows picks an even R (profiles/r05_defer/, bench A/B in fresh
 // processes, outputs rotating beyond the Infinity Cache; odd R re-reads a
@@ -254,9 +254,9 @@ inline int defer_rows(size_t nvec, size_t cus, int rmax) {
   return best;
 }
 
-// Does a launch of n inputs of nelem elements defer? Fixed fan-in: size class
-// 2 (>= 20 MB per stream), fan-in 11-14 from 16 rows per CU. Grouped (runtime)
-// fan-in, n > 14: from 20 MB (cfg3, 17 x 11.2 M: 123.8 -> 120.8 us; cfg5,
+// Does a launch of n inputs of nelem elements defer? From 10 MB per stream
+// (fan-in 11-14 from 16 rows per CU). Grouped (runtime) fan-in, n > 14, the
+// same (cfg3, 17 x 11.2 M: 123.8 -> 120.8 us; cfg5,
 // 100 x 11.2 M: 676.6 -> 659.0; 17 x 16 M 182.5 -> 171.9; 30 x 11.2 M 212.6
 // -> 204.3; profiles/r05_defer/r05ad_*). DLSIM_DEFER_GROUPED=0 (read once;
 // A/B runs): the tiled grouped kernel.
@@ -267,9 +267,24 @@ inline bool defer_grouped_on() {
   }();
   return on;
 }
+// From 10 MB per stream (profiles/r05_defer/r05bb_*, r05bc_*): the north
+// star's 4-rank slice (8 x 2.8 M) 16.55-16.58 against 17.08-17.19 us tiled,
+// 8 x 3.5 M 20.35 against 21.76, 17 x 2.8 M 33.88 against 34.30, 3 x 2.8 M
+// 9.01 against 9.15; below it the one round of rows leaves CUs idle or too
+// few rows to defer: 8 x 2.1 M +1.6 % but 4 x 2.1 M -5 %, the 8-rank slice
+// (8 x 1.4 M) 10.28-10.30 against 9.71, cfg2 (8 x 1 M) 9.06 against 7.62.
+// DLSIM_DEFER_MIN_MB=x (read once; A/B runs): from x MB instead.
+constexpr double kDeferMinMB = 10.0;
+inline double defer_min_mb() {
+  static const double x = [] {
+    const char* e = std::getenv("DLSIM_DEFER_MIN_MB");
+    return e ? std::atof(e) : kDeferMinMB;
+  }();
+  return x;
+}
 template <class Op> bool use_defer(int n, size_t nelem) {
   if (Op::kBytes != 4 || n < std::max(2, defer_min_fan_in()) || n > defer_max_fan_in() || !defer_on()) return false;
-  if (size_class<Op>(nelem, n <= max_fixed_fan_in<Op>() ? n : 0) != 2) return false;
+  if (static_cast<double>(nelem * Op::kBytes) < defer_min_mb() * 1e6) return false;
   if (n > max_fixed_fan_in<Op>()) return defer_grouped_on();
   if (n <= kDeferWideFanIn) return true;
   const size_t rows = nelem / Op::E / dlsim::kDeferBlock;
@@ -564,7 +579,7 @@ int run_batched(int b, const int* fan_in, const void* const* in, const float* w,
   auto batchable = [&](int t) {
     if (nelem[t] == 0 || fan_in[t] > 16) return false;
     if (nelem[t] * Op::kBytes > kMaxLaunchOutBytes) return false;
-    // a task the deferred-store kernel takes (>= 20 MB per stream) runs alone
+    // a task the deferred-store kernel takes (>= 10 MB per stream) runs alone
     // through it: a launch that size amortises its own overhead, and the
     // batch kernel interleaves its stores
     if (use_defer<Op>(fan_in[t], nelem[t])) return false;

@@ -542,7 +542,7 @@ void dlsim_pool_stats(unsigned long long* contiguous, unsigned long long* fallba
  * dlsim_kernel_name — the kernel dlsim_wreduce (mode DLSIM_EXACT or
  * DLSIM_FAST) or dlsim_mean (mode -1) launches for n 16-byte-aligned inputs
  * of n_elems elements of dtype on the current device: "dlsim::k_wreduce_defer"
- * (fp32, n >= 3, >= 20 MB per stream; for 11 <= n <= 14 from 8.4 M elements),
+ * (fp32, n >= 3, >= 10 MB per stream; for 11 <= n <= 14 from 8.4 M elements),
  * "dlsim::k_wreduce_tiles" otherwise (misaligned buffers take
  * "dlsim::k_wreduce_scalar"), "" for no launch (n_elems == 0) or bad
  * arguments. A static string, for profilers and benches that look a kernel up

@@ -170,7 +170,7 @@ def test_library_errors_stay_on_the_calling_thread():
 def test_kernel_name_follows_the_dispatch():
     """dlsim_kernel_name (host logic only, no GPU: 256 CUs assumed when the
     device query fails): the deferred-store kernel for fp32 fan-in 3-10 and
-    above 14 (grouped) from 20 MB per stream, 11-14 from 16 rows of 512
+    above 14 (grouped) from 10 MB per stream, 11-14 from 16 rows of 512
     vectors per CU; the tiled kernel otherwise (dispatch.hpp use_defer)."""
     import torch
     f32, bf16 = torch.float32, torch.bfloat16
@@ -178,8 +178,8 @@ def test_kernel_name_follows_the_dispatch():
     assert _native.kernel_name(8, 11_181_642, f32) == d  # the north star
     assert _native.kernel_name(8, 11_181_642, f32, _native.DLSIM_FAST) == d
     assert _native.kernel_name(8, 11_181_642, f32, None) == d  # dlsim_mean
-    assert _native.kernel_name(8, 4_999_999, f32) == t  # below 20 MB
-    assert _native.kernel_name(8, 5_000_000, f32) == d
+    assert _native.kernel_name(8, 2_499_999, f32) == t  # below 10 MB
+    assert _native.kernel_name(8, 2_500_000, f32) == d
     assert _native.kernel_name(3, 11_181_642, f32) == d
     assert _native.kernel_name(2, 11_181_642, f32) == t
     assert _native.kernel_name(2, 125_000_000, f32) == t
@@ -188,6 +188,6 @@ def test_kernel_name_follows_the_dispatch():
     assert _native.kernel_name(14, 8_388_608, f32) == d  # exactly 16 rows per CU
     assert _native.kernel_name(15, 11_181_642, f32) == d  # the grouped form
     assert _native.kernel_name(100, 11_181_642, f32) == d  # cfg5
-    assert _native.kernel_name(100, 4_999_999, f32) == t
+    assert _native.kernel_name(100, 2_499_999, f32) == t
     assert _native.kernel_name(8, 11_181_642, bf16) == t
     assert _native.kernel_name(8, 0, f32) == ""

@@ -303,11 +303,13 @@ def test_launch_shapes_either_side_of_the_size_switch(dtype, p, n):
     (12, 11_181_642 + 3),      # fan-in 11-14 from 16 rows per CU (RMAX 24)
     (6, 20_000_003),           # more rows than one round holds: R from the cost model
     (4, 67_108_864 + 5),       # many rounds of blocks
+    (8, 2_795_456),            # 10-20 MB per stream: the north star's 4-rank slice
+    (17, 2_600_001),           # the grouped form from 10 MB
     (17, 5_000_003),           # the grouped form: kernel-argument slots
     (130, 5_000_001),          # the grouped form: the device table
 ])
 def test_deferred_store_kernel_bit_exact(n, p):
-    """dlsim::k_wreduce_defer (fp32, fixed fan-in >= 4, >= 20 MB per stream;
+    """dlsim::k_wreduce_defer (fp32, fan-in >= 3, >= 10 MB per stream;
     dispatch.hpp launch_defer): full blocks keep R results per lane in
     registers and store them at the end, the last block folds its partial
     rows with bounds checks, block 0 the scalar tail. Every element against
