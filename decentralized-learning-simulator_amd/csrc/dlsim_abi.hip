@@ -490,6 +490,14 @@ int dlsim_host_wreduce(int n, int t, const void* const* h_srcs, const size_t* nu
   return ln.rc;
 }
 
+// Smallest chunk per model of a zero-copy task's pipeline (bytes):
+// DLSIM_ZC_CHUNK_KB, read per call (A/B runs); default 128 KiB.
+static size_t zc_chunk_bytes() {
+  const char* e = std::getenv("DLSIM_ZC_CHUNK_KB");
+  const long kb = e ? std::strtol(e, nullptr, 10) : 128;
+  return static_cast<size_t>(kb > 0 ? kb : 0) << 10;
+}
+
 int dlsim_host_wreduce_zc(int n, int t, const void* const* h_srcs, const size_t* numels, const float* h_weights,
                           void* h_staging, size_t row_stride, void* h_out, int dtype, int mode, int threads,
                           void* stream) {
@@ -528,25 +536,46 @@ int dlsim_host_wreduce_zc(int n, int t, const void* const* h_srcs, const size_t*
     return fail(DLSIM_E_ARG, "h_out is not page-locked host memory the device maps (hipHostMalloc)");
   }
   char* stage = static_cast<char*>(h_staging);
-  // one unit per model: its tensors packed into its row
+  // The element axis in K chunks, each a pack unit (every model's part of it,
+  // in chunk order): once chunk c is packed its reduce is launched, and it
+  // reads its rows over PCIe while the pack goes on with chunk c + 1.
+  // Chunks of >= zc_chunk_bytes() per model, a multiple of 1024 elements (16-B
+  // aligned ranges), for tasks of >= 1 MiB of rows (the 100-peer fan-in-7
+  // GNLeNet round: 229-243 -> 200-208 us per task, batched 139-145 -> 106-110;
+  // cfg1's 2 x 341 KB even or slower chunked, profiles/r05be_ab/);
+  // DLSIM_ZC_CHUNK_KB (read per call) sets it, 0 = one chunk.
+  const size_t min_chunk = zc_chunk_bytes() / esz;
+  size_t L = total;
+  if (min_chunk > 0 && total > 2 * min_chunk && total * esz * static_cast<size_t>(n) >= (size_t{1} << 20)) {
+    const size_t k = std::min<size_t>(8, total / min_chunk);
+    L = ((total + k - 1) / k + 1023) / 1024 * 1024;
+  }
+  const size_t K = (total + L - 1) / L;
   dlsim::PackJob job;
-  for (int i = 0; i < n; ++i) {
-    size_t off = 0;
-    for (int k = 0; k < t; ++k) {
-      if (numels[k] > 0)
-        job.add(static_cast<uint32_t>(i), static_cast<const char*>(h_srcs[static_cast<size_t>(i) * t + k]),
-                stage + i * row_bytes + off * esz, numels[k] * esz);
-      off += numels[k];
+  for (size_t c = 0; c < K; ++c) {
+    const size_t c0 = c * L, c1 = std::min(total, c0 + L);
+    for (int i = 0; i < n; ++i) {
+      size_t off = 0;
+      for (int k = 0; k < t; ++k) {
+        const size_t b = std::max(off, c0), e = std::min(off + numels[k], c1);
+        if (b < e)
+          job.add(static_cast<uint32_t>(c),
+                  static_cast<const char*>(h_srcs[static_cast<size_t>(i) * t + k]) + (b - off) * esz,
+                  stage + i * row_bytes + b * esz, (e - b) * esz);
+        off += numels[k];
+      }
     }
   }
-  job.seal(static_cast<size_t>(n));
+  job.seal(K);
   int rc = DLSIM_OK;
   std::vector<const void*> ins(static_cast<size_t>(n));
-  for (int r = 0; r < n; ++r) ins[r] = static_cast<const char*>(d_stage) + r * row_bytes;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  pack_and_dispatch(job, threads, total * esz * n, [&](size_t, size_t u1) {
-    if (u1 == static_cast<size_t>(n) && rc == DLSIM_OK)
-      rc = dispatch(ins.data(), n, h_weights, d_res, total, dtype, mode, st);
+  pack_and_dispatch(job, threads, total * esz * n, [&](size_t u0, size_t u1) {
+    for (size_t c = u0; c < u1 && rc == DLSIM_OK; ++c) {
+      const size_t c0 = c * L, len = std::min(total, c0 + L) - c0;
+      for (int r = 0; r < n; ++r) ins[r] = static_cast<const char*>(d_stage) + r * row_bytes + c0 * esz;
+      rc = dispatch(ins.data(), n, h_weights, static_cast<char*>(d_res) + c0 * esz, len, dtype, mode, st);
+    }
   });
   return rc;
 }

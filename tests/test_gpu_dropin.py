@@ -480,3 +480,32 @@ def test_zero_copy_small_host_tasks():
     torch.cuda.synchronize()
     assert orc.same_bits(res_pinned.numpy(), orc.wreduce([src.numpy(), src.numpy()],
                                                          orc.reference_weights(2, [0.5, 0.5]), "f32"))
+
+
+def test_zero_copy_pipelined_chunks(monkeypatch):
+    """dlsim_host_wreduce_zc over chunks of the element axis (tasks of >= 1 MiB
+    of rows): the pack of chunk c + 1 overlaps the reduce of chunk c reading
+    its rows over PCIe. Chunk boundaries inside parameters of ragged sizes,
+    fp32 and bf16, 7 models: bit-exact against the oracle."""
+    from dasklearn_amd import _native, arena
+    from dasklearn_amd.arena import aggregate_modules
+    monkeypatch.setenv("DLSIM_ZC_CHUNK_KB", "16")  # read per call: many small chunks
+    for dt in (torch.float32, torch.bfloat16):
+        torch.manual_seed(5)
+        ms = []
+        for _ in range(7):
+            m = torch.nn.Sequential(torch.nn.Linear(601, 131), torch.nn.Linear(131, 67), torch.nn.Linear(67, 5))
+            ms.append(m.to(dt))
+        calls = arena.ZC_CALLS[0]
+        w = [0.1, 0.2, 0.05, 0.15, 0.2, 0.1, 0.2]
+        out = aggregate_modules(ms, w, _native.DLSIM_EXACT)
+        assert arena.ZC_CALLS[0] == calls + 1
+        rows = [np.concatenate([p.detach().float().numpy().ravel() for p in m.parameters()]) for m in ms]
+        got = np.concatenate([p.detach().float().numpy().ravel() for p in out.parameters()])
+        if dt == torch.float32:
+            exp = orc.wreduce(rows, orc.reference_weights(7, w), "f32")
+            assert orc.same_bits(got, exp)
+        else:
+            bits = [orc.f32_to_bf16_bits(r.astype(np.float32)) for r in rows]
+            exp = orc.bf16_bits_to_f32(orc.wreduce(bits, orc.reference_weights(7, w), "bf16"))
+            assert orc.same_bits(got.astype(np.float32), exp.astype(np.float32))
