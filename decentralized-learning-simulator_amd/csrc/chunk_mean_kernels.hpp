@@ -557,4 +557,89 @@ __global__ __launch_bounds__(kDeferBlock) void k_chunk_mean_defer(const ChunkMea
     if (r < Rb) store_vec<kCmStore<Op>>(o, v0 + static_cast<size_t>(r) * kDeferBlock, res[r]);
 }
 
+// Fixed contributor count MF < 16 for every task of the launch (round 6;
+// VERDICT r05 next #3). Conflux rebuilds every chunk index from the same m
+// peers, and below 16 contributors the cascade is its level 0 alone: rows
+// folded in order from +0, the (zero) upper levels added, one division --
+// cm_rows_fold's order for m < 16. With MF known at compile time the U rows
+// of all MF contributors load back to back and fold straight-line (the
+// reduce's fixed fan-in form, defer_rows), and the stores run unguarded: a row
+// past the block's count goes to vector nvec, past the task's output range,
+// which the buffer store drops (the ragged block owns the partial row there).
+template <class Op, int MF, int RMAX, int U>
+__global__ __launch_bounds__(kDeferBlock) void k_chunk_mean_defer_m(const ChunkMeanSlots s, int R) {
+  static_assert(MF >= 1 && MF < 16, "level 0 only");
+  using T = acc_t<Op>;
+  const uint32_t bid = blockIdx.x;
+  int t = 0;
+  uint32_t local = 0;
+  if (bid < static_cast<uint32_t>(s.ntasks)) {
+    t = static_cast<int>(bid);
+  } else {
+    const uint32_t f = bid - static_cast<uint32_t>(s.ntasks);
+    while (t + 1 < s.ntasks && f >= s.block_start[t + 1]) ++t;  // wave-uniform scan
+    local = f - s.block_start[t] + 1;
+  }
+  const PtrArgs a{s.p + s.ptr_off[t]};
+  const size_t n = s.nelem[t], ilp_begin = s.ilp_begin[t];
+  const uint32_t head = s.head[t];
+  const float div = static_cast<float>(MF);
+  const size_t hb = static_cast<size_t>(head) * Op::kBytes;
+  const ShiftArgs<PtrArgs> sa{a, hb};
+  const size_t nvec = (ilp_begin - head) / Op::E;
+  const size_t rows = nvec / kDeferBlock;
+  const OutRef o = make_out<kCmStore<Op>>(static_cast<char*>(s.out[t]) + hb, nvec);
+  if (local == 0) {  // the ragged block, as k_chunk_mean_defer's
+    if (threadIdx.x >= kBlock) return;
+    if (rows * kDeferBlock < nvec) {
+      using PT = CmShape<kDeferBlock / kBlock, false, (MF <= 6 ? 4 : 8)>;  // dispatch.hpp CmFewRows / CmDefault RF
+      cm_tile<Op, ShiftArgs<PtrArgs>, PT, 2, true, true>(sa, MF, o, rows * kDeferBlock + threadIdx.x, nvec,
+                                                         ilp_begin - head, div);
+    }
+    if (head > 0) cm_scalar_cols<Op, PtrArgs>(a, MF, s.out[t], 0, head, ilp_begin, false, div);
+    const size_t c0 = head + nvec * Op::E;
+    if (c0 < n) cm_scalar_cols<Op, PtrArgs>(a, MF, s.out[t], c0, n, ilp_begin, (s.flags[t] & kCmInner) != 0, div);
+    return;
+  }
+  const size_t first = static_cast<size_t>(local - 1) * static_cast<size_t>(R);
+  const int Rb = static_cast<int>(rows - first < static_cast<size_t>(R) ? rows - first : static_cast<size_t>(R));
+  const size_t v0 = first * kDeferBlock + threadIdx.x;
+  u32x4 res[RMAX];
+#pragma unroll
+  for (int r0 = 0; r0 < RMAX; r0 += U) {
+    if (r0 < Rb) {
+      u32x4 x[MF][U];
+#pragma unroll
+      for (int i = 0; i < MF; ++i)
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int row = r0 + u < Rb ? r0 + u : r0;  // re-reads row r0 (in flight): no extra traffic
+          x[i][u] = ld16<1>(sa.ptr(i), v0 + static_cast<size_t>(row) * kDeferBlock);
+        }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        T acc[Op::E];
+#pragma unroll
+        for (int e = 0; e < Op::E; ++e) acc[e] = T(0);
+#pragma unroll
+        for (int i = 0; i < MF; ++i) {
+          T xv[Op::E];
+          unpack<Op>(x[i][u], xv);
+#pragma unroll
+          for (int e = 0; e < Op::E; ++e) acc[e] = acc[e] + xv[e];
+        }
+#pragma unroll
+        for (int e = 0; e < Op::E; ++e) acc[e] = acc[e] + T(0);  // + level 1 (zero below 16 rows)
+        res[r0 + u] = pack<Op>(acc, div);
+      }
+    }
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  static_assert(kCmStore<Op> >= 0, "buffer stores: out-of-range rows are dropped");
+#pragma unroll
+  for (int r = 0; r < RMAX; ++r)
+    store_vec<kCmStore<Op>>(o, r < Rb ? v0 + static_cast<size_t>(r) * kDeferBlock : nvec, res[r]);
+}
+
 }  // namespace dlsim

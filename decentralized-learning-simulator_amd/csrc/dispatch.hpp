@@ -19,6 +19,7 @@
 #include "dlsim.h"
 #include "wreduce_kernels.hpp"
 #include "chunk_mean_kernels.hpp"
+#include "ab_env.hpp"
 
 namespace dlsim_host __attribute__((visibility("hidden"))) {
 
@@ -107,13 +108,15 @@ template <class Op, int C> constexpr Shape fixed_shape() {
 // 11.09 against 11.78, 1.84 M 11.58 against 12.03; where they do not (the
 // 8-rank slice of the north star, 1.4 M: x4 = 1.33) VPT 2 stays (9.60 against
 // 10.45 us). Fan-in 2-4 showed no such rule and keep VPT 2.
+int device_cus();  // multiProcessorCount of the current device (cached per device; dlsim_abi.hip)
 inline bool v4_tiles_even(size_t nvec) {
-  const double x = static_cast<double>(nvec / (static_cast<size_t>(dlsim::kBlock) * 4)) / 256.0;
+  const double x = static_cast<double>(nvec / (static_cast<size_t>(dlsim::kBlock) * 4)) /
+                   static_cast<double>(device_cus());
   return x >= 0.75 && std::ceil(x) / x <= 1.25;
 }
 // DLSIM_SMALL_SHAPE_R04 (read once; A/B runs): round 4's rule, VPT 2 below 8 MB.
 inline bool small_shape_r04() {
-  static const bool on = std::getenv("DLSIM_SMALL_SHAPE_R04") != nullptr;
+  static const bool on = dlsim::ab_getenv("DLSIM_SMALL_SHAPE_R04") != nullptr;
   return on;
 }
 template <class Op> int size_class(size_t nelem, int fixed_fan_in = 0) {
@@ -204,7 +207,7 @@ template <class Op, int NF> constexpr int defer_rmax() { return NF >= 12 ? 24 : 
 template <class Op, int NF> constexpr bool defer_eligible() { return Op::kBytes == 4 && (NF >= 2 || NF == 0); }
 inline int defer_min_fan_in() {
   static const int k = [] {
-    const char* e = std::getenv("DLSIM_DEFER_MIN_FAN_IN");
+    const char* e = dlsim::ab_getenv("DLSIM_DEFER_MIN_FAN_IN");
     return e ? std::atoi(e) : 3;
   }();
   return k;
@@ -213,22 +216,21 @@ constexpr int kDeferWideFanIn = 10;
 constexpr size_t kDeferWideRowsPerCu = 16;
 inline bool defer_on() {
   static const bool on = [] {
-    const char* e = std::getenv("DLSIM_DEFER");
+    const char* e = dlsim::ab_getenv("DLSIM_DEFER");
     return !(e && e[0] == '0');
   }();
   return on;
 }
 inline int defer_max_fan_in() {
   static const int k = [] {
-    const char* e = std::getenv("DLSIM_DEFER_MAX_FAN_IN");
+    const char* e = dlsim::ab_getenv("DLSIM_DEFER_MAX_FAN_IN");
     return e ? std::atoi(e) : 1 << 30;
   }();
   return k;
 }
-int device_cus();  // multiProcessorCount of the current device (cached per device; dlsim_abi.hip)
 inline int defer_r_override() {
   static const int r = [] {
-    const char* e = std::getenv("DLSIM_DEFER_R");
+    const char* e = dlsim::ab_getenv("DLSIM_DEFER_R");
     return e ? std::atoi(e) : 0;
   }();
   return r;
@@ -262,7 +264,7 @@ inline int defer_rows(size_t nvec, size_t cus, int rmax) {
 // A/B runs): the tiled grouped kernel.
 inline bool defer_grouped_on() {
   static const bool on = [] {
-    const char* e = std::getenv("DLSIM_DEFER_GROUPED");
+    const char* e = dlsim::ab_getenv("DLSIM_DEFER_GROUPED");
     return !(e && e[0] == '0');
   }();
   return on;
@@ -277,7 +279,7 @@ inline bool defer_grouped_on() {
 constexpr double kDeferMinMB = 10.0;
 inline double defer_min_mb() {
   static const double x = [] {
-    const char* e = std::getenv("DLSIM_DEFER_MIN_MB");
+    const char* e = dlsim::ab_getenv("DLSIM_DEFER_MIN_MB");
     return e ? std::atof(e) : kDeferMinMB;
   }();
   return x;
@@ -331,8 +333,11 @@ hipError_t launch_defer(const S& s, int n, void* out, size_t nelem, hipStream_t 
   const size_t span = static_cast<size_t>(dlsim::kDeferBlock) * static_cast<size_t>(R);
   const size_t blocks = (nvec + span - 1) / span;
   if (blocks == 0 || blocks > 0x7fffffffu) return hipErrorInvalidValue;
-  if constexpr (NF > 0 && std::is_same<Op, dlsim::F32Exact>::value)
-    return launch_defer_rc<Op, S, NF, kDeferU>(s, n, out, nvec, nelem, R, static_cast<unsigned>(blocks), st);
+  // compiled R from kDeferRMin (defer_rows never returns less) for the fan-ins
+  // that defer by default (>= 3); R = 2 and fan-in 2 (reachable only through
+  // the A/B switches) take the runtime R
+  if constexpr (NF >= 3 && std::is_same<Op, dlsim::F32Exact>::value)
+    return launch_defer_rc<Op, S, NF, kDeferRMin>(s, n, out, nvec, nelem, R, static_cast<unsigned>(blocks), st);
   hipLaunchKernelGGL((dlsim::k_wreduce_defer<Op, S, NF, group_size<Op>(), defer_rmax<Op, NF>(), kDeferU, kStore>),
                      dim3(static_cast<unsigned>(blocks)), dim3(dlsim::kDeferBlock), 0, st, s, n, R, out, nvec, nelem);
   return hipGetLastError();
@@ -816,7 +821,7 @@ constexpr int kCmFewRowsMax = 6;
 constexpr int kCmDeferRMax = 32, kCmDeferU = kDeferU, kCmDeferMinRows = 16;
 inline bool chunk_defer_on() {
   static const bool on = [] {
-    const char* e = std::getenv("DLSIM_CHUNK_DEFER");
+    const char* e = dlsim::ab_getenv("DLSIM_CHUNK_DEFER");
     return !(e && e[0] == '0');
   }();
   return on;
@@ -824,24 +829,50 @@ inline bool chunk_defer_on() {
 // DLSIM_CHUNK_DEFER_MIN_M=k (read once; A/B runs): defer from k contributors
 inline int chunk_defer_min_m() {
   static const int k = [] {
-    const char* e = std::getenv("DLSIM_CHUNK_DEFER_MIN_M");
+    const char* e = dlsim::ab_getenv("DLSIM_CHUNK_DEFER_MIN_M");
     return e ? std::atoi(e) : kCmDeferMinRows;
   }();
   return k;
 }
-inline int chunk_defer_rows(const std::vector<size_t>& rows, size_t cus) {
-  if (defer_r_override() > 0) return std::min(defer_r_override(), kCmDeferRMax);
+// Fixed-m deferral (dlsim::k_chunk_mean_defer_m, round 6): every task of the
+// launch has the same m, 2 <= m < 16. DLSIM_CHUNK_DEFER_FIXED=0 (read once;
+// A/B runs, under DLSIM_AB=1): the tiled kernel there instead.
+constexpr int kCmFixedMaxM = 15;
+inline bool chunk_defer_fixed_on() {
+  static const bool on = [] {
+    const char* e = dlsim::ab_getenv("DLSIM_CHUNK_DEFER_FIXED");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+// results per lane beside MF x U loads, as the reduce's defer_rmax
+constexpr int cm_defer_m_rmax(int mf) { return mf >= 12 ? 24 : kCmDeferRMax; }
+template <class Op, int MF>
+hipError_t launch_chunk_defer_m(const dlsim::ChunkMeanSlots& s, int m, int R, unsigned grid, hipStream_t st) {
+  if constexpr (MF > kCmFixedMaxM || Op::kBytes != 4) {
+    return hipErrorInvalidValue;
+  } else {
+    if (m == MF) {
+      hipLaunchKernelGGL((dlsim::k_chunk_mean_defer_m<Op, MF, cm_defer_m_rmax(MF), kCmDeferU>), dim3(grid),
+                         dim3(dlsim::kDeferBlock), 0, st, s, R);
+      return hipGetLastError();
+    }
+    return launch_chunk_defer_m<Op, MF + 1>(s, m, R, grid, st);
+  }
+}
+inline int chunk_defer_rows(const std::vector<size_t>& rows, size_t cus, int rmax = kCmDeferRMax) {
+  if (defer_r_override() > 0) return std::min(defer_r_override(), rmax);
   const size_t nt = rows.size();
   auto blocks = [&](size_t R) {
     size_t b = 0;
     for (size_t r : rows) b += (r + R - 1) / R;
     return b;
   };
-  for (size_t R = 4; R <= static_cast<size_t>(kDeferOneRoundMax); R += 2)
+  for (size_t R = 4; R <= static_cast<size_t>(std::min(rmax, kDeferOneRoundMax)); R += 2)
     if (blocks(R) + nt <= cus) return static_cast<int>(R);
-  for (size_t R = 4; R <= static_cast<size_t>(kCmDeferRMax); R += 2)
+  for (size_t R = 4; R <= static_cast<size_t>(rmax); R += 2)
     if (blocks(R) + nt <= 2 * cus) return static_cast<int>(R);
-  return kCmDeferRMax;
+  return rmax;
 }
 
 template <class Op>
@@ -900,18 +931,26 @@ int run_chunk_mean(int b, const int* fan_in, const void* const* in, void* const*
     if (batch.empty()) return DLSIM_OK;
     dlsim::ChunkMeanSlots s;
     std::memset(&s, 0, sizeof(s));
-    // deferred stores: fp32, every task vector-aligned with m >= 16, >= 20 MB per stream
+    // deferred stores: fp32, every task vector-aligned with m >= 16 (or every
+    // task with one m, 2 <= m < 16: the fixed-m form), >= 20 MB per stream
     bool defer = Op::kBytes == 4 && chunk_defer_on();
+    bool fixed = Op::kBytes == 4 && chunk_defer_on() && chunk_defer_fixed_on();
+    const int m0 = fan_in[batch.front().t];
     size_t cols = 0;
     std::vector<size_t> rows;
     for (const CmTask& k : batch) {
-      defer = defer && (k.flags & dlsim::kCmVec) && fan_in[k.t] >= chunk_defer_min_m();
+      const bool vec = (k.flags & dlsim::kCmVec) != 0;
+      defer = defer && vec && fan_in[k.t] >= chunk_defer_min_m();
+      fixed = fixed && vec && fan_in[k.t] == m0;
       cols += nelem[k.t];
       rows.push_back((k.ib - k.head) / Op::E / dlsim::kDeferBlock);
     }
-    defer = defer && cols * Op::kBytes >= 20000000;
+    fixed = fixed && m0 >= 2 && m0 <= kCmFixedMaxM && !defer;
+    defer = (defer || fixed) && cols * Op::kBytes >= 20000000;
+    fixed = fixed && defer;
     int R = 0;
-    if (defer) R = chunk_defer_rows(rows, static_cast<size_t>(device_cus()));
+    if (defer)
+      R = chunk_defer_rows(rows, static_cast<size_t>(device_cus()), fixed ? cm_defer_m_rmax(m0) : kCmDeferRMax);
     size_t blocks = 0;
     int nt = 0, p = 0;
     for (const CmTask& k : batch) {
@@ -936,7 +975,10 @@ int run_chunk_mean(int b, const int* fan_in, const void* const* in, void* const*
     if (defer) {
       if constexpr (Op::kBytes == 4) {
         const unsigned grid = static_cast<unsigned>(blocks);
-        if (few_rows)
+        if (fixed) {
+          const hipError_t e = launch_chunk_defer_m<Op, 2>(s, m0, R, grid, st);
+          if (e != hipSuccess) return hip_fail(e, "chunk mean batch launch");
+        } else if (few_rows)
           hipLaunchKernelGGL((dlsim::k_chunk_mean_defer<Op, CmFewRows::RF, kCmDeferRMax, kCmDeferU>), dim3(grid),
                              dim3(dlsim::kDeferBlock), 0, st, s, R);
         else

@@ -84,7 +84,7 @@ struct StreamLinks {
 // they save on sources already in the CPU caches.
 constexpr long kPackHelpersMinKB = 1024;
 size_t pack_helpers_min_bytes() {
-  const char* e = std::getenv("DLSIM_PACK_HELPERS_MIN_KB");
+  const char* e = dlsim::ab_getenv("DLSIM_PACK_HELPERS_MIN_KB");
   const long kb = e ? std::strtol(e, nullptr, 10) : kPackHelpersMinKB;
   return static_cast<size_t>(kb > 0 ? kb : 0) << 10;
 }
@@ -92,7 +92,7 @@ size_t pack_helpers_min_bytes() {
 // DLSIM_PACK_THREADS=k (read per call; deployment A/B runs): pack on k
 // threads whatever the caller asked for.
 int pack_threads(int threads) {
-  const char* e = std::getenv("DLSIM_PACK_THREADS");
+  const char* e = dlsim::ab_getenv("DLSIM_PACK_THREADS");
   const long k = e ? std::strtol(e, nullptr, 10) : 0;
   return k > 0 ? static_cast<int>(std::min<long>(k, 64)) : threads;
 }
@@ -120,7 +120,7 @@ void pack_and_dispatch(dlsim::PackJob& job, int threads, size_t in_bytes, F&& on
 // Smallest H2D run of a one-chunk dlsim_host_wreduce (DLSIM_H2D_MIN_KB, read
 // per call: A/B probes; default 1 MiB).
 size_t h2d_min_bytes() {
-  const char* e = std::getenv("DLSIM_H2D_MIN_KB");
+  const char* e = dlsim::ab_getenv("DLSIM_H2D_MIN_KB");
   const long kb = e ? std::strtol(e, nullptr, 10) : 1024;
   return static_cast<size_t>(kb > 0 ? kb : 0) << 10;
 }
@@ -493,7 +493,7 @@ int dlsim_host_wreduce(int n, int t, const void* const* h_srcs, const size_t* nu
 // Smallest chunk per model of a zero-copy task's pipeline (bytes):
 // DLSIM_ZC_CHUNK_KB, read per call (A/B runs); default 128 KiB.
 static size_t zc_chunk_bytes() {
-  const char* e = std::getenv("DLSIM_ZC_CHUNK_KB");
+  const char* e = dlsim::ab_getenv("DLSIM_ZC_CHUNK_KB");
   const long kb = e ? std::strtol(e, nullptr, 10) : 128;
   return static_cast<size_t>(kb > 0 ? kb : 0) << 10;
 }

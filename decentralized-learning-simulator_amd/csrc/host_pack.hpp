@@ -31,6 +31,8 @@
 #include <thread>
 #include <vector>
 
+#include "ab_env.hpp"
+
 namespace dlsim {
 
 // Largest memcpy one thread takes at a time: small enough that a unit of a
@@ -68,7 +70,7 @@ inline void copy_stream(char* dst, const char* src, size_t bytes) {
 // DLSIM_PACK_COPY=memcpy selects plain memcpy, read per call (A/B probes:
 // scripts/probe_host_pack.py); default: streaming.
 inline bool pack_streaming() {
-  const char* e = std::getenv("DLSIM_PACK_COPY");
+  const char* e = dlsim::ab_getenv("DLSIM_PACK_COPY");
   return !(e && std::strcmp(e, "memcpy") == 0);
 }
 

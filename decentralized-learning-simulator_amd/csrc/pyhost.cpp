@@ -401,32 +401,42 @@ PyObject* py_shm_keys(PyObject*, PyObject* args) {
 }
 
 // Content fingerprint of model i's tensors [i*t, (i+1)*t) for the device
-// cache's stale-hit check: 8 bytes from the middle of up
-// to kFpTensors tensors spread over the group (the first and the last among
-// them), mixed with their positions. A model written in place after it was
-// cached (the reference trains its input model in place, functions.py:57)
-// changes essentially every element, so a changed word shows it; one word per
-// sampled tensor keeps the cost to a page touch each on freshly mapped shm.
-constexpr Py_ssize_t kFpTensors = 8;
+// cache's stale-hit check: EVERY tensor of
+// the model contributes words spread evenly along its bytes -- the first and
+// the last word, plus one more per MiB up to kFpMaxWords -- mixed with the
+// tensor's index and each word's offset. A model written in place after it
+// was cached (the reference trains its input model in place,
+// functions.py:57) changes essentially every element, so a changed word
+// shows it; a partial update (one layer fine-tuned, a frozen backbone) still
+// rewrites whole tensors, and every tensor is sampled. What it cannot see is
+// an update that leaves every sampled word as it was.
+// A strided view is sampled at its first element only (its other offsets
+// need not be inside its storage).
+constexpr size_t kFpMaxWords = 16;
+inline void fp_mix(uint64_t& h, uint64_t w, uint64_t where) {
+  h = (h ^ (w + where)) * 0x100000001b3ull;
+  h ^= h >> 31;
+}
 uint64_t content_fingerprint(const std::vector<const at::Tensor*>& ts, Py_ssize_t i, Py_ssize_t t) {
   uint64_t h = 0x9e3779b97f4a7c15ull;
-  const Py_ssize_t k = std::min(t, kFpTensors);
-  for (Py_ssize_t s = 0; s < k; ++s) {
-    const Py_ssize_t j = k > 1 ? s * (t - 1) / (k - 1) : 0;
+  for (Py_ssize_t j = 0; j < t; ++j) {
     const at::Tensor* x = ts[static_cast<size_t>(i * t + j)];
     const int64_t ne = x->numel();
-    uint64_t w = 0;
-    if (ne > 0) {
-      const size_t esz = x->element_size();
-      const char* base = static_cast<const char*>(x->const_data_ptr());
-      // the middle element of a contiguous tensor, else the first (a strided
-      // view's middle offset need not be inside its storage)
-      const size_t off = x->is_contiguous() ? static_cast<size_t>(ne / 2) * esz : 0;
-      const size_t avail = x->is_contiguous() ? static_cast<size_t>(ne) * esz - off : esz;
-      std::memcpy(&w, base + off, std::min<size_t>(8, avail));
+    if (ne <= 0) {
+      fp_mix(h, 0, static_cast<uint64_t>(j) << 32);
+      continue;
     }
-    h = (h ^ (w + static_cast<uint64_t>(j))) * 0x100000001b3ull;
-    h ^= h >> 31;
+    const char* base = static_cast<const char*>(x->const_data_ptr());
+    const size_t bytes = x->is_contiguous() ? static_cast<size_t>(ne) * x->element_size() : x->element_size();
+    const size_t words = bytes <= 8 ? 1 : std::min(kFpMaxWords, 2 + bytes / (size_t{1} << 20));
+    for (size_t q = 0; q < words; ++q) {
+      // word q at an 8-byte-granular offset from 0 to the last full word
+      const size_t last = bytes >= 8 ? bytes - 8 : 0;
+      const size_t off = words > 1 ? (last * q / (words - 1)) & ~size_t{7} : 0;
+      uint64_t w = 0;
+      std::memcpy(&w, base + off, std::min<size_t>(8, bytes - off));
+      fp_mix(h, w, (static_cast<uint64_t>(j) << 32) ^ off);
+    }
   }
   return h;
 }

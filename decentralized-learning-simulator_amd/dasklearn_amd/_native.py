@@ -30,6 +30,15 @@ DLSIM_GATHER_NONE = 0
 DLSIM_GATHER_BCAST = 1
 DLSIM_GATHER_ALLGATHER = 2
 
+
+def ab_env(name: str, default: Optional[str] = None) -> Optional[str]:
+    """A DLSIM_* A/B switch (tuning studies): os.environ[name] only when
+    DLSIM_AB=1 is set as well, else `default` -- the library's rule
+    (csrc/ab_env.hpp), so a stray variable cannot change what runs."""
+    if os.environ.get("DLSIM_AB") != "1":
+        return default
+    return os.environ.get(name, default)
+
 # Every symbol include/dlsim.h declares (tests/test_abi.py checks the header
 # against this list and the library's exports).
 EXPORTS = (

@@ -279,7 +279,7 @@ def arena_empty(numel: int, dtype: torch.dtype, device) -> torch.Tensor:
 # 4 MiB: the 8-rank slice of the north star (5.6 MB outputs) ran 9.55-9.60 us
 # with pooled outputs against 9.71-9.97 us in torch's allocator; cfg2's 4 MB
 # outputs measured neutral (profiles/r04s2_small/)
-OUT_POOL_MIN = int(float(os.environ.get("DLSIM_OUT_POOL_MIN_MB", "4")) * (1 << 20))  # bytes
+OUT_POOL_MIN = int(float(_native.ab_env("DLSIM_OUT_POOL_MIN_MB", "4")) * (1 << 20))  # bytes
 
 
 class _OutputPool:
@@ -308,8 +308,22 @@ class _OutputPool:
     their idle segments to the driver (and those still in use once their
     tensors are gone and the cache is emptied again); later outputs start a
     fresh pool. A forked child starts without pools (the parent's are left
-    alone: the child must not touch the parent's device state).
-    DLSIM_CONTIGUOUS=0 turns the pool off (A/B)."""
+    alone: the child must not touch the parent's device state). The ids of
+    retired pools are kept (`retired`, not the pools: a live MemPool keeps
+    torch from freeing its idle segments) until torch's snapshot of them
+    shows no segment left, so outputs still alive from them stay counted
+    (retired_bytes()).
+    The pool rests on torch.cuda.MemPool, CUDAPluggableAllocator and three
+    private torch._C calls (_cuda_beginAllocateCurrentThreadToPool,
+    _cuda_endAllocateToPool, _cuda_releasePool): they are feature-detected on
+    first use, and if any is missing or the pool cannot be made, the pool turns
+    itself off with one warning and outputs come from torch's allocator
+    (aligned_empty: the same alignment, torch's placement) -- a different
+    torch changes where outputs live, never whether an aggregate runs.
+    DLSIM_AB=1 DLSIM_CONTIGUOUS=0 turns the pool off (A/B)."""
+
+    # torch internals the pool needs (feature-detected by usable())
+    _TORCH_C_CALLS = ("_cuda_beginAllocateCurrentThreadToPool", "_cuda_endAllocateToPool", "_cuda_releasePool")
 
     _inherited: List[dict] = []  # a forked child's copy of the parent's pools, never released
 
@@ -319,6 +333,27 @@ class _OutputPool:
         self.lock = threading.Lock()
         self.made = 0  # outputs handed out of the pool
         self._allocator = None
+        self.retired: List[tuple] = []  # ids of released pools whose segments may still be held
+        self.disabled: Optional[str] = None  # why the pool turned itself off (None: usable)
+
+    @classmethod
+    def missing_features(cls) -> List[str]:
+        """The torch features the pool needs that this torch lacks."""
+        miss = []
+        if not hasattr(torch.cuda, "MemPool"):
+            miss.append("torch.cuda.MemPool")
+        if not hasattr(getattr(torch.cuda, "memory", None), "CUDAPluggableAllocator"):
+            miss.append("torch.cuda.memory.CUDAPluggableAllocator")
+        miss += [f"torch._C.{c}" for c in cls._TORCH_C_CALLS if not hasattr(torch._C, c)]
+        return miss
+
+    def _disable(self, why: str) -> None:
+        """Turn the pool off for this process (one warning)."""
+        if self.disabled is None:
+            self.disabled = why
+            import warnings
+            warnings.warn(f"dasklearn_amd: aggregate outputs come from torch's allocator ({why})",
+                          RuntimeWarning, stacklevel=3)
 
     def _mempool(self, idx: int):
         mp = self.pools.get(idx)
@@ -344,8 +379,25 @@ class _OutputPool:
             torch._C._cuda_releasePool(idx, mp.id)
 
     def take(self, numel: int, dtype: torch.dtype, device) -> Optional[torch.Tensor]:
-        if os.environ.get("DLSIM_CONTIGUOUS", "1") == "0":
+        """An output of `numel` elements from the pool, or None (the caller
+        then allocates from torch): the pool is off, or turned itself off."""
+        if self.disabled is not None or _native.ab_env("DLSIM_CONTIGUOUS", "1") == "0":
             return None
+        if self._allocator is None and not self.pools:
+            miss = self.missing_features()
+            if miss:
+                self._disable("this torch lacks " + ", ".join(miss))
+                return None
+        try:
+            return self._take(numel, dtype, device)
+        except torch.OutOfMemoryError:
+            raise
+        except (AttributeError, TypeError, RuntimeError) as e:
+            # a torch whose pool calls changed behaviour: off, not broken
+            self._disable(f"{type(e).__name__}: {e}"[:200])
+            return None
+
+    def _take(self, numel: int, dtype: torch.dtype, device) -> torch.Tensor:
         dev = torch.device(device)
         idx = dev.index if dev.index is not None else torch.cuda.current_device()
         nbytes = numel * _elem_size(dtype)
@@ -373,15 +425,33 @@ class _OutputPool:
             pools = list(self.pools.values())
         return sum(seg["total_size"] for mp in pools for seg in mp.snapshot())
 
+    def retired_bytes(self) -> int:
+        """Bytes of released pools' segments that are still held (outputs
+        alive since before release(), or cached until the next
+        torch.cuda.empty_cache()). Pools with no segment left are dropped."""
+        with self.lock:
+            keep, total = [], 0
+            for pid in self.retired:
+                b = sum(seg["total_size"] for seg in torch.cuda.memory_snapshot(pid))
+                if b:
+                    keep.append(pid)
+                    total += b
+            self.retired = keep
+        return total
+
     def release(self) -> int:
         """Retire every pool and empty torch's cache (a device-wide
         synchronisation, like torch.cuda.empty_cache itself); returns the
-        number of pools retired."""
+        number of pools retired. Their segments still in use stay counted
+        by retired_bytes() until they are gone."""
         with self.lock:
             n = len(self.pools)
+            self.retired.extend(mp.id for mp in self.pools.values())
             self.pools = {}
         if n and torch.cuda.is_initialized():
             torch.cuda.empty_cache()
+        if self.retired:
+            self.retired_bytes()  # drop the pools the empty_cache emptied
         return n
 
 
@@ -406,7 +476,7 @@ def resident_empty(numel: int, dtype: torch.dtype, device, align: int) -> torch.
     DLSIM_CONTIGUOUS=0 turns it off (A/B)."""
     esz = _elem_size(dtype)
     nbytes = numel * esz
-    if nbytes < RESIDENT_CONTIG_MIN or os.environ.get("DLSIM_CONTIGUOUS", "1") == "0" \
+    if nbytes < RESIDENT_CONTIG_MIN or _native.ab_env("DLSIM_CONTIGUOUS", "1") == "0" \
             or torch.device(device).type != "cuda":
         return aligned_empty(numel, dtype, device, align)
     align = max(align, 256)
@@ -591,7 +661,7 @@ def pipeline_chunk_elems(total: int, esz: int) -> int:
 # round 3's rule for A/B runs: results below PAGEABLE_RESULT_BYTES in pageable
 # memory (the runtime stages that copy, and the library call waits for it).
 PAGEABLE_RESULT_BYTES = 4 << 20
-HOST_RESULT_PINNED = os.environ.get("DLSIM_HOST_RESULT", "pinned") != "pageable"
+HOST_RESULT_PINNED = _native.ab_env("DLSIM_HOST_RESULT", "pinned") != "pageable"
 # torch's caching host allocator never gives page-locked memory back to the
 # OS and rounds blocks up to powers of two, so a caller that keeps many small
 # results alive (an in-process simulation holding one model per peer) would
@@ -644,8 +714,8 @@ def pinned_result(nbytes: int) -> bool:
 # DMA (dlsim_host_wreduce_zc). 2 x GNLeNet: the library call with its wait
 # 81 -> 63 us (profiles/r05d/zero_copy.json). DLSIM_ZERO_COPY=0 turns it off,
 # DLSIM_ZC_MAX_KB moves the 4 MiB.
-ZERO_COPY = os.environ.get("DLSIM_ZERO_COPY", "1") != "0"
-ZC_MAX_BYTES = int(float(os.environ.get("DLSIM_ZC_MAX_KB", "4096")) * 1024)
+ZERO_COPY = _native.ab_env("DLSIM_ZERO_COPY", "1") != "0"
+ZC_MAX_BYTES = int(float(_native.ab_env("DLSIM_ZC_MAX_KB", "4096")) * 1024)
 ZC_CALLS = [0]  # zero-copy dtype groups reduced (tests and probes)
 
 

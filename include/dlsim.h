@@ -392,11 +392,18 @@ int dlsim_host_wreduce(int n, int t, const void* const* h_srcs, const size_t* nu
  * 16-B aligned, row_stride a multiple of 8 and >= sum(numels)) and h_out
  * (sum(numels) elements) must be page-locked memory the device maps
  * (hipHostMalloc, torch's pin_memory); anything else is refused with
- * DLSIM_E_ARG before any launch. One launch after the pack; returns after
- * queueing it: synchronise `stream` before reading h_out or reusing the rows.
- * Results are bit-identical to dlsim_wreduce over the packed rows. For a
- * 2 x GNLeNet task (683 KB of rows) the kernel's PCIe reads cost less than
- * the two DMAs' setup; larger models take dlsim_host_wreduce.
+ * DLSIM_E_ARG before any launch. Below 1 MiB of rows: one launch after the
+ * pack. From 1 MiB: the parameter range is cut into up to 8 chunks (at least
+ * 128 KiB per model each; DLSIM_AB=1 DLSIM_ZC_CHUNK_KB=k for A/B runs), and
+ * each chunk's launch is queued as soon as its rows are packed, so the PCIe
+ * reads of chunk c overlap the pack of chunk c + 1. Returns after queueing
+ * the last launch: synchronise `stream` before reading h_out or reusing the
+ * rows. Results are bit-identical to dlsim_wreduce over the packed rows.
+ * The library sets no size cap: the caller chooses when to use it (the
+ * package routes tasks of up to 4 MiB of rows here, arena.py ZC_MAX_BYTES;
+ * for a 2 x GNLeNet task, 683 KB of rows, the kernel's PCIe reads cost less
+ * than the two DMAs' setup); larger models are better served
+ * by dlsim_host_wreduce.
  */
 int dlsim_host_wreduce_zc(int n, int t, const void* const* h_srcs, const size_t* numels, const float* h_weights,
                           void* h_staging, size_t row_stride, void* h_out, int dtype, int mode, int threads,

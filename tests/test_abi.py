@@ -168,13 +168,18 @@ def test_library_errors_stay_on_the_calling_thread():
 
 
 def test_kernel_name_follows_the_dispatch():
-    """dlsim_kernel_name (host logic only, no GPU: 256 CUs assumed when the
-    device query fails): the deferred-store kernel for fp32 fan-in 3-10 and
-    above 14 (grouped) from 10 MB per stream, 11-14 from 16 rows of 512
-    vectors per CU; the tiled kernel otherwise (dispatch.hpp use_defer)."""
+    """dlsim_kernel_name (host logic; the library reads the device's CU
+    count, 256 when the query fails, as here without a GPU): the
+    deferred-store kernel for fp32 fan-in 3-10 and above 14 (grouped) from
+    10 MB per stream, 11-14 from 16 rows of 512 vectors per CU; the tiled
+    kernel otherwise (dispatch.hpp use_defer)."""
     import torch
     f32, bf16 = torch.float32, torch.bfloat16
     d, t = "dlsim::k_wreduce_defer", "dlsim::k_wreduce_tiles"
+    cus = torch.cuda.get_device_properties(0).multi_processor_count if torch.cuda.is_available() else 256
+
+    def wide(nelem):  # fan-in 11-14: defer from 16 rows of 512 float4 vectors per CU
+        return d if nelem // 4 // 512 >= 16 * cus else t
     assert _native.kernel_name(8, 11_181_642, f32) == d  # the north star
     assert _native.kernel_name(8, 11_181_642, f32, _native.DLSIM_FAST) == d
     assert _native.kernel_name(8, 11_181_642, f32, None) == d  # dlsim_mean
@@ -183,9 +188,9 @@ def test_kernel_name_follows_the_dispatch():
     assert _native.kernel_name(3, 11_181_642, f32) == d
     assert _native.kernel_name(2, 11_181_642, f32) == t
     assert _native.kernel_name(2, 125_000_000, f32) == t
-    assert _native.kernel_name(12, 5_000_000, f32) == t  # < 16 rows per CU
-    assert _native.kernel_name(12, 11_181_642, f32) == d
-    assert _native.kernel_name(14, 8_388_608, f32) == d  # exactly 16 rows per CU
+    assert _native.kernel_name(12, 5_000_000, f32) == wide(5_000_000)  # < 16 rows per CU on 256 CUs
+    assert _native.kernel_name(12, 11_181_642, f32) == wide(11_181_642)
+    assert _native.kernel_name(14, 8_388_608, f32) == wide(8_388_608)  # exactly 16 rows per CU on 256 CUs
     assert _native.kernel_name(15, 11_181_642, f32) == d  # the grouped form
     assert _native.kernel_name(100, 11_181_642, f32) == d  # cfg5
     assert _native.kernel_name(100, 2_499_999, f32) == t

@@ -200,3 +200,73 @@ def test_eviction_with_fingerprints():
     c.put("k", t, 1)
     c._evict_one()
     assert len(c) == 0 and slab.free == [0] and c.stats["evictions"] == 1
+
+
+# ---- what the fingerprint samples ---------------
+# _pyhost.shm_rows fingerprints EVERY tensor of a model: its first and last
+# 8-byte word, plus one more per MiB (up to 16 words per tensor).
+
+def _deep_shm_model(seed, layers=12, width=16):
+    import torch.multiprocessing as tmp
+    from torch import nn
+    prev = tmp.get_sharing_strategy()
+    tmp.set_sharing_strategy("file_system")
+    try:
+        g = torch.Generator().manual_seed(seed)
+        m = nn.Sequential(*[nn.Linear(width, width) for _ in range(layers)], nn.Linear(width, 600_000))
+        with torch.no_grad():
+            for q in m.parameters():
+                q.copy_(torch.randn(q.shape, generator=g))
+        m.share_memory()
+        return m
+    finally:
+        tmp.set_sharing_strategy(prev)
+
+
+def _fp(m):
+    from dasklearn_amd import _pyhost
+    ps = [list(m.parameters())]
+    keys, _, fps = _pyhost.shm_rows(ps, list(range(len(ps[0]))))
+    assert keys[0] is not None  # file_system shm: cacheable
+    return fps[0]
+
+
+@pytest.mark.parametrize("where", ["middle_tensor_first", "middle_tensor_last", "big_tensor_last",
+                                   "big_tensor_interior", "last_bias", "first_weight_whole"])
+def test_fingerprint_sees_a_write_to_any_tensor(where):
+    """A write confined to ONE tensor of a 26-tensor model -- one a sample of
+    8 tensors would skip -- changes the fingerprint; round 5's sampled 8
+    words from the middle of 8 tensors and missed such writes."""
+    m = _deep_shm_model(3)
+    ps = list(m.parameters())
+    assert len(ps) == 26
+    before = _fp(m)
+    assert _fp(m) == before  # unchanged content, same fingerprint
+    with torch.no_grad():
+        if where == "middle_tensor_first":
+            ps[13].view(-1)[0] += 1.0  # a bias in the middle of the model (not among round 5's 8)
+        elif where == "middle_tensor_last":
+            ps[11].view(-1)[-1] += 1.0
+        elif where == "big_tensor_last":
+            ps[24].view(-1)[-1] += 1.0  # 600,000 x 16 fp32 (38 MB): its last word
+        elif where == "big_tensor_interior":
+            w = ps[24].view(-1)  # 38 MB: 16 words spread over it; one of them lies at 1/15 of its length
+            k = (w.numel() * 4 - 8) // 15 // 8 * 2  # element at the second sampled word
+            w[k] += 1.0
+        elif where == "last_bias":
+            ps[25].view(-1)[0] += 1.0  # the last tensor of the model
+        else:
+            ps[0].add_(0.01)
+    assert _fp(m) != before
+
+
+def test_fingerprint_blind_spot_is_documented():
+    """What the guard cannot see: a write to an element
+    between two sampled words of one tensor (here the middle of a 256-float
+    weight, which is sampled at its first and last word)."""
+    m = _deep_shm_model(4)
+    ps = list(m.parameters())
+    before = _fp(m)
+    with torch.no_grad():
+        ps[2].view(-1)[128] += 1.0
+    assert _fp(m) == before

@@ -186,3 +186,39 @@ def test_a_model_written_in_place_is_not_served_stale(shm_models, cache):
     assert cache.stats["stale"] == 1 and cache.stats["hits"] == 3 and cache.stats["misses"] == 5
     _check(ms[:4], [0.4, 0.3, 0.2, 0.1])  # the re-sent row is cached again
     assert cache.stats["hits"] == 7 and cache.stats["stale"] == 1
+
+
+class DeepNet(nn.Module):
+    """26 parameter tensors: more than round 5's fingerprint sampled (8)."""
+
+    def __init__(self, seed):
+        super().__init__()
+        g = torch.Generator().manual_seed(seed)
+        self.body = nn.Sequential(*[nn.Linear(32, 32) for _ in range(12)], nn.Linear(32, 1000))
+        with torch.no_grad():
+            for q in self.parameters():
+                q.copy_(torch.randn(q.shape, generator=g) * 0.05)
+
+
+def test_a_rewritten_middle_tensor_is_not_served_stale(cache):
+    """a cached model one of whose MIDDLE tensors alone is
+    rewritten in place (a partial fine-tune; round 5's guard sampled 8 of 26
+    tensors and not this one) is caught by the fingerprint of every tensor:
+    the entry is dropped ("stale"), the model re-sent, the result exact."""
+    prev = tmp.get_sharing_strategy()
+    tmp.set_sharing_strategy("file_system")
+    try:
+        ms = [DeepNet(s) for s in range(4)]
+        for m in ms:
+            m.share_memory()
+        assert len(list(ms[0].parameters())) == 26
+        _check(ms, None)
+        assert cache.stats["misses"] == 4 and cache.stats["stale"] == 0
+        _check(ms, None)
+        assert cache.stats["hits"] == 4
+        with torch.no_grad():
+            list(ms[2].parameters())[13].mul_(0.5)  # layer 6's bias only, same shm storage
+        _check(ms, [0.1, 0.2, 0.3, 0.4])
+        assert cache.stats["stale"] == 1 and cache.stats["hits"] == 7 and cache.stats["misses"] == 5
+    finally:
+        tmp.set_sharing_strategy(prev)

@@ -489,6 +489,7 @@ def test_zero_copy_pipelined_chunks(monkeypatch):
     fp32 and bf16, 7 models: bit-exact against the oracle."""
     from dasklearn_amd import _native, arena
     from dasklearn_amd.arena import aggregate_modules
+    monkeypatch.setenv("DLSIM_AB", "1")  # the library reads A/B switches only under DLSIM_AB=1
     monkeypatch.setenv("DLSIM_ZC_CHUNK_KB", "16")  # read per call: many small chunks
     for dt in (torch.float32, torch.bfloat16):
         torch.manual_seed(5)

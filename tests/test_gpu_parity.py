@@ -250,24 +250,25 @@ def test_cfg5_100way_11M_f32_bit_exact():
     torch.cuda.empty_cache()
 
 
-def test_cfg4_2way_125M_bf16_properties():
-    """2-way bf16 gossip merge of 125 M params with age weights [3/8, 5/8]:
-    size-independent properties at full size, bit-exact on a strided sample."""
+def test_cfg4_2way_125M_bf16_bit_exact():
+    """BASELINE.json configs[3] at full size on one GPU: the 2-way bf16 gossip
+    merge of 125,000,000 params with age weights [3/8, 5/8], EVERY element
+    against the oracle's fold with per-step bf16 rounding (fedavg.py:23-25;
+    VERDICT r05 missing #3: rounds 1-5 compared a 1-in-997 sample), plus the
+    one-hot property (a selected input comes back unchanged)."""
     p = 125_000_000
-    a = torch.randn(p, device=dev()).to(torch.bfloat16)
-    b = torch.randn(p, device=dev()).to(torch.bfloat16)
+    g = torch.Generator(device=dev()).manual_seed(4)
+    a = torch.randn(p, device=dev(), generator=g).to(torch.bfloat16)
+    b = torch.randn(p, device=dev(), generator=g).to(torch.bfloat16)
     w = orc.reference_weights(2, [3 / 8, 5 / 8])
     out = torch.empty_like(a)
     _native.wreduce([a, b], w, out)
-    # property 1: one-hot weights reproduce an input exactly
+    assert orc.same_bits(from_dev(out), orc.wreduce([from_dev(a), from_dev(b)], w, "bf16"))
     sel = torch.empty_like(a)
     _native.wreduce([a, b], orc.reference_weights(2, [0.0, 1.0]), sel)
     assert torch.equal(sel, b)
-    # property 2: swapping inputs and weights == same multiset but different
-    # order: equal to the oracle on a strided sample of elements
-    idx = torch.arange(0, p, 997, device=dev())
-    rows = [from_dev(a[idx]), from_dev(b[idx])]
-    assert orc.same_bits(from_dev(out[idx]), orc.wreduce(rows, w, "bf16"))
+    del a, b, out, sel
+    torch.cuda.empty_cache()
 
 
 @pytest.mark.parametrize("dtype,p", [("f32", 1_999_999), ("f32", 2_000_003), ("f32", 4_999_997), ("f32", 5_000_003),

@@ -30,6 +30,7 @@ def _bits(t: torch.Tensor) -> np.ndarray:
 def _case(rng, dt, h2d_kb, monkeypatch, all_resident=False, none_resident=False):
     from dasklearn_amd import _native
     from dasklearn_amd.arena import row_stride
+    monkeypatch.setenv("DLSIM_AB", "1")  # A/B switches are read only under DLSIM_AB=1
     monkeypatch.setenv("DLSIM_H2D_MIN_KB", str(h2d_kb))
     dev = torch.device("cuda", 0)
     tdt = DT[dt]

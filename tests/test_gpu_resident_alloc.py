@@ -148,6 +148,7 @@ def test_output_pool_is_per_stream():
 
 
 def test_output_pool_off_switch(monkeypatch):
+    monkeypatch.setenv("DLSIM_AB", "1")
     monkeypatch.setenv("DLSIM_CONTIGUOUS", "0")
     made = arena.OUTPUT_POOL.made
     a = arena.arena_empty(BIG, torch.float32, "cuda")
@@ -175,6 +176,24 @@ def test_output_pool_blocks_are_torch_allocations():
     torch.cuda.synchronize()
     arena.OUTPUT_POOL.release()
     assert torch.cuda.memory_reserved() <= r0
+    assert _native.pool_stats()["live_bytes"] == segs0["live_bytes"]
+
+
+def test_release_with_a_live_output_counts_it_as_retired():
+    """an output alive across release() keeps its segment; the
+    pool counts it in retired_bytes() (not in cached_bytes()) until the output
+    is gone and the cache emptied, and then the library's block is freed."""
+    _fresh_pool()
+    segs0 = _native.pool_stats()
+    x = arena.arena_empty(BIG, torch.float32, "cuda")
+    x.fill_(2.0)
+    assert arena.OUTPUT_POOL.release() == 1
+    assert arena.OUTPUT_POOL.cached_bytes() == 0 and arena.OUTPUT_POOL.retired_bytes() >= BIG * 4
+    assert float(x[-1]) == 2.0  # still a valid allocation
+    del x
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    assert arena.OUTPUT_POOL.retired_bytes() == 0 and arena.OUTPUT_POOL.retired == []
     assert _native.pool_stats()["live_bytes"] == segs0["live_bytes"]
 
 

@@ -21,7 +21,7 @@ def checker(tmp_path_factory):
 @pytest.mark.parametrize("mode", ["stream", "memcpy"])
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_pack_matches_concatenation(checker, mode, seed):
-    env = dict(os.environ, DLSIM_PACK_COPY=mode)
+    env = dict(os.environ, DLSIM_AB="1", DLSIM_PACK_COPY=mode)
     r = subprocess.run([checker, str(seed)], env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and r.stdout.strip() == "OK", r.stdout + r.stderr
 

@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import json
 import os
+import re
 import sys
 
 import pytest
@@ -83,8 +84,19 @@ def test_no_kernel_spills_and_deferred_kernels_present(report):
         for nf in list(range(2, 15)) + [0]:
             assert any(f"ELi{nf}ELi8ELi{32 if nf < 12 else 24}ELi2ELi2ELi0EE" in n for n in got), (pol, nf)
         assert not any(f"ELi1ELi8ELi32ELi2ELi2ELi0EE" in n for n in got), pol
-    # the exact policy's fixed fan-in kernels compiled per even R (dispatch.hpp launch_defer_rc)
+    # the exact policy's fixed fan-in kernels compiled per even R (dispatch.hpp
+    # launch_defer_rc): from R = 4 (defer_rows' least) for fan-in 3-14 (the
+    # default deferral floor is fan-in 3); R = 2 and fan-in 2 (reachable only
+    # through the A/B switches) take the runtime R. Round 6: 168 compiled-R
+    # kernels (round 5: 196, fan-in 2 and R = 2 included).
     exact = [n for n in names if "k_wreduce_defer" in n and "8F32Exact" in n]
-    for nf, rmax in ((3, 32), (8, 32), (11, 32), (12, 24), (14, 24)):
-        for rc in range(2, rmax + 1, 2):
-            assert any(f"ELi{nf}ELi8ELi{rmax}ELi2ELi2ELi{rc}EE" in n for n in exact), (nf, rc)
+    by_nf = {}
+    for n in exact:
+        m = re.search(r"EELi(\d+)ELi8ELi(\d+)ELi2ELi2ELi(\d+)EE", n)
+        if m and int(m.group(3)) > 0:
+            by_nf.setdefault(int(m.group(1)), set()).add((int(m.group(2)), int(m.group(3))))
+    assert sorted(by_nf) == list(range(3, 15)), sorted(by_nf)
+    for nf, got in by_nf.items():
+        rmax = 32 if nf < 12 else 24
+        assert got == {(rmax, rc) for rc in range(4, rmax + 1, 2)}, (nf, sorted(got))
+    assert sum(len(v) for v in by_nf.values()) == 168

@@ -11,6 +11,7 @@ from __future__ import annotations
 import os
 import threading
 import time
+import warnings
 
 import pytest
 import torch
@@ -50,15 +51,24 @@ class FakeDevice:
             self.active -= 1
 
 
+class IdleMemPool:
+    """A MemPool stand-in whose segments are all gone."""
+    id = (0, 1)
+
+    def snapshot(self):
+        return []
+
+
 @pytest.fixture()
 def pool(monkeypatch):
     fake = FakeDevice()
     p = arena._OutputPool()
-    monkeypatch.setattr(p, "_mempool", lambda idx: p.pools.setdefault(idx, object()))
+    monkeypatch.setattr(p, "_mempool", lambda idx: p.pools.setdefault(idx, IdleMemPool()))
     monkeypatch.setattr(p, "_empty_in", fake.empty_in)
     emptied = []
     monkeypatch.setattr(torch.cuda, "is_initialized", lambda: True)
     monkeypatch.setattr(torch.cuda, "empty_cache", lambda: emptied.append(1))
+    monkeypatch.setattr(torch.cuda, "memory_snapshot", lambda pid=None: [])
     monkeypatch.delenv("DLSIM_CONTIGUOUS", raising=False)
     p.fake, p.emptied = fake, emptied
     return p
@@ -114,6 +124,9 @@ def test_release_retires_the_pools_and_empties_the_cache(pool):
 
 def test_off_switch_and_fork(pool, monkeypatch):
     monkeypatch.setenv("DLSIM_CONTIGUOUS", "0")
+    monkeypatch.delenv("DLSIM_AB", raising=False)
+    assert pool.take(N, torch.float32, "cuda:0") is not None  # A/B switches are read only under DLSIM_AB=1
+    monkeypatch.setenv("DLSIM_AB", "1")
     assert pool.take(N, torch.float32, "cuda:0") is None
     monkeypatch.delenv("DLSIM_CONTIGUOUS")
     pool.take(N, torch.float32, "cuda:0")
@@ -154,3 +167,71 @@ def test_pinned_result_budget(monkeypatch):
     reserved["v"] = 0
     b.calls = 0
     assert not arena.pinned_result(1000)  # DLSIM_HOST_RESULT=pageable
+
+
+@pytest.mark.parametrize("missing", ["MemPool", "CUDAPluggableAllocator", *arena._OutputPool._TORCH_C_CALLS])
+def test_pool_falls_back_when_torch_lacks_a_feature(monkeypatch, missing):
+    """on a torch without one of the pool's features the
+    pool turns itself off with ONE warning and arena_empty hands out outputs
+    from torch's allocator (aligned_empty), instead of raising."""
+    owner = {"MemPool": torch.cuda, "CUDAPluggableAllocator": torch.cuda.memory}.get(missing, torch._C)
+    monkeypatch.delattr(owner, missing, raising=False)
+    p = arena._OutputPool()
+    monkeypatch.setattr(arena, "OUTPUT_POOL", p)
+    made = []
+
+    def fake_aligned(numel, dtype, device, align):
+        made.append((numel, dtype, str(device), align))
+        return torch.empty(numel, dtype=dtype)
+    monkeypatch.setattr(arena, "aligned_empty", fake_aligned)
+    monkeypatch.delenv("DLSIM_CONTIGUOUS", raising=False)
+    with pytest.warns(RuntimeWarning, match="torch's allocator"):
+        a = arena.arena_empty(N, torch.float32, "cuda:0")
+    assert a.numel() == N and p.disabled and missing in p.disabled
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")  # no second warning
+        b = arena.arena_empty(N, torch.float32, "cuda:0")
+    assert b.numel() == N and p.made == 0 and not p.pools
+    al = arena.base_align(N * 4, 4)  # aligned as arena_empty aligns any torch-allocated output
+    assert made == [(N, torch.float32, "cuda:0", al)] * 2
+
+
+def test_pool_falls_back_when_a_pool_call_raises(pool, monkeypatch):
+    """A torch whose pool calls exist but fail (changed signature or
+    behaviour): off, with the error recorded; out-of-memory still raises."""
+    def broken(mp, idx, nbytes):
+        raise TypeError("_cuda_beginAllocateCurrentThreadToPool(): incompatible function arguments")
+    monkeypatch.setattr(pool, "_empty_in", broken)
+    with pytest.warns(RuntimeWarning, match="TypeError"):
+        assert pool.take(N, torch.float32, "cuda:0") is None
+    assert pool.take(N, torch.float32, "cuda:0") is None and pool.made == 0
+    q = arena._OutputPool()
+    monkeypatch.setattr(q, "_mempool", lambda idx: q.pools.setdefault(idx, object()))
+
+    def oom(mp, idx, nbytes):
+        raise torch.OutOfMemoryError("HIP out of memory")
+    monkeypatch.setattr(q, "_empty_in", oom)
+    with pytest.raises(torch.OutOfMemoryError):
+        q.take(N, torch.float32, "cuda:0")
+    assert q.disabled is None
+
+
+def test_released_pools_stay_counted_until_empty(pool, monkeypatch):
+    """release() keeps the retired pools' ids (not the pools: a
+    live MemPool would keep torch from freeing its idle segments) and counts
+    their segments in retired_bytes() until torch's snapshot shows none."""
+    class FakeMemPool:
+        id = (0, 7)
+
+        def snapshot(self):
+            return segs.get(self.id, [])
+    segs = {(0, 7): [{"total_size": 6 << 20}]}
+    mp = FakeMemPool()
+    monkeypatch.setattr(torch.cuda, "memory_snapshot", lambda pid=None: segs.get(pid, []))
+    monkeypatch.setattr(pool, "_mempool", lambda idx: pool.pools.setdefault(idx, mp))
+    pool.take(N, torch.float32, "cuda:0")
+    assert pool.cached_bytes() == 6 << 20 and pool.retired_bytes() == 0
+    assert pool.release() == 1
+    assert pool.cached_bytes() == 0 and pool.retired_bytes() == 6 << 20 and pool.retired == [(0, 7)]
+    segs.clear()  # the output died and the cache was emptied
+    assert pool.retired_bytes() == 0 and pool.retired == []
