@@ -565,21 +565,24 @@ __global__ __launch_bounds__(kDeferBlock) void k_chunk_mean_defer(const ChunkMea
 // of all MF contributors load back to back and fold straight-line (the
 // reduce's fixed fan-in form, defer_rows), and the stores run unguarded: a row
 // past the block's count goes to vector nvec, past the task's output range,
-// which the buffer store drops (the ragged block owns the partial row there).
+// which the buffer store drops.
+// Layout: task t owns blocks [block_start[t], block_start[t + 1]), at least
+// one; block j of the task folds rows [j * R, min((j + 1) * R, rows)), and
+// the task's LAST block then also does its ragged end (the partial row, the
+// head and the scalar columns, on its first 256 lanes as cm_task's block 0).
+// No block is spent on ragged ends alone: k_chunk_mean_defer's separate
+// ragged blocks pushed Conflux's ten ResNet-18 chunks from R = 22 to 24 rows
+// per block to fit one round (38.8 against 37.5 us tiled at m = 4,
+// profiles/r06_chunk_ab/); here R = 22 fits, the reduce's grid.
 template <class Op, int MF, int RMAX, int U>
 __global__ __launch_bounds__(kDeferBlock) void k_chunk_mean_defer_m(const ChunkMeanSlots s, int R) {
   static_assert(MF >= 1 && MF < 16, "level 0 only");
   using T = acc_t<Op>;
   const uint32_t bid = blockIdx.x;
   int t = 0;
-  uint32_t local = 0;
-  if (bid < static_cast<uint32_t>(s.ntasks)) {
-    t = static_cast<int>(bid);
-  } else {
-    const uint32_t f = bid - static_cast<uint32_t>(s.ntasks);
-    while (t + 1 < s.ntasks && f >= s.block_start[t + 1]) ++t;  // wave-uniform scan
-    local = f - s.block_start[t] + 1;
-  }
+  while (t + 1 < s.ntasks && bid >= s.block_start[t + 1]) ++t;  // wave-uniform scan
+  const uint32_t local = bid - s.block_start[t];
+  const bool last = bid + 1 == s.block_start[t + 1];
   const PtrArgs a{s.p + s.ptr_off[t]};
   const size_t n = s.nelem[t], ilp_begin = s.ilp_begin[t];
   const uint32_t head = s.head[t];
@@ -589,20 +592,10 @@ __global__ __launch_bounds__(kDeferBlock) void k_chunk_mean_defer_m(const ChunkM
   const size_t nvec = (ilp_begin - head) / Op::E;
   const size_t rows = nvec / kDeferBlock;
   const OutRef o = make_out<kCmStore<Op>>(static_cast<char*>(s.out[t]) + hb, nvec);
-  if (local == 0) {  // the ragged block, as k_chunk_mean_defer's
-    if (threadIdx.x >= kBlock) return;
-    if (rows * kDeferBlock < nvec) {
-      using PT = CmShape<kDeferBlock / kBlock, false, (MF <= 6 ? 4 : 8)>;  // dispatch.hpp CmFewRows / CmDefault RF
-      cm_tile<Op, ShiftArgs<PtrArgs>, PT, 2, true, true>(sa, MF, o, rows * kDeferBlock + threadIdx.x, nvec,
-                                                         ilp_begin - head, div);
-    }
-    if (head > 0) cm_scalar_cols<Op, PtrArgs>(a, MF, s.out[t], 0, head, ilp_begin, false, div);
-    const size_t c0 = head + nvec * Op::E;
-    if (c0 < n) cm_scalar_cols<Op, PtrArgs>(a, MF, s.out[t], c0, n, ilp_begin, (s.flags[t] & kCmInner) != 0, div);
-    return;
-  }
-  const size_t first = static_cast<size_t>(local - 1) * static_cast<size_t>(R);
-  const int Rb = static_cast<int>(rows - first < static_cast<size_t>(R) ? rows - first : static_cast<size_t>(R));
+  const size_t first = static_cast<size_t>(local) * static_cast<size_t>(R);
+  const int Rb = first >= rows ? 0
+                               : static_cast<int>(rows - first < static_cast<size_t>(R) ? rows - first
+                                                                                        : static_cast<size_t>(R));
   const size_t v0 = first * kDeferBlock + threadIdx.x;
   u32x4 res[RMAX];
 #pragma unroll
@@ -640,6 +633,15 @@ __global__ __launch_bounds__(kDeferBlock) void k_chunk_mean_defer_m(const ChunkM
 #pragma unroll
   for (int r = 0; r < RMAX; ++r)
     store_vec<kCmStore<Op>>(o, r < Rb ? v0 + static_cast<size_t>(r) * kDeferBlock : nvec, res[r]);
+  if (!last || threadIdx.x >= kBlock) return;  // whole waves 4-7: the barriers below count the rest
+  if (rows * kDeferBlock < nvec) {  // the partial row: 256 lanes x 2 vectors, bounds-checked
+    using PT = CmShape<kDeferBlock / kBlock, false, (MF <= 6 ? 4 : 8)>;  // dispatch.hpp CmFewRows / CmDefault RF
+    cm_tile<Op, ShiftArgs<PtrArgs>, PT, 2, true, true>(sa, MF, o, rows * kDeferBlock + threadIdx.x, nvec,
+                                                       ilp_begin - head, div);
+  }
+  if (head > 0) cm_scalar_cols<Op, PtrArgs>(a, MF, s.out[t], 0, head, ilp_begin, false, div);
+  const size_t c0 = head + nvec * Op::E;
+  if (c0 < n) cm_scalar_cols<Op, PtrArgs>(a, MF, s.out[t], c0, n, ilp_begin, (s.flags[t] & kCmInner) != 0, div);
 }
 
 }  // namespace dlsim

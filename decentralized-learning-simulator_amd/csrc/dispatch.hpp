@@ -860,6 +860,23 @@ hipError_t launch_chunk_defer_m(const dlsim::ChunkMeanSlots& s, int m, int R, un
     return launch_chunk_defer_m<Op, MF + 1>(s, m, R, grid, st);
   }
 }
+// R of the fixed-m form (k_chunk_mean_defer_m: no separate ragged blocks, at
+// least one block per task): the fewest even rows per block with every block
+// of the launch resident at once (up to 24 rows), else two rounds, else rmax.
+inline size_t chunk_defer_m_blocks(size_t rows, size_t R) { return rows ? (rows + R - 1) / R : 1; }
+inline int chunk_defer_m_rows(const std::vector<size_t>& rows, size_t cus, int rmax) {
+  if (defer_r_override() > 0) return std::min(defer_r_override(), rmax);
+  auto blocks = [&](size_t R) {
+    size_t b = 0;
+    for (size_t r : rows) b += chunk_defer_m_blocks(r, R);
+    return b;
+  };
+  for (size_t R = 4; R <= static_cast<size_t>(std::min(rmax, kDeferOneRoundMax)); R += 2)
+    if (blocks(R) <= cus) return static_cast<int>(R);
+  for (size_t R = 4; R <= static_cast<size_t>(rmax); R += 2)
+    if (blocks(R) <= 2 * cus) return static_cast<int>(R);
+  return rmax;
+}
 inline int chunk_defer_rows(const std::vector<size_t>& rows, size_t cus, int rmax = kCmDeferRMax) {
   if (defer_r_override() > 0) return std::min(defer_r_override(), rmax);
   const size_t nt = rows.size();
@@ -949,14 +966,19 @@ int run_chunk_mean(int b, const int* fan_in, const void* const* in, void* const*
     defer = (defer || fixed) && cols * Op::kBytes >= 20000000;
     fixed = fixed && defer;
     int R = 0;
-    if (defer)
-      R = chunk_defer_rows(rows, static_cast<size_t>(device_cus()), fixed ? cm_defer_m_rmax(m0) : kCmDeferRMax);
+    if (fixed)
+      R = chunk_defer_m_rows(rows, static_cast<size_t>(device_cus()), cm_defer_m_rmax(m0));
+    else if (defer)
+      R = chunk_defer_rows(rows, static_cast<size_t>(device_cus()));
     size_t blocks = 0;
     int nt = 0, p = 0;
     for (const CmTask& k : batch) {
       const int m = fan_in[k.t];
-      const size_t tb = defer ? (rows[static_cast<size_t>(nt)] + R - 1) / R + 1 : task_blocks(k.ib, k.head);
-      s.block_start[nt] = static_cast<uint32_t>(blocks - static_cast<size_t>(nt));  // full blocks before task nt
+      const size_t rt = rows[static_cast<size_t>(nt)];
+      const size_t tb = fixed ? chunk_defer_m_blocks(rt, static_cast<size_t>(R))
+                              : defer ? (rt + R - 1) / R + 1 : task_blocks(k.ib, k.head);
+      // the fixed-m kernel: first block of task nt; the others: full blocks before it
+      s.block_start[nt] = static_cast<uint32_t>(fixed ? blocks : blocks - static_cast<size_t>(nt));
       s.ptr_off[nt] = static_cast<uint16_t>(p);
       s.m[nt] = static_cast<uint16_t>(m);
       s.out[nt] = outs[k.t];
@@ -970,7 +992,7 @@ int run_chunk_mean(int b, const int* fan_in, const void* const* in, void* const*
       ++nt;
     }
     s.ntasks = nt;
-    s.block_start[nt] = static_cast<uint32_t>(blocks - static_cast<size_t>(nt));
+    s.block_start[nt] = static_cast<uint32_t>(fixed ? blocks : blocks - static_cast<size_t>(nt));
     if (blocks > 0x7fffffffu) return fail(DLSIM_E_ARG, "chunk mean batch too large");
     if (defer) {
       if constexpr (Op::kBytes == 4) {

@@ -37,14 +37,20 @@ def main():
     rows = aligned_empty(sets * m * stride, torch.float32, dev, base_align(P * 4, 4)).view(sets, m, stride)
     g = torch.Generator(device=dev).manual_seed(1)
     rows[:, :, :P].copy_(torch.randn((sets, m, P), generator=g, device=dev) * 0.05)
-    outs = [arena_empty(P, torch.float32, dev) for _ in range(sets)]
+    # round 6: the outputs rotate over >= 1 GiB too (a multiple of the input
+    # sets), as bench.py and bench_chunks.py since round 5
+    nout = -(-max(sets, -(-(1 << 30) // (P * 4))) // sets) * sets
+    outs = [arena_empty(P, torch.float32, dev) for _ in range(nout)]
     bounds = [(c * (P // k), (c + 1) * (P // k) if c < k - 1 else P) for c in range(k)]
     w = _native.fp32_weights([1.0 / m] * m)
-    plans = [_native.ReducePlan([rows[s, i, :P] for i in range(m)], w, outs[s]) for s in range(sets)]
-    chunk_tasks = [[([rows[s, i, b:e] for i in range(m)], outs[s][b:e]) for b, e in bounds] for s in range(sets)]
-    one_task = [[([rows[s, i, :P] for i in range(m)], outs[s])] for s in range(sets)]
+    plans = [_native.ReducePlan([rows[j % sets, i, :P] for i in range(m)], w, outs[j]) for j in range(nout)]
+    chunk_tasks = [[([rows[j % sets, i, b:e] for i in range(m)], outs[j][b:e]) for b, e in bounds]
+                   for j in range(nout)]
+    one_task = [[([rows[j % sets, i, :P] for i in range(m)], outs[j])] for j in range(nout)]
+    mean_in = [[rows[j % sets, i, :P] for i in range(m)] for j in range(nout)]
     legs = {
         "reduce_n%d" % m: lambda s: plans[s].launch(),
+        "mean_n%d (dlsim_mean, deferred)" % m: lambda s: _native.mean(mean_in[s], outs[s]),
         "chunk_mean_k10": lambda s: _native.chunk_mean_batched(chunk_tasks[s], threads=4),
         "chunk_mean_one_task": lambda s: _native.chunk_mean_batched(one_task[s], threads=4),
         "input_order_mean_one_task": lambda s: _native.mean_batched(one_task[s]),
@@ -55,11 +61,11 @@ def main():
     for _ in range(3):
         for name, fn in legs.items():
             for r in range(10):
-                fn(r % sets)
+                fn(r % nout)
             torch.cuda.synchronize()
             e0.record()
             for r in range(reps):
-                fn(r % sets)
+                fn(r % nout)
             e1.record()
             torch.cuda.synchronize()
             res[name].append(e0.elapsed_time(e1) * 1e3 / reps)

@@ -1,0 +1,41 @@
+"""Child of tests/test_gpu_parity.py::test_deferred_kernel_odd_rows_under_the_ab_switch
+(TEST INFRASTRUCTURE). Runs under DLSIM_AB=1 DLSIM_DEFER_R=<odd r> (read once
+per process by the library): deferred launches with an odd row count per
+block, checked against the oracle. Prints one JSON line of named checks."""
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+for p in (ROOT, os.path.join(ROOT, "decentralized-learning-simulator_amd")):
+    sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def main():
+    from dasklearn_amd import _native
+    from oracle import oracle as orc
+    dev = torch.device("cuda", 0)
+    checks = {"switch_seen": os.environ.get("DLSIM_AB") == "1" and int(os.environ["DLSIM_DEFER_R"]) % 2 == 1}
+    for n, p in ((4, 5_000_003), (8, 11_181_642), (17, 2_600_001)):
+        assert _native.kernel_name(n, p, torch.float32) == "dlsim::k_wreduce_defer"
+        g = torch.Generator(device=dev).manual_seed(p + n)
+        xs = [torch.randn(p, generator=g, device=dev) * 0.05 for _ in range(n)]
+        host = np.stack([x.cpu().numpy() for x in xs])
+        w = orc.reference_weights(n, list(np.random.default_rng(n).dirichlet(np.ones(n))))
+        out = torch.empty_like(xs[0])
+        _native.wreduce(xs, w, out)
+        checks[f"exact_n{n}"] = orc.same_bits(out.cpu().numpy(), orc.wreduce_rows_f32(host, w))
+        _native.wreduce(xs, w, out, _native.DLSIM_FAST)
+        checks[f"fast_n{n}"] = orc.same_bits(out.cpu().numpy(), orc.wreduce(list(host), w, "f32", mode="fast"))
+        _native.mean(xs, out)
+        checks[f"mean_n{n}"] = orc.same_bits(out.cpu().numpy(), orc.mean(list(host), "f32"))
+    torch.cuda.synchronize()
+    print(json.dumps({"r": int(os.environ["DLSIM_DEFER_R"]), "checks": checks}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

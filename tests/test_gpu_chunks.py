@@ -461,12 +461,41 @@ def test_chunk_mean_deferred_launch(m, k):
     (line-misaligned heads, partial rows, scalar tails), the level-1 flush at
     16 rows (m = 16, 17, 31), launches split at the 192-input limit (m = 40:
     some below 20 MB, tiled), m = 5 tiled: every element bit-identical to the
-    order-exact oracle at 4 worker threads."""
+    order-exact oracle at 4 worker threads. (Round 6: m = 5 now takes the
+    fixed-m form, k_chunk_mean_defer_m.)"""
     P = 6_300_001
     g = torch.Generator(device=dev()).manual_seed(m * 100 + k)
     flats = [torch.randn(P, generator=g, device=dev()) * 0.05 for _ in range(m)]
     rng = np.random.default_rng(m + k)
     cuts = sorted(set(int(c) // 4 * 4 for c in rng.integers(1, P - 1, size=k - 1)))
+    bounds = list(zip([0] + cuts, cuts + [P]))
+    tasks = [([f[b:e] for f in flats], torch.empty(e - b, device=dev())) for b, e in bounds]
+    _native.chunk_mean_batched(tasks, threads=4)
+    host = [f.cpu().numpy() for f in flats]
+    for (b, e), (_, out) in zip(bounds, tasks):
+        assert orc.same_bits(out.cpu().numpy(), orc.chunk_mean([h[b:e] for h in host], "f32", 4)), (b, e)
+    del flats, tasks
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("m,k", [(2, 3), (4, 10), (7, 1), (10, 10), (12, 6), (15, 4)])
+def test_chunk_mean_fixed_m_deferred_launch(m, k):
+    """Round 6: an fp32 launch whose tasks all have the same m < 16 (>= 20 MB
+    per stream, 16-B aligned) takes the fixed-m deferred kernel
+    (k_chunk_mean_defer_m: MF contributors folded straight-line, each task's
+    last row block also doing its ragged end). Arbitrary cuts plus a tiny
+    chunk (no whole row: only the last-block ragged work), a chunk of whole
+    rows exactly, line-misaligned heads and scalar tails: every element
+    bit-identical to the order-exact oracle at 4 worker threads."""
+    P = 6_300_001 if m < 12 else 3_900_001
+    g = torch.Generator(device=dev()).manual_seed(m * 1000 + k)
+    flats = [torch.randn(P, generator=g, device=dev()) * 0.05 for _ in range(m)]
+    rng = np.random.default_rng(m * 7 + k)
+    cuts = set(int(c) // 4 * 4 for c in rng.integers(1, P - 1, size=k - 1))
+    if k >= 4:
+        c0 = min(cuts)
+        cuts |= {c0 + 1000, c0 + 1000 + 4 * 512 * 40}  # a 1,000-element chunk, then 40 whole rows
+    cuts = sorted(c for c in cuts if 0 < c < P)
     bounds = list(zip([0] + cuts, cuts + [P]))
     tasks = [([f[b:e] for f in flats], torch.empty(e - b, device=dev())) for b, e in bounds]
     _native.chunk_mean_batched(tasks, threads=4)

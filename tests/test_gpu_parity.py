@@ -8,7 +8,10 @@ each test.
 """
 from __future__ import annotations
 
+import json
 import os
+import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -20,6 +23,9 @@ from oracle import oracle as orc
 pytestmark = pytest.mark.gpu
 
 from dasklearn_amd import _native  # noqa: E402
+
+
+HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 def dev():
@@ -298,8 +304,8 @@ def test_launch_shapes_either_side_of_the_size_switch(dtype, p, n):
     (4, 5_000_003),            # ragged last block (bounds-checked rows) and an E tail of 3
     (3, 5_000_002),            # the smallest deferred fan-in
     (5, 4 * 512 * 10 * 245),   # whole rows only, no tail
-    (7, 11_181_642 + 1),       # the north star's grid (R = 12), E tail of 1
-    (10, 8_392_711),           # the largest deferred fan-in, odd R (duplicate-row loads)
+    (7, 11_181_642 + 1),       # the north star's grid (R = 22), E tail of 1
+    (10, 8_392_711),           # the largest fan-in deferred at any size (R = 18)
     (9, 5_000_011),
     (12, 11_181_642 + 3),      # fan-in 11-14 from 16 rows per CU (RMAX 24)
     (6, 20_000_003),           # more rows than one round holds: R from the cost model
@@ -471,3 +477,19 @@ def test_batched_call_runs_large_tasks_through_the_deferred_kernel():
         assert orc.same_bits(out.cpu().numpy(), orc.wreduce_rows_f32(hx, hw))
     del tasks, host
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("r", [5, 7])
+def test_deferred_kernel_odd_rows_under_the_ab_switch(r):
+    """defer_rows only returns even R, so the runtime-R kernel's
+    re-read of row r0 for a row group past R (`row = r0 + u < R ? r0 + u : r0`)
+    runs only under the A/B switch DLSIM_DEFER_R (read once per process: a
+    fresh interpreter). Fixed fan-in (exact, fast, mean) and the grouped form,
+    a ragged last block and an E tail, every element against the oracle."""
+    env = dict(os.environ, DLSIM_AB="1", DLSIM_DEFER_R=str(r))
+    out = subprocess.run([sys.executable, os.path.join(HERE, "_defer_r_child.py")], env=env,
+                         capture_output=True, text=True, timeout=180)
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert out.returncode == 0 and lines, out.stdout[-2000:] + out.stderr[-3000:]
+    res = json.loads(lines[-1])
+    assert res["checks"] and all(res["checks"].values()), res
