@@ -552,6 +552,7 @@ int dlsim_host_wreduce_zc(int n, int t, const void* const* h_srcs, const size_t*
   }
   const size_t K = (total + L - 1) / L;
   dlsim::PackJob job;
+  job.streaming = dlsim::pack_streaming(true);  // rows read over PCIe next: leave them in the CPU caches
   for (size_t c = 0; c < K; ++c) {
     const size_t c0 = c * L, c1 = std::min(total, c0 + L);
     for (int i = 0; i < n; ++i) {

@@ -67,11 +67,18 @@ inline void copy_stream(char* dst, const char* src, size_t bytes) {
   std::memcpy(dst + body, src + body, bytes - body);
 }
 
-// DLSIM_PACK_COPY=memcpy selects plain memcpy, read per call (A/B probes:
-// scripts/probe_host_pack.py); default: streaming.
-inline bool pack_streaming() {
+// Streaming (non-temporal) stores for the packs whose rows go out by DMA: the
+// rows are read once, by the copy engine, from DRAM. The zero-copy pack
+// (dlsim_host_wreduce_zc) uses plain memcpy instead: its rows are read by the
+// kernel over PCIe moments later, and stores that leave them in the CPU
+// caches cut a 2 x GNLeNet pack + launch from 46-49 to 36-41 us and a
+// fan-in-7 one from 96-98 to 73-75 (profiles/r06_zc_pack_ab/). Under DLSIM_AB=1,
+// DLSIM_PACK_COPY=memcpy|stream (read per call) forces either.
+inline bool pack_streaming(bool zero_copy = false) {
   const char* e = dlsim::ab_getenv("DLSIM_PACK_COPY");
-  return !(e && std::strcmp(e, "memcpy") == 0);
+  if (e && std::strcmp(e, "memcpy") == 0) return false;
+  if (e && std::strcmp(e, "stream") == 0) return true;
+  return !zero_copy;
 }
 
 struct PackSlice {
@@ -89,7 +96,7 @@ struct PackJob {
   std::unique_ptr<std::atomic<uint32_t>[]> left;  // per unit: slices not yet copied
   size_t units = 0;
   std::atomic<size_t> next{0};
-  const bool streaming = pack_streaming();
+  bool streaming = pack_streaming();  // the zero-copy entry sets pack_streaming(true)
 
   void add(uint32_t unit, const char* src, char* dst, size_t bytes) {
     for (size_t o = 0; o < bytes; o += kPackSliceBytes)

@@ -870,6 +870,93 @@ PyObject* py_wreduce_rows(PyObject*, PyObject* args) {
   return result;
 }
 
+// ---- a small host task's zero-copy reduce in one call (round 6) -------------
+//
+// dlsim_host_wreduce_zc (include/dlsim.h) bound by address from _native.py:
+// arena._host_zc_aggregate hands over the models' parameter lists, and the
+// data pointers, element counts and weights go to the library from here --
+// no Python list of pointers, no ctypes arrays.
+using HostZcFn = int (*)(int, int, const void* const*, const size_t*, const float*, void*, size_t, void*, int, int,
+                         int, void*);
+HostZcFn g_host_zc = nullptr;
+
+PyObject* py_bind_host_zc(PyObject*, PyObject* addr) {
+  void* p = PyLong_AsVoidPtr(addr);
+  if (!p && PyErr_Occurred()) return nullptr;
+  g_host_zc = reinterpret_cast<HostZcFn>(p);
+  Py_RETURN_NONE;
+}
+
+// host_zc(rows, idx, numels, weights_f32, staging, host_out, dtype, mode,
+//         threads, stream) -> rc, or None (nothing launched) if a tensor is
+// not a contiguous host tensor. rows[i][idx[j]] is tensor j of model i;
+// numels[j] its element count; weights_f32 a C-contiguous buffer of len(rows)
+// floats; staging a page-locked 2-D [>= n, stride] tensor; host_out a
+// page-locked tensor of sum(numels) elements.
+PyObject* py_host_zc(PyObject*, PyObject* args) {
+  PyObject *rows, *idx, *numels, *weights, *staging, *host;
+  int dtype, mode, threads;
+  unsigned long long stream;
+  if (!PyArg_ParseTuple(args, "OOOOOOiiiK", &rows, &idx, &numels, &weights, &staging, &host, &dtype, &mode, &threads,
+                        &stream))
+    return nullptr;
+  if (!g_host_zc) {
+    PyErr_SetString(PyExc_RuntimeError, "bind_host_zc was not called");
+    return nullptr;
+  }
+  std::vector<const at::Tensor*> ts;
+  Py_ssize_t n, t;
+  if (!row_tensors(rows, idx, ts, &n, &t)) return nullptr;
+  for (const at::Tensor* x : ts)
+    if (!x->is_contiguous() || !x->is_cpu()) Py_RETURN_NONE;
+  const at::Tensor* st = tensor_of(staging);
+  const at::Tensor* ho = st ? tensor_of(host) : nullptr;
+  if (!ho) return nullptr;
+  if (st->dim() != 2 || !st->is_cpu() || !ho->is_cpu()) {
+    PyErr_SetString(PyExc_ValueError, "staging: a page-locked [n, stride] host tensor; host_out: a host tensor");
+    return nullptr;
+  }
+  PyObject* ns = PySequence_Fast(numels, "numels must be a sequence");
+  if (!ns) return nullptr;
+  PyObject* result = nullptr;
+  Py_buffer wb{};
+  bool have_wb = false;
+  do {
+    if (PySequence_Fast_GET_SIZE(ns) != t) {
+      PyErr_SetString(PyExc_ValueError, "idx and numels differ in length");
+      break;
+    }
+    if (PyObject_GetBuffer(weights, &wb, PyBUF_C_CONTIGUOUS) < 0) break;
+    have_wb = true;
+    if (wb.len != static_cast<Py_ssize_t>(n * sizeof(float))) {
+      PyErr_SetString(PyExc_ValueError, "weights_f32 must hold one float per model");
+      break;
+    }
+    std::vector<size_t> ne(static_cast<size_t>(t));
+    bool ok = true;
+    for (Py_ssize_t j = 0; ok && j < t; ++j) {
+      ne[static_cast<size_t>(j)] = PyLong_AsSize_t(PySequence_Fast_GET_ITEM(ns, j));
+      ok = !PyErr_Occurred();
+    }
+    if (!ok) break;
+    std::vector<const void*> ptrs(ts.size());
+    for (size_t q = 0; q < ts.size(); ++q) ptrs[q] = ts[q]->const_data_ptr();
+    const float* w = static_cast<const float*>(wb.buf);
+    void* sp = st->data_ptr();
+    const size_t stride = static_cast<size_t>(st->stride(0));
+    void* hp = ho->data_ptr();
+    int rc;
+    Py_BEGIN_ALLOW_THREADS
+    rc = g_host_zc(static_cast<int>(n), static_cast<int>(t), ptrs.data(), ne.data(), w, sp, stride, hp, dtype, mode,
+                   threads, reinterpret_cast<void*>(static_cast<uintptr_t>(stream)));
+    Py_END_ALLOW_THREADS
+    result = PyLong_FromLong(rc);
+  } while (false);
+  if (have_wb) PyBuffer_Release(&wb);
+  Py_DECREF(ns);
+  return result;
+}
+
 // ---- many device tasks' reduces in one library call ------------------------
 //
 // RoundExecutor's wave (dasklearn_amd/batch.py): every task whose models keep
@@ -1275,6 +1362,10 @@ PyMethodDef kMethods[] = {
     {"clone_module", py_clone_module, METH_VARARGS, "clone_module(module, memo): arena._clone_module in C"},
     {"bind_wreduce_tensors", py_bind_wreduce_tensors, METH_O, "bind dlsim_wreduce_tensors by address"},
     {"bind_wreduce_batched", py_bind_wreduce_batched, METH_O, "bind dlsim_wreduce_batched by address"},
+    {"bind_host_zc", py_bind_host_zc, METH_O, "bind dlsim_host_wreduce_zc by address"},
+    {"host_zc", py_host_zc, METH_VARARGS,
+     "host_zc(rows, idx, numels, weights_f32, staging, host_out, dtype, mode, threads, stream): "
+     "dlsim_host_wreduce_zc on the models' data pointers; None if a tensor is not a contiguous host tensor"},
     {"wreduce_rows_multi", py_wreduce_rows_multi, METH_VARARGS,
      "wreduce_rows_multi(tasks, dtype, mode, stream, device): many tasks' tensor rows in one dlsim_wreduce_batched"},
     {"fill_param_views", py_fill_param_views, METH_VARARGS,

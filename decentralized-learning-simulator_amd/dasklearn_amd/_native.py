@@ -962,6 +962,27 @@ def host_wreduce_zc_raw(src_ptrs: Sequence[int], n: int, numels: Sequence[int], 
     _check("dlsim_host_wreduce_zc", rc)
 
 
+_HOST_ZC_BOUND = [False]
+
+
+def host_zc(all_params, idx, numels: Sequence[int], weights_f32: np.ndarray, staging, host_out, dtype: int,
+            mode: int, threads: int, stream_handle: int) -> bool:
+    """dlsim_host_wreduce_zc over the models' parameter tensors
+    (all_params[i][k] for k in idx), the pointers read in C (_pyhost.host_zc,
+    the library bound by address). False (nothing launched) if a tensor is
+    not a contiguous host tensor; raises DlsimError on a library error."""
+    from . import _pyhost
+    if not _HOST_ZC_BOUND[0]:
+        _pyhost.bind_host_zc(ctypes.cast(load().dlsim_host_wreduce_zc, ctypes.c_void_p).value)
+        _HOST_ZC_BOUND[0] = True
+    rc = _pyhost.host_zc(all_params, idx, numels, weights_f32, staging, host_out, dtype, mode, threads,
+                         stream_handle or 0)
+    if rc is None:
+        return False
+    _check("dlsim_host_wreduce_zc", rc)
+    return True
+
+
 def host_wreduce_resident_raw(src_ptrs: Sequence[int], n: int, numels: Sequence[int], weights_f32,
                               resident: Sequence[bool], row_ptrs: Sequence[int], staging, out, host_out, dtype: int,
                               mode: int, threads: int, stream_handle) -> None:

@@ -1231,6 +1231,83 @@ def input_arenas(models: Sequence[nn.Module]):
     return layout, all_params, views
 
 
+# the current stream's torch object per raw handle (torch.cuda.current_stream
+# costs a few us of Python per call; the raw handle is one C call)
+_STREAM_OBJS: Dict[int, torch.cuda.Stream] = {}
+_DEVICES: Dict[int, torch.device] = {}
+
+
+def _current_stream(idx: int, raw: int) -> torch.cuda.Stream:
+    s = _STREAM_OBJS.get(raw)
+    if s is None or s.cuda_stream != raw or s.device_index != idx:
+        s = torch.cuda.current_stream(idx)
+        if len(_STREAM_OBJS) > 64:
+            _STREAM_OBJS.clear()
+        _STREAM_OBJS[raw] = s
+    return s
+
+
+def _host_zc_aggregate(models: List[nn.Module], w32: np.ndarray, mode: int) -> Optional[nn.Module]:
+    """The small host task in one pass (round 6): the
+    reference's default deployment (host GNLeNets, worker.py:24-33 ->
+    functions.py:89-106) with the zero-copy reduce. What
+    reduce_modules_to_arenas + _host_pipeline(out=None) + module_from_arenas
+    do for such a task, minus their generic machinery: the models' class
+    layout (one dtype group), each model's parameters walked and checked
+    against it in C, one _pyhost call that hands the data pointers to
+    dlsim_host_wreduce_zc (pack, then the reduce reading the page-locked rows
+    and writing the page-locked result over PCIe), the output module built
+    while the kernel runs, one wait. None when the task is not such a task
+    (the general path then runs it): another signature or layout class, a
+    device model, a non-contiguous parameter, more than ZC_MAX_BYTES of rows,
+    fp64, the device cache on, or the page-locked result budget spent."""
+    if not ZERO_COPY or device_cache._CACHE is not None:
+        return None
+    m0 = models[0]
+    known = _CLASS_LAYOUTS.get(type(m0))
+    if known is None or len(known.groups) != 1:
+        return None
+    (dt, idx), = known.groups.items()
+    n = len(models)
+    total = known.totals[dt]
+    esz = _elem_size(dt)
+    if dt is torch.float64 or total == 0 or n * total * esz > ZC_MAX_BYTES:
+        return None
+    sig = known._signature
+    k0 = idx[0]
+    all_params = []
+    for m in models:
+        ps = _pyhost.checked_params(m, sig)
+        if ps is None or ps[k0].is_cuda:
+            return None
+        all_params.append(ps)
+    if not pinned_result(total * esz):
+        return None
+    di = torch.cuda.current_device()
+    dev = _DEVICES.get(di)
+    if dev is None:
+        dev = _DEVICES[di] = torch.device("cuda", di)
+    raw = torch._C._cuda_getCurrentRawStream(di)
+    host = torch.empty(total, dtype=dt, pin_memory=True)
+    _, rows = STAGING.acquire(dev, dt, n, total, None, device_rows=False)
+    launched = waited = False
+    try:
+        launched = _native.host_zc(all_params, idx, known.split_sizes[dt], w32, rows, host, _native.dtype_code(dt),
+                                   mode, torch.get_num_threads(), raw)
+        if not launched:  # a non-contiguous or device tensor: the general path
+            return None
+        ZC_CALLS[0] += 1
+        layout = known.rebind(all_params[0])
+        out = module_from_arenas(m0, layout, {dt: host})  # while the kernel runs
+        _current_stream(di, raw).synchronize()
+        waited = True
+        return out
+    finally:
+        if launched and not waited:  # the rows are free once the kernel is done
+            _current_stream(di, raw).synchronize()
+        STAGING.release(dev, dt, None, True, device_rows=False)
+
+
 def aggregate_modules(models: List[nn.Module], weights: Optional[Sequence[float]], mode: int,
                       device=None, to_host: Optional[bool] = None,
                       timing: Optional[dict] = None) -> nn.Module:
@@ -1246,6 +1323,10 @@ def aggregate_modules(models: List[nn.Module], weights: Optional[Sequence[float]
         assert len(weights) == len(models)
     model0 = models[0]  # IndexError for an empty list, as the reference
     w32 = _native.fp32_weights(weights)
+    if timing is None and device is None and to_host is not False:
+        out = _host_zc_aggregate(models, w32, mode)
+        if out is not None:
+            return out
     try:
         layout, arenas, dev, on_host, host_out, staged, pending = reduce_modules_to_arenas(
             models, w32, mode, device, timing, to_host, weights_f64=weights, defer_host_sync=timing is None)

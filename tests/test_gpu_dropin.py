@@ -510,3 +510,83 @@ def test_zero_copy_pipelined_chunks(monkeypatch):
             bits = [orc.f32_to_bf16_bits(r.astype(np.float32)) for r in rows]
             exp = orc.bf16_bits_to_f32(orc.wreduce(bits, orc.reference_weights(7, w), "bf16"))
             assert orc.same_bits(got.astype(np.float32), exp.astype(np.float32))
+
+
+def test_small_host_task_fast_path(monkeypatch):
+    """Round 6: once a model class's layout is known,
+    a small host task runs arena._host_zc_aggregate -- parameters walked and
+    checked in C, one _pyhost call into dlsim_host_wreduce_zc, the module
+    built while the kernel runs. Bit-exact against the oracle (fp32, bf16,
+    fp16; weights None and a list), the reference's output contract
+    (deepcopy of models[0]: buffers and requires_grad from it, page-locked
+    host parameters), an output fed back in as an input, and the cases it
+    hands to the general path (same bits there): a non-contiguous parameter,
+    a model on the GPU, models whose parameter lists differ."""
+    from dasklearn_amd import _native, arena
+    from dasklearn_amd.gradient_aggregation.fedavg import FedAvg
+    real = arena._host_zc_aggregate
+    taken = []
+
+    def spy(models, w32, mode):
+        r = real(models, w32, mode)
+        taken.append(r is not None)
+        return r
+    monkeypatch.setattr(arena, "_host_zc_aggregate", spy)
+
+    class Net(torch.nn.Module):
+        def __init__(self, dt):
+            super().__init__()
+            self.conv = torch.nn.Conv2d(3, 8, 3)
+            self.gn = torch.nn.GroupNorm(2, 8)
+            self.fc = torch.nn.Linear(72, 10)
+            self.register_buffer("steps", torch.tensor(7))
+            self.to(dt)
+
+    def flat(m):
+        return np.concatenate([p.detach().float().numpy().ravel() for p in m.parameters()])
+
+    def expect(ms, w, dt):
+        rows = [flat(m) for m in ms]
+        wf = orc.reference_weights(len(ms), w)
+        if dt == torch.float32:
+            return orc.wreduce(rows, wf, "f32")
+        conv = orc.f32_to_bf16_bits if dt == torch.bfloat16 else orc.f32_to_f16_bits
+        back = orc.bf16_bits_to_f32 if dt == torch.bfloat16 else orc.f16_bits_to_f32
+        return back(orc.wreduce([conv(r.astype(np.float32)) for r in rows], wf,
+                                "bf16" if dt == torch.bfloat16 else "f16")).astype(np.float32)
+
+    for dt in (torch.float32, torch.bfloat16, torch.float16):
+        torch.manual_seed(3)
+        ms = [Net(dt) for _ in range(4)]
+        ms[0].fc.bias.requires_grad_(False)
+        for w in (None, [0.4, 0.3, 0.2, 0.1]):
+            taken.clear()
+            FedAvg.aggregate(ms, w)  # may learn the class layout on the general path
+            out = FedAvg.aggregate(ms, w)
+            assert taken[-1], dt
+            assert orc.same_bits(flat(out).astype(np.float32), expect(ms, w, dt)), (dt, w)
+            assert type(out) is Net and out is not ms[0] and int(out.steps) == 7
+            assert not out.fc.bias.requires_grad and out.fc.weight.requires_grad
+            p0 = next(out.parameters())
+            assert not p0.is_cuda and p0.is_pinned() and p0.dtype == dt
+        again = FedAvg.aggregate([out, ms[1]], None)  # an output as an input (a registered host arena)
+        assert taken[-1]
+        assert orc.same_bits(flat(again).astype(np.float32), expect([out, ms[1]], None, dt))
+    # handed to the general path, same bits
+    torch.manual_seed(4)
+    ms = [Net(torch.float32) for _ in range(3)]
+    FedAvg.aggregate(ms, None)
+    ms[1].fc.weight.data = ms[1].fc.weight.data.t().contiguous().t()  # non-contiguous
+    taken.clear()
+    out = FedAvg.aggregate(ms, None)
+    assert taken == [False] and orc.same_bits(flat(out), expect(ms, None, torch.float32))
+    dev_model = Net(torch.float32).cuda()
+    taken.clear()
+    out = FedAvg.aggregate([ms[0], dev_model], None)
+    assert taken == [False]
+    assert orc.same_bits(flat(out.cpu()), expect([ms[0], dev_model.cpu()], None, torch.float32))
+    other = torch.nn.Sequential(torch.nn.Linear(4, 3))
+    taken.clear()
+    with pytest.raises(RuntimeError):  # zip over different parameter lists: torch's add_ raises, as the reference
+        FedAvg.aggregate([ms[0], other], None)
+    assert taken == [False]
