@@ -21,6 +21,9 @@
 #include "chunk_mean_kernels.hpp"
 #include "ab_env.hpp"
 
+// Every DLSIM_* switch named below is an A/B switch, read through
+// dlsim::ab_getenv: only when DLSIM_AB=1 is set as well (ab_env.hpp).
+
 namespace dlsim_host __attribute__((visibility("hidden"))) {
 
 // error reporting of the ABI (dlsim_abi.hip): set the thread's message, return code

@@ -18,6 +18,9 @@
 
 #include "abi_common.hpp"
 #include "dispatch.hpp"
+
+// Every DLSIM_* switch named below is an A/B switch, read through
+// dlsim::ab_getenv: only when DLSIM_AB=1 is set as well (ab_env.hpp).
 #include "host_pack.hpp"
 
 namespace dlsim_host __attribute__((visibility("hidden"))) {

@@ -473,7 +473,7 @@ def resident_empty(numel: int, dtype: torch.dtype, device, align: int) -> torch.
     at the fast end every time (profiles/r04s2_contig/).
     Freeing such a block synchronises the device, so per-call buffers
     (aggregate outputs, a wave's uploads) stay in torch's caching allocator.
-    DLSIM_CONTIGUOUS=0 turns it off (A/B)."""
+    DLSIM_AB=1 DLSIM_CONTIGUOUS=0 turns it off (A/B)."""
     esz = _elem_size(dtype)
     nbytes = numel * esz
     if nbytes < RESIDENT_CONTIG_MIN or _native.ab_env("DLSIM_CONTIGUOUS", "1") == "0" \
@@ -657,7 +657,7 @@ def pipeline_chunk_elems(total: int, esz: int) -> int:
 # allocator: the D2H is then asynchronous, so the output module is built while
 # the pipeline still runs (round 4), and once the simulation's results turn
 # over, a result reuses a freed block (a fresh hipHostMalloc costs ~0.2 ms,
-# scripts/probes/probe_result_alloc.py). DLSIM_HOST_RESULT=pageable restores
+# scripts/probes/probe_result_alloc.py). DLSIM_AB=1 DLSIM_HOST_RESULT=pageable restores
 # round 3's rule for A/B runs: results below PAGEABLE_RESULT_BYTES in pageable
 # memory (the runtime stages that copy, and the library call waits for it).
 PAGEABLE_RESULT_BYTES = 4 << 20
@@ -712,7 +712,8 @@ def pinned_result(nbytes: int) -> bool:
 # host are packed into page-locked rows that the reduce kernel reads in place
 # over PCIe, and the kernel writes the page-locked result: no H2D and no D2H
 # DMA (dlsim_host_wreduce_zc). 2 x GNLeNet: the library call with its wait
-# 81 -> 63 us (profiles/r05d/zero_copy.json). DLSIM_ZERO_COPY=0 turns it off,
+# 81 -> 63 us (profiles/r05d/zero_copy.json). Under DLSIM_AB=1 (the A/B
+# switches, _native.ab_env), DLSIM_ZERO_COPY=0 turns it off and
 # DLSIM_ZC_MAX_KB moves the 4 MiB.
 ZERO_COPY = _native.ab_env("DLSIM_ZERO_COPY", "1") != "0"
 ZC_MAX_BYTES = int(float(_native.ab_env("DLSIM_ZC_MAX_KB", "4096")) * 1024)
