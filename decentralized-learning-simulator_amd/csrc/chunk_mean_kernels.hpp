@@ -56,18 +56,34 @@ constexpr int kCmTailCols = 64;  // scalar columns of a task (< E + 32)
 
 enum : uint8_t { kCmVec = 1, kCmInner = 2 };
 
+// Per-task fields are 32-bit or wider (round 6): a block reads its task's
+// fields at a run-time index, and 8- or 16-bit fields there compiled to
+// vector global loads (scalar loads read whole dwords) on the path from the
+// block's start to its first input load.
 struct ChunkMeanSlots {
   const void* p[kCmMaxPtrs];
   void* out[kCmMaxTasks];
   size_t nelem[kCmMaxTasks];
   size_t ilp_begin[kCmMaxTasks];
   uint32_t block_start[kCmMaxTasks + 1];  // first full tile of each task (k_chunk_mean_batch)
-  uint16_t ptr_off[kCmMaxTasks];
-  uint16_t m[kCmMaxTasks];
-  uint8_t flags[kCmMaxTasks];
-  uint8_t head[kCmMaxTasks];  // leading columns folded by block 0 (see cm_task)
+  uint32_t ptr_off[kCmMaxTasks];
+  uint32_t m[kCmMaxTasks];
+  uint32_t flags[kCmMaxTasks];
+  uint32_t head[kCmMaxTasks];  // leading columns folded by block 0 (see cm_task)
   int ntasks;
 };
+
+// The task of block-start entry f: the last t with block_start[t] <= f (the
+// entries are non-decreasing over the ntasks tasks). A count over a
+// compile-time range: the entries load with a few wide scalar loads and the
+// compares are scalar ALU work, where a `while` scan waited on one dependent
+// load per task passed (round 6: ~0.3 us each, on every block's start).
+__device__ __forceinline__ int cm_find_task(const ChunkMeanSlots& s, uint32_t f) {
+  int t = 0;
+#pragma unroll
+  for (int j = 1; j < kCmMaxTasks; ++j) t += (j < s.ntasks && f >= s.block_start[j]) ? 1 : 0;
+  return t;
+}
 
 struct PtrArgs {
   const void* const* p;
@@ -412,7 +428,7 @@ __global__ __launch_bounds__(kBlock) void k_chunk_mean_batch(const ChunkMeanSlot
     t = static_cast<int>(bid);
   } else {
     const uint32_t f = bid - static_cast<uint32_t>(s.ntasks);
-    while (t + 1 < s.ntasks && f >= s.block_start[t + 1]) ++t;  // wave-uniform scan
+    t = cm_find_task(s, f);
     local = f - s.block_start[t] + 1;
   }
   const PtrArgs a{s.p + s.ptr_off[t]};
@@ -512,7 +528,7 @@ __global__ __launch_bounds__(kDeferBlock) void k_chunk_mean_defer(const ChunkMea
     t = static_cast<int>(bid);
   } else {
     const uint32_t f = bid - static_cast<uint32_t>(s.ntasks);
-    while (t + 1 < s.ntasks && f >= s.block_start[t + 1]) ++t;  // wave-uniform scan
+    t = cm_find_task(s, f);
     local = f - s.block_start[t] + 1;
   }
   const PtrArgs a{s.p + s.ptr_off[t]};
@@ -574,16 +590,26 @@ __global__ __launch_bounds__(kDeferBlock) void k_chunk_mean_defer(const ChunkMea
 // ragged blocks pushed Conflux's ten ResNet-18 chunks from R = 22 to 24 rows
 // per block to fit one round (38.8 against 37.5 us tiled at m = 4,
 // profiles/r06_chunk_ab/); here R = 22 fits, the reduce's grid.
+// MF input pointers and the divisor in registers, as a reduce slot set
+// (ptr / wt / divisor) for defer_rows
+template <int MF>
+struct FixedPtrs {
+  const void* p[MF];
+  float div;
+  __device__ const void* ptr(int i) const { return p[i]; }
+  __device__ float wt(int) const { return 1.0f; }
+  __device__ float divisor() const { return div; }
+};
+
 template <class Op, int MF, int RMAX, int U>
 __global__ __launch_bounds__(kDeferBlock) void k_chunk_mean_defer_m(const ChunkMeanSlots s, int R) {
   static_assert(MF >= 1 && MF < 16, "level 0 only");
-  using T = acc_t<Op>;
+  static_assert(std::is_same<Op, F32Mean>::value, "the input-order mean's fold is the cascade's below 16 rows");
   const uint32_t bid = blockIdx.x;
-  int t = 0;
-  while (t + 1 < s.ntasks && bid >= s.block_start[t + 1]) ++t;  // wave-uniform scan
+  const int t = cm_find_task(s, bid);
   const uint32_t local = bid - s.block_start[t];
   const bool last = bid + 1 == s.block_start[t + 1];
-  const PtrArgs a{s.p + s.ptr_off[t]};
+  const PtrArgs a{s.p + t * MF};  // every task has MF inputs, packed in task order (ptr_off[t] == t * MF)
   const size_t n = s.nelem[t], ilp_begin = s.ilp_begin[t];
   const uint32_t head = s.head[t];
   const float div = static_cast<float>(MF);
@@ -597,42 +623,15 @@ __global__ __launch_bounds__(kDeferBlock) void k_chunk_mean_defer_m(const ChunkM
                                : static_cast<int>(rows - first < static_cast<size_t>(R) ? rows - first
                                                                                         : static_cast<size_t>(R));
   const size_t v0 = first * kDeferBlock + threadIdx.x;
-  u32x4 res[RMAX];
+  // Below 16 contributors the cascade columns' order is the input-order
+  // mean's (F32Mean: from +0, in order, one division; the level-1 add of +0
+  // changes no bit), so the rows run the reduce's own deferred fold,
+  // defer_rows, on the task's pointers held in registers.
+  FixedPtrs<MF> fp;
 #pragma unroll
-  for (int r0 = 0; r0 < RMAX; r0 += U) {
-    if (r0 < Rb) {
-      u32x4 x[MF][U];
-#pragma unroll
-      for (int i = 0; i < MF; ++i)
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int row = r0 + u < Rb ? r0 + u : r0;  // re-reads row r0 (in flight): no extra traffic
-          x[i][u] = ld16<1>(sa.ptr(i), v0 + static_cast<size_t>(row) * kDeferBlock);
-        }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        T acc[Op::E];
-#pragma unroll
-        for (int e = 0; e < Op::E; ++e) acc[e] = T(0);
-#pragma unroll
-        for (int i = 0; i < MF; ++i) {
-          T xv[Op::E];
-          unpack<Op>(x[i][u], xv);
-#pragma unroll
-          for (int e = 0; e < Op::E; ++e) acc[e] = acc[e] + xv[e];
-        }
-#pragma unroll
-        for (int e = 0; e < Op::E; ++e) acc[e] = acc[e] + T(0);  // + level 1 (zero below 16 rows)
-        res[r0 + u] = pack<Op>(acc, div);
-      }
-    }
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  static_assert(kCmStore<Op> >= 0, "buffer stores: out-of-range rows are dropped");
-#pragma unroll
-  for (int r = 0; r < RMAX; ++r)
-    store_vec<kCmStore<Op>>(o, r < Rb ? v0 + static_cast<size_t>(r) * kDeferBlock : nvec, res[r]);
+  for (int i = 0; i < MF; ++i) fp.p[i] = sa.ptr(i);
+  fp.div = div;
+  defer_rows<Op, FixedPtrs<MF>, MF, 8, RMAX, U, kCmStore<Op>>(fp, MF, o, v0, Rb, nvec);
   if (!last || threadIdx.x >= kBlock) return;  // whole waves 4-7: the barriers below count the rest
   if (rows * kDeferBlock < nvec) {  // the partial row: 256 lanes x 2 vectors, bounds-checked
     using PT = CmShape<kDeferBlock / kBlock, false, (MF <= 6 ? 4 : 8)>;  // dispatch.hpp CmFewRows / CmDefault RF

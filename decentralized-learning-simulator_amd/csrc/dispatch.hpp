@@ -549,8 +549,8 @@ hipError_t launch_batch(const int* fan_in, const size_t* in_off, const void* con
     s.nvec[k] = nvec;
     s.nelem[k] = nelem[t];
     s.block_start[k] = blocks - static_cast<uint32_t>(k);  // full tiles before task k (ragged ends first)
-    s.ptr_off[k] = static_cast<uint16_t>(ptrs);
-    s.fan_in[k] = static_cast<uint16_t>(fan_in[t]);
+    s.ptr_off[k] = static_cast<uint32_t>(ptrs);
+    s.fan_in[k] = static_cast<uint32_t>(fan_in[t]);
     s.div[k] = divs ? divs[t] : 1.0f;
     for (int i = 0; i < fan_in[t]; ++i) {
       s.p[ptrs + i] = in[in_off[t] + i];
@@ -852,7 +852,7 @@ inline bool chunk_defer_fixed_on() {
 constexpr int cm_defer_m_rmax(int mf) { return mf >= 12 ? 24 : kCmDeferRMax; }
 template <class Op, int MF>
 hipError_t launch_chunk_defer_m(const dlsim::ChunkMeanSlots& s, int m, int R, unsigned grid, hipStream_t st) {
-  if constexpr (MF > kCmFixedMaxM || Op::kBytes != 4) {
+  if constexpr (MF > kCmFixedMaxM || !std::is_same<Op, dlsim::F32Mean>::value) {
     return hipErrorInvalidValue;
   } else {
     if (m == MF) {
@@ -954,7 +954,7 @@ int run_chunk_mean(int b, const int* fan_in, const void* const* in, void* const*
     // deferred stores: fp32, every task vector-aligned with m >= 16 (or every
     // task with one m, 2 <= m < 16: the fixed-m form), >= 20 MB per stream
     bool defer = Op::kBytes == 4 && chunk_defer_on();
-    bool fixed = Op::kBytes == 4 && chunk_defer_on() && chunk_defer_fixed_on();
+    bool fixed = std::is_same<Op, dlsim::F32Mean>::value && chunk_defer_on() && chunk_defer_fixed_on();
     const int m0 = fan_in[batch.front().t];
     size_t cols = 0;
     std::vector<size_t> rows;
@@ -982,13 +982,13 @@ int run_chunk_mean(int b, const int* fan_in, const void* const* in, void* const*
                               : defer ? (rt + R - 1) / R + 1 : task_blocks(k.ib, k.head);
       // the fixed-m kernel: first block of task nt; the others: full blocks before it
       s.block_start[nt] = static_cast<uint32_t>(fixed ? blocks : blocks - static_cast<size_t>(nt));
-      s.ptr_off[nt] = static_cast<uint16_t>(p);
-      s.m[nt] = static_cast<uint16_t>(m);
+      s.ptr_off[nt] = static_cast<uint32_t>(p);
+      s.m[nt] = static_cast<uint32_t>(m);
       s.out[nt] = outs[k.t];
       s.nelem[nt] = nelem[k.t];
       s.ilp_begin[nt] = k.ib;
       s.flags[nt] = k.flags;
-      s.head[nt] = static_cast<uint8_t>(k.head);
+      s.head[nt] = k.head;
       for (int i = 0; i < m; ++i) s.p[p + i] = in[off[k.t] + i];
       p += m;
       blocks += tb;

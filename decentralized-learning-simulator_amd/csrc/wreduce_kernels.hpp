@@ -831,10 +831,21 @@ struct BatchSlots {
   size_t nelem[kBatchMaxTasks];
   float div[kBatchMaxTasks];  // final divisor per task (mean policies; 1 for the reduce)
   uint32_t block_start[kBatchMaxTasks + 1];  // first full tile of each task
-  uint16_t ptr_off[kBatchMaxTasks];
-  uint16_t fan_in[kBatchMaxTasks];
+  uint32_t ptr_off[kBatchMaxTasks];  // 32-bit: read with scalar loads at a run-time index (16-bit
+  uint32_t fan_in[kBatchMaxTasks];   // fields compiled to vector loads; round 6)
   int ntasks;
 };
+static_assert(sizeof(BatchSlots) <= 4096, "kernel arguments");
+
+// The task of full-tile entry f: the last t with block_start[t] <= f, as a
+// count over a compile-time range (wide scalar loads, scalar compares) instead
+// of a scan waiting on one dependent load per task passed (round 6).
+__device__ __forceinline__ int batch_find_task(const BatchSlots& s, uint32_t f) {
+  int t = 0;
+#pragma unroll
+  for (int j = 1; j < kBatchMaxTasks; ++j) t += (j < s.ntasks && f >= s.block_start[j]) ? 1 : 0;
+  return t;
+}
 
 // One task's view of the batch (same accessor interface as Slots).
 struct TaskArgs {
@@ -855,11 +866,11 @@ __global__ __launch_bounds__(kBlock) void k_wreduce_batch(const BatchSlots s) {
     t = static_cast<int>(bid);
   } else {
     const uint32_t f = bid - static_cast<uint32_t>(s.ntasks);
-    while (t + 1 < s.ntasks && f >= s.block_start[t + 1]) ++t;  // wave-uniform scan
+    t = batch_find_task(s, f);
     local = f - s.block_start[t] + 1;
   }
-  const TaskArgs a{s, s.ptr_off[t], s.div[t]};
-  const int n = NF > 0 ? NF : s.fan_in[t];
+  const TaskArgs a{s, static_cast<int>(s.ptr_off[t]), s.div[t]};
+  const int n = NF > 0 ? NF : static_cast<int>(s.fan_in[t]);
   const size_t nvec = s.nvec[t];
   constexpr size_t kTile = static_cast<size_t>(kBlock) * VPT;
   const size_t full = nvec / kTile;

@@ -1291,20 +1291,20 @@ def _host_zc_aggregate(models: List[nn.Module], w32: np.ndarray, mode: int) -> O
     raw = torch._C._cuda_getCurrentRawStream(di)
     host = torch.empty(total, dtype=dt, pin_memory=True)
     _, rows = STAGING.acquire(dev, dt, n, total, None, device_rows=False)
-    launched = waited = False
+    done = False  # the rows are free: nothing launched, or the kernel waited for
     try:
-        launched = _native.host_zc(all_params, idx, known.split_sizes[dt], w32, rows, host, _native.dtype_code(dt),
-                                   mode, torch.get_num_threads(), raw)
-        if not launched:  # a non-contiguous or device tensor: the general path
+        if not _native.host_zc(all_params, idx, known.split_sizes[dt], w32, rows, host, _native.dtype_code(dt),
+                               mode, torch.get_num_threads(), raw):
+            done = True  # a non-contiguous or device tensor, refused before any launch: the general path
             return None
         ZC_CALLS[0] += 1
         layout = known.rebind(all_params[0])
         out = module_from_arenas(m0, layout, {dt: host})  # while the kernel runs
         _current_stream(di, raw).synchronize()
-        waited = True
+        done = True
         return out
     finally:
-        if launched and not waited:  # the rows are free once the kernel is done
+        if not done:  # an error after (or during) the library call: some chunks may be queued
             _current_stream(di, raw).synchronize()
         STAGING.release(dev, dt, None, True, device_rows=False)
 
