@@ -601,12 +601,21 @@ struct FixedPtrs {
   __device__ float divisor() const { return div; }
 };
 
+//
+// The scalars come first: they are preloaded into SGPRs at wave launch
+// (-mllvm -amdgpu-kernarg-preload-count, __graft_entry__.HIP_FLAGS), so with
+// bpt > 0 (every task but the last has bpt blocks; the host checks) a block
+// finds its task with no load at all, and its first loads are its task's
+// fields and pointers. Every deferred block of the launch starts at once, so
+// each dependent load before the first input load is on the kernel's
+// critical path (round 6: one task of 4 x 11.2 M, 36.9 against 35.3-35.6 us
+// for dlsim_mean's deferred kernel on the same rows, profiles/r06_cvr/).
 template <class Op, int MF, int RMAX, int U>
-__global__ __launch_bounds__(kDeferBlock) void k_chunk_mean_defer_m(const ChunkMeanSlots s, int R) {
+__global__ __launch_bounds__(kDeferBlock) void k_chunk_mean_defer_m(int bpt, int nt, int R, const ChunkMeanSlots s) {
   static_assert(MF >= 1 && MF < 16, "level 0 only");
   static_assert(std::is_same<Op, F32Mean>::value, "the input-order mean's fold is the cascade's below 16 rows");
   const uint32_t bid = blockIdx.x;
-  const int t = cm_find_task(s, bid);
+  const int t = bpt > 0 ? min(static_cast<int>(bid / static_cast<uint32_t>(bpt)), nt - 1) : cm_find_task(s, bid);
   const uint32_t local = bid - s.block_start[t];
   const bool last = bid + 1 == s.block_start[t + 1];
   const PtrArgs a{s.p + t * MF};  // every task has MF inputs, packed in task order (ptr_off[t] == t * MF)

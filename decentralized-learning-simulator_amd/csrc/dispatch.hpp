@@ -838,9 +838,12 @@ inline int chunk_defer_min_m() {
   return k;
 }
 // Fixed-m deferral (dlsim::k_chunk_mean_defer_m, round 6): every task of the
-// launch has the same m, 2 <= m < 16. DLSIM_CHUNK_DEFER_FIXED=0 (read once;
-// A/B runs, under DLSIM_AB=1): the tiled kernel there instead.
-constexpr int kCmFixedMaxM = 15;
+// launch has the same m, 4 <= m < 16 (ResNet-18 chunks, k = 10, against the
+// tiled kernel on one box, profiles/r06_chunk_ab6/: m = 4 36.7-36.8 against
+// 37.8, m = 10 77.3 against 77.9, m = 15 110.9 against 112.8; m = 2 loses,
+// 24.1 against 23.7). DLSIM_CHUNK_DEFER_FIXED=0 (read once; A/B runs, under
+// DLSIM_AB=1): the tiled kernel there instead.
+constexpr int kCmFixedMinM = 4, kCmFixedMaxM = 15;  // m = 2 measured slower than the tiled kernel (24.1 / 23.7 us)
 inline bool chunk_defer_fixed_on() {
   static const bool on = [] {
     const char* e = dlsim::ab_getenv("DLSIM_CHUNK_DEFER_FIXED");
@@ -850,17 +853,20 @@ inline bool chunk_defer_fixed_on() {
 }
 // results per lane beside MF x U loads, as the reduce's defer_rmax
 constexpr int cm_defer_m_rmax(int mf) { return mf >= 12 ? 24 : kCmDeferRMax; }
+// bpt: blocks of every task but the last when they are all equal (the
+// kernel then maps a block to its task by a division), else 0 (a search).
 template <class Op, int MF>
-hipError_t launch_chunk_defer_m(const dlsim::ChunkMeanSlots& s, int m, int R, unsigned grid, hipStream_t st) {
+hipError_t launch_chunk_defer_m(const dlsim::ChunkMeanSlots& s, int m, int R, int bpt, unsigned grid,
+                                hipStream_t st) {
   if constexpr (MF > kCmFixedMaxM || !std::is_same<Op, dlsim::F32Mean>::value) {
     return hipErrorInvalidValue;
   } else {
     if (m == MF) {
       hipLaunchKernelGGL((dlsim::k_chunk_mean_defer_m<Op, MF, cm_defer_m_rmax(MF), kCmDeferU>), dim3(grid),
-                         dim3(dlsim::kDeferBlock), 0, st, s, R);
+                         dim3(dlsim::kDeferBlock), 0, st, bpt, s.ntasks, R, s);
       return hipGetLastError();
     }
-    return launch_chunk_defer_m<Op, MF + 1>(s, m, R, grid, st);
+    return launch_chunk_defer_m<Op, MF + 1>(s, m, R, bpt, grid, st);
   }
 }
 // R of the fixed-m form (k_chunk_mean_defer_m: no separate ragged blocks, at
@@ -965,7 +971,7 @@ int run_chunk_mean(int b, const int* fan_in, const void* const* in, void* const*
       cols += nelem[k.t];
       rows.push_back((k.ib - k.head) / Op::E / dlsim::kDeferBlock);
     }
-    fixed = fixed && m0 >= 2 && m0 <= kCmFixedMaxM && !defer;
+    fixed = fixed && m0 >= kCmFixedMinM && m0 <= kCmFixedMaxM && !defer;
     defer = (defer || fixed) && cols * Op::kBytes >= 20000000;
     fixed = fixed && defer;
     int R = 0;
@@ -1001,7 +1007,10 @@ int run_chunk_mean(int b, const int* fan_in, const void* const* in, void* const*
       if constexpr (Op::kBytes == 4) {
         const unsigned grid = static_cast<unsigned>(blocks);
         if (fixed) {
-          const hipError_t e = launch_chunk_defer_m<Op, 2>(s, m0, R, grid, st);
+          int bpt = static_cast<int>(nt > 1 ? s.block_start[1] - s.block_start[0] : s.block_start[1]);
+          for (int k = 1; bpt > 0 && k + 1 < nt; ++k)
+            if (s.block_start[k + 1] - s.block_start[k] != static_cast<uint32_t>(bpt)) bpt = 0;
+          const hipError_t e = launch_chunk_defer_m<Op, 2>(s, m0, R, bpt, grid, st);
           if (e != hipSuccess) return hip_fail(e, "chunk mean batch launch");
         } else if (few_rows)
           hipLaunchKernelGGL((dlsim::k_chunk_mean_defer<Op, CmFewRows::RF, kCmDeferRMax, kCmDeferU>), dim3(grid),

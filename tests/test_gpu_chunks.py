@@ -480,8 +480,9 @@ def test_chunk_mean_deferred_launch(m, k):
 
 @pytest.mark.parametrize("m,k", [(2, 3), (4, 10), (7, 1), (10, 10), (12, 6), (15, 4)])
 def test_chunk_mean_fixed_m_deferred_launch(m, k):
-    """Round 6: an fp32 launch whose tasks all have the same m < 16 (>= 20 MB
-    per stream, 16-B aligned) takes the fixed-m deferred kernel
+    """Round 6: an fp32 launch whose tasks all have the same m, 4 <= m < 16
+    (>= 20 MB per stream, 16-B aligned; m = 2 stays tiled) takes the fixed-m
+    deferred kernel
     (k_chunk_mean_defer_m: MF contributors folded straight-line, each task's
     last row block also doing its ragged end). Arbitrary cuts plus a tiny
     chunk (no whole row: only the last-block ragged work), a chunk of whole
