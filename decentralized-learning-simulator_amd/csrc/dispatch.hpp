@@ -135,6 +135,18 @@ template <class Op> int size_class(size_t nelem, int fixed_fan_in = 0) {
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
+// The fixed fan-in deferred launches pass nvec, the output and the first kPre
+// input pointers as the leading, preloaded kernel arguments
+// (k_wreduce_defer_pre, wreduce_kernels.hpp PreSlots). Measured in fresh
+// bench processes, one box, two passes each (profiles/r06_preload_ab/): the
+// 4-rank slice 16.66-16.70 -> 16.45-16.54 us, the north star 61.41-61.50 ->
+// 61.29-61.43; the tiled kernel preloaded lost at small sizes (the 8-rank
+// slice 9.76-9.77 -> 9.93-9.99, cfg2 7.63-7.75 -> 7.76-7.81: its blocks launch
+// in several rounds and each wave's launch carries the preload), so it takes
+// its arguments as before.
+template <class S> inline const void* pre_ptr(const S& s, int nf, int i) { return i < nf ? s.p[i] : nullptr; }
+static_assert(dlsim::kPre == 5, "the launches below pass five leading pointers");
+
 template <class Op, class S, int NF, int VPT, int STP, bool WAVE>
 hipError_t launch_shape(const S& s, int n, void* out, size_t nelem, hipStream_t st) {
   const size_t nvec = nelem / Op::E;
@@ -300,7 +312,8 @@ template <class Op> bool use_defer(int n, size_t nelem) {
 template <class Op> const char* kernel_name(int n, size_t nelem) {
   if (nelem == 0 || n < 1) return "";
   const size_t first = std::min(nelem, kMaxLaunchOutBytes / Op::kBytes);
-  return use_defer<Op>(n, first) ? "dlsim::k_wreduce_defer" : "dlsim::k_wreduce_tiles";
+  if (use_defer<Op>(n, first)) return n <= max_fixed_fan_in<Op>() ? "dlsim::k_wreduce_defer_pre" : "dlsim::k_wreduce_defer";
+  return "dlsim::k_wreduce_tiles";
 }
 
 // The exact fp32 policy with a fixed fan-in launches the kernel compiled for
@@ -311,20 +324,31 @@ template <class Op> const char* kernel_name(int n, size_t nelem) {
 // policies (FAST, mean, the probe) and the grouped form take the runtime R
 // (the grouped form compiled per R measured the same: cfg3 120.76-120.90 us,
 // cfg5 661.9-662.3, profiles/r05_defer/r05az_*).
+// One deferred launch, compiled for R = RC (0: runtime R); fixed fan-in with
+// the leading arguments preloaded.
+template <class Op, class S, int NF, int RC>
+hipError_t launch_defer_kernel(const S& s, int n, void* out, size_t nvec, size_t nelem, int R, unsigned blocks,
+                               hipStream_t st) {
+  if constexpr (NF > 0) {
+    hipLaunchKernelGGL(
+        (dlsim::k_wreduce_defer_pre<Op, S, NF, group_size<Op>(), defer_rmax<Op, NF>(), kDeferU, kStore, RC>),
+        dim3(blocks), dim3(dlsim::kDeferBlock), 0, st, nvec, out, pre_ptr(s, NF, 0), pre_ptr(s, NF, 1),
+        pre_ptr(s, NF, 2), pre_ptr(s, NF, 3), pre_ptr(s, NF, 4), s, n, R, nelem);
+  } else {
+    hipLaunchKernelGGL(
+        (dlsim::k_wreduce_defer<Op, S, NF, group_size<Op>(), defer_rmax<Op, NF>(), kDeferU, kStore, RC>),
+        dim3(blocks), dim3(dlsim::kDeferBlock), 0, st, s, n, R, out, nvec, nelem);
+  }
+  return hipGetLastError();
+}
+
 template <class Op, class S, int NF, int RC>
 hipError_t launch_defer_rc(const S& s, int n, void* out, size_t nvec, size_t nelem, int R, unsigned blocks,
                            hipStream_t st) {
   if constexpr (RC > defer_rmax<Op, NF>()) {
-    hipLaunchKernelGGL((dlsim::k_wreduce_defer<Op, S, NF, group_size<Op>(), defer_rmax<Op, NF>(), kDeferU, kStore>),
-                       dim3(blocks), dim3(dlsim::kDeferBlock), 0, st, s, n, R, out, nvec, nelem);
-    return hipGetLastError();
+    return launch_defer_kernel<Op, S, NF, 0>(s, n, out, nvec, nelem, R, blocks, st);
   } else {
-    if (R == RC) {
-      hipLaunchKernelGGL(
-          (dlsim::k_wreduce_defer<Op, S, NF, group_size<Op>(), defer_rmax<Op, NF>(), kDeferU, kStore, RC>),
-          dim3(blocks), dim3(dlsim::kDeferBlock), 0, st, s, n, R, out, nvec, nelem);
-      return hipGetLastError();
-    }
+    if (R == RC) return launch_defer_kernel<Op, S, NF, RC>(s, n, out, nvec, nelem, R, blocks, st);
     return launch_defer_rc<Op, S, NF, RC + kDeferU>(s, n, out, nvec, nelem, R, blocks, st);
   }
 }
@@ -341,9 +365,7 @@ hipError_t launch_defer(const S& s, int n, void* out, size_t nelem, hipStream_t 
   // the A/B switches) take the runtime R
   if constexpr (NF >= 3 && std::is_same<Op, dlsim::F32Exact>::value)
     return launch_defer_rc<Op, S, NF, kDeferRMin>(s, n, out, nvec, nelem, R, static_cast<unsigned>(blocks), st);
-  hipLaunchKernelGGL((dlsim::k_wreduce_defer<Op, S, NF, group_size<Op>(), defer_rmax<Op, NF>(), kDeferU, kStore>),
-                     dim3(static_cast<unsigned>(blocks)), dim3(dlsim::kDeferBlock), 0, st, s, n, R, out, nvec, nelem);
-  return hipGetLastError();
+  return launch_defer_kernel<Op, S, NF, 0>(s, n, out, nvec, nelem, R, static_cast<unsigned>(blocks), st);
 }
 
 template <class Op, class S, int NF>

@@ -607,10 +607,8 @@ __device__ __forceinline__ void reduce_tile(const S& s, int n, const OutRef& out
 // measured and did not pay: profiles/r01_tune_ragged.log.)
 // WAVEMAP: lane l of wave w reads vectors w*64*VPT + l + k*64 of a tile (each
 // wave sweeps VPT contiguous KiB per stream) instead of l' + k*kBlock.
-template <class Op, class S, int NF, int G, int VPT, int NT, int STP = (NT ? kStNT : kStPlain),
-          bool WAVEMAP = false>
-__global__ __launch_bounds__(kBlock) void k_wreduce_tiles(const S s, int n, void* __restrict__ out, size_t nvec,
-                                                          size_t nelem) {
+template <class Op, class S, int NF, int G, int VPT, int NT, int STP, bool WAVEMAP>
+__device__ __forceinline__ void tiles_body(const S& s, int n, void* __restrict__ out, size_t nvec, size_t nelem) {
   constexpr size_t kTile = static_cast<size_t>(kBlock) * VPT;
   const size_t full = nvec / kTile;
   const OutRef o = make_out<STP>(out, nvec);
@@ -633,6 +631,37 @@ __global__ __launch_bounds__(kBlock) void k_wreduce_tiles(const S s, int n, void
       reduce_tile<Op, S, NF, G, VPT, NT, false, STP>(s, n, o, t * kTile + threadIdx.x, nvec);
   }
 }
+
+template <class Op, class S, int NF, int G, int VPT, int NT, int STP = (NT ? kStNT : kStPlain),
+          bool WAVEMAP = false>
+__global__ __launch_bounds__(kBlock) void k_wreduce_tiles(const S s, int n, void* __restrict__ out, size_t nvec,
+                                                          size_t nelem) {
+  tiles_body<Op, S, NF, G, VPT, NT, STP, WAVEMAP>(s, n, out, nvec, nelem);
+}
+
+// ---- preloaded arguments (round 6) ----------------------------------------------
+// A block's first input loads wait for the kernel arguments that address them.
+// Arguments that lead the list are preloaded into SGPRs at wave launch
+// (-mllvm -amdgpu-kernarg-preload-count; 14 dwords fit beside the kernarg
+// segment pointer): the fixed fan-in deferred kernel takes nvec, the output
+// and the first kPre input pointers there, so those loads issue at once and
+// only the rest wait for the argument loads (the output must be among them:
+// the buffer resource built from it is set up before the first load, and a
+// wait for one scalar load waits for all of them). Every deferred block of a
+// launch starts at once, so that wait is on the kernel's critical path
+// (scripts/probes/kernarg_preload_probe.hip, profiles/r06_kpp/: an 8-input
+// reduce 10.04-10.08 -> 9.75-9.79 us; the product's gains and the tiled
+// kernel's loss: dispatch.hpp launch_defer_kernel).
+constexpr int kPre = 5;
+template <class S>
+struct PreSlots {
+  const void* q[kPre];
+  const S& s;
+  __device__ const void* ptr(int i) const { return i < kPre ? q[i] : s.ptr(i); }
+  __device__ auto wt(int i) const { return s.wt(i); }
+  __device__ float divisor() const { return s.divisor(); }
+};
+
 
 // ---- deferred-store kernel (round 5) -----------------------------------------
 // HBM pays a bus turnaround each time the traffic switches between reads and
@@ -776,9 +805,9 @@ __device__ __forceinline__ void defer_rows(const S& s, int n, const OutRef& o, s
 // Full blocks defer; the grid's last block, when partial, folds its rows one
 // at a time with bounds checks; block 0 also folds the < E scalar tail.
 // NF > 0: fixed fan-in n == NF; NF == 0: runtime n in groups of G.
-template <class Op, class S, int NF, int G, int RMAX, int U, int STP, int RC = 0>
-__global__ __launch_bounds__(kDeferBlock) void k_wreduce_defer(const S s, int n, int Rrt, void* __restrict__ out,
-                                                               size_t nvec, size_t nelem) {
+template <class Op, class S, int NF, int G, int RMAX, int U, int STP, int RC>
+__device__ __forceinline__ void defer_body(const S& s, int n, int Rrt, void* __restrict__ out, size_t nvec,
+                                           size_t nelem) {
   const int R = RC > 0 ? RC : Rrt;
   const size_t span = static_cast<size_t>(kDeferBlock) * static_cast<size_t>(R);
   const size_t base = static_cast<size_t>(blockIdx.x) * span + threadIdx.x;
@@ -808,6 +837,25 @@ __global__ __launch_bounds__(kDeferBlock) void k_wreduce_defer(const S s, int n,
     const size_t j = nvec * Op::E + threadIdx.x;
     if (j < nelem) fold_scalar<Op, S>(s, NF > 0 ? NF : n, out, j);
   }
+}
+
+template <class Op, class S, int NF, int G, int RMAX, int U, int STP, int RC = 0>
+__global__ __launch_bounds__(kDeferBlock) void k_wreduce_defer(const S s, int n, int Rrt, void* __restrict__ out,
+                                                               size_t nvec, size_t nelem) {
+  defer_body<Op, S, NF, G, RMAX, U, STP, RC>(s, n, Rrt, out, nvec, nelem);
+}
+
+// The fixed fan-in deferred kernel with nvec and the first kPre pointers
+// preloaded (PreSlots above). The grouped form (NF == 0) reads its slots in
+// place in the kernarg segment, at offset 0: it keeps k_wreduce_defer.
+template <class Op, class S, int NF, int G, int RMAX, int U, int STP, int RC = 0>
+__global__ __launch_bounds__(kDeferBlock) void k_wreduce_defer_pre(size_t nvec, void* __restrict__ out,
+                                                                   const void* q0, const void* q1, const void* q2,
+                                                                   const void* q3, const void* q4, const S s, int n,
+                                                                   int Rrt, size_t nelem) {
+  static_assert(NF > 0, "fixed fan-in");
+  const PreSlots<S> ps{{q0, q1, q2, q3, q4}, s};
+  defer_body<Op, PreSlots<S>, NF, G, RMAX, U, STP, RC>(ps, n, Rrt, out, nvec, nelem);
 }
 
 // ---- batched launch: many independent aggregates in one grid -----------------

@@ -21,7 +21,7 @@ def main():
     dev = torch.device("cuda", 0)
     checks = {"switch_seen": os.environ.get("DLSIM_AB") == "1" and int(os.environ["DLSIM_DEFER_R"]) % 2 == 1}
     for n, p in ((4, 5_000_003), (8, 11_181_642), (17, 2_600_001)):
-        assert _native.kernel_name(n, p, torch.float32) == "dlsim::k_wreduce_defer"
+        assert _native.kernel_name(n, p, torch.float32).startswith("dlsim::k_wreduce_defer")
         g = torch.Generator(device=dev).manual_seed(p + n)
         xs = [torch.randn(p, generator=g, device=dev) * 0.05 for _ in range(n)]
         host = np.stack([x.cpu().numpy() for x in xs])

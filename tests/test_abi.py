@@ -172,27 +172,30 @@ def test_kernel_name_follows_the_dispatch():
     count, 256 when the query fails, as here without a GPU): the
     deferred-store kernel for fp32 fan-in 3-10 and above 14 (grouped) from
     10 MB per stream, 11-14 from 16 rows of 512 vectors per CU; the tiled
-    kernel otherwise (dispatch.hpp use_defer)."""
+    kernel otherwise (dispatch.hpp use_defer). Fixed fan-in deferred launches
+    (fp32 up to 14 inputs) take the form with preloaded leading arguments
+    (`k_wreduce_defer_pre`, round 6); the grouped form keeps its name."""
     import torch
     f32, bf16 = torch.float32, torch.bfloat16
     d, t = "dlsim::k_wreduce_defer", "dlsim::k_wreduce_tiles"
+    dp, tp = d + "_pre", t
     cus = torch.cuda.get_device_properties(0).multi_processor_count if torch.cuda.is_available() else 256
 
     def wide(nelem):  # fan-in 11-14: defer from 16 rows of 512 float4 vectors per CU
-        return d if nelem // 4 // 512 >= 16 * cus else t
-    assert _native.kernel_name(8, 11_181_642, f32) == d  # the north star
-    assert _native.kernel_name(8, 11_181_642, f32, _native.DLSIM_FAST) == d
-    assert _native.kernel_name(8, 11_181_642, f32, None) == d  # dlsim_mean
-    assert _native.kernel_name(8, 2_499_999, f32) == t  # below 10 MB
-    assert _native.kernel_name(8, 2_500_000, f32) == d
-    assert _native.kernel_name(3, 11_181_642, f32) == d
-    assert _native.kernel_name(2, 11_181_642, f32) == t
-    assert _native.kernel_name(2, 125_000_000, f32) == t
+        return dp if nelem // 4 // 512 >= 16 * cus else tp
+    assert _native.kernel_name(8, 11_181_642, f32) == dp  # the north star
+    assert _native.kernel_name(8, 11_181_642, f32, _native.DLSIM_FAST) == dp
+    assert _native.kernel_name(8, 11_181_642, f32, None) == dp  # dlsim_mean
+    assert _native.kernel_name(8, 2_499_999, f32) == tp  # below 10 MB
+    assert _native.kernel_name(8, 2_500_000, f32) == dp
+    assert _native.kernel_name(3, 11_181_642, f32) == dp
+    assert _native.kernel_name(2, 11_181_642, f32) == tp
+    assert _native.kernel_name(2, 125_000_000, f32) == tp
     assert _native.kernel_name(12, 5_000_000, f32) == wide(5_000_000)  # < 16 rows per CU on 256 CUs
     assert _native.kernel_name(12, 11_181_642, f32) == wide(11_181_642)
     assert _native.kernel_name(14, 8_388_608, f32) == wide(8_388_608)  # exactly 16 rows per CU on 256 CUs
     assert _native.kernel_name(15, 11_181_642, f32) == d  # the grouped form
     assert _native.kernel_name(100, 11_181_642, f32) == d  # cfg5
     assert _native.kernel_name(100, 2_499_999, f32) == t
-    assert _native.kernel_name(8, 11_181_642, bf16) == t
+    assert _native.kernel_name(8, 11_181_642, bf16) == tp
     assert _native.kernel_name(8, 0, f32) == ""
