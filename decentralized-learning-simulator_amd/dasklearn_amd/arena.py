@@ -1248,6 +1248,33 @@ def _current_stream(idx: int, raw: int) -> torch.cuda.Stream:
     return s
 
 
+def _host_zc_task(models: List[nn.Module]):
+    """(class layout, dtype, parameter indices, every model's parameters) when
+    `models` is a task _host_zc_aggregate runs, else None (host-side checks
+    only; no device call)."""
+    if not ZERO_COPY or device_cache._CACHE is not None:
+        return None
+    known = _CLASS_LAYOUTS.get(type(models[0]))
+    if known is None or len(known.groups) != 1:
+        return None
+    (dt, idx), = known.groups.items()
+    total = known.totals[dt]
+    esz = _elem_size(dt)
+    if dt is torch.float64 or total == 0 or len(models) * total * esz > ZC_MAX_BYTES:
+        return None
+    sig = known._signature
+    k0 = idx[0]
+    all_params = []
+    for m in models:
+        ps = _pyhost.checked_params(m, sig)
+        if ps is None or ps[k0].is_cuda:
+            return None
+        all_params.append(ps)
+    if not pinned_result(total * esz):
+        return None
+    return known, dt, idx, all_params
+
+
 def _host_zc_aggregate(models: List[nn.Module], w32: np.ndarray, mode: int) -> Optional[nn.Module]:
     """The small host task in one pass (round 6): the
     reference's default deployment (host GNLeNets, worker.py:24-33 ->
@@ -1262,28 +1289,13 @@ def _host_zc_aggregate(models: List[nn.Module], w32: np.ndarray, mode: int) -> O
     (the general path then runs it): another signature or layout class, a
     device model, a non-contiguous parameter, more than ZC_MAX_BYTES of rows,
     fp64, the device cache on, or the page-locked result budget spent."""
-    if not ZERO_COPY or device_cache._CACHE is not None:
+    task = _host_zc_task(models)
+    if task is None:
         return None
-    m0 = models[0]
-    known = _CLASS_LAYOUTS.get(type(m0))
-    if known is None or len(known.groups) != 1:
-        return None
-    (dt, idx), = known.groups.items()
+    known, dt, idx, all_params = task
     n = len(models)
     total = known.totals[dt]
-    esz = _elem_size(dt)
-    if dt is torch.float64 or total == 0 or n * total * esz > ZC_MAX_BYTES:
-        return None
-    sig = known._signature
-    k0 = idx[0]
-    all_params = []
-    for m in models:
-        ps = _pyhost.checked_params(m, sig)
-        if ps is None or ps[k0].is_cuda:
-            return None
-        all_params.append(ps)
-    if not pinned_result(total * esz):
-        return None
+    m0 = models[0]
     di = torch.cuda.current_device()
     dev = _DEVICES.get(di)
     if dev is None:
