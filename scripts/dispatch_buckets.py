@@ -3,7 +3,8 @@ trace, bucketed by rotating input set and by position in the timed burst
 (does the spread of the small slices follow the set —
 placement, translation — or the position — launch jitter, clocks?).
 
-bench.py launches step k on set k mod S: W warm-up launches (k = 0..W-1),
+bench.py launches step k on set k mod S: (from round 6) P launches on a
+decoy set first (bench.PRIME_LAUNCHES; --prime P skips them), W warm-up launches (k = 0..W-1),
 then the K timed ones (k = 0..K-1), then launch_floor's backlog (k = 0..B-1);
 the pattern probe and the floor's tiny launches are other kernels.
 
@@ -43,10 +44,11 @@ def main():
     ap.add_argument("--sets", type=int, required=True)
     ap.add_argument("--warmup", type=int, required=True)
     ap.add_argument("--steps", type=int, required=True)
+    ap.add_argument("--prime", type=int, default=0)
     ap.add_argument("--kernel", default="k_wreduce_tiles")
     ap.add_argument("--out")
     a = ap.parse_args()
-    rows = load(a.trace, a.kernel)
+    rows = load(a.trace, a.kernel)[a.prime:]
     names = sorted({r[2] for r in rows})
     if len(names) != 1:
         raise SystemExit(f"expected one reduce kernel, found {names}")

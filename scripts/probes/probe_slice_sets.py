@@ -11,8 +11,10 @@ each set alone (outputs rotating as in the bench), HIP events:
   aligned   the same allocation with every set's first row on a 2 MiB boundary
   per_set   each set its own allocation (arena.resident_empty)
 Prints one JSON line per layout: the per-set means and their spread.
+`--offsets` places one set at 21 offsets into a 4 GiB block instead.
 
     python scripts/probes/probe_slice_sets.py [K]
+    python scripts/probes/probe_slice_sets.py --offsets
 """
 import json
 import os
@@ -79,5 +81,62 @@ def main():
         del keep
 
 
+def offsets_main(k_steps=200):
+    """`--offsets`: one 4 GiB contiguous block, the slice's set placed at every
+    192 MiB step into it (2 MiB aligned), each timed alone; does the fast set
+    follow the offset into the first allocation (a translation fragment or a
+    physical region) or something else? PROBE_ORDER=A0,A10,B0,... visits
+    offsets (192 MiB steps) of blocks A, B, ... (each allocated on first use)
+    in any order; PROBE_FILL=each (fill a set just before timing it) or all
+    (fill a whole block when it is allocated); the token X copies 2 x 1 GiB
+    with ordinary loads and stores (evicts the caches) before the next set."""
+    b, e = _native.shard_range(bench.RESNET18_P, 8, 0, 64)
+    p = e - b
+    stride = row_stride(p, 4)
+    set_elems = N * stride
+    w32 = _native.fp32_weights(bench.weights_for("dirichlet", N))
+    outs = [arena_empty(p, torch.float32, dev) for _ in range(9)]
+    blocks = {}
+    step = (192 << 20) // 4
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    res = []
+    order = os.environ.get("PROBE_ORDER", ",".join(f"A{k}" for k in range(21))).split(",")
+    fill = os.environ.get("PROBE_FILL", "each")
+    for tok in order:
+        if tok == "X":  # stream 2 x 1 GiB through the caches with ordinary copies
+            src = torch.empty((1 << 30) // 4, device=dev).normal_()
+            dst = torch.empty_like(src)
+            for _ in range(2):
+                dst.copy_(src)
+            torch.cuda.synchronize()
+            del src, dst
+            res.append(("X", None, None))
+            continue
+        blk, k = tok[0], int(tok[1:])
+        if blk not in blocks:
+            blocks[blk] = resident_empty((4 << 30) // 4, torch.float32, dev, 2 << 20)
+            if fill == "all":
+                blocks[blk].normal_(0, 0.05)
+        rows = blocks[blk][k * step:k * step + set_elems].view(N, stride)
+        if fill == "each":
+            rows[:, :p].normal_(0, 0.05)
+        plans = [_native.ReducePlan([rows[i, :p] for i in range(N)], w32, o) for o in outs]
+        for j in range(10):
+            plans[j % 9].launch()
+        torch.cuda.synchronize()
+        e0.record()
+        for j in range(k_steps):
+            plans[j % 9].launch()
+        e1.record()
+        torch.cuda.synchronize()
+        res.append((tok, k * 192, round(e0.elapsed_time(e1) * 1e3 / k_steps, 3)))
+    print(json.dumps({"layout": "offsets_in_4GiB", "fill": fill,
+                      "base_va_mod_1GiB": {b: t.data_ptr() % (1 << 30) for b, t in blocks.items()},
+                      "block_offset_MiB_us": res}), flush=True)
+
+
 if __name__ == "__main__":
-    main()
+    if "--offsets" in sys.argv:
+        offsets_main()
+    else:
+        main()
