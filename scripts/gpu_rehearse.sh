@@ -40,5 +40,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/trace_ns_s8 -o r
   > $O/trace_ns_s8.log 2>&1 || exit 1
 SETS=$(python3 -c "import json; print(json.load(open('$O/ns_s8.json'))['data'].split(' rotating input')[0].split()[-1])")
 TRACE=$(find $O/trace_ns_s8 -name '*kernel_trace.csv' | head -1)
-python3 scripts/dispatch_buckets.py "$TRACE" --sets $SETS --warmup 20 --steps 200 --kernel k_wreduce --out $O/ns_s8_buckets.json || exit 1
+python3 scripts/dispatch_buckets.py "$TRACE" --sets $SETS --warmup 20 --steps 200 --prime 8 --kernel k_wreduce --out $O/ns_s8_buckets.json || exit 1
 step done
