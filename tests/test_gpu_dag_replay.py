@@ -16,7 +16,6 @@ from __future__ import annotations
 import copy
 import math
 
-import numpy as np
 import pytest
 import torch
 from torch import nn
