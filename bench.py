@@ -335,7 +335,7 @@ class ReduceWorkload:
         scripts/probes/probe_slice_sets.py). The decoy takes
         that place, so every timed set streams from HBM."""
         from dasklearn_amd import _native
-        from dasklearn_amd.arena import resident_empty
+        from dasklearn_amd.arena import aligned_empty, resident_empty
         if os.environ.get("DLSIM_BENCH_PRIME", "1") == "0":  # A/B of the study only
             return
         rows = resident_empty(batch * n * p_pad, tdt, dev, al).view(batch, n, p_pad)
@@ -344,8 +344,9 @@ class ReduceWorkload:
             out = _out_alloc(p, tdt, dev)
             plan = _native.ReducePlan([rows[0, i, :p] for i in range(n)], w32, out, mode)
         else:
-            out = torch.empty((batch, p), dtype=tdt, device=dev)
-            plan = _native.BatchPlan([([rows[b, i, :p] for i in range(n)], w32, out[b]) for b in range(batch)], mode)
+            out = aligned_empty(batch * p_pad, tdt, dev, al).view(batch, p_pad)  # the timed outputs' layout
+            plan = _native.BatchPlan([([rows[b, i, :p] for i in range(n)], w32, out[b, :p]) for b in range(batch)],
+                                     mode)
         for _ in range(PRIME_LAUNCHES):
             plan.launch(self.stream)
         torch.cuda.synchronize(dev)
