@@ -60,3 +60,19 @@ def test_decoy_is_read_first_and_is_not_a_rotating_set(monkeypatch):
             assert not lo <= t.data_ptr() < hi
     wl2, _ = _workload(n, p, monkeypatch, prime="0")
     assert not [x for x in wl2._keep if isinstance(x, tuple) and len(x) == 3]
+
+
+def test_batched_workload_with_ragged_rows_builds_and_runs(monkeypatch):
+    # p * 4 bytes not a multiple of 16: every task's rows and outputs must still
+    # be 16-B aligned for the table batch (the decoy's included)
+    from dasklearn_amd import _native
+    monkeypatch.setenv("DLSIM_BENCH_PRIME", "1")
+    dev = torch.device("cuda", 0)
+    n, p = 4, 100_003
+    w32 = _native.fp32_weights(bench.weights_for("dirichlet", n))
+    wl = bench.ReduceWorkload(n, p, "f32", w32, _native.DLSIM_EXACT, 3, dev, 9, torch.cuda.current_stream(dev))
+    for k in range(3):
+        wl.launch(k)
+    torch.cuda.synchronize()
+    assert wl.kernel == "dlsim::k_wreduce_batch_table"
+    assert all(torch.isfinite(o).all().item() for o in wl.outs[:3])
